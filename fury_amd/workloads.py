@@ -1,0 +1,274 @@
+"""Synthetic workloads of BASELINE.json's configs: schemas and seeded column generators.
+
+Schemas are written in slot order (Descriptor order: lexicographic Java field name,
+fury-core type/Descriptor.java:324-332) with TypeInference's nullability (primitives non-null,
+boxed/String/List nullable; TypeInference.java:136-238).
+
+Values come from SplitMix64 keyed by (seed, column, GLOBAL row index), so any row range (a shard
+of a multi-GPU run) reproduces exactly the rows a single-GPU run would generate.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .types import (BINARY, BOOL, DATE32, DECIMAL, FLOAT32, FLOAT64, INT8, INT16, INT32, INT64,
+                    LIST, MAP, STRING, STRUCT, TIMESTAMP, Field, array_field, field, map_field,
+                    not_null_field, struct_field, type_width)
+
+
+@dataclass
+class Column:
+    """Arrow-style column (include/fury_row.h ``fury_column``); arrays are numpy (host) or
+    torch tensors (device).  ``child`` is a list: LIST -> [elements], STRUCT -> children,
+    MAP -> [keys, values]."""
+    values: Optional[object] = None
+    validity: Optional[object] = None
+    offsets: Optional[object] = None
+    child: Optional[List["Column"]] = None
+
+
+# ---------------------------------------------------------------------------------------------
+# Schemas
+# ---------------------------------------------------------------------------------------------
+def struct100() -> List[Field]:
+    """C2/C5: f00..f99, even int64 / odd float64, primitive (non-null).  Zero-padded names so
+    lexicographic order = numeric order."""
+    return [not_null_field(f"f{i:02d}", INT64 if i % 2 == 0 else FLOAT64) for i in range(100)]
+
+
+def docs_struct() -> List[Field]:
+    """C1: docs/benchmarks `Struct` (java/benchmark/.../data/Struct.java:136-175): 104 primitive
+    fields f0..f103 typed int/long/float/double by i % 4, sorted by Java name (f0, f1, f10,
+    f100, ...)."""
+    kinds = [INT32, INT64, FLOAT32, FLOAT64]
+    fs = [(f"f{i}", not_null_field(f"f{i}", kinds[i % 4])) for i in range(104)]
+    fs.sort(key=lambda p: p[0])
+    return [f for _, f in fs]
+
+
+def mixed() -> List[Field]:
+    """C3: a:Integer, b:Long, c:Double, s1..s3:String — all nullable."""
+    return [field("a", INT32), field("b", INT64), field("c", FLOAT64),
+            field("s1", STRING), field("s2", STRING), field("s3", STRING)]
+
+
+def nested() -> List[Field]:
+    """C4: id:long, score:double, vals:List<Long>."""
+    return [not_null_field("id", INT64), not_null_field("score", FLOAT64),
+            array_field("vals", INT64, elem_nullable=True)]
+
+
+def narrow() -> List[Field]:
+    """Every fixed-width and var-length scalar type the device path handles, all nullable."""
+    return [field("a_bool", BOOL), field("b_byte", INT8), field("c_short", INT16),
+            field("d_int", INT32), field("e_float", FLOAT32), field("f_date", DATE32),
+            field("g_ts", TIMESTAMP), field("h_dec", DECIMAL), field("i_bin", BINARY),
+            field("j_double", FLOAT64), field("k_ints", LIST, True, (field("item", INT32),)),
+            field("l_shorts", LIST, True, (not_null_field("item", INT16),)),
+            field("m_long", INT64)]
+
+
+def bar() -> List[Field]:
+    """RowEncoderTest.Bar {int f1; String f2} (FMTT/encoder/RowEncoderTest.java:82-92)."""
+    return [not_null_field("f1", INT32), field("f2", STRING)]
+
+
+def beanb() -> List[Field]:
+    """fury-test-core BeanB (test/bean/BeanB.java:28-38)."""
+    return [not_null_field("f1", INT16), field("f2", INT32), not_null_field("f3", INT64),
+            field("f4", FLOAT32), not_null_field("f5", FLOAT64),
+            array_field("int_arr", INT32, elem_nullable=False),
+            array_field("int_list", INT32, elem_nullable=True)]
+
+
+def foo() -> List[Field]:
+    """RowEncoderTest.Foo {int f1; String f2; List<String> f3; Map<String,Integer> f4; Bar f5}."""
+    return [not_null_field("f1", INT32), field("f2", STRING), array_field("f3", STRING),
+            map_field("f4", field("key", STRING), field("value", INT32)),
+            struct_field("f5", bar())]
+
+
+SCHEMAS: Dict[str, List[Field]] = {
+    "struct100": struct100(), "docs_struct": docs_struct(), "mixed": mixed(),
+    "nested": nested(), "narrow": narrow(), "bar": bar(), "beanb": beanb(), "foo": foo(),
+}
+
+# ---------------------------------------------------------------------------------------------
+# SplitMix64 generators (numpy, host)
+# ---------------------------------------------------------------------------------------------
+_M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def _keys(seed: int, col: int, rows: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        k = np.uint64((seed * 0x9E3779B97F4A7C15 + (col + 1) * 0xD1B54A32D192ED03)
+                      & 0xFFFFFFFFFFFFFFFF)
+        return splitmix64(rows.astype(np.uint64) ^ k)
+
+
+def _validity_from_mask(valid: np.ndarray) -> np.ndarray:
+    return np.packbits(valid.astype(np.uint8), bitorder="little")
+
+
+def _gen_fixed(t: int, h: np.ndarray) -> np.ndarray:
+    if t == FLOAT64:
+        return ((h >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53)))
+    if t == FLOAT32:
+        return ((h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / (1 << 24)))
+    if t in (INT64, TIMESTAMP):
+        return h.view(np.int64)
+    w = type_width(t)
+    dt = {1: np.int8, 2: np.int16, 4: np.int32}[w]
+    return h.astype(dt)          # truncation of the 64-bit hash
+
+
+def gen_column(f: Field, seed: int, col: int, start: int, n: int, null_pct: int,
+               str_max: int = 32, list_max: int = 16, list_null_pct: int = 5,
+               elem_null_pct: int = 0) -> Column:
+    rows = np.arange(start, start + n, dtype=np.uint64)
+    h = _keys(seed, col, rows)
+    validity = None
+    valid = np.ones(n, bool)
+    pct = list_null_pct if f.type_id == LIST else null_pct
+    if f.nullable and pct > 0:
+        valid = (((h >> np.uint64(7)) % np.uint64(100)) >= np.uint64(pct))
+        validity = _validity_from_mask(valid)
+    t = f.type_id
+    if t == BOOL:
+        bitv = ((h >> np.uint64(3)) & np.uint64(1)).astype(bool) & valid
+        return Column(values=_validity_from_mask(bitv), validity=validity)
+    if type_width(t) > 0:
+        v = _gen_fixed(t, h)
+        if f.nullable and pct > 0:
+            v = np.where(valid, v, np.zeros_like(v))
+        return Column(values=np.ascontiguousarray(v), validity=validity)
+    if t == DECIMAL:
+        h2 = _keys(seed, col + 1000, rows)
+        v = np.stack([h, h2], axis=1).view(np.uint8).reshape(n, 16).copy()
+        v[~valid] = 0
+        return Column(values=v.reshape(-1), validity=validity)
+    if t in (STRING, BINARY):
+        lens = ((h >> np.uint64(17)) % np.uint64(str_max + 1)).astype(np.int64)
+        lens[~valid] = 0
+        offsets = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        total = int(offsets[-1])
+        rid = np.repeat(rows, lens)
+        pos = np.arange(total, dtype=np.int64) - np.repeat(offsets[:-1], lens)
+        hb = splitmix64(_keys(seed, col + 2000, rid) ^ pos.astype(np.uint64))
+        if t == STRING:
+            data = (np.uint64(32) + hb % np.uint64(95)).astype(np.uint8)   # printable ASCII
+        else:
+            data = (hb >> np.uint64(13)).astype(np.uint8)
+        return Column(values=data, validity=validity, offsets=offsets.astype(np.int32))
+    if t == LIST:
+        elem = f.children[0]
+        lens = ((h >> np.uint64(19)) % np.uint64(list_max + 1)).astype(np.int64)
+        lens[~valid] = 0
+        offsets = np.zeros(n + 1, np.int64)
+        np.cumsum(lens, out=offsets[1:])
+        total = int(offsets[-1])
+        rid = np.repeat(rows, lens)
+        pos = np.arange(total, dtype=np.int64) - np.repeat(offsets[:-1], lens)
+        eh = splitmix64(_keys(seed, col + 3000, rid) ^ (pos.astype(np.uint64) << np.uint64(32)))
+        evalid = np.ones(total, bool)
+        evalidity = None
+        if elem.nullable and elem_null_pct > 0:
+            evalid = ((eh >> np.uint64(5)) % np.uint64(100)) >= np.uint64(elem_null_pct)
+            evalidity = _validity_from_mask(evalid)
+        if elem.type_id == BOOL:
+            ev = _validity_from_mask(((eh >> np.uint64(3)) & np.uint64(1)).astype(bool) & evalid)
+        else:
+            ev = _gen_fixed(elem.type_id, eh)
+            ev = np.where(evalid, ev, np.zeros_like(ev))
+        child = Column(values=np.ascontiguousarray(ev), validity=evalidity)
+        return Column(validity=validity, offsets=offsets.astype(np.int32), child=[child])
+    raise ValueError(f"no generator for type {t}")
+
+
+# per-config generator knobs (BASELINE.json configs + SURVEY §8(d) table)
+_KNOBS = {
+    "struct100": dict(null_pct=0),
+    "docs_struct": dict(null_pct=0),
+    "mixed": dict(null_pct=10, str_max=32),
+    "nested": dict(null_pct=0, list_max=16, list_null_pct=5),
+    "narrow": dict(null_pct=10, str_max=40, list_max=70, list_null_pct=10, elem_null_pct=10),
+    "bar": dict(null_pct=10),
+    "beanb": dict(null_pct=10, list_max=5, list_null_pct=10, elem_null_pct=10),
+}
+
+
+def gen_columns(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
+                start: int = 0, **over) -> List[Column]:
+    knobs = dict(_KNOBS.get(name, dict(null_pct=10)))
+    knobs.update(over)
+    return [gen_column(f, seed, k, start, n, **knobs) for k, f in enumerate(fields)]
+
+
+def algorithmic_bytes_fixed(fields: Sequence[Field], nrows: int) -> dict:
+    """SURVEY §8(d) / BASELINE.md §4 accounting for fixed-width schemas: encode reads the value
+    columns and writes rows; decode the reverse."""
+    col_bytes = sum(type_width(f.type_id) for f in fields) * nrows
+    row_bytes = (((len(fields) + 63) // 64) * 8 + 8 * len(fields)) * nrows
+    return {"encode": col_bytes + row_bytes, "decode": row_bytes + col_bytes,
+            "total": 2 * (col_bytes + row_bytes), "col_bytes": col_bytes, "row_bytes": row_bytes}
+
+
+# ---------------------------------------------------------------------------------------------
+# java.util.Random restatement for the docs Struct values (Struct.java:112-134 uses
+# new Random(17) over getDeclaredFields() declaration order).
+# ---------------------------------------------------------------------------------------------
+class JavaRandom:
+    _MUL = 0x5DEECE66D
+    _MASK = (1 << 48) - 1
+
+    def __init__(self, seed: int):
+        self.seed = (seed ^ self._MUL) & self._MASK
+
+    def _next(self, bits: int) -> int:
+        self.seed = (self.seed * self._MUL + 0xB) & self._MASK
+        r = self.seed >> (48 - bits)
+        if bits == 32 and r >= 1 << 31:
+            r -= 1 << 32
+        return r
+
+    def next_int(self) -> int:
+        return self._next(32)
+
+    def next_long(self) -> int:
+        v = ((self._next(32) << 32) + self._next(32)) & 0xFFFFFFFFFFFFFFFF
+        return v - (1 << 64) if v >= 1 << 63 else v
+
+    def next_float(self) -> float:
+        return self._next(24) / float(1 << 24)
+
+    def next_double(self) -> float:
+        return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
+
+
+def docs_struct_values(fields: Sequence[Field]) -> List[Column]:
+    """One docs-Struct object as 1-row columns (values per Struct.createPOJO)."""
+    rnd = JavaRandom(17)
+    vals = {}
+    for i in range(104):                          # declaration order f0..f103
+        k = i % 4
+        if k == 0:
+            vals[f"f{i}"] = np.array([rnd.next_int()], np.int32)
+        elif k == 1:
+            vals[f"f{i}"] = np.array([rnd.next_long()], np.int64)
+        elif k == 2:
+            vals[f"f{i}"] = np.array([rnd.next_float()], np.float32)
+        else:
+            vals[f"f{i}"] = np.array([rnd.next_double()], np.float64)
+    return [Column(values=vals[f.name]) for f in fields]

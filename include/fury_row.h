@@ -1,0 +1,194 @@
+/*
+ * fury_row.h — C ABI of the MI355X-native Fury row-format codec.
+ *
+ * This is the drop-in boundary for the hot path named by BASELINE.json `north_star`:
+ * java/fury-format's row encode/decode and row -> Arrow-column conversion.  Java objects
+ * cannot cross onto the device, so the boundary is batches of Arrow-style columns <-> batches
+ * of Fury rows; every row's bytes are identical to what the reference writes for the same
+ * field values (see DESIGN.md "Parity").
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference root,
+ * FMT = java/fury-format/src/main/java/org/apache/fury/format):
+ *
+ *   fury_schema_create      TypeInference.inferSchema + BinaryRowWriter ctor layout
+ *                           (FMT/type/TypeInference.java:64-76,136-238,
+ *                            FMT/row/binary/writer/BinaryRowWriter.java:46-52)
+ *   fury_schema_hash        DataTypes.computeSchemaHash (FMT/type/DataTypes.java:499-544)
+ *   fury_type_width         DataTypes.getTypeWidth (FMT/type/DataTypes.java:68-133,225-227)
+ *   fury_row_measure        the writerIndex growth of generated toRow
+ *                           (FMT/encoder/RowEncoderBuilder.java:154-179) — row sizes + scan
+ *   fury_row_encode         RowEncoder.toRow over a batch: generated toRow + BinaryRowWriter /
+ *                           BinaryWriter / BinaryArrayWriter (FMT/encoder/Encoders.java:88-93,
+ *                           FMT/encoder/BaseBinaryEncoderBuilder.java:138-453,
+ *                           FMT/row/binary/writer/BinaryWriter.java:106-194,
+ *                           FMT/row/binary/writer/BinaryRowWriter.java:76-124,
+ *                           FMT/row/binary/writer/BinaryArrayWriter.java:77-118)
+ *   fury_row_decode_measure the Arrow offsets fromRow/ArrowWriter would produce
+ *   fury_row_decode         RowEncoder.fromRow over a batch: BinaryRow getters
+ *                           (FMT/encoder/RowEncoderBuilder.java:185-217,
+ *                            FMT/row/binary/UnsafeTrait.java:68-197,
+ *                            FMT/row/binary/BinaryArray.java:69-78,157-197)
+ *   fury_rows_to_arrow      ArrowWriter.write(row)* + finishAsRecordBatch
+ *                           (FMT/vectorized/ArrowWriter.java:74-99,205-225,519-540)
+ *   fury_frame_rows /       RowEncoder.encode(MemoryBuffer, T) / decode(MemoryBuffer) stream
+ *   fury_unframe_rows       framing [int32 len][int64 schemaHash][row]
+ *                           (FMT/encoder/Encoders.java:165-182,201-213)
+ *
+ * Conventions
+ *   - Every function returns an int status (FURY_OK == 0).  On failure a message is kept per
+ *     thread and can be read with fury_last_error().  Status codes map 1:1 onto the
+ *     reference's exception types (see fury_status).
+ *   - Pointers passed to the fury_row_* / fury_rows_* / fury_*frame* functions are DEVICE
+ *     pointers on the calling thread's current HIP device; `stream` is a hipStream_t (NULL =
+ *     the legacy default stream).  Calls are asynchronous on `stream` unless documented.
+ *   - Arrow layout: validity bitmaps are LSB-first with bit = 1 meaning VALID (Arrow); the row
+ *     bitmap inside a Fury row is LSB-first with bit = 1 meaning NULL (BitUtils.set,
+ *     fury-core memory/BitUtils.java:36-43,175-177).  All integers little-endian, floats as raw
+ *     bits (MemoryBuffer.putFloat64 = doubleToRawLongBits).
+ *   - Canonical bytes are the fresh-buffer bytes of RowEncoder.toRow(obj) (Encoders.java:88-93):
+ *     a null field's slot is 0.  See DESIGN.md "Null slots" for RowEncoder.encode(obj)'s reused
+ *     buffer.
+ */
+#ifndef FURY_ROW_H_
+#define FURY_ROW_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FURY_ROW_ABI_VERSION 1
+
+/* Status codes; the reference exception each one stands for is named. */
+typedef enum fury_status {
+  FURY_OK = 0,
+  FURY_ERR_INVALID_ARGUMENT = 1,       /* IllegalArgumentException / checkArgument          */
+  FURY_ERR_UNSUPPORTED = 2,            /* UnsupportedOperationException
+                                          (TypeInference.java:233-237, BinaryArrayWriter.java:99-101) */
+  FURY_ERR_CLASS_NOT_COMPATIBLE = 3,   /* ClassNotCompatibleException (Encoders.java:170-178) */
+  FURY_ERR_OUT_OF_BOUNDS = 4,          /* IndexOutOfBoundsException (MemoryBuffer bounds)    */
+  FURY_ERR_ENCODER = 5,                /* EncoderException (Encoders.java:215-218)          */
+  FURY_ERR_DEVICE = 6,                 /* HIP runtime failure (no reference equivalent)     */
+  FURY_ERR_CAPACITY = 7                /* output buffer too small for measured bytes        */
+} fury_status;
+
+/* Type ids = org.apache.fury.format.type.ArrowType ids (FMT/type/ArrowType.java:25-148);
+ * they are also the ids hashed by DataTypes.computeSchemaHash. */
+typedef enum fury_type_id {
+  FURY_TYPE_BOOL = 1,
+  FURY_TYPE_INT8 = 3,
+  FURY_TYPE_INT16 = 5,
+  FURY_TYPE_INT32 = 7,
+  FURY_TYPE_INT64 = 9,
+  FURY_TYPE_FLOAT32 = 11,
+  FURY_TYPE_FLOAT64 = 12,
+  FURY_TYPE_STRING = 13,   /* Arrow utf8  */
+  FURY_TYPE_BINARY = 14,
+  FURY_TYPE_DATE32 = 16,
+  FURY_TYPE_TIMESTAMP = 18, /* microseconds */
+  FURY_TYPE_DECIMAL = 23,  /* decimal128, 16 bytes */
+  FURY_TYPE_LIST = 25,
+  FURY_TYPE_STRUCT = 26,
+  FURY_TYPE_MAP = 30
+} fury_type_id;
+
+/* A schema field (a node of org.apache.arrow.vector.types.pojo.Field as built by
+ * TypeInference.inferField).  Fields are given in slot order, i.e. already sorted the way
+ * Descriptor orders bean fields (lexicographic Java field name, Descriptor.java:324-332);
+ * fury_sort_bean_fields() performs that ordering. */
+typedef struct fury_field {
+  const char* name;
+  int32_t type_id;                  /* fury_type_id                                    */
+  int32_t nullable;                 /* FieldType.nullable                              */
+  int32_t num_children;             /* LIST: 1 (element), STRUCT: n, MAP: 2 (key, value) */
+  const struct fury_field* children;
+} fury_field;
+
+typedef struct fury_schema fury_schema; /* opaque, immutable after creation, thread-safe */
+
+/* Arrow-style column (one per top-level field, in schema order).  Array offset is 0.
+ *   fixed width : values = n * width bytes (BOOL: bit-packed, Arrow), validity optional
+ *   STRING/BINARY: offsets = n+1 int32, values = payload bytes
+ *   DECIMAL     : values = n * 16 bytes (decimal128 little-endian)
+ *   LIST        : offsets = n+1 int32 element offsets, child = element column (flattened)
+ * validity: encode input NULL = all valid; decode output NULL = do not write validity.
+ * capacity: decode output only — bytes available in `values` for STRING/BINARY payloads. */
+typedef struct fury_column {
+  void* values;
+  uint8_t* validity;
+  int32_t* offsets;
+  int64_t capacity;
+  struct fury_column* child;
+} fury_column;
+
+/* Describes the computed layout of a schema (BinaryRowWriter ctor, BinaryRowWriter.java:46-52). */
+typedef struct fury_schema_info {
+  int32_t num_fields;
+  int32_t bitmap_bytes;   /* BitUtils.calculateBitmapWidthInBytes(numFields) */
+  int32_t fixed_size;     /* bitmap_bytes + 8 * num_fields                   */
+  int32_t is_fixed;       /* 1 when every field is fixed width: rows are fixed_size bytes */
+  int64_t schema_hash;    /* DataTypes.computeSchemaHash                     */
+} fury_schema_info;
+
+/* ---- version / errors ---------------------------------------------------------------- */
+int32_t fury_abi_version(void);
+/* Copies the calling thread's last error message (NUL-terminated, truncated to len). */
+size_t fury_last_error(char* buf, size_t len);
+
+/* ---- schema (host) --------------------------------------------------------------------- */
+/* DataTypes.getTypeWidth: byte width of a fixed-width type, -1 for variable-length types. */
+int32_t fury_type_width(int32_t type_id);
+/* Sort `n` field indices by Java field name the way Descriptor does (String.compareTo on
+ * UTF-16 code units); writes the permutation to order[0..n). */
+int fury_sort_bean_fields(const char* const* java_names, int32_t n, int32_t* order);
+/* StringUtils.lowerCamelToLowerUnderscore (fury-core util/StringUtils.java:252-271).
+ * Returns the length written (excluding NUL); out must hold 2*strlen(in)+1 bytes. */
+int32_t fury_lower_camel_to_lower_underscore(const char* in, char* out, size_t out_len);
+int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema** out);
+void fury_schema_destroy(fury_schema* schema);
+int fury_schema_get_info(const fury_schema* schema, fury_schema_info* info);
+
+/* ---- device batch codec ---------------------------------------------------------------- */
+/* Row sizes and their exclusive scan: row_offsets[0..nrows] (int64, device); row i occupies
+ * [row_offsets[i], row_offsets[i+1]) and row_offsets[nrows] is the batch's byte total.
+ * For is_fixed schemas this is optional (rows sit at i * fixed_size). */
+int fury_row_measure(const fury_schema* schema, const fury_column* columns, int64_t nrows,
+                     int64_t* row_offsets, void* stream);
+/* Encode nrows rows into `rows` (device, 8-byte aligned, row_offsets[nrows] bytes, or
+ * nrows * fixed_size when row_offsets is NULL and the schema is fixed). */
+int fury_row_encode(const fury_schema* schema, const fury_column* columns, int64_t nrows,
+                    const int64_t* row_offsets, void* rows, void* stream);
+/* Decode pass 1 for variable-length outputs: writes columns[i].offsets (STRING/BINARY/LIST)
+ * and, for LIST, nothing else.  The caller reads offsets[nrows] to size values/child buffers. */
+int fury_row_decode_measure(const fury_schema* schema, const void* rows,
+                            const int64_t* row_offsets, int64_t nrows, fury_column* columns,
+                            void* stream);
+/* Decode rows into columns (RowEncoder.fromRow semantics: a null field leaves 0 bytes and,
+ * when validity != NULL, a cleared validity bit). */
+int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                    int64_t nrows, fury_column* columns, void* stream);
+/* ArrowWriter.write(row) for every row + finishAsRecordBatch: as fury_row_decode but every
+ * column's validity is required (Arrow vectors always carry one) and null lists become
+ * zero-length entries (ListVector fillHoles, ArrowWriter.java:539,223-225). */
+int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                       int64_t nrows, fury_column* columns, void* stream);
+
+/* ---- framing (Encoders.java:201-213 / 165-182) ------------------------------------------ */
+/* Writes the stream RowEncoder.encode(MemoryBuffer, T) produces for each row in turn:
+ * [int32 len = 8 + rowSize][int64 schemaHash][row bytes].  frame_offsets (device, nrows+1)
+ * receives where each frame starts; frame i starts at row_offsets[i] + 12 * i. */
+int fury_frame_rows(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                    int64_t nrows, void* out, int64_t* frame_offsets, void* stream);
+/* Parses such a stream back (sequential frame walk on device): writes row_offsets[0..nrows]
+ * into a packed copy `rows_out` and checks every schemaHash; a mismatch returns
+ * FURY_ERR_CLASS_NOT_COMPATIBLE.  Synchronises `stream`. */
+int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64_t stream_len,
+                      int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FURY_ROW_H_ */

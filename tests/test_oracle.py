@@ -1,0 +1,188 @@
+"""Pins the CPU oracle (oracle/row_oracle.c + oracle/bean_oracle.py) against the reference's own
+known answers and reference-produced schema hashes (tests/golden/), and cross-checks the two
+independent restatements against each other.  CPU only."""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fury_amd import types as T
+from fury_amd.workloads import SCHEMAS, docs_struct_values, gen_columns
+from oracle import bean_oracle as B
+from tests.helpers import assert_columns_equal, columns_to_beans
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _known():
+    return json.load(open(os.path.join(GOLDEN, "known_answers.json")))
+
+
+def test_schema_hash_matches_reference_infer_py(oracle):
+    """DataTypes.computeSchemaHash restatement == the reference's own infer.py output."""
+    d = json.load(open(os.path.join(GOLDEN, "schema_hashes.json")))
+    assert d["schemas"], "no golden schemas"
+    for name, rec in d["schemas"].items():
+        fields = T.schema_from_spec(rec["fields"])
+        assert oracle.schema_hash(fields) == rec["hash"], name
+        assert T.schema_spec(SCHEMAS[name]) == rec["fields"], name
+
+
+def test_schema_hash_overflow_shift(oracle):
+    """computeHash's ArithmeticException path (h >>= 2 then retry) is exercised by wide schemas:
+    the docs Struct hash is the reference's value (checked above) and must be positive."""
+    h = oracle.schema_hash(SCHEMAS["docs_struct"])
+    assert h == 2926194988097786773
+
+
+def test_bar_row_bytes_known_answer(oracle):
+    fields = SCHEMAS["bar"]
+    from fury_amd.workloads import Column
+    cols = [Column(values=np.array([1], np.int32)),
+            Column(values=np.frombuffer(b"str", np.uint8).copy(),
+                   offsets=np.array([0, 3], np.int32))]
+    rows, offs = oracle.encode(fields, cols, 1)
+    assert rows.tobytes().hex() == _known()["bar_row_hex"]["value"]
+    assert B.encode_row(fields, {"f1": 1, "f2": "str"}).hex() == _known()["bar_row_hex"]["value"]
+
+
+def test_array_encoder_list_bar_224():
+    """ArrayEncoderTest.testListEncoder: encode(5 bars).length == 224 (8 + array bytes, see
+    SURVEY §7 trap 5: ArrayEncoder.encode returns getBytes(0, 8 + size))."""
+    elem = T.struct_field("item", SCHEMAS["bar"])
+    bars = [{"f1": k, "f2": f"i{k}"} for k in range(5)]
+    assert 8 + len(B.encode_array(elem, bars)) == _known()["array_encoder_list_bar_bytes"]["value"]
+
+
+def test_array_encoder_nested_1576():
+    bar = T.struct_field("item", SCHEMAS["bar"])
+    l1 = T.Field("item", T.LIST, True, (bar,))
+    l2 = T.Field("item", T.LIST, True, (l1,))
+    vals = [[[{"f1": k, "f2": f"s{k}"} for k in range(3)] for _ in range(i)] for i in range(5)]
+    n = 8 + len(B.encode_array(l2, vals))
+    assert n == _known()["array_encoder_nested_list_bar_bytes"]["value"]
+
+
+def test_array_encoder_list_list_map_10824():
+    bar = T.struct_field("item", SCHEMAS["bar"])
+    foo = SCHEMAS["foo"]
+    key = T.Field("key", T.STRUCT, False, tuple(foo))
+    value = T.Field("value", T.LIST, True, (bar,))
+    m = T.Field("item", T.MAP, True, (key, value))
+    l1 = T.Field("item", T.LIST, True, (m,))
+    foo_val = {"f1": 2, "f2": "str", "f3": ["a", "b", "c"], "f4": [("k1", 1), ("k2", 2)],
+               "f5": {"f1": 1, "f2": "str"}}
+    vals = [[[(foo_val, [{"f1": j, "f2": f"x{j}"}])] for j in range(3)] for _ in range(10)]
+    n = 8 + len(B.encode_array(l1, vals))
+    assert n == _known()["array_encoder_list_list_map_bytes"]["value"]
+
+
+def test_cpp_row_to_string_known_answer():
+    """cpp/fury/row/row_test.cc:96-98 (C++ sibling, same wire format)."""
+    fields = [T.field("f1", T.STRING), T.field("f2", T.INT32),
+              T.array_field("f3", T.INT32),
+              T.map_field("f4", T.field("key", T.STRING), T.field("value", T.FLOAT32)),
+              T.struct_field("f5", [T.field("n1", T.STRING), T.field("n2", T.INT32)])]
+    row = B.encode_row(fields, {"f1": "str", "f2": 1, "f3": [2, 2],
+                                "f4": [("key1", 1.0), ("key2", 1.0)],
+                                "f5": {"n1": "str", "n2": 1}})
+    assert B.row_to_string(fields, row) == _known()["cpp_row_to_string"]["value"]
+
+
+def test_docs_struct_848(oracle):
+    fields = SCHEMAS["docs_struct"]
+    rows, offs = oracle.encode(fields, docs_struct_values(fields), 1)
+    assert len(rows) + 8 == _known()["docs_struct_encode_bytes"]["value"]
+    assert [f.name for f in fields][:8] == ["f0", "f1", "f10", "f100", "f101", "f102", "f103",
+                                            "f11"]
+
+
+@pytest.mark.parametrize("name,n", [("bar", 40), ("beanb", 60), ("mixed", 200), ("nested", 200),
+                                    ("narrow", 150), ("struct100", 20)])
+def test_columnar_oracle_matches_bean_oracle(oracle, name, n):
+    """Two independent restatements (columnar C / value-level Python) give identical bytes."""
+    fields = SCHEMAS[name]
+    cols = gen_columns(name, fields, n, seed=99)
+    rows, offs = oracle.encode(fields, cols, n)
+    beans = columns_to_beans(fields, cols, n)
+    for i, bean in enumerate(beans):
+        want = B.encode_row(fields, bean)
+        got = rows[offs[i]:offs[i + 1]].tobytes()
+        assert got == want, f"{name} row {i}"
+
+
+@pytest.mark.parametrize("name,n", [("mixed", 300), ("nested", 300), ("narrow", 200),
+                                    ("struct100", 50), ("beanb", 80)])
+def test_oracle_roundtrip(oracle, name, n):
+    fields = SCHEMAS[name]
+    cols = gen_columns(name, fields, n, seed=5)
+    rows, offs = oracle.encode(fields, cols, n)
+    dec = oracle.decode(fields, rows, offs, n)
+    assert_columns_equal(fields, dec, cols, n)
+
+
+def test_foo_struct_and_map_roundtrip(oracle):
+    """Nested bean + map + list<string> through the columnar oracle vs the value oracle."""
+    fields = SCHEMAS["foo"]
+    bean = {"f1": 2, "f2": "str", "f3": ["a", "b", "c"], "f4": [("k1", 1), ("k2", 2)],
+            "f5": {"f1": 1, "f2": "str"}}
+    row = B.encode_row(fields, bean)
+    assert B.read_row(row, 0, fields) == bean
+    from fury_amd.workloads import Column
+    cols = [
+        Column(values=np.array([2], np.int32)),
+        Column(values=np.frombuffer(b"str", np.uint8).copy(), offsets=np.array([0, 3], np.int32)),
+        Column(offsets=np.array([0, 3], np.int32),
+               child=[Column(values=np.frombuffer(b"abc", np.uint8).copy(),
+                             offsets=np.array([0, 1, 2, 3], np.int32))]),
+        Column(offsets=np.array([0, 2], np.int32),
+               child=[Column(values=np.frombuffer(b"k1k2", np.uint8).copy(),
+                             offsets=np.array([0, 2, 4], np.int32)),
+                      Column(values=np.array([1, 2], np.int32))]),
+        Column(child=[Column(values=np.array([1], np.int32)),
+                      Column(values=np.frombuffer(b"str", np.uint8).copy(),
+                             offsets=np.array([0, 3], np.int32))]),
+    ]
+    rows, offs = oracle.encode(fields, cols, 1)
+    assert rows.tobytes() == row
+
+
+def test_encode_reuse_differs_only_in_null_slots(oracle):
+    """RowEncoder.encode(obj) reuses one buffer (Encoders.java:146,191-198): a null slot keeps the
+    previous row's slot bytes.  Canonical (toRow) bytes zero it.  Everything else is equal."""
+    fields = SCHEMAS["mixed"]
+    n = 200
+    cols = gen_columns("mixed", fields, n, seed=11)
+    fresh, offs = oracle.encode(fields, cols, n)
+    reused, offs2 = oracle.encode(fields, cols, n, reuse=True)
+    assert np.array_equal(offs, offs2)
+    diff_rows = 0
+    for i in range(n):
+        a = fresh[offs[i]:offs[i + 1]]
+        b = reused[offs[i]:offs[i + 1]]
+        if a.tobytes() != b.tobytes():
+            diff_rows += 1
+            nb = T.bitmap_bytes(len(fields))
+            for k in range(len(fields)):
+                s = slice(nb + 8 * k, nb + 8 * k + 8)
+                if a[s].tobytes() != b[s].tobytes():
+                    assert (a[k >> 3] >> (k & 7)) & 1, "only null slots may differ"
+                    assert not a[s].any()
+    assert diff_rows > 0
+
+
+@pytest.mark.parametrize("name", ["struct100", "mixed", "nested", "narrow", "docs_struct"])
+def test_golden_fixture_regression(oracle, name):
+    d = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    fields = SCHEMAS[name]
+    if name == "docs_struct":
+        cols, n = docs_struct_values(fields), 1
+    else:
+        n = len(d["row_offsets"]) - 1
+        cols = gen_columns(name, fields, n, seed=1234)
+    rows, offs = oracle.encode(fields, cols, n)
+    assert np.array_equal(offs, d["row_offsets"])
+    assert np.array_equal(rows, d["rows"])
