@@ -1,0 +1,264 @@
+"""Headline benchmark: device-resident Fury row-format encode+decode throughput (BASELINE.json).
+
+One step = encode one batch of Arrow-style columns into Fury rows (HBM -> HBM) + decode those
+rows back into columns, through the HIP kernels behind the C ABI.  Default workload is
+configs[1]: 1M rows of Struct-100 (f00..f99, int64/float64, non-null) per GPU; with --gpus N
+(torch.distributed.run, one process per GPU) every rank runs its own independent shard
+(weak scaling, no data-path collective: rows are independent).
+
+Prints ONE JSON line (rank 0).  `value` = total algorithmic bytes of all ranks / max-over-ranks
+time (encode reads 800 B + writes 816 B per row, decode the reverse; 3,232 B/row).
+Also reports the dominant kernel's roofline (HIP events on the launch stream) and the CPU
+baseline (oracle C restatement of the Java writer/reader, 1 thread, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "row-format encode+decode GB/s (device-resident), Struct-100, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def _parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    p.add_argument("--workload", default="struct100", choices=["struct100", "mixed", "nested"])
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-e2e", action="store_true")
+    return p.parse_args()
+
+
+def _buffers(col):
+    out = [t for t in (col.values, col.validity, col.offsets) if t is not None]
+    for c in col.child or []:
+        out.extend(_buffers(c))
+    return out
+
+
+def _nbytes(cols):
+    return sum(t.numel() * t.element_size() for c in cols for t in _buffers(c))
+
+
+def make_device_columns(name, fields, rows, rank, dev):
+    """Synthetic columns resident in HBM.  Struct-100: random 64-bit patterns generated on the
+    device (shard-keyed seed).  Var-length workloads: SplitMix64 generator on the host (shard =
+    global row range), copied once before timing."""
+    import torch
+    from fury_amd.encoder import column_to_device
+    from fury_amd.workloads import Column, gen_columns
+    if name == "struct100":
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        cols = []
+        for f in fields:
+            v = torch.randint(-2**63, 2**63 - 1, (rows,), dtype=torch.int64, device=dev,
+                              generator=g)
+            cols.append(Column(values=v.view(torch.float64) if f.type_id == 12 else v))
+        return cols
+    host = gen_columns(name, fields, rows, seed=1234, start=rank * rows)
+    return [column_to_device(c, dev) for c in host]
+
+
+def cpu_baseline(name, fields, budget_s):
+    """Oracle C restatement (kind "port"), 1 thread, timed on this host on a bounded sample."""
+    import numpy as np
+    from oracle import oracle as O
+    from fury_amd.workloads import gen_columns
+    sample = 20_000 if name == "struct100" else 50_000
+    host = gen_columns(name, fields, sample, seed=99)
+    rows, offs = O.encode(fields, host, sample)
+    col_bytes = sum(a.nbytes for c in host for a in (c.values, c.validity, c.offsets) if a is not None)
+    col_bytes += sum(a.nbytes for c in host for ch in (c.child or []) for a in
+                     (ch.values, ch.validity, ch.offsets) if a is not None)
+    row_bytes = rows.nbytes + (0 if name == "struct100" else offs.nbytes)
+    per_pass = 2 * (col_bytes + row_bytes)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        r, o = O.encode(fields, host, sample)
+        O.decode(fields, r, None if name == "struct100" else o, sample, with_validity=False)
+        reps += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(per_pass * reps / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{reps} x encode+decode of {sample} {name} rows (oracle/row_oracle.c, "
+                      f"toRow/fromRow restatement, 1 thread) in {dt:.1f} s"}
+
+
+def main():
+    args = _parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # orchestration only (barrier + max of timings); the data path has no collective
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from fury_amd.encoder import Encoders
+    from fury_amd.workloads import SCHEMAS
+    fields = SCHEMAS[args.workload]
+    enc = Encoders.bean(fields, device=dev)
+    n = args.rows
+    cols = make_device_columns(args.workload, fields, n, rank, dev)
+    out_cols = enc.alloc_columns(n, validity=False) if enc.schema().is_fixed else None
+    stream = torch.cuda.current_stream()
+
+    # pre-size the row buffer once (measure for var-length schemas)
+    offs = enc.measure(cols, n)
+    total_row_bytes = n * enc.schema().fixed_size if offs is None else int(offs[n].item())
+    rows = torch.empty(max(total_row_bytes, 16), dtype=torch.uint8, device=dev)
+    from fury_amd.encoder import RowBatch
+    batch = RowBatch(rows[:total_row_bytes], offs, n, enc.schema_hash)
+
+    col_bytes = _nbytes(cols)
+    row_bytes = total_row_bytes + (0 if offs is None else offs.numel() * 8)
+    enc_bytes = col_bytes + row_bytes           # read columns, write rows
+    dec_bytes = row_bytes + col_bytes           # read rows, write columns
+    step_bytes = enc_bytes + dec_bytes
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        if offs is not None:       # variable-length rows: sizes + scan are part of encode
+            enc.measure_into(cols, n, offs, stream=stream)
+        enc.encode_into(cols, n, batch.rows, batch.row_offsets, stream=stream)
+        if ev is not None:
+            ev[1].record(stream)
+        if out_cols is not None:
+            enc.decode_batch(batch, validity=False, stream=stream, out=out_cols)
+        else:
+            enc.decode_batch(batch, validity=True, stream=stream)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+
+    t = torch.tensor([dt], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt_max = float(t[0])
+
+    # correctness spot check after timing (cheap, device-side): decoded == input
+    dec_cols = out_cols if out_cols is not None else enc.decode_batch(batch)
+    if args.workload == "struct100":
+        for c, d in zip(cols[:4], dec_cols[:4]):
+            assert torch.equal(c.values.view(torch.uint8), d.values), "decode mismatch"
+
+    e2e = None
+    if rank == 0 and not args.no_e2e and args.workload == "struct100":
+        e2e = end_to_end(enc, cols, n, dev, stream)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    dominant = ("encode", enc_ms, enc_bytes) if enc_ms >= dec_ms else ("decode", dec_ms, dec_bytes)
+    achieved = dominant[2] / (dominant[1] * 1e-3) / 1e9
+    traffic = None
+    pmc_file = os.path.join(ROOT, "profiles", "pmc_struct100.json")
+    if args.workload == "struct100" and os.path.exists(pmc_file) and n == 1_000_000:
+        pm = json.load(open(pmc_file))
+        traffic = pm.get(f"{dominant[0]}_hbm_bytes_per_launch")
+    line = {
+        "metric": METRIC,
+        "value": round(step_bytes * world * args.steps / dt_max / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt_max * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64" if args.workload == "struct100" else "u8",
+        "data": "synthetic (random 64-bit patterns in HBM; no dataset)",
+        "config": {"workload": {"struct100": "Struct-100 encode+decode (configs[1])",
+                                "mixed": "mixed int32/int64/double + 3 utf8 + nulls (configs[2])",
+                                "nested": "id/score + list<int64> (configs[3])"}[args.workload],
+                   "rows_per_gpu": n, "row_bytes": enc.schema().fixed_size if offs is None
+                   else round(total_row_bytes / n, 2),
+                   "algorithmic_bytes_per_step_per_gpu": step_bytes,
+                   "parallelism": f"{world} independent shard(s), no collective"},
+        "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                     "encode_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
+                     "decode_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+    }
+    if e2e is not None:
+        line["e2e_pcie"] = e2e
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds)
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def end_to_end(enc, cols, n, dev, stream):
+    """Host(pinned) columns -> H2D -> encode -> D2H rows, then back: the PCIe-inclusive rate
+    (reported in DESIGN.md, never `value`)."""
+    import torch
+    from fury_amd.encoder import RowBatch
+    host_cols = [c.values.to("cpu").pin_memory() for c in cols]
+    fixed = enc.schema().fixed_size
+    host_rows = torch.empty(n * fixed, dtype=torch.uint8).pin_memory()
+    dev_rows = torch.empty(n * fixed, dtype=torch.uint8, device=dev)
+    from fury_amd.workloads import Column
+    dcols = [Column(values=torch.empty_like(c.values)) for c in cols]
+    out = enc.alloc_columns(n, validity=False)
+    reps = 3
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for h, d in zip(host_cols, dcols):
+            d.values.copy_(h, non_blocking=True)
+        enc.encode_into(dcols, n, dev_rows, None, stream=stream)
+        host_rows.copy_(dev_rows, non_blocking=True)
+        dev_rows.copy_(host_rows, non_blocking=True)
+        enc.decode_batch(RowBatch(dev_rows, None, n, enc.schema_hash), validity=False,
+                         stream=stream, out=out)
+        for h, o in zip(host_cols, out):
+            h.view(torch.uint8).copy_(o.values, non_blocking=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    alg = 2 * (n * 800 + n * fixed)
+    return {"GBps_algorithmic": round(alg / dt / 1e9, 2), "ms_per_step": round(dt * 1e3, 2),
+            "what": "pinned host columns -> H2D -> encode -> D2H rows -> H2D -> decode -> D2H"}
+
+
+if __name__ == "__main__":
+    main()

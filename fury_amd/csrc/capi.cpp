@@ -1,0 +1,259 @@
+// capi.cpp — the extern "C" device entry points of include/fury_row.h: argument checks, then
+// dispatch to the fixed-width tile kernels (fixed.hip) or the variable-length kernels (var.hip).
+// Error statuses mirror the reference's exceptions (see fury_status).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "internal.h"
+#include "kernels.h"
+
+namespace fury {
+
+int check_hip(int hip_status, const char* what) {
+  if (hip_status == hipSuccess) return FURY_OK;
+  return set_error(FURY_ERR_DEVICE, std::string(what) + ": " +
+                                        hipGetErrorString(static_cast<hipError_t>(hip_status)));
+}
+
+namespace {
+
+bool misaligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; }
+
+int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const char* fn) {
+  if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(fn) + ": schema is null");
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(fn) + ": nrows < 0");
+  if (nrows > 0 && s->num_fields > 0 && !cols)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(fn) + ": columns is null");
+  if (!s->device_ok)
+    return set_error(FURY_ERR_UNSUPPORTED,
+                     std::string(fn) + ": no device kernel for " + s->device_reason);
+  return FURY_OK;
+}
+
+int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
+               bool need_validity, FixedArgs* a, bool* fast) {
+  if (s->num_fields > kMaxFixedCols)
+    return set_error(FURY_ERR_UNSUPPORTED, "fixed-width device path handles at most " +
+                                               std::to_string(kMaxFixedCols) + " fields");
+  *a = FixedArgs{};
+  a->ncols = s->num_fields;
+  a->bitmap_bytes = s->bitmap_bytes;
+  a->row_size = s->fixed_size;
+  a->nrows = nrows;
+  bool all8 = true, anyv = false;
+  for (int k = 0; k < s->num_fields; k++) {
+    const FieldPlan& p = s->plan[k];
+    const fury_column& c = cols[k];
+    if (nrows > 0 && !c.values)
+      return set_error(FURY_ERR_INVALID_ARGUMENT,
+                       "column " + std::to_string(k) + " (" + s->fields[k].name + "): values is null");
+    const int w = p.kind == kBool ? 0 : p.width;
+    if (w > 1 && misaligned(c.values, static_cast<uintptr_t>(w)))
+      return set_error(FURY_ERR_INVALID_ARGUMENT,
+                       "column " + std::to_string(k) + ": values not " + std::to_string(w) +
+                           "-byte aligned");
+    if (need_validity && !c.validity)
+      return set_error(FURY_ERR_INVALID_ARGUMENT,
+                       "column " + std::to_string(k) + ": Arrow output needs a validity buffer");
+    a->values[k] = static_cast<const uint8_t*>(c.values);
+    a->validity[k] = c.validity;
+    a->width[k] = static_cast<int8_t>(w);
+    if (w != 8) all8 = false;
+    if (c.validity) anyv = true;
+  }
+  (void)decode;
+  *fast = all8 && !anyv;
+  return FURY_OK;
+}
+
+int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
+             bool need_validity, VarArgs* a) {
+  if (s->num_fields > kMaxVarCols)
+    return set_error(FURY_ERR_UNSUPPORTED, "variable-length device path handles at most " +
+                                               std::to_string(kMaxVarCols) + " fields");
+  *a = VarArgs{};
+  a->ncols = s->num_fields;
+  a->bitmap_bytes = s->bitmap_bytes;
+  a->fixed_size = s->fixed_size;
+  a->nrows = nrows;
+  int nvar = 0;
+  for (int k = 0; k < s->num_fields; k++) {
+    const FieldPlan& p = s->plan[k];
+    const fury_column& c = cols[k];
+    VarCol& v = a->col[k];
+    const std::string who = "column " + std::to_string(k) + " (" + s->fields[k].name + ")";
+    v.kind = p.kind;
+    v.nullable = p.nullable;
+    v.var_slot = -1;
+    v.validity = c.validity;
+    if (need_validity && !c.validity)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": Arrow output needs a validity buffer");
+    switch (p.kind) {
+      case kFixed:
+      case kBool:
+        v.width = p.kind == kBool ? 0 : p.width;
+        v.values = static_cast<const uint8_t*>(c.values);
+        if (nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
+        if (v.width > 1 && misaligned(c.values, v.width))
+          return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values misaligned");
+        break;
+      case kBytes:
+        v.width = 1;
+        v.values = static_cast<const uint8_t*>(c.values);
+        v.offsets = c.offsets;
+        v.var_slot = nvar++;
+        if (nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
+        break;
+      case kDecimal:
+        v.width = 16;
+        v.values = static_cast<const uint8_t*>(c.values);
+        v.var_slot = nvar++;
+        if (nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
+        break;
+      case kListFixed: {
+        v.width = p.elem_type == FURY_TYPE_BOOL ? 0 : p.elem_width;
+        v.offsets = c.offsets;
+        v.var_slot = nvar++;
+        if (nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
+        if (!c.child) {
+          if (!decode || nrows > 0)
+            return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": list needs a child column");
+        } else {
+          v.values = static_cast<const uint8_t*>(c.child->values);
+          v.elem_validity = c.child->validity;
+          if (need_validity && !c.child->validity)
+            return set_error(FURY_ERR_INVALID_ARGUMENT,
+                             who + ": Arrow output needs element validity");
+          if (v.width > 1 && misaligned(v.values, v.width))
+            return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": element values misaligned");
+        }
+        break;
+      }
+      default:
+        return set_error(FURY_ERR_UNSUPPORTED, who + ": no device kernel");
+    }
+  }
+  a->nvar = nvar;
+  return FURY_OK;
+}
+
+}  // namespace
+}  // namespace fury
+
+using namespace fury;
+
+extern "C" {
+
+int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrows,
+                     int64_t* row_offsets, void* stream) {
+  int st = common_checks(s, cols, nrows, "fury_row_measure");
+  if (st) return st;
+  if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
+  if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
+  VarArgs a;
+  st = var_args(s, cols, nrows, false, false, &a);
+  if (st) return st;
+  return launch_measure_rows(a, row_offsets, static_cast<hipStream_t>(stream));
+}
+
+int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows,
+                    const int64_t* row_offsets, void* rows, void* stream) {
+  int st = common_checks(s, cols, nrows, "fury_row_encode");
+  if (st) return st;
+  if (nrows == 0) return FURY_OK;
+  if (!rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
+  if (misaligned(rows, 16)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 16-byte aligned");
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (s->is_fixed) {
+    // Fixed schemas: rows are contiguous at i * fixed_size (row_offsets, when given, are those).
+    FixedArgs a;
+    bool fast = false;
+    st = fixed_args(s, cols, nrows, false, false, &a, &fast);
+    if (st) return st;
+    return launch_encode_fixed(a, static_cast<uint8_t*>(rows), hs, fast);
+  }
+  if (!row_offsets)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "variable-length schema needs row_offsets from fury_row_measure");
+  VarArgs a;
+  st = var_args(s, cols, nrows, false, false, &a);
+  if (st) return st;
+  return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), hs);
+}
+
+int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                            int64_t nrows, fury_column* cols, void* stream) {
+  int st = common_checks(s, cols, nrows, "fury_row_decode_measure");
+  if (st) return st;
+  if (s->is_fixed || nrows == 0) return FURY_OK;   // nothing variable to size
+  if (!rows || !row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/row_offsets null");
+  VarArgs a;
+  st = var_args(s, cols, nrows, true, false, &a);
+  if (st) return st;
+  return launch_decode_measure(a, static_cast<const uint8_t*>(rows), row_offsets,
+                               static_cast<hipStream_t>(stream));
+}
+
+static int decode_impl(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                       int64_t nrows, fury_column* cols, void* stream, bool arrow,
+                       const char* fn) {
+  int st = common_checks(s, cols, nrows, fn);
+  if (st) return st;
+  if (nrows == 0) return FURY_OK;
+  if (!rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (s->is_fixed) {
+    if (misaligned(rows, 16)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 16-byte aligned");
+    FixedArgs a;
+    bool fast = false;
+    st = fixed_args(s, cols, nrows, true, arrow, &a, &fast);
+    if (st) return st;
+    return launch_decode_fixed(a, static_cast<const uint8_t*>(rows), hs, fast);
+  }
+  if (!row_offsets)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "variable-length rows need row_offsets");
+  if (misaligned(rows, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 8-byte aligned");
+  VarArgs a;
+  st = var_args(s, cols, nrows, true, arrow, &a);
+  if (st) return st;
+  return launch_decode_var(a, static_cast<const uint8_t*>(rows), row_offsets, hs, arrow);
+}
+
+int fury_row_decode(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                    int64_t nrows, fury_column* cols, void* stream) {
+  return decode_impl(s, rows, row_offsets, nrows, cols, stream, false, "fury_row_decode");
+}
+
+int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                       int64_t nrows, fury_column* cols, void* stream) {
+  return decode_impl(s, rows, row_offsets, nrows, cols, stream, true, "fury_rows_to_arrow");
+}
+
+int fury_frame_rows(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                    int64_t nrows, void* out, int64_t* frame_offsets, void* stream) {
+  if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (nrows == 0) return FURY_OK;
+  if (!rows || !out) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/out is null");
+  if (!s->is_fixed && !row_offsets)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "variable-length rows need row_offsets");
+  return launch_frame_rows(static_cast<const uint8_t*>(rows), s->is_fixed ? nullptr : row_offsets,
+                           nrows, s->fixed_size, s->schema_hash, static_cast<uint8_t*>(out),
+                           frame_offsets, static_cast<hipStream_t>(stream));
+}
+
+int fury_unframe_rows(const fury_schema* s, const void* stream_bytes, int64_t stream_len,
+                      int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream) {
+  if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
+  if (nrows < 0 || stream_len < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "negative size");
+  if (nrows == 0) return FURY_OK;
+  if (!stream_bytes || !rows_out || !row_offsets)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "null buffer");
+  return launch_unframe_rows(static_cast<const uint8_t*>(stream_bytes), stream_len, nrows,
+                             s->schema_hash, static_cast<uint8_t*>(rows_out), row_offsets,
+                             static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+// kernels.h — launch interfaces between the C-ABI layer (capi.cpp) and the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "internal.h"
+
+namespace fury {
+
+// Columns per fixed-tile launch: the pointer table travels in the kernel argument block
+// (scalar-loaded, no per-call device upload).  Wider schemas are rejected.
+constexpr int kMaxFixedCols = 128;
+
+struct FixedArgs {
+  const uint8_t* values[kMaxFixedCols];
+  uint8_t* validity[kMaxFixedCols];   // encode: input (NULL = all valid); decode: output or NULL
+  int8_t width[kMaxFixedCols];        // 1, 2, 4, 8; 0 = BOOL (bit-packed)
+  int32_t ncols;
+  int32_t bitmap_bytes;
+  int32_t row_size;
+  int32_t pad_;
+  int64_t nrows;
+};
+
+int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast);
+int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast);
+
+// ---- variable-length schemas ----------------------------------------------------------------
+constexpr int kMaxVarCols = 64;
+
+// One top-level field as seen by the var kernels.
+struct VarCol {
+  const uint8_t* values;     // fixed values / bytes payload / decimal values / list child values
+  uint8_t* validity;         // field validity (Arrow bits) or NULL
+  int32_t* offsets;          // bytes / list offsets (n + 1)
+  uint8_t* elem_validity;    // list element validity or NULL
+  int32_t kind;              // FieldKind
+  int32_t width;             // fixed: 1/2/4/8, 0 = bool; list: element width (0 = bool elements)
+  int32_t var_slot;          // index among var fields (decode measure scratch), -1 otherwise
+  int32_t nullable;
+};
+
+struct VarArgs {
+  VarCol col[kMaxVarCols];
+  int32_t ncols;
+  int32_t bitmap_bytes;
+  int32_t fixed_size;
+  int32_t nvar;
+  int64_t nrows;
+};
+
+// Device scratch for scans; grown on demand (hipMalloc outside graph capture only).
+struct Workspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+int workspace_reserve(size_t bytes, void** out);
+
+int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
+int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows,
+                      hipStream_t stream);
+int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
+                          hipStream_t stream);
+int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
+                      hipStream_t stream, bool arrow);
+int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t nrows,
+                      int64_t fixed_size, int64_t schema_hash, uint8_t* out,
+                      int64_t* frame_offsets, hipStream_t stream);
+int launch_unframe_rows(const uint8_t* in, int64_t in_len, int64_t nrows, int64_t schema_hash,
+                        uint8_t* rows_out, int64_t* row_offsets, hipStream_t stream);
+
+}  // namespace fury

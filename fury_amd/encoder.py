@@ -1,0 +1,405 @@
+"""Host-side mirror of ``org.apache.fury.format.encoder.Encoders`` / ``RowEncoder`` over the
+device C ABI.
+
+Reference surface (FMT = java/fury-format/src/main/java/org/apache/fury/format):
+  Encoders.bean(beanClass) -> RowEncoder<T>     FMT/encoder/Encoders.java:60-219
+  RowEncoder.schema / toRow / fromRow / encode / decode   FMT/encoder/RowEncoder.java:26-32,
+                                                          FMT/encoder/Encoder.java:31-40
+  ArrowWriter.write(row) / finishAsRecordBatch  FMT/vectorized/ArrowWriter.java:74-99
+
+A Java bean cannot cross onto the GPU, so the batch methods take/return Arrow-style columns
+(``workloads.Column`` of torch tensors on the device) and ``RowBatch`` objects holding packed
+rows in HBM.  The single-object methods (to_row / from_row / encode / decode) accept a bean as
+a ``dict`` and run through the same device kernels as a batch of one.
+
+Errors raise the Python counterparts of the reference's exceptions (see ``errors``).
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .types import (BINARY, BOOL, DECIMAL, FLOAT32, FLOAT64, LIST, STRING, Field, type_width)
+from .workloads import Column
+
+# ---------------------------------------------------------------------------------------------
+# Errors (status codes of include/fury_row.h fury_status)
+# ---------------------------------------------------------------------------------------------
+
+
+class FuryError(Exception):
+    status = -1
+
+
+class IllegalArgumentException(FuryError, ValueError):
+    status = 1
+
+
+class UnsupportedOperationException(FuryError, NotImplementedError):
+    status = 2
+
+
+class ClassNotCompatibleException(FuryError):
+    """Schema hash mismatch on decode (Encoders.java:170-178)."""
+    status = 3
+
+
+class IndexOutOfBoundsException(FuryError, IndexError):
+    status = 4
+
+
+class EncoderException(FuryError):
+    status = 5
+
+
+class FuryDeviceError(FuryError, RuntimeError):
+    status = 6
+
+
+class CapacityError(FuryError):
+    status = 7
+
+
+_ERRORS = {c.status: c for c in (IllegalArgumentException, UnsupportedOperationException,
+                                 ClassNotCompatibleException, IndexOutOfBoundsException,
+                                 EncoderException, FuryDeviceError, CapacityError)}
+
+
+def _check(status: int):
+    if status != 0:
+        raise _ERRORS.get(status, FuryError)(N.last_error())
+
+
+# ---------------------------------------------------------------------------------------------
+# Schema
+# ---------------------------------------------------------------------------------------------
+def _c_fields(fields: Sequence[Field], keep: list):
+    arr = (N.FuryField * max(len(fields), 1))()
+    for i, f in enumerate(fields):
+        nm = f.name.encode("utf-8")
+        keep.append(nm)
+        arr[i].name = nm
+        arr[i].type_id = f.type_id
+        arr[i].nullable = int(bool(f.nullable))
+        arr[i].num_children = len(f.children)
+        arr[i].children = _c_fields(f.children, keep) if f.children else None
+    keep.append(arr)
+    return arr
+
+
+class Schema:
+    """A schema handle (``fury_schema``): layout + ``DataTypes.computeSchemaHash``."""
+
+    def __init__(self, fields: Sequence[Field]):
+        self.fields: List[Field] = list(fields)
+        keep: list = []
+        h = ctypes.c_void_p()
+        _check(N.lib().fury_schema_create(_c_fields(self.fields, keep), len(self.fields),
+                                          ctypes.byref(h)))
+        self._h = h
+        info = N.FurySchemaInfo()
+        _check(N.lib().fury_schema_get_info(h, ctypes.byref(info)))
+        self.num_fields = info.num_fields
+        self.bitmap_bytes = info.bitmap_bytes
+        self.fixed_size = info.fixed_size
+        self.is_fixed = bool(info.is_fixed)
+        self.schema_hash = int(info.schema_hash)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.lib().fury_schema_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def __repr__(self):
+        return f"Schema({self.fields}, hash={self.schema_hash})"
+
+
+# ---------------------------------------------------------------------------------------------
+# Device columns <-> C structs
+# ---------------------------------------------------------------------------------------------
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        raise IllegalArgumentException("device columns must be torch tensors")
+    if t.device.type != "cuda":
+        raise IllegalArgumentException(f"tensor on {t.device}, expected a GPU tensor")
+    if not t.is_contiguous():
+        raise IllegalArgumentException("tensor must be contiguous")
+    return t.data_ptr()
+
+
+def _c_columns(cols: Sequence[Column], keep: list):
+    arr = (N.FuryColumn * max(len(cols), 1))()
+    for i, c in enumerate(cols):
+        arr[i].values = _ptr(c.values)
+        arr[i].validity = _ptr(c.validity)
+        arr[i].offsets = _ptr(c.offsets)
+        arr[i].capacity = 0 if c.values is None else c.values.numel() * c.values.element_size()
+        arr[i].child = _c_columns(c.child, keep) if c.child else None
+    keep.append(arr)
+    return arr
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def column_to_device(c: Column, device) -> Column:
+    def t(a):
+        if a is None:
+            return None
+        if isinstance(a, torch.Tensor):
+            return a.to(device)
+        return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+    return Column(values=t(c.values), validity=t(c.validity), offsets=t(c.offsets),
+                  child=[column_to_device(x, device) for x in c.child] if c.child else None)
+
+
+def column_to_host(c: Column) -> Column:
+    def h(a):
+        if a is None:
+            return None
+        return a.detach().cpu().numpy()
+    return Column(values=h(c.values), validity=h(c.validity), offsets=h(c.offsets),
+                  child=[column_to_host(x) for x in c.child] if c.child else None)
+
+
+@dataclass
+class RowBatch:
+    """Packed rows in device memory: row i = rows[row_offsets[i]:row_offsets[i+1]] (or
+    i * fixed_size for fixed-width schemas, where row_offsets is None)."""
+    rows: torch.Tensor
+    row_offsets: Optional[torch.Tensor]
+    nrows: int
+    schema_hash: int
+
+    def row_bytes(self, i: int, fixed_size: int) -> bytes:
+        if self.row_offsets is None:
+            b, e = i * fixed_size, (i + 1) * fixed_size
+        else:
+            b, e = int(self.row_offsets[i]), int(self.row_offsets[i + 1])
+        return bytes(self.rows[b:e].cpu().numpy())
+
+
+# ---------------------------------------------------------------------------------------------
+# RowEncoder
+# ---------------------------------------------------------------------------------------------
+class RowEncoder:
+    """``RowEncoder<T>`` with batch methods; not thread-safe per instance (like the reference,
+    Encoders.java:74,146)."""
+
+    def __init__(self, fields: Sequence[Field], device=None):
+        self._schema = Schema(fields)
+        self.device = torch.device(device if device is not None else "cuda")
+
+    # -- RowEncoder API ------------------------------------------------------------------
+    def schema(self) -> Schema:
+        return self._schema
+
+    @property
+    def schema_hash(self) -> int:
+        return self._schema.schema_hash
+
+    # -- batch API -----------------------------------------------------------------------
+    def measure(self, columns: Sequence[Column], nrows: int, stream=None) -> Optional[torch.Tensor]:
+        """Row offsets (int64[nrows+1], device) for variable-length schemas; None if fixed."""
+        if self._schema.is_fixed:
+            return None
+        offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
+        keep: list = []
+        _check(N.lib().fury_row_measure(self._schema.handle, _c_columns(columns, keep), nrows,
+                                        offs.data_ptr(), _stream_handle(stream)))
+        return offs
+
+    def measure_into(self, columns: Sequence[Column], nrows: int, offs: torch.Tensor,
+                     stream=None) -> None:
+        keep: list = []
+        _check(N.lib().fury_row_measure(self._schema.handle, _c_columns(columns, keep), nrows,
+                                        _ptr(offs), _stream_handle(stream)))
+
+    def encode_into(self, columns: Sequence[Column], nrows: int, rows: torch.Tensor,
+                    row_offsets: Optional[torch.Tensor], stream=None) -> None:
+        keep: list = []
+        _check(N.lib().fury_row_encode(self._schema.handle, _c_columns(columns, keep), nrows,
+                                       _ptr(row_offsets), _ptr(rows), _stream_handle(stream)))
+
+    def encode_batch(self, columns: Sequence[Column], nrows: int, stream=None) -> RowBatch:
+        offs = self.measure(columns, nrows, stream)
+        if offs is None:
+            total = nrows * self._schema.fixed_size
+        else:
+            total = int(offs[nrows].item())
+        rows = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
+        self.encode_into(columns, nrows, rows, offs, stream)
+        return RowBatch(rows[:total] if total else rows[:0], offs, nrows, self.schema_hash)
+
+    def alloc_columns(self, nrows: int, validity: bool = True) -> List[Column]:
+        """Output columns for fixed-width fields (variable ones are sized by decode_measure)."""
+        out = []
+        for f in self._schema.fields:
+            vb = (torch.empty((nrows + 7) // 8, dtype=torch.uint8, device=self.device)
+                  if validity else None)
+            if f.type_id == BOOL:
+                out.append(Column(values=torch.empty((nrows + 7) // 8, dtype=torch.uint8,
+                                                     device=self.device), validity=vb))
+            elif type_width(f.type_id) > 0:
+                out.append(Column(values=torch.empty(nrows * type_width(f.type_id),
+                                                     dtype=torch.uint8, device=self.device),
+                                  validity=vb))
+            elif f.type_id == DECIMAL:
+                out.append(Column(values=torch.empty(nrows * 16, dtype=torch.uint8,
+                                                     device=self.device), validity=vb))
+            elif f.type_id in (STRING, BINARY):
+                out.append(Column(offsets=torch.empty(nrows + 1, dtype=torch.int32,
+                                                      device=self.device), validity=vb))
+            elif f.type_id == LIST:
+                out.append(Column(offsets=torch.empty(nrows + 1, dtype=torch.int32,
+                                                      device=self.device), validity=vb,
+                                  child=[Column()]))
+            else:
+                raise UnsupportedOperationException(f"no device decode for {f}")
+        return out
+
+    def _decode(self, batch: RowBatch, validity: bool, arrow: bool, stream=None,
+                out: Optional[List[Column]] = None) -> List[Column]:
+        n = batch.nrows
+        cols = out if out is not None else self.alloc_columns(n, validity)
+        keep: list = []
+        sh = _stream_handle(stream)
+        if not self._schema.is_fixed:
+            _check(N.lib().fury_row_decode_measure(self._schema.handle, _ptr(batch.rows),
+                                                   _ptr(batch.row_offsets), n,
+                                                   _c_columns(cols, keep), sh))
+            for f, c in zip(self._schema.fields, cols):
+                if f.type_id in (STRING, BINARY):
+                    total = int(c.offsets[n].item()) if n else 0
+                    c.values = torch.empty(max(total, 1), dtype=torch.uint8, device=self.device)
+                elif f.type_id == LIST:
+                    total = int(c.offsets[n].item()) if n else 0
+                    e = f.children[0]
+                    nbytes = (total + 7) // 8 if e.type_id == BOOL else total * type_width(e.type_id)
+                    c.child = [Column(
+                        values=torch.empty(nbytes + 8, dtype=torch.uint8, device=self.device),
+                        validity=(torch.zeros((total + 7) // 8 + 4, dtype=torch.uint8,
+                                              device=self.device) if validity else None))]
+            keep = []
+        fn = N.lib().fury_rows_to_arrow if arrow else N.lib().fury_row_decode
+        _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), n,
+                  _c_columns(cols, keep), sh))
+        return cols
+
+    def decode_batch(self, batch: RowBatch, validity: bool = True, stream=None,
+                     out: Optional[List[Column]] = None) -> List[Column]:
+        """Rows -> columns (generated fromRow semantics)."""
+        if batch.schema_hash != self.schema_hash:
+            raise ClassNotCompatibleException(
+                f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
+                f"hash are {self.schema_hash}/{batch.schema_hash}. Please check writer schema.")
+        return self._decode(batch, validity, False, stream, out)
+
+    # -- framing (Encoders.java:165-182, 201-213) ------------------------------------------
+    def frame(self, batch: RowBatch, stream=None):
+        """Java ``encode(MemoryBuffer, T)`` stream for every row: returns (bytes, frame_offsets)."""
+        n = batch.nrows
+        total = batch.rows.numel() + 12 * n
+        out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
+        fo = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        _check(N.lib().fury_frame_rows(self._schema.handle, _ptr(batch.rows),
+                                       _ptr(batch.row_offsets), n, _ptr(out), _ptr(fo),
+                                       _stream_handle(stream)))
+        return out[:total], fo
+
+    def unframe(self, stream_bytes: torch.Tensor, nrows: int, stream=None) -> RowBatch:
+        """Parses a ``decode(MemoryBuffer)`` stream; raises ClassNotCompatibleException on a
+        schema-hash mismatch."""
+        rows = torch.empty(max(stream_bytes.numel(), 16), dtype=torch.uint8, device=self.device)
+        offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
+        _check(N.lib().fury_unframe_rows(self._schema.handle, _ptr(stream_bytes),
+                                         stream_bytes.numel(), nrows, _ptr(rows), _ptr(offs),
+                                         _stream_handle(stream)))
+        total = int(offs[nrows].item()) if nrows else 0
+        return RowBatch(rows[:total], None if self._schema.is_fixed else offs, nrows,
+                        self.schema_hash)
+
+    # -- single-object API (a bean is a dict name -> value) --------------------------------
+    def to_row(self, bean: dict) -> bytes:
+        """``toRow(obj).toBytes()``: canonical row bytes of one bean."""
+        from .beans import beans_to_columns
+        cols = [column_to_device(c, self.device)
+                for c in beans_to_columns(self._schema.fields, [bean])]
+        b = self.encode_batch(cols, 1)
+        return b.row_bytes(0, self._schema.fixed_size)
+
+    def from_row(self, row: bytes) -> dict:
+        from .beans import columns_to_beans
+        t = torch.frombuffer(bytearray(row), dtype=torch.uint8).to(self.device)
+        offs = None if self._schema.is_fixed else torch.tensor([0, len(row)], dtype=torch.int64,
+                                                              device=self.device)
+        cols = self.decode_batch(RowBatch(t, offs, 1, self.schema_hash))
+        return columns_to_beans(self._schema.fields, [column_to_host(c) for c in cols], 1)[0]
+
+    def encode(self, bean: dict) -> bytes:
+        """``encode(T)``: [int64 schemaHash][row] (Encoders.java:191-198)."""
+        return struct.pack("<q", self.schema_hash) + self.to_row(bean)
+
+    def decode(self, data: bytes) -> dict:
+        """``decode(byte[])``: checks the 8-byte schema hash first (Encoders.java:169-188)."""
+        if len(data) < 8:
+            raise IndexOutOfBoundsException("buffer shorter than the schema hash")
+        peer = struct.unpack_from("<q", data, 0)[0]
+        if peer != self.schema_hash:
+            raise ClassNotCompatibleException(
+                f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
+                f"hash are {self.schema_hash}/{peer}. Please check writer schema.")
+        return self.from_row(data[8:])
+
+
+class Encoders:
+    """``Encoders`` factory (Encoders.java:60-73)."""
+
+    @staticmethod
+    def bean(fields: Sequence[Field], device=None) -> RowEncoder:
+        return RowEncoder(fields, device)
+
+
+class ArrowWriter:
+    """``ArrowWriter`` (ArrowWriter.java:55-99) over a RowBatch: ``write(batch)`` converts a
+    whole batch on the device; ``finish()`` returns device Arrow columns and
+    ``finish_as_record_batch()`` a pyarrow.RecordBatch on the host."""
+
+    def __init__(self, encoder: RowEncoder):
+        self._enc = encoder
+        self._cols: Optional[List[Column]] = None
+        self._n = 0
+
+    def write(self, batch: RowBatch, stream=None) -> None:
+        self._cols = self._enc._decode(batch, True, True, stream)
+        self._n = batch.nrows
+
+    def finish(self) -> List[Column]:
+        return self._cols or []
+
+    def finish_as_record_batch(self):
+        from .arrow import columns_to_record_batch
+        return columns_to_record_batch(self._enc.schema().fields,
+                                       [column_to_host(c) for c in self.finish()], self._n)
+
+    def reset(self) -> None:
+        self._cols = None
+        self._n = 0

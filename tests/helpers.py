@@ -9,45 +9,7 @@ import numpy as np
 from fury_amd.types import (BINARY, BOOL, DATE32, DECIMAL, FLOAT32, FLOAT64, INT8, INT16, INT32,
                             INT64, LIST, MAP, STRING, STRUCT, TIMESTAMP, Field, type_width)
 
-_NP = {INT8: np.int8, INT16: np.int16, INT32: np.int32, INT64: np.int64, FLOAT32: np.float32,
-       FLOAT64: np.float64, DATE32: np.int32, TIMESTAMP: np.int64}
-
-
-def _valid(c, i):
-    return c.validity is None or bool((int(c.validity[i >> 3]) >> (i & 7)) & 1)
-
-
-def value_at(f: Field, c, i: int):
-    """Python value of entry i (None for null), matching oracle/bean_oracle.py conventions."""
-    if not _valid(c, i):
-        return None
-    t = f.type_id
-    if t == BOOL:
-        return bool((int(np.asarray(c.values).view(np.uint8)[i >> 3]) >> (i & 7)) & 1)
-    if type_width(t) > 0:
-        v = np.asarray(c.values).view(np.uint8).view(_NP[t])[i]
-        if t in (FLOAT32, FLOAT64):
-            # keep the raw bits: return the float but through struct to preserve NaN payloads
-            return float(v)
-        return int(v)
-    if t in (STRING, BINARY):
-        b = bytes(np.asarray(c.values).view(np.uint8)[int(c.offsets[i]):int(c.offsets[i + 1])])
-        return b.decode("utf-8") if t == STRING else b
-    if t == DECIMAL:
-        return bytes(np.asarray(c.values).view(np.uint8)[16 * i:16 * i + 16])
-    if t == LIST:
-        return [value_at(f.children[0], c.child[0], j)
-                for j in range(int(c.offsets[i]), int(c.offsets[i + 1]))]
-    if t == STRUCT:
-        return {fc.name: value_at(fc, cc, i) for fc, cc in zip(f.children, c.child)}
-    if t == MAP:
-        return [(value_at(f.children[0], c.child[0], j), value_at(f.children[1], c.child[1], j))
-                for j in range(int(c.offsets[i]), int(c.offsets[i + 1]))]
-    raise ValueError(t)
-
-
-def columns_to_beans(fields: Sequence[Field], cols, n: int) -> List[dict]:
-    return [{f.name: value_at(f, c, i) for f, c in zip(fields, cols)} for i in range(n)]
+from fury_amd.beans import columns_to_beans, value_at  # noqa: F401
 
 
 def as_u8(a) -> np.ndarray:

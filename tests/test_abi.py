@@ -1,0 +1,120 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol include/fury_row.h declares
+with the signatures the bindings use, and its host-side schema logic (layout, schema hash,
+field order, name conversion, argument errors) matches the reference.  No GPU compute."""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import re
+import subprocess
+
+import pytest
+
+from fury_amd import types as T
+from fury_amd.workloads import SCHEMAS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fury_row.h")
+
+
+def _declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(fury_[a-z_0-9]+)\s*\(", src, re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_entry_points():
+    names = _declared_functions()
+    assert "fury_row_encode" in names and "fury_rows_to_arrow" in names
+    assert len(names) >= 15
+
+
+def test_library_exports_every_declared_symbol():
+    from fury_amd import _native as N
+    L = N.lib()
+    for name in _declared_functions():
+        assert hasattr(L, name), f"{name} declared in fury_row.h but not exported"
+    assert set(_declared_functions()) == set(N.SIGNATURES), "bindings table out of sync"
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (fury_[a-z_0-9]+)$", out, re.M))
+    assert set(_declared_functions()) <= exported
+
+
+def test_abi_version():
+    from fury_amd import _native as N
+    assert N.lib().fury_abi_version() == 1
+
+
+def test_type_width_matches_datatypes():
+    from fury_amd import _native as N
+    for tid in (T.BOOL, T.INT8, T.INT16, T.INT32, T.INT64, T.FLOAT32, T.FLOAT64, T.DATE32,
+                T.TIMESTAMP, T.STRING, T.BINARY, T.DECIMAL, T.LIST, T.STRUCT, T.MAP):
+        assert N.lib().fury_type_width(tid) == T.type_width(tid)
+
+
+def test_schema_layout_and_hash_match_golden():
+    from fury_amd.encoder import Schema
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "schema_hashes.json")))
+    for name, rec in d["schemas"].items():
+        s = Schema(T.schema_from_spec(rec["fields"]))
+        assert s.schema_hash == rec["hash"], name
+        assert s.fixed_size == T.fixed_size(s.fields)
+        assert s.is_fixed == T.is_fixed_schema(s.fields)
+    s = Schema(SCHEMAS["struct100"])
+    assert (s.bitmap_bytes, s.fixed_size, s.num_fields) == (16, 816, 100)
+    s = Schema(SCHEMAS["docs_struct"])
+    assert s.fixed_size == 848
+
+
+def test_sort_bean_fields_like_descriptor():
+    from fury_amd import _native as N
+    names = [f"f{i}" for i in range(104)] + ["beanB", "b", "Z", "élan", "a\U0001F600", "a￿"]
+    arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+    order = (ctypes.c_int32 * len(names))()
+    assert N.lib().fury_sort_bean_fields(arr, len(names), order) == 0
+    got = [names[i] for i in order]
+    # String.compareTo = UTF-16 code-unit order (surrogate pair D83D < FFFF)
+    assert got == sorted(names, key=lambda s: s.encode("utf-16-be"))
+    assert got[:3] == ["Z", "a\U0001F600", "a￿"]
+    assert [f.name for f in T.infer_bean_schema([(n, T.field(n, T.INT32)) for n in
+                                                 ("intList", "f1", "intArr")])] == \
+        ["f1", "int_arr", "int_list"]
+
+
+@pytest.mark.parametrize("src,want", [("doubleList", "double_list"), ("f1", "f1"),
+                                      ("beanBIterable", "bean_b_iterable"),
+                                      ("stringBeanBMap", "string_bean_b_map"), ("ABC", "_a_b_c")])
+def test_lower_camel_to_lower_underscore(src, want):
+    from fury_amd import _native as N
+    out = ctypes.create_string_buffer(2 * len(src) + 1)
+    n = N.lib().fury_lower_camel_to_lower_underscore(src.encode(), out, len(out))
+    assert out.value.decode() == want and n == len(want)
+    assert T.lower_camel_to_lower_underscore(src) == want
+
+
+def test_schema_create_errors():
+    from fury_amd.encoder import IllegalArgumentException, Schema, UnsupportedOperationException
+    with pytest.raises(UnsupportedOperationException):
+        Schema([T.Field("x", 99)])
+    with pytest.raises(IllegalArgumentException):
+        Schema([T.Field("l", T.LIST, True, ())])       # list without element field
+
+
+def test_device_calls_reject_bad_arguments_without_touching_gpu():
+    """Argument validation happens on the host before any HIP call."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Schema
+    L = N.lib()
+    assert L.fury_row_encode(None, None, 1, None, None, None) == 1
+    s = Schema(SCHEMAS["foo"])       # nested struct + map: no device kernel yet
+    cols = (N.FuryColumn * 5)()
+    assert L.fury_row_encode(s.handle, cols, 1, None, None, None) == 2
+    assert "nested struct" in N.last_error() or "map" in N.last_error() or \
+        "variable-length" in N.last_error()
+    s2 = Schema(SCHEMAS["struct100"])
+    cols2 = (N.FuryColumn * 100)()
+    assert L.fury_row_encode(s2.handle, cols2, 4, None, None, None) == 1   # rows is null
+    assert L.fury_row_encode(s2.handle, cols2, -1, None, None, None) == 1  # nrows < 0
