@@ -57,9 +57,9 @@ int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, boo
     if (need_validity && !c.validity)
       return set_error(FURY_ERR_INVALID_ARGUMENT,
                        "column " + std::to_string(k) + ": Arrow output needs a validity buffer");
-    a->values[k] = static_cast<const uint8_t*>(c.values);
-    a->validity[k] = c.validity;
-    a->width[k] = static_cast<int8_t>(w);
+    a->col[k].values = static_cast<const uint8_t*>(c.values);
+    a->col[k].validity = c.validity;
+    a->col[k].width = w;
     if (w != 8) all8 = false;
     if (c.validity) anyv = true;
   }

@@ -114,13 +114,13 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
       if (idx < total && r < nr) {
         const int64_t row = r0 + r;
         if (kFast) {
-          v[u] = *reinterpret_cast<const uint64_t*>(a.values[c] + row * 8);
+          v[u] = *reinterpret_cast<const uint64_t*>(a.col[c].values + row * 8);
         } else {
-          const uint8_t* vb = a.validity[c];
+          const uint8_t* vb = a.col[c].validity;
           if (vb && !((vb[row >> 3] >> (row & 7)) & 1)) {
             isnull[u] = true;
           } else {
-            v[u] = load_value(a.values[c], row, a.width[c]);
+            v[u] = load_value(a.col[c].values, row, a.col[c].width);
           }
         }
       }
@@ -170,15 +170,15 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       if (kFast) {
         if (live) {
           uint64_t v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-          *reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(a.values[c]) + row * 8) = v;
+          *reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(a.col[c].values) + row * 8) = v;
         }
         continue;
       }
       bool isnull = live && ((rowp[c >> 3] >> (c & 7)) & 1);
       uint64_t v = 0;
       if (live && !isnull) v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-      const int w = a.width[c];
-      uint8_t* dst = const_cast<uint8_t*>(a.values[c]);
+      const int w = a.col[c].width;
+      uint8_t* dst = const_cast<uint8_t*>(a.col[c].values);
       // rows [rbase, rbase + 64) of this wave; rbase % 64 == 0 and R % 64 == 0
       const int64_t rbase = row - lane;
       const int64_t nvalid = a.nrows - rbase;                    // >= 1 for live waves
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       } else if (live) {
         store_value(dst, row, w, v);
       }
-      uint8_t* vb = a.validity[c];
+      uint8_t* vb = a.col[c].validity;
       if (vb) {
         uint64_t ok = __ballot(live && !isnull);
         if (lane < nbytes) vb[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));

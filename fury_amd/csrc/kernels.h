@@ -13,10 +13,19 @@ namespace fury {
 // (scalar-loaded, no per-call device upload).  Wider schemas are rejected.
 constexpr int kMaxFixedCols = 128;
 
+// Per-column record.  Every member is naturally aligned inside an 8-byte-aligned record: the
+// kernels index this table with a wave-uniform column number, which the compiler turns into
+// scalar (SMEM) loads; an int8 side array produced a byte-offset SMEM base that gfx950 masks
+// to dword alignment (observed as an aperture fault), so keep all members >= 4 bytes.
+struct FixedCol {
+  const uint8_t* values;
+  uint8_t* validity;                  // encode: input (NULL = all valid); decode: output or NULL
+  int32_t width;                      // 1, 2, 4, 8; 0 = BOOL (bit-packed)
+  int32_t pad_;
+};
+
 struct FixedArgs {
-  const uint8_t* values[kMaxFixedCols];
-  uint8_t* validity[kMaxFixedCols];   // encode: input (NULL = all valid); decode: output or NULL
-  int8_t width[kMaxFixedCols];        // 1, 2, 4, 8; 0 = BOOL (bit-packed)
+  FixedCol col[kMaxFixedCols];
   int32_t ncols;
   int32_t bitmap_bytes;
   int32_t row_size;
