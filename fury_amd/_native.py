@@ -63,6 +63,8 @@ SIGNATURES = {
                                                _P]),
     "fury_row_decode": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(FuryColumn), _P]),
     "fury_rows_to_arrow": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(FuryColumn), _P]),
+    "fury_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _I32]),
+    "fury_get_tuning": (_I32, [ctypes.c_char_p]),
     "fury_frame_rows": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P]),
     "fury_unframe_rows": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P]),
 }

@@ -231,6 +231,21 @@ int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* ro
   return decode_impl(s, rows, row_offsets, nrows, cols, stream, true, "fury_rows_to_arrow");
 }
 
+int fury_set_tuning(const char* key, int32_t value) {
+  if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
+  if (std::string(key) == "fixed_variant") {
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..2");
+    set_fixed_variant(value);
+    return FURY_OK;
+  }
+  return set_error(FURY_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
+}
+
+int32_t fury_get_tuning(const char* key) {
+  if (key && std::string(key) == "fixed_variant") return fixed_variant();
+  return -1;
+}
+
 int fury_frame_rows(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, void* out, int64_t* frame_offsets, void* stream) {
   if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");

@@ -19,6 +19,7 @@
 // No MFMA: the kernel is HBM-bound byte movement; LDS only re-shapes the access pattern.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 
 #include "internal.h"
@@ -198,6 +199,184 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
   }
 }
 
+// ---- pipelined persistent variants (fast path: all 8-byte columns, no validity) ------------
+// One workgroup walks tiles blockIdx.x, +gridDim.x, ...; while tile t's LDS image streams out to
+// HBM, tile t+1's global loads are already in flight (register staging).  Barriers only order
+// LDS (lgkmcnt(0) + s_barrier): no vmcnt(0) drain, so the prefetch survives them.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool kNT>
+__device__ __forceinline__ void store16(uint8_t* p, const __attribute__((ext_vector_type(4))) uint32_t& v) {
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  if (kNT) __builtin_nontemporal_store(v, reinterpret_cast<v4*>(p));
+  else *reinterpret_cast<v4*>(p) = v;
+}
+
+template <int MAXU, bool kNT>
+__global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
+                                                              uint8_t* __restrict__ rows,
+                                                              int64_t ntiles) {
+  constexpr int R = 64;   // lane == row of the tile; wave w owns columns w, w+4, ...
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  const int rs = a.row_size;
+  const int bm = a.bitmap_bytes;
+  const int bw = bm >> 3;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncols = a.ncols;
+  for (int i = threadIdx.x; i < R * bw; i += kThreads) {
+    const int r = i / bw, w = i - r * bw;
+    *reinterpret_cast<uint64_t*>(lds + r * rs + 8 * w) = 0;   // never nulls on this path
+  }
+  // Column pointers are loop invariant and wave uniform: load them once into SGPRs (the
+  // record table always has kMaxFixedCols entries, so reading past ncols is in bounds).
+  static_assert(4 * MAXU <= kMaxFixedCols, "column table");
+  const uint8_t* p[MAXU];
+#pragma unroll
+  for (int u = 0; u < MAXU; u++) p[u] = a.col[wid + 4 * u].values;
+  uint64_t v[MAXU];
+  int64_t tile = blockIdx.x;
+  auto load = [&](int64_t t) {
+    const int64_t row = t * R + lane;
+    const bool ok = row < a.nrows;
+#pragma unroll
+    for (int u = 0; u < MAXU; u++) {
+      const int c = wid + 4 * u;
+      if (c < ncols && ok) v[u] = *reinterpret_cast<const uint64_t*>(p[u] + row * 8);
+    }
+  };
+  if (tile < ntiles) load(tile);
+  while (tile < ntiles) {
+    const int64_t r0 = tile * R;
+    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
+#pragma unroll
+    for (int u = 0; u < MAXU; u++) {
+      const int c = wid + 4 * u;
+      if (c < ncols && lane < nr) *reinterpret_cast<uint64_t*>(lds + lane * rs + bm + 8 * c) = v[u];
+    }
+    lds_barrier();
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) load(next);
+    const int64_t bytes = static_cast<int64_t>(nr) * rs;
+    uint8_t* g = rows + r0 * rs;
+    const int n16 = static_cast<int>(bytes >> 4);
+    for (int i = threadIdx.x; i < n16; i += kThreads)
+      store16<kNT>(g + 16 * i, *reinterpret_cast<const v4*>(lds + 16 * i));
+    if ((bytes & 15) && threadIdx.x == 0)
+      *reinterpret_cast<uint64_t*>(g + 16 * n16) = *reinterpret_cast<const uint64_t*>(lds + 16 * n16);
+    lds_barrier();
+    tile = next;
+  }
+}
+
+template <int MAXL, bool kNT>
+__global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
+                                                              const uint8_t* __restrict__ rows,
+                                                              int64_t ntiles) {
+  constexpr int R = 64;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  const int rs = a.row_size;
+  const int bm = a.bitmap_bytes;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ncols = a.ncols;
+  const uint8_t* q[32];
+#pragma unroll
+  for (int u = 0; u < 32; u++) q[u] = a.col[wid + 4 * u].values;
+  v4 t16[MAXL];
+  int64_t tile = blockIdx.x;
+  auto load = [&](int64_t t) {
+    const int64_t r0 = t * R;
+    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
+    const int n16 = (nr * rs) >> 4;
+    const v4* g = reinterpret_cast<const v4*>(rows + r0 * rs);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      const int i = threadIdx.x + k * kThreads;
+      if (i < n16) t16[k] = g[i];
+    }
+  };
+  if (tile < ntiles) load(tile);
+  while (tile < ntiles) {
+    const int64_t r0 = tile * R;
+    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
+    const int64_t bytes = static_cast<int64_t>(nr) * rs;
+    const int n16 = static_cast<int>(bytes >> 4);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      const int i = threadIdx.x + k * kThreads;
+      if (i < n16) *reinterpret_cast<v4*>(lds + 16 * i) = t16[k];
+    }
+    if ((bytes & 15) && threadIdx.x == 0)
+      *reinterpret_cast<uint64_t*>(lds + 16 * n16) =
+          *reinterpret_cast<const uint64_t*>(rows + r0 * rs + 16 * n16);
+    lds_barrier();
+    const int64_t next = tile + gridDim.x;
+    if (next < ntiles) load(next);
+    const int64_t row = r0 + lane;
+    if (lane < nr) {
+#pragma unroll
+      for (int u = 0; u < 32; u++) {
+        const int c = wid + 4 * u;
+        if (c < ncols) {
+          const uint64_t x = *reinterpret_cast<const uint64_t*>(lds + lane * rs + bm + 8 * c);
+          uint64_t* dst = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(q[u])) + row;
+          if (kNT) __builtin_nontemporal_store(x, dst);
+          else *dst = x;
+        }
+      }
+    }
+    lds_barrier();
+    tile = next;
+  }
+}
+
+}  // namespace
+
+// Kernel variant for fixed-width fast-path schemas (fury_set_tuning("fixed_variant", v) or env
+// FURY_FIXED_VARIANT): 0 one tile per workgroup, 1 pipelined persistent, 2 = 1 + nt stores.
+static int g_variant = -1;
+
+int fixed_variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("FURY_FIXED_VARIANT");
+    g_variant = e ? atoi(e) : 1;
+  }
+  return g_variant;
+}
+
+void set_fixed_variant(int v) { g_variant = v; }
+
+namespace {
+
+template <typename K>
+int launch_pipe(K kernel, int row_size, int64_t nrows, hipStream_t stream, const FixedArgs& a,
+                uint8_t* rows) {
+  const size_t lds = static_cast<size_t>(64) * row_size;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(lds));
+    if (e != hipSuccess) return check_hip(e, "hipFuncSetAttribute");
+  }
+  const int64_t ntiles = (nrows + 63) / 64;
+  int dev = 0, cus = 256, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel),
+                                                     kThreads, lds);
+  if (per_cu < 1) per_cu = 1;
+  const int64_t cap = static_cast<int64_t>(cus) * per_cu;
+  const int64_t grid = ntiles < cap ? ntiles : cap;
+  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(grid)), dim3(kThreads), lds, stream, a,
+                     rows, ntiles);
+  return check_hip(hipGetLastError(), "fixed pipelined kernel launch");
+}
+
 int pick_rows_per_tile(int row_size) {
   if (row_size * 256 <= 48 * 1024) return 256;
   if (row_size * 128 <= 64 * 1024) return 128;
@@ -226,6 +405,11 @@ int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t
 
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
+  const int var = fixed_variant();
+  if (fast && var >= 1 && a.ncols <= 128) {
+    return var == 2 ? launch_pipe(encode_fixed_pipe<32, true>, a.row_size, a.nrows, stream, a, rows)
+                    : launch_pipe(encode_fixed_pipe<32, false>, a.row_size, a.nrows, stream, a, rows);
+  }
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                         \
   if (R == RR) {                                                                             \
@@ -243,8 +427,13 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
 
 int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
-  const int R = pick_rows_per_tile(a.row_size);
   uint8_t* r = const_cast<uint8_t*>(rows);
+  const int var = fixed_variant();
+  if (fast && var >= 1 && a.row_size * 64 <= 17 * 16 * kThreads) {
+    return var == 2 ? launch_pipe(decode_fixed_pipe<17, true>, a.row_size, a.nrows, stream, a, r)
+                    : launch_pipe(decode_fixed_pipe<17, false>, a.row_size, a.nrows, stream, a, r);
+  }
+  const int R = pick_rows_per_tile(a.row_size);
 #define FURY_DEC(RR)                                                                         \
   if (R == RR) {                                                                             \
     return fast ? launch_tile_kernel(decode_fixed_kernel<RR, true>, RR, a.row_size, a.nrows, \

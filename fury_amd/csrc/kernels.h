@@ -33,6 +33,8 @@ struct FixedArgs {
   int64_t nrows;
 };
 
+int fixed_variant();
+void set_fixed_variant(int v);
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast);
 int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast);
 

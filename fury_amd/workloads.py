@@ -154,7 +154,8 @@ def gen_column(f: Field, seed: int, col: int, start: int, n: int, null_pct: int,
             v = np.where(valid, v, np.zeros_like(v))
         return Column(values=np.ascontiguousarray(v), validity=validity)
     if t == DECIMAL:
-        h2 = _keys(seed, col + 1000, rows)
+        # decimal128 two's complement, |value| < 2**125 < 10**38 (fits precision 38)
+        h2 = (_keys(seed, col + 1000, rows).view(np.int64) >> np.int64(3)).view(np.uint64)
         v = np.stack([h, h2], axis=1).view(np.uint8).reshape(n, 16).copy()
         v[~valid] = 0
         return Column(values=v.reshape(-1), validity=validity)

@@ -175,6 +175,13 @@ int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* 
 int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* columns, void* stream);
 
+/* ---- tuning (no reference equivalent) ---------------------------------------------------- */
+/* Process-wide kernel selection knobs for A/B measurement.  Keys: "fixed_variant" (fixed-width
+ * 8-byte no-null schemas: 0 = one tile per workgroup, 1 = pipelined persistent (default),
+ * 2 = pipelined + non-temporal stores).  Results are bit-identical across variants. */
+int fury_set_tuning(const char* key, int32_t value);
+int32_t fury_get_tuning(const char* key);
+
 /* ---- framing (Encoders.java:201-213 / 165-182) ------------------------------------------ */
 /* Writes the stream RowEncoder.encode(MemoryBuffer, T) produces for each row in turn:
  * [int32 len = 8 + rowSize][int64 schemaHash][row bytes].  frame_offsets (device, nrows+1)
