@@ -234,7 +234,7 @@ int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* ro
 int fury_set_tuning(const char* key, int32_t value) {
   if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
   if (std::string(key) == "fixed_variant") {
-    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..2");
+    if (value < 0 || value > 7) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..7");
     set_fixed_variant(value);
     return FURY_OK;
   }

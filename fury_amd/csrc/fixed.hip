@@ -52,27 +52,57 @@ __device__ __forceinline__ void store_value(uint8_t* p, int64_t row, int width, 
   }
 }
 
+// Global access helpers; NT bit 0 = non-temporal loads, bit 1 = non-temporal stores (streamed
+// bytes are touched once, so keeping them out of L2/MALL leaves room for the other stream).
+using v4u = __attribute__((ext_vector_type(4))) uint32_t;
+template <int NT>
+__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+  if (NT & 1) return __builtin_nontemporal_load(q);
+  return *q;
+}
+template <int NT>
+__device__ __forceinline__ void st8(uint8_t* p, uint64_t v) {
+  uint64_t* q = reinterpret_cast<uint64_t*>(p);
+  if (NT & 2) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+template <int NT>
+__device__ __forceinline__ v4u ld16(const uint8_t* p) {
+  const v4u* q = reinterpret_cast<const v4u*>(p);
+  if (NT & 1) return __builtin_nontemporal_load(q);
+  return *q;
+}
+template <int NT>
+__device__ __forceinline__ void st16(uint8_t* p, const v4u& v) {
+  v4u* q = reinterpret_cast<v4u*>(p);
+  if (NT & 2) __builtin_nontemporal_store(v, q);
+  else *q = v;
+}
+
 // Copies `bytes` (multiple of 8) between LDS and global, 16 B per lane where possible.
-template <bool kToGlobal>
+template <bool kToGlobal, int NT>
 __device__ __forceinline__ void copy_tile(uint8_t* __restrict__ g, uint8_t* __restrict__ lds,
                                           int64_t bytes) {
   const int64_t n16 = bytes >> 4;
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  v4* g16 = reinterpret_cast<v4*>(g);
-  v4* l16 = reinterpret_cast<v4*>(lds);
+  v4u* l16 = reinterpret_cast<v4u*>(lds);
   int64_t i = threadIdx.x;
   for (; i + 3 * kThreads < n16; i += 4 * kThreads) {
     if (kToGlobal) {
-      v4 a = l16[i], b = l16[i + kThreads], c = l16[i + 2 * kThreads], d = l16[i + 3 * kThreads];
-      g16[i] = a; g16[i + kThreads] = b; g16[i + 2 * kThreads] = c; g16[i + 3 * kThreads] = d;
+      v4u a = l16[i], b = l16[i + kThreads], c = l16[i + 2 * kThreads], d = l16[i + 3 * kThreads];
+      st16<NT>(g + 16 * i, a);
+      st16<NT>(g + 16 * (i + kThreads), b);
+      st16<NT>(g + 16 * (i + 2 * kThreads), c);
+      st16<NT>(g + 16 * (i + 3 * kThreads), d);
     } else {
-      v4 a = g16[i], b = g16[i + kThreads], c = g16[i + 2 * kThreads], d = g16[i + 3 * kThreads];
+      v4u a = ld16<NT>(g + 16 * i), b = ld16<NT>(g + 16 * (i + kThreads));
+      v4u c = ld16<NT>(g + 16 * (i + 2 * kThreads)), d = ld16<NT>(g + 16 * (i + 3 * kThreads));
       l16[i] = a; l16[i + kThreads] = b; l16[i + 2 * kThreads] = c; l16[i + 3 * kThreads] = d;
     }
   }
   for (; i < n16; i += kThreads) {
-    if (kToGlobal) g16[i] = l16[i];
-    else l16[i] = g16[i];
+    if (kToGlobal) st16<NT>(g + 16 * i, l16[i]);
+    else l16[i] = ld16<NT>(g + 16 * i);
   }
   if ((bytes & 15) && threadIdx.x == 0) {
     uint64_t* g8 = reinterpret_cast<uint64_t*>(g + (n16 << 4));
@@ -83,7 +113,7 @@ __device__ __forceinline__ void copy_tile(uint8_t* __restrict__ g, uint8_t* __re
 }
 
 // kFast: every column is 8 bytes wide and no column carries validity.
-template <int R, bool kFast>
+template <int R, bool kFast, int NT>
 __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
                                                                  uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -115,7 +145,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
       if (idx < total && r < nr) {
         const int64_t row = r0 + r;
         if (kFast) {
-          v[u] = *reinterpret_cast<const uint64_t*>(a.col[c].values + row * 8);
+          v[u] = ld8<NT>(a.col[c].values + row * 8);
         } else {
           const uint8_t* vb = a.col[c].validity;
           if (vb && !((vb[row >> 3] >> (row & 7)) & 1)) {
@@ -141,10 +171,10 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
     }
   }
   __syncthreads();
-  copy_tile<true>(rows + r0 * rs, lds, static_cast<int64_t>(nr) * rs);
+  copy_tile<true, NT>(rows + r0 * rs, lds, static_cast<int64_t>(nr) * rs);
 }
 
-template <int R, bool kFast>
+template <int R, bool kFast, int NT>
 __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
                                                                  const uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -153,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
 
-  copy_tile<false>(const_cast<uint8_t*>(rows + r0 * rs), lds, static_cast<int64_t>(nr) * rs);
+  copy_tile<false, NT>(const_cast<uint8_t*>(rows + r0 * rs), lds, static_cast<int64_t>(nr) * rs);
   __syncthreads();
 
   const int total = a.ncols * R;
@@ -171,7 +201,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       if (kFast) {
         if (live) {
           uint64_t v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-          *reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(a.col[c].values) + row * 8) = v;
+          st8<NT>(const_cast<uint8_t*>(a.col[c].values) + row * 8, v);
         }
         continue;
       }
@@ -207,14 +237,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool kNT>
-__device__ __forceinline__ void store16(uint8_t* p, const __attribute__((ext_vector_type(4))) uint32_t& v) {
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  if (kNT) __builtin_nontemporal_store(v, reinterpret_cast<v4*>(p));
-  else *reinterpret_cast<v4*>(p) = v;
-}
-
-template <int MAXU, bool kNT>
+template <int MAXU, int NT>
 __global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
                                                               uint8_t* __restrict__ rows,
                                                               int64_t ntiles) {
@@ -245,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
 #pragma unroll
     for (int u = 0; u < MAXU; u++) {
       const int c = wid + 4 * u;
-      if (c < ncols && ok) v[u] = *reinterpret_cast<const uint64_t*>(p[u] + row * 8);
+      if (c < ncols && ok) v[u] = ld8<NT>(p[u] + row * 8);
     }
   };
   if (tile < ntiles) load(tile);
@@ -264,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
     uint8_t* g = rows + r0 * rs;
     const int n16 = static_cast<int>(bytes >> 4);
     for (int i = threadIdx.x; i < n16; i += kThreads)
-      store16<kNT>(g + 16 * i, *reinterpret_cast<const v4*>(lds + 16 * i));
+      st16<NT>(g + 16 * i, *reinterpret_cast<const v4*>(lds + 16 * i));
     if ((bytes & 15) && threadIdx.x == 0)
       *reinterpret_cast<uint64_t*>(g + 16 * n16) = *reinterpret_cast<const uint64_t*>(lds + 16 * n16);
     lds_barrier();
@@ -272,7 +295,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
   }
 }
 
-template <int MAXL, bool kNT>
+template <int MAXL, int NT>
 __global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
                                                               const uint8_t* __restrict__ rows,
                                                               int64_t ntiles) {
@@ -297,7 +320,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       const int i = threadIdx.x + k * kThreads;
-      if (i < n16) t16[k] = g[i];
+      if (i < n16) t16[k] = ld16<NT>(reinterpret_cast<const uint8_t*>(g + i));
     }
   };
   if (tile < ntiles) load(tile);
@@ -325,8 +348,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
         if (c < ncols) {
           const uint64_t x = *reinterpret_cast<const uint64_t*>(lds + lane * rs + bm + 8 * c);
           uint64_t* dst = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(q[u])) + row;
-          if (kNT) __builtin_nontemporal_store(x, dst);
-          else *dst = x;
+          st8<NT>(reinterpret_cast<uint8_t*>(dst), x);
         }
       }
     }
@@ -403,20 +425,37 @@ int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t
 
 }  // namespace
 
+// Variant bits (fury_set_tuning("fixed_variant")): bit 0 = pipelined persistent kernel,
+// bit 1 = non-temporal stores, bit 2 = non-temporal loads.  Only the fast path (8-byte columns,
+// no validity) has variants; the general path always runs the tile kernel.
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
   const int var = fixed_variant();
-  if (fast && var >= 1 && a.ncols <= 128) {
-    return var == 2 ? launch_pipe(encode_fixed_pipe<32, true>, a.row_size, a.nrows, stream, a, rows)
-                    : launch_pipe(encode_fixed_pipe<32, false>, a.row_size, a.nrows, stream, a, rows);
+  const int nt = ((var >> 2) & 1) | (var & 2);          // NT bit0 loads, bit1 stores
+  if (fast && (var & 1) && a.ncols <= 128) {
+    switch (nt) {
+      case 1: return launch_pipe(encode_fixed_pipe<32, 1>, a.row_size, a.nrows, stream, a, rows);
+      case 2: return launch_pipe(encode_fixed_pipe<32, 2>, a.row_size, a.nrows, stream, a, rows);
+      case 3: return launch_pipe(encode_fixed_pipe<32, 3>, a.row_size, a.nrows, stream, a, rows);
+      default: return launch_pipe(encode_fixed_pipe<32, 0>, a.row_size, a.nrows, stream, a, rows);
+    }
   }
   const int R = pick_rows_per_tile(a.row_size);
-#define FURY_ENC(RR)                                                                         \
-  if (R == RR) {                                                                             \
-    return fast ? launch_tile_kernel(encode_fixed_kernel<RR, true>, RR, a.row_size, a.nrows, \
-                                     stream, a, rows)                                        \
-                : launch_tile_kernel(encode_fixed_kernel<RR, false>, RR, a.row_size,         \
-                                     a.nrows, stream, a, rows);                              \
+#define FURY_ENC(RR)                                                                          \
+  if (R == RR) {                                                                              \
+    if (!fast)                                                                                \
+      return launch_tile_kernel(encode_fixed_kernel<RR, false, 0>, RR, a.row_size, a.nrows,   \
+                                stream, a, rows);                                             \
+    switch (nt) {                                                                             \
+      case 1: return launch_tile_kernel(encode_fixed_kernel<RR, true, 1>, RR, a.row_size,     \
+                                        a.nrows, stream, a, rows);                            \
+      case 2: return launch_tile_kernel(encode_fixed_kernel<RR, true, 2>, RR, a.row_size,     \
+                                        a.nrows, stream, a, rows);                            \
+      case 3: return launch_tile_kernel(encode_fixed_kernel<RR, true, 3>, RR, a.row_size,     \
+                                        a.nrows, stream, a, rows);                            \
+      default: return launch_tile_kernel(encode_fixed_kernel<RR, true, 0>, RR, a.row_size,    \
+                                         a.nrows, stream, a, rows);                           \
+    }                                                                                         \
   }
   FURY_ENC(256)
   FURY_ENC(128)
@@ -429,17 +468,40 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
   if (a.nrows == 0) return FURY_OK;
   uint8_t* r = const_cast<uint8_t*>(rows);
   const int var = fixed_variant();
-  if (fast && var >= 1 && a.row_size * 64 <= 17 * 16 * kThreads) {
-    return var == 2 ? launch_pipe(decode_fixed_pipe<17, true>, a.row_size, a.nrows, stream, a, r)
-                    : launch_pipe(decode_fixed_pipe<17, false>, a.row_size, a.nrows, stream, a, r);
+  const int nt = ((var >> 2) & 1) | (var & 2);
+  const int64_t tile_bytes = static_cast<int64_t>(a.row_size) * 64;
+  if (fast && (var & 1) && tile_bytes <= 17 * 16 * kThreads) {
+    if (tile_bytes <= 13 * 16 * kThreads) {
+      switch (nt) {
+        case 1: return launch_pipe(decode_fixed_pipe<13, 1>, a.row_size, a.nrows, stream, a, r);
+        case 2: return launch_pipe(decode_fixed_pipe<13, 2>, a.row_size, a.nrows, stream, a, r);
+        case 3: return launch_pipe(decode_fixed_pipe<13, 3>, a.row_size, a.nrows, stream, a, r);
+        default: return launch_pipe(decode_fixed_pipe<13, 0>, a.row_size, a.nrows, stream, a, r);
+      }
+    }
+    switch (nt) {
+      case 1: return launch_pipe(decode_fixed_pipe<17, 1>, a.row_size, a.nrows, stream, a, r);
+      case 2: return launch_pipe(decode_fixed_pipe<17, 2>, a.row_size, a.nrows, stream, a, r);
+      case 3: return launch_pipe(decode_fixed_pipe<17, 3>, a.row_size, a.nrows, stream, a, r);
+      default: return launch_pipe(decode_fixed_pipe<17, 0>, a.row_size, a.nrows, stream, a, r);
+    }
   }
   const int R = pick_rows_per_tile(a.row_size);
-#define FURY_DEC(RR)                                                                         \
-  if (R == RR) {                                                                             \
-    return fast ? launch_tile_kernel(decode_fixed_kernel<RR, true>, RR, a.row_size, a.nrows, \
-                                     stream, a, r)                                           \
-                : launch_tile_kernel(decode_fixed_kernel<RR, false>, RR, a.row_size,         \
-                                     a.nrows, stream, a, r);                                 \
+#define FURY_DEC(RR)                                                                          \
+  if (R == RR) {                                                                              \
+    if (!fast)                                                                                \
+      return launch_tile_kernel(decode_fixed_kernel<RR, false, 0>, RR, a.row_size, a.nrows,   \
+                                stream, a, r);                                                \
+    switch (nt) {                                                                             \
+      case 1: return launch_tile_kernel(decode_fixed_kernel<RR, true, 1>, RR, a.row_size,     \
+                                        a.nrows, stream, a, r);                               \
+      case 2: return launch_tile_kernel(decode_fixed_kernel<RR, true, 2>, RR, a.row_size,     \
+                                        a.nrows, stream, a, r);                               \
+      case 3: return launch_tile_kernel(decode_fixed_kernel<RR, true, 3>, RR, a.row_size,     \
+                                        a.nrows, stream, a, r);                               \
+      default: return launch_tile_kernel(decode_fixed_kernel<RR, true, 0>, RR, a.row_size,    \
+                                         a.nrows, stream, a, r);                              \
+    }                                                                                         \
   }
   FURY_DEC(256)
   FURY_DEC(128)

@@ -176,9 +176,10 @@ int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_
                        int64_t nrows, fury_column* columns, void* stream);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
-/* Process-wide kernel selection knobs for A/B measurement.  Keys: "fixed_variant" (fixed-width
- * 8-byte no-null schemas: 0 = one tile per workgroup, 1 = pipelined persistent (default),
- * 2 = pipelined + non-temporal stores).  Results are bit-identical across variants. */
+/* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,
+ * 8-byte, no-null schemas) is a bit set: bit 0 = pipelined persistent kernel (else one tile per
+ * workgroup), bit 1 = non-temporal stores, bit 2 = non-temporal loads.  Results are
+ * bit-identical across variants. */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 

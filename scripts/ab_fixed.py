@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0,1,2,3,6,7")
     args = ap.parse_args()
     import torch
     from fury_amd import _native as N
@@ -86,7 +86,6 @@ def main():
                           "encdec_GBps": round(2 * nbytes / (e + dd) / 1e6, 1),
                           "enc_min_ms": round(min(d["enc"]), 4), "dec_min_ms": round(min(d["dec"]), 4)}
     print(json.dumps({"rows": n, "variants": report}, indent=1))
-    N.lib().fury_set_tuning(b"fixed_variant", 1)
 
 
 if __name__ == "__main__":
