@@ -360,13 +360,13 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
 }  // namespace
 
 // Kernel variant for fixed-width fast-path schemas (fury_set_tuning("fixed_variant", v) or env
-// FURY_FIXED_VARIANT): 0 one tile per workgroup, 1 pipelined persistent, 2 = 1 + nt stores.
+// FURY_FIXED_VARIANT), a bit set: 1 = pipelined persistent kernel, 2 = nt stores, 4 = nt loads.
 static int g_variant = -1;
 
 int fixed_variant() {
   if (g_variant < 0) {
     const char* e = getenv("FURY_FIXED_VARIANT");
-    g_variant = e ? atoi(e) : 1;
+    g_variant = e ? atoi(e) : 6;   // tile kernel + nt loads + nt stores (A/B: profiles/r01_ab_fixed.json)
   }
   return g_variant;
 }

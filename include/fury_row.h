@@ -179,7 +179,7 @@ int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_
 /* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,
  * 8-byte, no-null schemas) is a bit set: bit 0 = pipelined persistent kernel (else one tile per
  * workgroup), bit 1 = non-temporal stores, bit 2 = non-temporal loads.  Results are
- * bit-identical across variants. */
+ * bit-identical across variants.  Default 6 (tile + nt loads + nt stores). */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 

@@ -62,6 +62,19 @@ __global__ __launch_bounds__(256) void write_k(v4* __restrict__ d, size_t n) {
   }
 }
 
+// 8-byte-per-lane streams (the encode kernel's column reads / decode kernel's column writes),
+// for calibrating FETCH_SIZE / WRITE_SIZE at that access width.
+__global__ __launch_bounds__(256) void read8_k(const uint64_t* __restrict__ s, size_t n, uint32_t* out) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t acc = 0;
+  for (; i < n; i += (size_t)gridDim.x * 256) acc ^= __builtin_nontemporal_load(s + i);
+  if (acc == 0x12345678ull) *out = 1;
+}
+__global__ __launch_bounds__(256) void write8_k(uint64_t* __restrict__ d, size_t n) {
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i < n; i += (size_t)gridDim.x * 256) __builtin_nontemporal_store((uint64_t)i, d + i);
+}
+
 template <typename F>
 float time_ms(F f, int iters) {
   hipEvent_t a, b;
@@ -91,7 +104,7 @@ int main(int argc, char** argv) {
   int cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   printf("{\"bytes_per_buffer\": %zu, \"cus\": %d, \"results\": [\n", bytes, cus);
-  const int iters = 20;
+  const int iters = argc > 2 ? atoi(argv[2]) : 20;
   bool first = true;
   auto rep = [&](const char* name, int grid, double moved, float ms) {
     printf("%s {\"kernel\": \"%s\", \"grid\": %d, \"ms\": %.4f, \"GBps\": %.1f}\n",
@@ -105,6 +118,10 @@ int main(int argc, char** argv) {
     rep("read_u4", grid, 1.0 * bytes, time_ms([&] { read_k<4><<<grid, 256>>>(s, n, o); }, iters));
     rep("write_u4", grid, 1.0 * bytes, time_ms([&] { write_k<4><<<grid, 256>>>(d, n); }, iters));
   }
+  rep("read8_nt", cus * 16, 1.0 * bytes,
+      time_ms([&] { read8_k<<<cus * 16, 256>>>((const uint64_t*)s, bytes / 8, o); }, iters));
+  rep("write8_nt", cus * 16, 1.0 * bytes,
+      time_ms([&] { write8_k<<<cus * 16, 256>>>((uint64_t*)d, bytes / 8); }, iters));
   rep("hipMemcpyD2D", 0, 2.0 * bytes,
       time_ms([&] { CHECK(hipMemcpyAsync(d, s, bytes, hipMemcpyDeviceToDevice, 0)); }, iters));
   printf("]}\n");
