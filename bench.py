@@ -31,12 +31,17 @@ def _parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    p.add_argument("--rows", type=int, default=None,
+                   help="rows per GPU (default: BASELINE config size: struct100 1M, mixed 10M, "
+                        "nested 4M)")
     p.add_argument("--workload", default="struct100", choices=["struct100", "mixed", "nested"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-e2e", action="store_true")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.rows is None:
+        a.rows = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}[a.workload]
+    return a
 
 
 def _buffers(col):
@@ -50,7 +55,7 @@ def _nbytes(cols):
     return sum(t.numel() * t.element_size() for c in cols for t in _buffers(c))
 
 
-def make_device_columns(name, fields, rows, rank, dev):
+def make_device_columns(name, fields, rows, rank, start, dev):
     """Synthetic columns resident in HBM.  Struct-100: random 64-bit patterns generated on the
     device (shard-keyed seed).  Var-length workloads: SplitMix64 generator on the host (shard =
     global row range), copied once before timing."""
@@ -65,7 +70,7 @@ def make_device_columns(name, fields, rows, rank, dev):
                               generator=g)
             cols.append(Column(values=v.view(torch.float64) if f.type_id == 12 else v))
         return cols
-    host = gen_columns(name, fields, rows, seed=1234, start=rank * rows)
+    host = gen_columns(name, fields, rows, seed=1234, start=start)
     return [column_to_device(c, dev) for c in host]
 
 
@@ -100,15 +105,12 @@ def cpu_baseline(name, fields, budget_s):
 def main():
     args = _parse()
     import torch
-    import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # orchestration only (barrier + max of timings); the data path has no collective
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fury_amd.shard import Orchestrator, from_env, weak_shard
+    r = from_env()
+    world, rank, local = r.world, r.rank, r.local
+    # orchestration only (gloo barrier + max of timings); the data path has no collective
+    orch = Orchestrator(r)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -117,7 +119,8 @@ def main():
     fields = SCHEMAS[args.workload]
     enc = Encoders.bean(fields, device=dev)
     n = args.rows
-    cols = make_device_columns(args.workload, fields, n, rank, dev)
+    start, n = weak_shard(args.rows, rank)
+    cols = make_device_columns(args.workload, fields, n, rank, start, dev)
     out_cols = enc.alloc_columns(n, validity=False) if enc.schema().is_fixed else None
     stream = torch.cuda.current_stream()
 
@@ -128,6 +131,10 @@ def main():
     from fury_amd.encoder import RowBatch
     batch = RowBatch(rows[:total_row_bytes], offs, n, enc.schema_hash)
 
+    var_out = None
+    if out_cols is None:      # size the variable-length outputs once (first decode syncs)
+        enc.encode_into(cols, n, batch.rows, batch.row_offsets, stream=stream)
+        var_out = enc.decode_batch(batch, validity=True, stream=stream)
     col_bytes = _nbytes(cols)
     row_bytes = total_row_bytes + (0 if offs is None else offs.numel() * 8)
     enc_bytes = col_bytes + row_bytes           # read columns, write rows
@@ -145,7 +152,7 @@ def main():
         if out_cols is not None:
             enc.decode_batch(batch, validity=False, stream=stream, out=out_cols)
         else:
-            enc.decode_batch(batch, validity=True, stream=stream)
+            enc.decode_into(batch, var_out, stream=stream)
         if ev is not None:
             ev[2].record(stream)
 
@@ -153,37 +160,34 @@ def main():
         step()
     torch.cuda.synchronize()
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    orch.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    orch.barrier()
     dt = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
 
-    t = torch.tensor([dt], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt_max = float(t[0])
+    dt_max = orch.max(dt)
 
     # correctness spot check after timing (cheap, device-side): decoded == input
-    dec_cols = out_cols if out_cols is not None else enc.decode_batch(batch)
     if args.workload == "struct100":
-        for c, d in zip(cols[:4], dec_cols[:4]):
+        for c, d in zip(cols[:4], out_cols[:4]):
             assert torch.equal(c.values.view(torch.uint8), d.values), "decode mismatch"
+    else:
+        for c, d in zip(cols, var_out):
+            if c.offsets is not None and c.child is None:
+                assert torch.equal(c.offsets, d.offsets), "decode offsets mismatch"
 
     e2e = None
     if rank == 0 and not args.no_e2e and args.workload == "struct100":
         e2e = end_to_end(enc, cols, n, dev, stream)
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        orch.close()
         return
     dominant = ("encode", enc_ms, enc_bytes) if enc_ms >= dec_ms else ("decode", dec_ms, dec_bytes)
     achieved = dominant[2] / (dominant[1] * 1e-3) / 1e9
@@ -224,8 +228,7 @@ def main():
     if not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds)
     print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    orch.close()
 
 
 def end_to_end(enc, cols, n, dev, stream):

@@ -304,6 +304,21 @@ class RowEncoder:
                   _c_columns(cols, keep), sh))
         return cols
 
+    def decode_into(self, batch: RowBatch, cols: List[Column], stream=None,
+                    arrow: bool = False) -> None:
+        """Decode into preallocated columns (variable-length buffers must already be large
+        enough, e.g. from a previous decode of the same batch shape): no host synchronisation,
+        so the call can be captured/timed back to back."""
+        keep: list = []
+        sh = _stream_handle(stream)
+        if not self._schema.is_fixed:
+            _check(N.lib().fury_row_decode_measure(self._schema.handle, _ptr(batch.rows),
+                                                   _ptr(batch.row_offsets), batch.nrows,
+                                                   _c_columns(cols, keep), sh))
+        fn = N.lib().fury_rows_to_arrow if arrow else N.lib().fury_row_decode
+        _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), batch.nrows,
+                  _c_columns(cols, keep), sh))
+
     def decode_batch(self, batch: RowBatch, validity: bool = True, stream=None,
                      out: Optional[List[Column]] = None) -> List[Column]:
         """Rows -> columns (generated fromRow semantics)."""

@@ -1,0 +1,86 @@
+"""Multi-GPU orchestration for the row codec: one process per GPU, independent row shards.
+
+Rows are independent, so there is NO data-path collective: every rank encodes and
+decodes its own contiguous global row range.  The only inter-process traffic is orchestration —
+a barrier around the timed region and a max-reduce of the elapsed time — over gloo (CPU), so
+xGMI/RCCL stay idle.  A concatenated global row buffer, if ever wanted, needs only a host-side
+exclusive scan of per-shard byte totals (``global_row_base``).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import List, Tuple
+
+
+@dataclass
+class Rank:
+    rank: int
+    world: int
+    local: int
+
+
+def from_env() -> Rank:
+    return Rank(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+                int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def weak_shard(rows_per_rank: int, rank: int) -> Tuple[int, int]:
+    """Weak scaling: rank r owns global rows [r * rows_per_rank, (r + 1) * rows_per_rank)."""
+    return rank * rows_per_rank, rows_per_rank
+
+
+def strong_shard(total_rows: int, world: int, rank: int) -> Tuple[int, int]:
+    """Strong scaling (C5: 100M rows over 8 GPUs): contiguous near-equal ranges."""
+    base, extra = divmod(total_rows, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def global_row_base(shard_bytes: List[int]) -> List[int]:
+    """Exclusive scan of per-shard row-byte totals: where each shard's rows would start in a
+    concatenated batch (8-element host scan at 8 GPUs)."""
+    out, acc = [], 0
+    for b in shard_bytes:
+        out.append(acc)
+        acc += b
+    return out
+
+
+class Orchestrator:
+    """Barrier + max-over-ranks timing for the bench contract."""
+
+    def __init__(self, r: Rank):
+        self.r = r
+        self._dist = None
+        if r.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if not dist.is_initialized():
+                dist.init_process_group("gloo", rank=r.rank, world_size=r.world)
+            self._dist = dist
+
+    def barrier(self) -> None:
+        if self._dist is not None:
+            self._dist.barrier()
+
+    def max(self, value: float) -> float:
+        if self._dist is None:
+            return value
+        import torch
+        t = torch.tensor([value], dtype=torch.float64)
+        self._dist.all_reduce(t, op=self._dist.ReduceOp.MAX)
+        return float(t[0])
+
+    def gather_ints(self, value: int) -> List[int]:
+        if self._dist is None:
+            return [value]
+        import torch
+        t = torch.tensor([value], dtype=torch.int64)
+        out = [torch.zeros(1, dtype=torch.int64) for _ in range(self.r.world)]
+        self._dist.all_gather(out, t)
+        return [int(x[0]) for x in out]
+
+    def close(self) -> None:
+        if self._dist is not None and self._dist.is_initialized():
+            self._dist.destroy_process_group()
