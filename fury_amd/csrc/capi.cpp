@@ -88,6 +88,8 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     v.nullable = p.nullable;
     v.var_slot = -1;
     v.validity = c.validity;
+    if (decode && c.validity && misaligned(c.validity, 4))
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": validity must be 4-byte aligned");
     if (need_validity && !c.validity)
       return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": Arrow output needs a validity buffer");
     switch (p.kind) {
@@ -123,6 +125,10 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
         } else {
           v.values = static_cast<const uint8_t*>(c.child->values);
           v.elem_validity = c.child->validity;
+          if (decode && (misaligned(c.child->validity, 4) ||
+                         (v.width == 0 && misaligned(c.child->values, 4))))
+            return set_error(FURY_ERR_INVALID_ARGUMENT,
+                             who + ": element bitmaps must be 4-byte aligned");
           if (need_validity && !c.child->validity)
             return set_error(FURY_ERR_INVALID_ARGUMENT,
                              who + ": Arrow output needs element validity");

@@ -33,9 +33,9 @@ namespace fury {
 namespace {
 
 constexpr int kThreads = 256;                 // = rows per workgroup
-constexpr int kEncodeStage = 40 * 1024;       // LDS image of the group's row range (encode)
+constexpr int kEncodeStage = 48 * 1024;       // LDS pool: row image + staged sources (encode)
 constexpr int kDecodeStage = 32 * 1024;       // LDS image of the group's row range (decode)
-constexpr int kStrStage = 12 * 1024;          // LDS image of one column's Arrow payload range
+constexpr int kStrStage = 16 * 1024;          // LDS image of one column's Arrow output range
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
@@ -129,9 +129,12 @@ __device__ __forceinline__ void copy_to_aligned(uint64_t* dst, const uint8_t* sr
   }
 }
 
-// BinaryArrayWriter image of elements [b, b+n) of a fixed-width list column; returns its size.
-__device__ int64_t write_array(uint8_t* dst, const VarCol& c, int64_t b, int64_t n) {
-  const int ew = c.width == 0 ? 1 : c.width;
+// BinaryArrayWriter image of n elements of a fixed-width list column; returns its size.
+// `vals` points at the first element's value bytes, `vbits`/`vbit0` at its Arrow validity bit
+// (vbits == nullptr: no element nulls).  Sources may be global or an LDS staging copy.
+__device__ int64_t write_array(uint8_t* dst, int width, const uint8_t* vals, const uint8_t* vbits,
+                               int64_t vbit0, int64_t n) {
+  const int ew = width == 0 ? 1 : width;
   const int64_t hb = 8 + bm_bytes(n);
   const int64_t data = n * ew;
   const int64_t fp = rnd8(data);
@@ -139,17 +142,17 @@ __device__ int64_t write_array(uint8_t* dst, const VarCol& c, int64_t b, int64_t
   d64[0] = static_cast<uint64_t>(n);                     // numElements as an 8-byte word
   for (int64_t w = 0; w < (hb - 8) >> 3; w++) {          // element null bits (bit = 1 null)
     uint64_t word = 0;
-    if (c.elem_validity) {
+    if (vbits) {
       const int64_t lim = min<int64_t>(64, n - 64 * w);
       for (int64_t t = 0; t < lim; t++)
-        if (!bit_at(c.elem_validity, b + 64 * w + t)) word |= 1ull << t;
+        if (!bit_at(vbits, vbit0 + 64 * w + t)) word |= 1ull << t;
     }
     d64[1 + w] = word;
   }
-  uint64_t* vals = reinterpret_cast<uint64_t*>(dst + hb);
-  if (c.width == 8 && !c.elem_validity) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(c.values) + b;
-    for (int64_t j = 0; j < n; j++) vals[j] = src[j];
+  uint64_t* out = reinterpret_cast<uint64_t*>(dst + hb);
+  if (width == 8 && !vbits) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(vals);
+    for (int64_t j = 0; j < n; j++) out[j] = src[j];
     return hb + fp;
   }
   const int per = 8 / ew;
@@ -158,18 +161,42 @@ __device__ int64_t write_array(uint8_t* dst, const VarCol& c, int64_t b, int64_t
     for (int t = 0; t < per; t++) {
       const int64_t j = q * per + t;
       if (j >= n) break;
-      const int64_t e = b + j;
-      if (c.elem_validity && !bit_at(c.elem_validity, e)) continue;   // null element stays 0
-      const uint64_t v = load_fixed(c.values, e, c.width);
+      if (vbits && !bit_at(vbits, vbit0 + j)) continue;   // null element stays 0
+      uint64_t v;
+      switch (width) {
+        case 8: v = reinterpret_cast<const uint64_t*>(vals)[j]; break;
+        case 4: v = reinterpret_cast<const uint32_t*>(vals)[j]; break;
+        case 2: v = reinterpret_cast<const uint16_t*>(vals)[j]; break;
+        case 1: v = vals[j]; break;
+        default: v = bit_at(vals, vbit0 + j); break;       // bool: bit-packed, same bit origin
+      }
       word |= (ew == 8) ? v : (v << (8 * ew * t));
     }
-    vals[q] = word;
+    out[q] = word;
   }
   return hb + fp;
 }
 
-// Builds row r at dst (8-byte aligned, row_size_of(r) bytes) exactly as toRow does.
-__device__ __forceinline__ void build_row(const VarArgs& a, int64_t r, uint8_t* dst) {
+// Staged source regions of one workgroup (LDS copies of the contiguous global byte ranges its
+// rows read): per var column, region 2k = payload/values bytes, 2k+1 = list element validity.
+struct StagePlan {
+  uint32_t lds[2 * kMaxVarCols];
+  uint64_t glo[2 * kMaxVarCols];   // 16-byte aligned global base of the region
+  uint32_t len[2 * kMaxVarCols];   // bytes (multiple of 16), 0 = not staged
+};
+
+template <bool kSrcLds>
+__device__ __forceinline__ const uint8_t* src_at(const uint8_t* pool, const StagePlan& sp, int reg,
+                                                 const uint8_t* g) {
+  if (!kSrcLds) return g;
+  return pool + sp.lds[reg] + static_cast<uint32_t>(reinterpret_cast<uint64_t>(g) - sp.glo[reg]);
+}
+
+// Builds row r at dst (8-byte aligned, row_size_of(r) bytes) exactly as toRow does.  kSrcLds:
+// string payloads and list values/validity come from the workgroup's LDS staging copies.
+template <bool kSrcLds>
+__device__ __forceinline__ void build_row(const VarArgs& a, int64_t r, uint8_t* dst,
+                                          const uint8_t* pool, const StagePlan& sp) {
   uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
   const int nslot0 = a.bitmap_bytes >> 3;
   int64_t cursor = a.fixed_size;
@@ -188,7 +215,7 @@ __device__ __forceinline__ void build_row(const VarArgs& a, int64_t r, uint8_t* 
         case kBytes: {
           const int64_t b = c.offsets[r];
           const int64_t len = c.offsets[r + 1] - b;
-          copy_to_aligned(d64 + (cursor >> 3), c.values + b, len);
+          copy_to_aligned(d64 + (cursor >> 3), src_at<kSrcLds>(pool, sp, 2 * k, c.values + b), len);
           slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
           cursor += rnd8(len);
           break;
@@ -203,7 +230,14 @@ __device__ __forceinline__ void build_row(const VarArgs& a, int64_t r, uint8_t* 
         }
         default: {   // kListFixed
           const int64_t b = c.offsets[r];
-          const int64_t sz = write_array(dst + cursor, c, b, c.offsets[r + 1] - b);
+          const int64_t n = c.offsets[r + 1] - b;
+          const uint8_t* vals;
+          if (c.width == 0) vals = src_at<kSrcLds>(pool, sp, 2 * k, c.values + (b >> 3));
+          else vals = src_at<kSrcLds>(pool, sp, 2 * k, c.values + b * c.width);
+          const uint8_t* vb = c.elem_validity
+                                  ? src_at<kSrcLds>(pool, sp, 2 * k + 1, c.elem_validity + (b >> 3))
+                                  : nullptr;
+          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, b & 7, n);
           slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
           cursor += sz;
           break;
@@ -236,9 +270,9 @@ __device__ __forceinline__ void copy_range(uint8_t* g, uint8_t* l, int64_t bytes
       v4 v;
       v.x = static_cast<uint32_t>(x); v.y = static_cast<uint32_t>(x >> 32);
       v.z = static_cast<uint32_t>(y); v.w = static_cast<uint32_t>(y >> 32);
-      *reinterpret_cast<v4*>(gp) = v;
+      __builtin_nontemporal_store(v, reinterpret_cast<v4*>(gp));
     } else {
-      const v4 v = *reinterpret_cast<const v4*>(gp);
+      const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(gp));
       reinterpret_cast<uint64_t*>(lp)[0] = (static_cast<uint64_t>(v.y) << 32) | v.x;
       reinterpret_cast<uint64_t*>(lp)[1] = (static_cast<uint64_t>(v.w) << 32) | v.z;
     }
@@ -286,21 +320,84 @@ __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict
   if (r == n - 1) offs[n] = *total;
 }
 
+// Plans the LDS staging of one workgroup's source ranges (uniform across the group; computed by
+// thread 0).  Returns the staged byte total after the row image (`base`).
+__device__ uint32_t plan_sources(const VarArgs& a, int64_t r0, int64_t nr, uint32_t base,
+                                 StagePlan& sp) {
+  uint32_t at = base;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    sp.len[2 * k] = sp.len[2 * k + 1] = 0;
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
+    if (e <= b) continue;
+    uint64_t lo, hi;
+    if (c.kind == kBytes) {
+      lo = reinterpret_cast<uint64_t>(c.values + b);
+      hi = reinterpret_cast<uint64_t>(c.values + e);
+    } else if (c.width == 0) {
+      lo = reinterpret_cast<uint64_t>(c.values + (b >> 3));
+      hi = reinterpret_cast<uint64_t>(c.values + ((e + 7) >> 3));
+    } else {
+      lo = reinterpret_cast<uint64_t>(c.values + b * c.width);
+      hi = reinterpret_cast<uint64_t>(c.values + e * c.width);
+    }
+    lo &= ~uint64_t(15);
+    hi = (hi + 15) & ~uint64_t(15);
+    sp.glo[2 * k] = lo;
+    sp.lds[2 * k] = at;
+    sp.len[2 * k] = static_cast<uint32_t>(min<uint64_t>(hi - lo, 0xffffffffull));
+    at += sp.len[2 * k];
+    if (c.kind == kListFixed && c.elem_validity) {
+      lo = reinterpret_cast<uint64_t>(c.elem_validity + (b >> 3)) & ~uint64_t(15);
+      hi = (reinterpret_cast<uint64_t>(c.elem_validity + ((e + 7) >> 3)) + 15) & ~uint64_t(15);
+      sp.glo[2 * k + 1] = lo;
+      sp.lds[2 * k + 1] = at;
+      sp.len[2 * k + 1] = static_cast<uint32_t>(hi - lo);
+      at += sp.len[2 * k + 1];
+    }
+  }
+  return at;
+}
+
+// Encode: 256 rows per workgroup.  Mode 2 stages every source range the group reads (string
+// payloads, list values/validity: each a contiguous range) in LDS with 16-B loads and builds the
+// rows in an LDS image of the group's contiguous output range; mode 1 stages only the output
+// image; mode 0 (oversized rows) builds rows straight in HBM.
 __global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a,
                                                               const int64_t* __restrict__ offs,
                                                               uint8_t* __restrict__ rows) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kEncodeStage];
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncodeStage];
+  __shared__ StagePlan sp;
+  __shared__ uint32_t need;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
   const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
   const int64_t rbeg = offs[r0];
   const int64_t bytes = offs[r0 + nr] - rbeg;
   const int64_t r = r0 + threadIdx.x;
-  if (bytes <= kEncodeStage) {
-    if (r < a.nrows) build_row(a, r, stage + (offs[r] - rbeg));
+  const uint32_t img = static_cast<uint32_t>((bytes + 15) & ~int64_t(15));
+  if (bytes <= kEncodeStage && threadIdx.x == 0) need = plan_sources(a, r0, nr, img, sp);
+  __syncthreads();
+  if (bytes <= kEncodeStage && need <= kEncodeStage) {
+    using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+    for (int k = 0; k < 2 * a.ncols; k++) {
+      const uint32_t len = sp.len[k];
+      if (!len) continue;
+      const v4* g = reinterpret_cast<const v4*>(sp.glo[k]);
+      v4* l = reinterpret_cast<v4*>(pool + sp.lds[k]);
+      for (uint32_t i = threadIdx.x; i < (len >> 4); i += kThreads)
+        l[i] = __builtin_nontemporal_load(g + i);
+    }
     __syncthreads();
-    copy_range<true>(rows + rbeg, stage, bytes);
+    if (r < a.nrows) build_row<true>(a, r, pool + (offs[r] - rbeg), pool, sp);
+    __syncthreads();
+    copy_range<true>(rows + rbeg, pool, bytes);
+  } else if (bytes <= kEncodeStage) {
+    if (r < a.nrows) build_row<false>(a, r, pool + (offs[r] - rbeg), pool, sp);
+    __syncthreads();
+    copy_range<true>(rows + rbeg, pool, bytes);
   } else {
-    if (r < a.nrows) build_row(a, r, rows + offs[r]);
+    if (r < a.nrows) build_row<false>(a, r, rows + offs[r], pool, sp);
   }
 }
 
@@ -362,11 +459,88 @@ __device__ __forceinline__ void put_bits_atomic(uint8_t* bits, int64_t i, bool v
   else atomicAnd(w, ~(1u << sh));
 }
 
+// Byte i (0 <= i < len) of an 8-byte-aligned source, read as whole aligned words.
+__device__ __forceinline__ uint32_t src_byte(const uint8_t* src, int64_t i) {
+  const uint64_t w = reinterpret_cast<const uint64_t*>(src)[i >> 3];
+  return static_cast<uint32_t>((w >> (8 * (i & 7))) & 0xff);
+}
+
+// Writes src[0, len) (8-byte-aligned source: a row's var section) to dst + q (any alignment).
+// 32-bit words wholly inside the destination range are written whole; the partial words at the
+// two ends are written byte by byte, so neighbouring strings (other threads) are never touched
+// and no atomics or pre-zeroing are needed (byte stores are masked in LDS and in HBM).
+__device__ __forceinline__ void put_bytes(uint8_t* dst, int64_t q, const uint8_t* src, int64_t len) {
+  if (len <= 0) return;
+  const int64_t end = q + len;
+  const int64_t w0 = (q + 3) >> 2;                 // first whole word
+  const int64_t w1 = end >> 2;                     // one past the last whole word
+  if (w0 >= w1) {
+    for (int64_t i = 0; i < len; i++) dst[q + i] = static_cast<uint8_t>(src_byte(src, i));
+    return;
+  }
+  for (int64_t i = q; i < 4 * w0; i++) dst[i] = static_cast<uint8_t>(src_byte(src, i - q));
+  const int64_t d = 4 * w0 - q;                    // source index of the first whole word
+  const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+  for (int64_t w = w0; w < w1; w++) {
+    const int64_t si = d + 4 * (w - w0);           // 4 source bytes [si, si + 4)
+    const int64_t j = si >> 3;
+    const int o = static_cast<int>(si & 7);
+    uint64_t x = s64[j] >> (8 * o);
+    if (o > 4) x |= s64[j + 1] << (64 - 8 * o);
+    d32[w] = static_cast<uint32_t>(x);
+  }
+  for (int64_t i = 4 * w1; i < end; i++) dst[i] = static_cast<uint8_t>(src_byte(src, i - q));
+}
+
+// Writes the bit range [b, e) of `img` (LDS words aligned to global word b >> 5) into the Arrow
+// bitmap `g` (4-byte aligned): whole words by plain stores, the two boundary words (shared with
+// neighbouring workgroups) by atomic and/or of exactly this range's bits.
+__device__ __forceinline__ void flush_bits(uint32_t* g, const uint32_t* img, int64_t b, int64_t e) {
+  if (e <= b) return;
+  const int64_t wb = b >> 5, we = (e - 1) >> 5;
+  for (int64_t w = wb + threadIdx.x; w <= we; w += kThreads) {
+    uint32_t mask = ~0u;
+    if (w == wb) mask &= ~0u << (b & 31);
+    if (w == we && (e & 31)) mask &= ~0u >> (32 - (e & 31));
+    const uint32_t v = img[w - wb] & mask;
+    if (mask == ~0u) {
+      g[w] = v;
+    } else {
+      atomicAnd(&g[w], ~mask);
+      atomicOr(&g[w], v);
+    }
+  }
+}
+
+__device__ __forceinline__ void or_bits(uint32_t* img, int64_t base_word, int64_t e, bool v) {
+  if (!v) return;
+  atomicOr(&img[(e >> 5) - base_word], 1u << (e & 31));
+}
+
+template <bool kToGlobal>
+__device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, int64_t p0, int64_t p1,
+                                                 int64_t a0) {
+  // [p0, p1) of g <- l[p - a0]: unaligned ends byte by byte, aligned middle 16 B per lane.
+  const int64_t m0 = min<int64_t>((p0 + 15) & ~int64_t(15), p1);
+  const int64_t m1 = max<int64_t>(p1 & ~int64_t(15), m0);
+  for (int64_t i = p0 + threadIdx.x; i < m0; i += kThreads) g[i] = l[i - a0];
+  for (int64_t i = m1 + threadIdx.x; i < p1; i += kThreads) g[i] = l[i - a0];
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  for (int64_t i = m0 + 16 * threadIdx.x; i < m1; i += 16 * kThreads)
+    __builtin_nontemporal_store(*reinterpret_cast<const v4*>(l + (i - a0)),
+                                reinterpret_cast<v4*>(g + i));
+}
+
+// Decode / row->Arrow: 256 rows per workgroup.  The group's row range is staged in LDS with 16-B
+// loads; fixed fields leave as coalesced per-column stores with ballot-built validity; each
+// string column's Arrow payload range and each list column's child values/validity range are
+// assembled in an LDS image and written out as one contiguous range.
 __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
                                                               const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
-  __shared__ __attribute__((aligned(16))) uint32_t sstage[kStrStage / 4];
+  __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
   const int lane = threadIdx.x & 63;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
   const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
@@ -398,7 +572,7 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
         uint8_t* dst = const_cast<uint8_t*>(c.values);
         if (live) {
           switch (c.width) {
-            case 8: reinterpret_cast<uint64_t*>(dst)[r] = slot; break;
+            case 8: __builtin_nontemporal_store(slot, reinterpret_cast<uint64_t*>(dst) + r); break;
             case 4: reinterpret_cast<uint32_t*>(dst)[r] = static_cast<uint32_t>(slot); break;
             case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(slot); break;
             default: dst[r] = static_cast<uint8_t>(slot); break;
@@ -427,61 +601,82 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
         break;
       }
       case kBytes: {
-        // Arrow payload range of this group for column k: [p0, p1) in c.values.
+        // Arrow payload range of this group for column k: [p0, p1) of c.values.
+        uint8_t* gdst = const_cast<uint8_t*>(c.values);
+        if (!gdst) break;
         const int64_t p0 = c.offsets[r0];
         const int64_t p1 = c.offsets[r0 + nr];
-        uint8_t* gdst = const_cast<uint8_t*>(c.values);
         const int64_t len = (live && !isnull) ? static_cast<uint32_t>(slot) : 0;
         const uint8_t* src = row ? row + static_cast<int32_t>(slot >> 32) : nullptr;
         const int64_t pos = live ? c.offsets[r] : 0;
-        const int64_t a0 = p0 & ~int64_t(15);                    // LDS byte i <-> global a0 + i
-        const bool sfit = (p1 - a0) <= kStrStage && gdst != nullptr;
-        if (sfit) {
-          for (int64_t i = threadIdx.x; i < ((p1 - a0 + 3) >> 2); i += kThreads) sstage[i] = 0;
+        // LDS byte i <-> global byte a0 + i, a0 = 16-aligned address of payload byte p0
+        const int64_t a0 = p0 - static_cast<int64_t>(reinterpret_cast<uintptr_t>(gdst + p0) & 15);
+        if (p1 - a0 <= kStrStage) {
+          put_bytes(oimg, pos - a0, src, len);
           __syncthreads();
-          // OR this row's bytes into the zeroed image, 8 source bytes at a time (source is
-          // 8-byte aligned inside the row).
-          for (int64_t j = 0; j < len; j += 8) {
-            const uint64_t w = *reinterpret_cast<const uint64_t*>(src + j);
-            const int64_t nb = min<int64_t>(8, len - j);
-            for (int t = 0; t < nb; t++) {
-              const int64_t at = pos + j + t - a0;
-              const uint32_t byte = static_cast<uint32_t>((w >> (8 * t)) & 0xff);
-              if (byte) atomicOr(&sstage[at >> 2], byte << (8 * (at & 3)));
-            }
-          }
+          copy_bytes_range<true>(gdst, oimg, p0, p1, a0);
           __syncthreads();
-          // write [p0, p1): bytes before the first 16-byte boundary and after the last one
-          // individually, the aligned middle 16 B per lane.
-          const int64_t m0 = min<int64_t>((p0 + 15) & ~int64_t(15), p1);
-          const int64_t m1 = max<int64_t>(p1 & ~int64_t(15), m0);
-          const uint8_t* sb = reinterpret_cast<const uint8_t*>(sstage);
-          for (int64_t i = p0 + threadIdx.x; i < m0; i += kThreads) gdst[i] = sb[i - a0];
-          for (int64_t i = m1 + threadIdx.x; i < p1; i += kThreads) gdst[i] = sb[i - a0];
-          using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-          for (int64_t i = m0 + 16 * threadIdx.x; i < m1; i += 16 * kThreads)
-            *reinterpret_cast<v4*>(gdst + i) = *reinterpret_cast<const v4*>(sb + (i - a0));
-          __syncthreads();
-        } else if (gdst) {
-          for (int64_t j = 0; j < len; j++) gdst[pos + j] = src[j];
+        } else {
+          put_bytes(gdst, pos, src, len);
         }
         break;
       }
       default: {   // kListFixed -> Arrow list child (values + element validity)
-        if (!live || isnull) break;
-        const uint8_t* arr = row + static_cast<int32_t>(slot >> 32);
-        const int64_t n = static_cast<int32_t>(*reinterpret_cast<const int64_t*>(arr));
-        const int64_t hb = 8 + bm_bytes(n);
-        const int64_t e0 = c.offsets[r];
         uint8_t* dst = const_cast<uint8_t*>(c.values);
         const int ew = c.width == 0 ? 1 : c.width;
-        if (c.width == 8 && !c.elem_validity) {
-          const uint64_t* s = reinterpret_cast<const uint64_t*>(arr + hb);
-          uint64_t* d = reinterpret_cast<uint64_t*>(dst) + e0;
-          for (int64_t j = 0; j < n; j++) d[j] = s[j];
+        const int64_t e_b = c.offsets[r0], e_e = c.offsets[r0 + nr];
+        const uint8_t* arr = (live && !isnull) ? row + static_cast<int32_t>(slot >> 32) : nullptr;
+        const int64_t n = arr ? static_cast<int32_t>(*reinterpret_cast<const int64_t*>(arr)) : 0;
+        const int64_t hb = 8 + bm_bytes(n);
+        const int64_t e0 = live ? c.offsets[r] : 0;
+        // images: element values (bytes; bool elements as bits) and element validity bits
+        const int64_t vwb = e_b >> 5;                              // first global bit word
+        const int64_t nvw = e_e > e_b ? ((e_e - 1) >> 5) - vwb + 1 : 0;
+        const bool bits_vals = c.width == 0;
+        int64_t a0 = 0, vbytes = 0;
+        if (!bits_vals) {
+          a0 = e_b * ew - static_cast<int64_t>(reinterpret_cast<uintptr_t>(dst + e_b * ew) & 15);
+          vbytes = e_e * ew - a0;
+        }
+        const int64_t need = (bits_vals ? 4 * nvw : ((vbytes + 15) & ~int64_t(15))) +
+                             (c.elem_validity ? 4 * nvw : 0);
+        if (need <= kStrStage && dst) {
+          uint32_t* vimg = reinterpret_cast<uint32_t*>(
+              oimg + (bits_vals ? 0 : ((vbytes + 15) & ~int64_t(15))));
+          uint32_t* bimg = reinterpret_cast<uint32_t*>(oimg);    // bool element values
+          if (bits_vals)
+            vimg = reinterpret_cast<uint32_t*>(oimg + 4 * nvw);
+          const int64_t zero_words = bits_vals ? 2 * nvw : (c.elem_validity ? nvw : 0);
+          uint32_t* zbase = bits_vals ? bimg : vimg;
+          for (int64_t i = threadIdx.x; i < zero_words; i += kThreads) zbase[i] = 0;
+          __syncthreads();
+          for (int64_t j = 0; j < n; j++) {
+            const bool enull = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
+            const int64_t e = e0 + j;
+            if (c.elem_validity) or_bits(vimg, vwb, e, !enull);
+            const uint8_t* p = arr + hb + j * ew;
+            if (bits_vals) {
+              or_bits(bimg, vwb, e, !enull && *p != 0);
+              continue;
+            }
+            uint8_t* q = oimg + (e * ew - a0);
+            switch (ew) {
+              case 8: *reinterpret_cast<uint64_t*>(q) = enull ? 0 : *reinterpret_cast<const uint64_t*>(p); break;
+              case 4: *reinterpret_cast<uint32_t*>(q) = enull ? 0 : *reinterpret_cast<const uint32_t*>(p); break;
+              case 2: *reinterpret_cast<uint16_t*>(q) = enull ? 0 : *reinterpret_cast<const uint16_t*>(p); break;
+              default: *q = enull ? 0 : *p; break;
+            }
+          }
+          __syncthreads();
+          if (bits_vals) flush_bits(reinterpret_cast<uint32_t*>(dst), bimg, e_b, e_e);
+          else copy_bytes_range<true>(dst, oimg, e_b * ew, e_e * ew, a0);
+          if (c.elem_validity)
+            flush_bits(reinterpret_cast<uint32_t*>(c.elem_validity), vimg, e_b, e_e);
+          __syncthreads();
           break;
         }
-        for (int64_t j = 0; j < n; j++) {
+        if (!arr || !dst) break;
+        for (int64_t j = 0; j < n; j++) {                          // oversized: direct path
           const bool enull = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
           if (c.elem_validity) put_bits_atomic(c.elem_validity, e0 + j, !enull);
           uint64_t v = 0;
