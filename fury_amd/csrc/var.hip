@@ -295,21 +295,25 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* _
   if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
-// Exclusive scan of nb block sums (one workgroup), per sequence k (gridDim.x sequences).
+// Exclusive scan of nb block sums (one workgroup per sequence; gridDim.x sequences).  Each thread
+// owns a contiguous chunk (independent loads, one pass), one block-wide scan combines the chunk
+// totals, then every chunk is rewritten with its prefix: two barriers instead of one per 256.
 __global__ __launch_bounds__(kThreads) void scan_block_sums(int64_t* __restrict__ sums, int64_t nb,
                                                             int64_t* __restrict__ totals) {
   __shared__ int64_t tmp[kThreads / 64];
   int64_t* s = sums + blockIdx.x * nb;
-  int64_t carry = 0;
-  for (int64_t base = 0; base < nb; base += kThreads) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < nb ? s[i] : 0;
-    int64_t tot;
-    const int64_t ex = block_excl_scan(v, &tot, tmp);
-    if (i < nb) s[i] = carry + ex;
-    carry += tot;
+  const int64_t per = (nb + kThreads - 1) / kThreads;
+  const int64_t b = min<int64_t>(nb, per * threadIdx.x), e = min<int64_t>(nb, b + per);
+  int64_t local = 0;
+  for (int64_t i = b; i < e; i++) local += s[i];
+  int64_t tot;
+  int64_t run = block_excl_scan(local, &tot, tmp);
+  for (int64_t i = b; i < e; i++) {
+    const int64_t v = s[i];
+    s[i] = run;
+    run += v;
   }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+  if (threadIdx.x == 0) totals[blockIdx.x] = tot;
 }
 
 __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict__ offs, int64_t n,
@@ -422,8 +426,20 @@ __global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
                                                                   int64_t* __restrict__ sums,
                                                                   int64_t nb) {
   __shared__ int64_t tmp[kThreads / 64];
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  const uint8_t* row = r < a.nrows ? rows + offs[r] : nullptr;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
+  const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
+  const int64_t rbeg = offs[r0];
+  const int64_t bytes = offs[r0 + nr] - rbeg;
+  const int64_t r = r0 + threadIdx.x;
+  // stage the group's contiguous row range (16-B coalesced loads) so the per-row slot reads
+  // below hit LDS instead of scattered HBM lines
+  const bool staged = bytes <= kDecodeStage;
+  if (staged) {
+    copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
+    __syncthreads();
+  }
+  const uint8_t* row = r < a.nrows ? (staged ? stage + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
