@@ -295,25 +295,40 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* _
   if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
-// Exclusive scan of nb block sums (one workgroup per sequence; gridDim.x sequences).  Each thread
-// owns a contiguous chunk (independent loads, one pass), one block-wide scan combines the chunk
-// totals, then every chunk is rewritten with its prefix: two barriers instead of one per 256.
-__global__ __launch_bounds__(kThreads) void scan_block_sums(int64_t* __restrict__ sums, int64_t nb,
-                                                            int64_t* __restrict__ totals) {
+// Exclusive scan of small arrays (<= kSmallScan entries): one workgroup, a few block scans.
+constexpr int64_t kSmallScan = 16 * kThreads;
+__global__ __launch_bounds__(kThreads) void scan_small(int64_t* __restrict__ s, int64_t n,
+                                                       int64_t* __restrict__ total) {
   __shared__ int64_t tmp[kThreads / 64];
-  int64_t* s = sums + blockIdx.x * nb;
-  const int64_t per = (nb + kThreads - 1) / kThreads;
-  const int64_t b = min<int64_t>(nb, per * threadIdx.x), e = min<int64_t>(nb, b + per);
-  int64_t local = 0;
-  for (int64_t i = b; i < e; i++) local += s[i];
-  int64_t tot;
-  int64_t run = block_excl_scan(local, &tot, tmp);
-  for (int64_t i = b; i < e; i++) {
-    const int64_t v = s[i];
-    s[i] = run;
-    run += v;
+  int64_t carry = 0;
+  for (int64_t base = 0; base < n; base += kThreads) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < n ? s[i] : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan(v, &tot, tmp);
+    if (i < n) s[i] = carry + ex;
+    carry += tot;
   }
-  if (threadIdx.x == 0) totals[blockIdx.x] = tot;
+  if (threadIdx.x == 0) *total = carry;
+}
+
+// One level of the hierarchical scan: each workgroup scans 256 entries in place (exclusive) and
+// emits their total.
+__global__ __launch_bounds__(kThreads) void scan_groups(int64_t* __restrict__ s, int64_t n,
+                                                        int64_t* __restrict__ gsum) {
+  __shared__ int64_t tmp[kThreads / 64];
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  const int64_t v = i < n ? s[i] : 0;
+  int64_t tot;
+  const int64_t ex = block_excl_scan(v, &tot, tmp);
+  if (i < n) s[i] = ex;
+  if (threadIdx.x == 0) gsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kThreads) void add_groups(int64_t* __restrict__ s, int64_t n,
+                                                       const int64_t* __restrict__ gpre) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n) s[i] += gpre[blockIdx.x];
 }
 
 __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict__ offs, int64_t n,
@@ -788,16 +803,40 @@ int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 }  // namespace
 
+// Device exclusive scan of s[0..n) (int64) with the total written to *total; `ws` needs
+// scan_workspace(n) entries.  Hierarchical: levels of 256-entry group scans until one workgroup
+// can finish, so no step is a long serial walk.
+int64_t scan_workspace(int64_t n) {
+  int64_t w = 0;
+  while (n > kSmallScan) {
+    n = (n + kThreads - 1) / kThreads;
+    w += n;
+  }
+  return w + 1;
+}
+
+void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream) {
+  if (n <= kSmallScan) {
+    hipLaunchKernelGGL(scan_small, dim3(1), dim3(kThreads), 0, stream, s, n, total);
+    return;
+  }
+  const int64_t g = (n + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(scan_groups, dim3(g), dim3(kThreads), 0, stream, s, n, ws);
+  device_scan(ws, g, total, ws + g, stream);
+  hipLaunchKernelGGL(add_groups, dim3(g), dim3(kThreads), 0, stream, s, n, ws);
+}
+
 int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t n = a.nrows;
   if (n == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
   const int64_t nb = nblocks(n);
   int64_t* ws = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), (nb + 1) * 8, stream),
+  const int64_t wsn = nb + 1 + scan_workspace(nb);
+  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
                      "hipMallocAsync");
   if (st) return st;
   hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
-  hipLaunchKernelGGL(scan_block_sums, dim3(1), dim3(kThreads), 0, stream, ws, nb, ws + nb);
+  device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
   hipLaunchKernelGGL(add_block_prefix, dim3(nb), dim3(kThreads), 0, stream, offs, n, ws, ws + nb);
   st = check_hip(hipGetLastError(), "measure launch");
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
@@ -819,13 +858,14 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   if (nseq == 0 || a.nrows == 0) return FURY_OK;
   const int64_t nb = nblocks(a.nrows);
   int64_t* ws = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), (nb + 1) * 8 * nseq, stream),
-                     "hipMallocAsync");
+  const int64_t scr = scan_workspace(nb);
+  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), (nb * nseq + nseq + scr) * 8,
+                                    stream), "hipMallocAsync");
   if (st) return st;
   int64_t* totals = ws + nb * nseq;
   hipLaunchKernelGGL(decode_measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs, ws,
                      nb);
-  hipLaunchKernelGGL(scan_block_sums, dim3(nseq), dim3(kThreads), 0, stream, ws, nb, totals);
+  for (int q = 0; q < nseq; q++) device_scan(ws + q * nb, nb, totals + q, totals + nseq, stream);
   hipLaunchKernelGGL(decode_measure_fix, dim3(nb), dim3(kThreads), 0, stream, a, ws, totals, nb);
   st = check_hip(hipGetLastError(), "decode measure launch");
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");

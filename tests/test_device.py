@@ -233,3 +233,9 @@ def test_struct100_full_size_roundtrip_property(dev, rows):
     dec = enc.decode_batch(b, validity=False)
     for c, d in zip(cols, dec):
         assert torch.equal(c.values.view(torch.uint8), d.values)
+
+
+def test_var_large_batch_hierarchical_scan(oracle, dev):
+    """> 4096 workgroups: exercises the multi-level device scan of row sizes and of the Arrow
+    offsets on decode; full byte comparison against the oracle."""
+    _roundtrip(oracle, "mixed", 1_500_000, dev, seed=13)
