@@ -10,7 +10,7 @@ import numpy as np
 import pyarrow as pa
 
 from .types import (BINARY, BOOL, DATE32, DECIMAL, FLOAT32, FLOAT64, INT8, INT16, INT32, INT64,
-                    LIST, STRING, TIMESTAMP, Field)
+                    LIST, MAP, STRING, STRUCT, TIMESTAMP, Field)
 from .workloads import Column
 
 _PA = {BOOL: pa.bool_(), INT8: pa.int8(), INT16: pa.int16(), INT32: pa.int32(),
@@ -25,6 +25,11 @@ def pa_type(f: Field) -> pa.DataType:
     if f.type_id == LIST:
         e = f.children[0]
         return pa.list_(pa.field(e.name, pa_type(e), e.nullable))
+    if f.type_id == STRUCT:
+        return pa.struct([pa.field(c.name, pa_type(c), c.nullable) for c in f.children])
+    if f.type_id == MAP:
+        k, v = f.children
+        return pa.map_(pa.field(k.name, pa_type(k), False), pa.field(v.name, pa_type(v), v.nullable))
     raise NotImplementedError(f"no Arrow export for {f}")
 
 
@@ -41,6 +46,15 @@ def column_to_array(f: Field, c: Column, n: int) -> pa.Array:
         m = int(np.asarray(c.offsets)[n])
         child = column_to_array(f.children[0], c.child[0], m)
         return pa.Array.from_buffers(t, n, [vb, _buf(c.offsets)], children=[child])
+    if f.type_id == STRUCT:
+        kids = [column_to_array(fc, cc, n) for fc, cc in zip(f.children, c.child)]
+        return pa.Array.from_buffers(t, n, [vb], children=kids)
+    if f.type_id == MAP:
+        m = int(np.asarray(c.offsets)[n])
+        k = column_to_array(f.children[0], c.child[0], m)
+        v = column_to_array(f.children[1], c.child[1], m)
+        entries = pa.StructArray.from_arrays([k, v], fields=[t.key_field, t.item_field])
+        return pa.Array.from_buffers(t, n, [vb, _buf(c.offsets)], children=[entries])
     return pa.Array.from_buffers(t, n, [vb, _buf(c.values)])
 
 

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "internal.h"
 #include "kernels.h"
@@ -145,8 +146,80 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   return FURY_OK;
 }
 
+// Generic engine arguments: schema nodes (breadth-first) + the column tree walked in the same
+// order (LIST: child[0] = elements; STRUCT: child[0..n); MAP: child[0] keys, child[1] values).
+int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
+             bool need_validity, GenArgs* g) {
+  const size_t nn = s->nodes.size();
+  if (nn > static_cast<size_t>(kGenMaxNodes))
+    return set_error(FURY_ERR_UNSUPPORTED, "nested schema has more than " +
+                                               std::to_string(kGenMaxNodes) + " nodes");
+  *g = GenArgs{};
+  g->nnodes = static_cast<int32_t>(nn);
+  g->ntop = s->num_fields;
+  g->nrows = nrows;
+  g->err = nullptr;
+  std::vector<const fury_column*> col(nn, nullptr);
+  for (int k = 0; k < s->num_fields; k++) col[k] = &cols[k];
+  for (size_t i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    const fury_column* c = col[i];
+    const std::string who = "schema node " + std::to_string(i);
+    if (!c) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": missing column");
+    GenNode& n = g->node[i];
+    n.values = static_cast<const uint8_t*>(c->values);
+    n.validity = c->validity;
+    n.offsets = c->offsets;
+    n.type = t.type_id;
+    n.first_child = t.first_child;
+    n.num_children = t.num_children;
+    if (t.num_children > 0) {
+      if (!c->child) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": child columns missing");
+      for (int j = 0; j < t.num_children; j++) col[t.first_child + j] = &c->child[j];
+    }
+    const bool var = t.type_id == FURY_TYPE_STRING || t.type_id == FURY_TYPE_BINARY ||
+                     t.type_id == FURY_TYPE_LIST || t.type_id == FURY_TYPE_MAP;
+    if (nrows > 0 && var && !c->offsets)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
+    if (need_validity && !c->validity)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": Arrow output needs a validity buffer");
+    if (decode && c->validity && misaligned(c->validity, 4))
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": validity must be 4-byte aligned");
+    if (decode && t.type_id == FURY_TYPE_BOOL && c->values && misaligned(c->values, 4))
+      return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": bool bitmap must be 4-byte aligned");
+  }
+  return FURY_OK;
+}
+
+int gen_measure(const fury_schema* s, const fury_column* cols, int64_t nrows, int64_t* offs,
+                hipStream_t stream) {
+  GenArgs g;
+  int st = gen_args(s, cols, nrows, false, false, &g);
+  if (st) return st;
+  if (nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
+  st = launch_gen_measure(g, offs, stream);
+  if (st) return st;
+  int64_t* ws = nullptr;
+  st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), scan_workspace(nrows) * 8, stream),
+                 "hipMallocAsync");
+  if (st) return st;
+  device_scan(offs, nrows, offs + nrows, ws, stream);
+  st = check_hip(hipGetLastError(), "scan launch");
+  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
+  return st ? st : st2;
+}
+
 }  // namespace
 }  // namespace fury
+
+struct fury_decode_plan {
+  const fury_schema* schema = nullptr;
+  const uint8_t* rows = nullptr;
+  const int64_t* offs = nullptr;
+  int64_t nrows = 0;
+  int64_t* cnt = nullptr;      // [2 * nodes][nrows] scanned start positions
+  bool arrow = false;
+};
 
 using namespace fury;
 
@@ -158,6 +231,7 @@ int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrow
   if (st) return st;
   if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
   if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
+  if (s->generic) return gen_measure(s, cols, nrows, row_offsets, static_cast<hipStream_t>(stream));
   VarArgs a;
   st = var_args(s, cols, nrows, false, false, &a);
   if (st) return st;
@@ -183,6 +257,12 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
   if (!row_offsets)
     return set_error(FURY_ERR_INVALID_ARGUMENT,
                      "variable-length schema needs row_offsets from fury_row_measure");
+  if (s->generic) {
+    GenArgs g;
+    st = gen_args(s, cols, nrows, false, false, &g);
+    if (st) return st;
+    return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), hs);
+  }
   VarArgs a;
   st = var_args(s, cols, nrows, false, false, &a);
   if (st) return st;
@@ -194,6 +274,9 @@ int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_
   int st = common_checks(s, cols, nrows, "fury_row_decode_measure");
   if (st) return st;
   if (s->is_fixed || nrows == 0) return FURY_OK;   // nothing variable to size
+  if (s->generic)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "nested schema: size outputs with fury_decode_prepare / fury_decode_execute");
   if (!rows || !row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/row_offsets null");
   VarArgs a;
   st = var_args(s, cols, nrows, true, false, &a);
@@ -221,6 +304,9 @@ static int decode_impl(const fury_schema* s, const void* rows, const int64_t* ro
   if (!row_offsets)
     return set_error(FURY_ERR_INVALID_ARGUMENT, "variable-length rows need row_offsets");
   if (misaligned(rows, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 8-byte aligned");
+  if (s->generic)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "nested schema: decode with fury_decode_prepare / fury_decode_execute");
   VarArgs a;
   st = var_args(s, cols, nrows, true, arrow, &a);
   if (st) return st;
@@ -235,6 +321,74 @@ int fury_row_decode(const fury_schema* s, const void* rows, const int64_t* row_o
 int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* cols, void* stream) {
   return decode_impl(s, rows, row_offsets, nrows, cols, stream, true, "fury_rows_to_arrow");
+}
+
+int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                        int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
+                        fury_decode_plan** plan, void* stream) {
+  if (!s || !plan) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_decode_prepare: null argument");
+  *plan = nullptr;
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
+  if (nrows > 0 && (!rows || !row_offsets))
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "rows / row_offsets is null");
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  const int nn = static_cast<int>(s->nodes.size());
+  fury_decode_plan* p = new fury_decode_plan();
+  p->schema = s;
+  p->rows = static_cast<const uint8_t*>(rows);
+  p->offs = row_offsets;
+  p->nrows = nrows;
+  std::vector<int64_t> totals(2 * nn, 0);
+  if (nrows > 0) {
+    // Count pass: the column tree is not needed (null columns everywhere).
+    std::vector<fury_column> dummy(nn);
+    std::vector<fury_column> top(s->num_fields);
+    GenArgs g{};
+    g.nnodes = nn;
+    g.ntop = s->num_fields;
+    g.nrows = nrows;
+    for (int i = 0; i < nn; i++) {
+      g.node[i].type = s->nodes[i].type_id;
+      g.node[i].first_child = s->nodes[i].first_child;
+      g.node[i].num_children = s->nodes[i].num_children;
+    }
+    const int64_t cells = 2 * static_cast<int64_t>(nn) * nrows;
+    int64_t* dev = nullptr;
+    int st = check_hip(hipMalloc(reinterpret_cast<void**>(&dev),
+                                 (cells + 2 * nn + scan_workspace(nrows)) * 8), "hipMalloc");
+    if (st) { delete p; return st; }
+    p->cnt = dev;
+    st = launch_gen_count(g, p->rows, row_offsets, dev, hs);
+    int64_t* tot = dev + cells;
+    int64_t* ws = tot + 2 * nn;
+    for (int q = 0; q < 2 * nn && !st; q++) device_scan(dev + q * nrows, nrows, tot + q, ws, hs);
+    if (!st) st = check_hip(hipMemcpyAsync(totals.data(), tot, 2 * nn * 8, hipMemcpyDeviceToHost, hs),
+                            "hipMemcpyAsync");
+    if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+    if (st) { fury_decode_plan_destroy(p); return st; }
+  }
+  for (int i = 0; i < nn; i++) {
+    if (node_entries) node_entries[i] = totals[2 * i];
+    if (node_bytes) node_bytes[i] = totals[2 * i + 1];
+  }
+  *plan = p;
+  return FURY_OK;
+}
+
+int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, void* stream) {
+  if (!p) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_decode_execute: plan is null");
+  if (p->nrows == 0) return FURY_OK;
+  GenArgs g;
+  int st = gen_args(p->schema, cols, p->nrows, true, arrow != 0, &g);
+  if (st) return st;
+  return launch_gen_decode(g, p->rows, p->offs, p->cnt, static_cast<hipStream_t>(stream));
+}
+
+void fury_decode_plan_destroy(fury_decode_plan* p) {
+  if (!p) return;
+  if (p->cnt) (void)hipFree(p->cnt);
+  delete p;
 }
 
 int fury_set_tuning(const char* key, int32_t value) {

@@ -1,0 +1,449 @@
+// generic.hip — schema-interpreting kernels for ANY schema the reference row format supports:
+// nested STRUCT (bean fields), LIST of any element type (incl. strings, structs, lists, maps),
+// MAP (key / value arrays), plus every scalar type.  The specialised kernels in fixed.hip /
+// var.hip cover flat schemas at full speed; this engine covers the rest of the type system.
+//
+// Reference semantics (FMT = java/fury-format/src/main/java/org/apache/fury/format):
+//   encode   BaseBinaryEncoderBuilder.serializeFor (FMT/encoder/BaseBinaryEncoderBuilder.java:
+//            138-453): primitives into 8-byte slots, var values appended at the writer index and
+//            padded to 8 (BinaryWriter.java:106-121,187-194), List -> BinaryArrayWriter image
+//            [int64 n][bitmap][n x elemSize, tail zeroed][var section] (BinaryArrayWriter.java:
+//            91-163), bean -> child BinaryRowWriter row (:363-417), Map -> [int64 keyBytes]
+//            [key array][value array] (:298-357); null -> setNullAt only.
+//   decode   getters + ArrowWriter (FMT/vectorized/ArrowWriter.java:205-640): a null struct
+//            appends a null to every child (StructWriter.appendNull :577-584), null lists/maps
+//            are zero-length entries (ListWriter/MapWriter.appendNull no-op + fillHoles).
+//
+// MI355X design: the flattened schema and the per-call column pointers travel in the kernel
+// argument block (scalar-loaded).  Encode is one thread per row (measure pass -> device scan ->
+// build pass).  Decode counts, per row and per schema node, the Arrow entries and payload bytes
+// the row contributes; device scans turn those into each row's starting positions in every
+// output buffer, and a second thread-per-row pass writes them.  Validity bits go through 32-bit
+// atomics on buffers the host zeroes; everything else is plain stores into disjoint ranges.
+// Recursion is depth-unrolled (template<int D>), at most kMaxDepth levels of nesting.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "kernels.h"
+
+namespace fury {
+
+namespace {
+
+constexpr int kThreads = 64;          // decode keeps per-thread node counters in LDS
+constexpr int kEncThreads = 256;
+
+__device__ __forceinline__ bool gbit(const uint8_t* bits, int64_t i) {
+  return (bits[i >> 3] >> (i & 7)) & 1;
+}
+__device__ __forceinline__ int64_t g8(int64_t n) { return (n + 7) & ~int64_t(7); }
+__device__ __forceinline__ int64_t gbm(int64_t n) { return ((n + 63) >> 6) << 3; }
+
+__device__ __forceinline__ int gwidth(int t) {
+  switch (t) {
+    case FURY_TYPE_BOOL: case FURY_TYPE_INT8: return 1;
+    case FURY_TYPE_INT16: return 2;
+    case FURY_TYPE_INT32: case FURY_TYPE_FLOAT32: case FURY_TYPE_DATE32: return 4;
+    case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
+    default: return -1;
+  }
+}
+
+__device__ __forceinline__ void st8(uint8_t* p, uint64_t v) {
+  memcpy(p, &v, 8);   // p is 8-byte aligned by construction; memcpy keeps it a single store
+}
+__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+
+// ---- encode ----------------------------------------------------------------------------------
+
+__device__ __forceinline__ void zero_bytes(uint8_t* p, int64_t n) {
+  // 8-byte aligned start; n multiple of 8 in every use
+  for (int64_t i = 0; i < n; i += 8) st8(p + i, 0);
+}
+
+// Appends len bytes (unaligned source) at dst (8-aligned), zero-padding to 8.
+__device__ __forceinline__ void append_unaligned(uint8_t* dst, const uint8_t* src, int64_t len) {
+  const int64_t nw = (len + 7) >> 3;
+  for (int64_t w = 0; w < nw; w++) {
+    uint64_t x = 0;
+    const int64_t lim = min<int64_t>(8, len - 8 * w);
+    for (int64_t t = 0; t < lim; t++) x |= static_cast<uint64_t>(src[8 * w + t]) << (8 * t);
+    st8(dst + 8 * w, x);
+  }
+}
+
+template <int D, bool W>
+__device__ __attribute__((noinline)) void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+                          int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
+                          int64_t& cursor);
+
+// BinaryArrayWriter image of elements [b, b + m) of node `ei` at buf + cursor.
+template <int D, bool W>
+__device__ __attribute__((noinline)) void put_array(const GenNode* nodes, int ei, int64_t b, int64_t m, uint8_t* buf,
+                          int64_t& cursor) {
+  const GenNode& e = nodes[ei];
+  const int w = gwidth(e.type);
+  const int es = w > 0 ? w : 8;
+  const int64_t start = cursor;
+  const int64_t hb = 8 + gbm(m);
+  const int64_t fp = g8(m * es);
+  if (W) {
+    st8(buf + start, static_cast<uint64_t>(m));
+    zero_bytes(buf + start + 8, hb - 8 + fp);     // bitmap, element slots, alignment tail
+  }
+  int64_t c2 = start + hb + fp;
+  for (int64_t j = 0; j < m; j++)
+    put_value<D + 1, W>(nodes, ei, b + j, buf, start, start + hb + j * es, es, true, start + 8, j, c2);
+  cursor = c2;
+}
+
+template <int D, bool W>
+__device__ __attribute__((noinline)) void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+                          int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
+                          int64_t& cursor) {
+  if constexpr (D >= kGenMaxDepth) {
+    (void)nodes;
+    return;
+  } else {
+    const GenNode& n = nodes[ni];
+    if (n.validity && !gbit(n.validity, idx)) {      // setNullAt: bit only, slot stays 0
+      if (W) buf[bitmap + (ordinal >> 3)] |= static_cast<uint8_t>(1u << (ordinal & 7));
+      return;
+    }
+    const int w = gwidth(n.type);
+    if (w > 0) {
+      if (W) {
+        uint64_t v;
+        if (n.type == FURY_TYPE_BOOL) v = gbit(n.values, idx);
+        else if (w == 8) v = ld8(n.values + idx * 8);
+        else if (w == 4) v = *reinterpret_cast<const uint32_t*>(n.values + idx * 4);
+        else if (w == 2) v = *reinterpret_cast<const uint16_t*>(n.values + idx * 2);
+        else v = n.values[idx];
+        if (!in_array) {
+          st8(buf + slot, v);                           // putInt64(0) + narrow put
+        } else {
+          switch (es) {
+            case 8: st8(buf + slot, v); break;
+            case 4: *reinterpret_cast<uint32_t*>(buf + slot) = static_cast<uint32_t>(v); break;
+            case 2: *reinterpret_cast<uint16_t*>(buf + slot) = static_cast<uint16_t>(v); break;
+            default: buf[slot] = static_cast<uint8_t>(v); break;
+          }
+        }
+      }
+      return;
+    }
+    const int64_t start = cursor;
+    switch (n.type) {
+      case FURY_TYPE_STRING:
+      case FURY_TYPE_BINARY: {
+        const int64_t b = n.offsets[idx];
+        const int64_t len = n.offsets[idx + 1] - b;
+        if (W) append_unaligned(buf + start, n.values + b, len);
+        cursor = start + g8(len);
+        if (W) st8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
+        return;
+      }
+      case FURY_TYPE_DECIMAL: {
+        if (W) {
+          st8(buf + start, ld8(n.values + 16 * idx));
+          st8(buf + start + 8, ld8(n.values + 16 * idx + 8));
+          st8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | 16u);
+        }
+        cursor = start + 16;
+        return;
+      }
+      case FURY_TYPE_LIST: {
+        const int64_t b = n.offsets[idx];
+        put_array<D, W>(nodes, n.first_child, b, n.offsets[idx + 1] - b, buf, cursor);
+        break;
+      }
+      case FURY_TYPE_STRUCT: {
+        const int nc = n.num_children;
+        const int64_t bmb = gbm(nc);
+        const int64_t fixed = bmb + 8 * nc;
+        if (W) zero_bytes(buf + start, fixed);
+        int64_t c2 = start + fixed;
+        for (int k = 0; k < nc; k++)
+          put_value<D + 1, W>(nodes, n.first_child + k, idx, buf, start, start + bmb + 8 * k, 8, false,
+                              start, k, c2);
+        cursor = c2;
+        break;
+      }
+      case FURY_TYPE_MAP: {
+        const int64_t b = n.offsets[idx];
+        const int64_t m = n.offsets[idx + 1] - b;
+        int64_t c2 = start + 8;                         // writeDirectly(-1) placeholder
+        put_array<D, W>(nodes, n.first_child, b, m, buf, c2);
+        if (W) st8(buf + start, static_cast<uint64_t>(c2 - (start + 8)));   // key array size
+        put_array<D, W>(nodes, n.first_child + 1, b, m, buf, c2);
+        cursor = c2;
+        break;
+      }
+      default:
+        
+        return;
+    }
+    if (W) st8(buf + slot, (static_cast<uint64_t>(start - container) << 32) |
+                               static_cast<uint32_t>(cursor - start));
+  }
+}
+
+template <bool W>
+__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf) {
+  const int64_t bmb = gbm(ntop);
+  const int64_t fixed = bmb + 8 * ntop;
+  if (W) zero_bytes(buf, fixed);                       // fresh buffer: bitmap + slots zero
+  int64_t cursor = fixed;
+  for (int k = 0; k < ntop; k++)
+    put_value<1, W>(nodes, k, r, buf, 0, bmb + 8 * k, 8, false, 0, k, cursor);
+  return cursor;
+}
+
+// The node table is copied from the argument block into LDS once per workgroup and passed to
+// the (non-inlined, recursive-by-depth) helpers as a pointer: taking the address of the kernel
+// argument itself would make the compiler copy the whole block into per-lane scratch.
+__device__ __forceinline__ const GenNode* stage_nodes(const GenArgs& g, GenNode* lds) {
+  for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) lds[i] = g.node[i];
+  __syncthreads();
+  return lds;
+}
+
+__global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int64_t* __restrict__ sizes) {
+  __shared__ GenNode sn[kGenMaxNodes];
+  const GenNode* nodes = stage_nodes(g, sn);
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
+  if (r < g.nrows) sizes[r] = put_row<false>(nodes, g.ntop, r, nullptr);
+}
+
+__global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
+                                                                 const int64_t* __restrict__ offs,
+                                                                 uint8_t* __restrict__ rows) {
+  __shared__ GenNode sn[kGenMaxNodes];
+  const GenNode* nodes = stage_nodes(g, sn);
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
+  if (r < g.nrows) put_row<true>(nodes, g.ntop, r, rows + offs[r]);
+}
+
+// ---- decode ----------------------------------------------------------------------------------
+// Per thread, per node: running Arrow entry index and payload byte position, in LDS.
+struct Cursors {
+  int64_t* e;   // [node]
+  int64_t* b;   // [node]
+};
+
+template <int D, bool W>
+__device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
+                          int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
+                          int64_t ordinal, Cursors cur);
+
+// Elements of a BinaryArray at `arr` into node ei's Arrow column (m entries).
+template <int D, bool W>
+__device__ __attribute__((noinline)) void get_array(const GenNode* nodes, int ei, const uint8_t* arr, int64_t m, Cursors cur) {
+  const GenNode& e = nodes[ei];
+  const int w = gwidth(e.type);
+  const int es = w > 0 ? w : 8;
+  const int64_t hb = 8 + gbm(m);
+  for (int64_t j = 0; j < m; j++)
+    get_value<D + 1, W>(nodes, ei, true, arr, hb + j * es, es, true, arr + 8, j, cur);
+}
+
+// A null (or absent) entry for node ni and, for structs, one null entry in every child.
+template <int D, bool W>
+__device__ __attribute__((noinline)) void null_entry(const GenNode* nodes, int ni, Cursors cur) {
+  if constexpr (D >= kGenMaxDepth) {
+    return;
+  } else {
+    const GenNode& n = nodes[ni];
+    const int64_t e = cur.e[ni]++;
+    if (W) {
+      const int w = gwidth(n.type);
+      if (w > 0 && n.type != FURY_TYPE_BOOL && n.values) {
+        uint8_t* p = const_cast<uint8_t*>(n.values) + e * w;
+        for (int t = 0; t < w; t++) p[t] = 0;
+      } else if (n.type == FURY_TYPE_DECIMAL && n.values) {
+        st8(const_cast<uint8_t*>(n.values) + 16 * e, 0);
+        st8(const_cast<uint8_t*>(n.values) + 16 * e + 8, 0);
+      } else if (n.offsets) {                          // zero-length string / list / map
+        const int64_t pos = (n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY)
+                                ? cur.b[ni] : cur.e[n.first_child];
+        n.offsets[e + 1] = static_cast<int32_t>(pos);
+      }
+    }
+    if (n.type == FURY_TYPE_STRUCT)
+      for (int k = 0; k < n.num_children; k++) null_entry<D + 1, W>(nodes, n.first_child + k, cur);
+  }
+}
+
+__device__ __forceinline__ void set_valid_bit(uint8_t* bits, int64_t i) {
+  uint32_t* wp = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits + (i >> 3)) & ~uintptr_t(3));
+  const int sh = static_cast<int>((reinterpret_cast<uintptr_t>(bits + (i >> 3)) & 3) * 8 + (i & 7));
+  atomicOr(wp, 1u << sh);
+}
+
+template <int D, bool W>
+__device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
+                          int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
+                          int64_t ordinal, Cursors cur) {
+  if constexpr (D >= kGenMaxDepth) {
+    return;
+  } else {
+    const GenNode& n = nodes[ni];
+    const bool isnull = !present || ((bitmap[ordinal >> 3] >> (ordinal & 7)) & 1);
+    if (isnull) {
+      null_entry<D, W>(nodes, ni, cur);
+      return;
+    }
+    const int64_t e = cur.e[ni]++;
+    if (W && n.validity) set_valid_bit(n.validity, e);
+    const uint8_t* sp = base + slot_addr;
+    const int w = gwidth(n.type);
+    if (w > 0) {
+      if (!W) return;
+      uint64_t v;
+      if (es == 8) v = ld8(sp);
+      else if (es == 4) v = *reinterpret_cast<const uint32_t*>(sp);
+      else if (es == 2) v = *reinterpret_cast<const uint16_t*>(sp);
+      else v = *sp;
+      uint8_t* dst = const_cast<uint8_t*>(n.values);
+      if (!dst) return;
+      if (n.type == FURY_TYPE_BOOL) {
+        if (v & 0xff) set_valid_bit(dst, e);
+      } else if (w == 8) {
+        st8(dst + 8 * e, v);
+      } else if (w == 4) {
+        *reinterpret_cast<uint32_t*>(dst + 4 * e) = static_cast<uint32_t>(v);
+      } else if (w == 2) {
+        *reinterpret_cast<uint16_t*>(dst + 2 * e) = static_cast<uint16_t>(v);
+      } else {
+        dst[e] = static_cast<uint8_t>(v);
+      }
+      return;
+    }
+    const uint64_t oas = ld8(sp);
+    const uint8_t* vp = base + static_cast<int32_t>(oas >> 32);
+    const int64_t size = static_cast<uint32_t>(oas);
+    switch (n.type) {
+      case FURY_TYPE_STRING:
+      case FURY_TYPE_BINARY: {
+        const int64_t pos = cur.b[ni];
+        cur.b[ni] = pos + size;
+        if (W) {
+          uint8_t* dst = const_cast<uint8_t*>(n.values);
+          if (dst)
+            for (int64_t t = 0; t < size; t++) dst[pos + t] = vp[t];
+          n.offsets[e + 1] = static_cast<int32_t>(pos + size);
+        }
+        return;
+      }
+      case FURY_TYPE_DECIMAL:
+        if (W && n.values) {
+          st8(const_cast<uint8_t*>(n.values) + 16 * e, ld8(vp));
+          st8(const_cast<uint8_t*>(n.values) + 16 * e + 8, ld8(vp + 8));
+        }
+        return;
+      case FURY_TYPE_LIST: {
+        const int64_t m = static_cast<int32_t>(ld8(vp));
+        get_array<D, W>(nodes, n.first_child, vp, m, cur);
+        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e[n.first_child]);
+        return;
+      }
+      case FURY_TYPE_STRUCT: {
+        const int nc = n.num_children;
+        const int64_t bmb = gbm(nc);
+        for (int k = 0; k < nc; k++)
+          get_value<D + 1, W>(nodes, n.first_child + k, true, vp, bmb + 8 * k, 8, false, vp, k, cur);
+        return;
+      }
+      case FURY_TYPE_MAP: {
+        const int64_t key_bytes = static_cast<int64_t>(ld8(vp));
+        const uint8_t* ka = vp + 8;
+        const uint8_t* va = vp + 8 + key_bytes;
+        const int64_t m = static_cast<int32_t>(ld8(ka));
+        get_array<D, W>(nodes, n.first_child, ka, m, cur);
+        get_array<D, W>(nodes, n.first_child + 1, va, m, cur);
+        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e[n.first_child]);
+        return;
+      }
+      default:
+        return;
+    }
+  }
+}
+
+// Pass 1 (W = false): per row, per node, Arrow entries and payload bytes -> cnt[2*node][row],
+// cnt[2*node+1][row].  Pass 2 (W = true): cursors start at the scanned positions.
+template <bool W>
+__global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const uint8_t* __restrict__ rows,
+                                                              const int64_t* __restrict__ offs,
+                                                              int64_t* __restrict__ cnt) {
+  __shared__ int64_t ce[kThreads * kGenMaxNodes];
+  __shared__ int64_t cb[kThreads * kGenMaxNodes];
+  __shared__ GenNode sn[kGenMaxNodes];
+  const GenNode* nodes = stage_nodes(g, sn);
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (r >= g.nrows) return;
+  int64_t* e = ce + threadIdx.x * kGenMaxNodes;
+  int64_t* b = cb + threadIdx.x * kGenMaxNodes;
+  for (int i = 0; i < g.nnodes; i++) {
+    e[i] = W ? cnt[(2 * i) * g.nrows + r] : 0;
+    b[i] = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
+  }
+  const uint8_t* row = rows + offs[r];
+  const int64_t bmb = gbm(g.ntop);
+  Cursors cur{e, b};
+  for (int k = 0; k < g.ntop; k++)
+    get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
+  if (!W) {
+    for (int i = 0; i < g.nnodes; i++) {
+      cnt[(2 * i) * g.nrows + r] = e[i];
+      cnt[(2 * i + 1) * g.nrows + r] = b[i];
+    }
+  }
+}
+
+// Arrow offsets start at 0 for every node that has them.
+__global__ void gen_offsets_zero(GenArgs g) {
+  const int i = threadIdx.x;
+  if (i < g.nnodes && g.node[i].offsets) g.node[i].offsets[0] = 0;
+}
+
+}  // namespace
+
+int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
+  const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
+  hipLaunchKernelGGL(gen_measure_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
+  return check_hip(hipGetLastError(), "gen_measure launch");
+}
+
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
+  const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
+  hipLaunchKernelGGL(gen_encode_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, offs, rows);
+  return check_hip(hipGetLastError(), "gen_encode launch");
+}
+
+int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
+                     hipStream_t stream) {
+  const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(gen_decode_kernel<false>, dim3(blocks), dim3(kThreads), 0, stream, g, rows,
+                     offs, cnt);
+  return check_hip(hipGetLastError(), "gen_count launch");
+}
+
+int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(gen_offsets_zero, dim3(1), dim3(kGenMaxNodes), 0, stream, g);
+  const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(gen_decode_kernel<true>, dim3(blocks), dim3(kThreads), 0, stream, g, rows,
+                     offs, cnt);
+  return check_hip(hipGetLastError(), "gen_decode launch");
+}
+
+}  // namespace fury

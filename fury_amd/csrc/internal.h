@@ -29,6 +29,15 @@ struct FieldPlan {
   int32_t elem_nullable;
 };
 
+// Node of the flattened schema tree used by the generic (nested) engine: breadth-first, the
+// top-level fields first, every node's children contiguous.
+struct GenTpl {
+  int32_t type_id;
+  int32_t first_child;
+  int32_t num_children;
+  int32_t nullable;
+};
+
 struct OwnedField {
   std::string name;
   int32_t type_id = 0;
@@ -49,6 +58,9 @@ struct fury_schema {
   int32_t device_ok = 1;          // every field kind has a device kernel
   std::string device_reason;      // why not, when device_ok == 0
   int32_t num_var = 0;            // fields of kind kBytes / kDecimal / kListFixed
+  int32_t generic = 0;            // nested schema: encode/decode run the generic engine
+  int32_t depth = 0;              // deepest nesting level (top-level fields = 1)
+  std::vector<fury::GenTpl> nodes;
 };
 
 namespace fury {

@@ -76,6 +76,38 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
                           hipStream_t stream);
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                       hipStream_t stream, bool arrow);
+// ---- generic (nested) schema engine: generic.hip --------------------------------------------
+constexpr int kGenMaxNodes = 48;      // schema tree nodes (fields at every level)
+constexpr int kGenMaxDepth = 8;       // nesting levels (checked at schema creation)
+
+struct GenNode {
+  const uint8_t* values;   // fixed values / bytes payload / decimal values (bool: bit-packed)
+  uint8_t* validity;       // Arrow validity or NULL
+  int32_t* offsets;        // STRING/BINARY byte offsets, LIST/MAP entry offsets
+  int32_t type;            // fury_type_id
+  int32_t first_child;     // node index of the first child (children are contiguous)
+  int32_t num_children;
+  int32_t pad_;
+};
+
+struct GenArgs {
+  GenNode node[kGenMaxNodes];
+  int32_t nnodes;
+  int32_t ntop;            // top-level fields = nodes [0, ntop)
+  int64_t nrows;
+  int32_t* err;            // optional device flag (never NULL when set by the host)
+};
+
+int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, hipStream_t stream);
+int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
+                     hipStream_t stream);
+int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
+                      hipStream_t stream);
+// Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
+int64_t scan_workspace(int64_t n);
+void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);
+
 int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t nrows,
                       int64_t fixed_size, int64_t schema_hash, uint8_t* out,
                       int64_t* frame_offsets, hipStream_t stream);

@@ -15,6 +15,10 @@
 
 namespace fury {
 
+// keep in sync with kGenMaxNodes / kGenMaxDepth (kernels.h; this TU is host-only C++)
+constexpr int kGenMaxNodesHost = 48;
+constexpr int kGenMaxDepthHost = 8;
+
 static thread_local std::string g_last_error;
 
 int set_error(int status, const std::string& msg) {
@@ -249,8 +253,42 @@ int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema
     if (p.kind == kBytes || p.kind == kDecimal || p.kind == kListFixed) s->num_var++;
     s->plan.push_back(p);
   }
+  // Flattened node tree (breadth-first) for the generic engine.
+  {
+    std::vector<const OwnedField*> q;
+    std::vector<int32_t> depth;
+    for (const auto& f : s->fields) {
+      q.push_back(&f);
+      depth.push_back(1);
+    }
+    for (size_t i = 0; i < q.size(); i++) {
+      GenTpl t{q[i]->type_id, 0, static_cast<int32_t>(q[i]->children.size()), q[i]->nullable};
+      t.first_child = static_cast<int32_t>(q.size());
+      for (const auto& c : q[i]->children) {
+        q.push_back(&c);
+        depth.push_back(depth[i] + 1);
+      }
+      s->nodes.push_back(t);
+      s->depth = std::max(s->depth, depth[i]);
+    }
+  }
+  if (!s->device_ok) {
+    // nested fields: the generic engine handles them within its table limits
+    if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost) {
+      s->device_ok = 1;
+      s->generic = 1;
+      s->device_reason.clear();
+    } else {
+      s->device_reason += " (nested schema beyond " + std::to_string(kGenMaxNodesHost) +
+                          " nodes / " + std::to_string(kGenMaxDepthHost - 1) + " levels)";
+    }
+  }
   *out = s;
   return FURY_OK;
+}
+
+int32_t fury_schema_num_nodes(const fury_schema* s) {
+  return s ? static_cast<int32_t>(s->nodes.size()) : -1;
 }
 
 void fury_schema_destroy(fury_schema* schema) { delete schema; }

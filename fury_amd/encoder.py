@@ -25,7 +25,8 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .types import (BINARY, BOOL, DECIMAL, FLOAT32, FLOAT64, LIST, STRING, Field, type_width)
+from .types import (BINARY, BOOL, DECIMAL, FLOAT32, FLOAT64, LIST, MAP, STRING, STRUCT, Field,
+                    type_width)
 from .workloads import Column
 
 # ---------------------------------------------------------------------------------------------
@@ -276,8 +277,50 @@ class RowEncoder:
                 raise UnsupportedOperationException(f"no device decode for {f}")
         return out
 
+    @property
+    def nested(self) -> bool:
+        """True when the schema has STRUCT / MAP / LIST-of-variable-length fields (decoded by the
+        two-step plan API)."""
+        def deep(f: Field) -> bool:
+            if f.type_id in (STRUCT, MAP):
+                return True
+            if f.type_id == LIST:
+                e = f.children[0]
+                return type_width(e.type_id) < 0 or deep(e)
+            return False
+        return any(deep(f) for f in self._schema.fields)
+
+    def _decode_nested(self, batch: RowBatch, validity: bool, arrow: bool,
+                       stream=None) -> List[Column]:
+        L = N.lib()
+        h = self._schema.handle
+        nn = L.fury_schema_num_nodes(h)
+        entries = (ctypes.c_int64 * max(nn, 1))()
+        nbytes = (ctypes.c_int64 * max(nn, 1))()
+        plan = ctypes.c_void_p()
+        sh = _stream_handle(stream)
+        _check(L.fury_decode_prepare(h, _ptr(batch.rows), _ptr(batch.row_offsets), batch.nrows,
+                                     entries, nbytes, ctypes.byref(plan), sh))
+        try:
+            order = _bfs(self._schema.fields)
+            cols: List[Column] = []
+            for i, (f, first) in enumerate(order):
+                cols.append(_alloc_node(f, int(entries[i]), int(nbytes[i]), validity or arrow,
+                                        self.device))
+            for i, (f, first) in enumerate(order):
+                if f.children:
+                    cols[i].child = [cols[first + j] for j in range(len(f.children))]
+            top = cols[:len(self._schema.fields)]
+            keep: list = []
+            _check(L.fury_decode_execute(plan, _c_columns(top, keep), int(arrow), sh))
+        finally:
+            L.fury_decode_plan_destroy(plan)
+        return top
+
     def _decode(self, batch: RowBatch, validity: bool, arrow: bool, stream=None,
                 out: Optional[List[Column]] = None) -> List[Column]:
+        if self.nested:
+            return self._decode_nested(batch, validity, arrow, stream)
         n = batch.nrows
         cols = out if out is not None else self.alloc_columns(n, validity)
         keep: list = []
@@ -383,6 +426,44 @@ class RowEncoder:
                 f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
                 f"hash are {self.schema_hash}/{peer}. Please check writer schema.")
         return self.from_row(data[8:])
+
+
+def _bfs(fields: Sequence[Field]):
+    """Schema nodes in the C ABI's breadth-first order: [(field, first_child_index)]."""
+    q = list(fields)
+    out = []
+    i = 0
+    while i < len(q):
+        f = q[i]
+        out.append((f, len(q)))
+        q.extend(f.children)
+        i += 1
+    return out
+
+
+def _alloc_node(f: Field, m: int, nbytes: int, validity: bool, device) -> Column:
+    """Output buffers for one schema node with m Arrow entries (validity / bool bitmaps zeroed:
+    the decode kernel only sets bits)."""
+    def zeros(k):
+        return torch.zeros(k, dtype=torch.uint8, device=device)
+
+    def empty(k, dt=torch.uint8):
+        return torch.empty(k, dtype=dt, device=device)
+    vb = zeros((m + 7) // 8 + 4) if validity else None
+    t = f.type_id
+    if t == BOOL:
+        return Column(values=zeros((m + 7) // 8 + 4), validity=vb)
+    if type_width(t) > 0:
+        return Column(values=empty(m * type_width(t) + 8), validity=vb)
+    if t in (STRING, BINARY):
+        return Column(values=empty(max(nbytes, 1)), validity=vb, offsets=empty(m + 1, torch.int32))
+    if t == DECIMAL:
+        return Column(values=empty(16 * m + 16), validity=vb)
+    if t in (LIST, MAP):
+        return Column(validity=vb, offsets=empty(m + 1, torch.int32))
+    if t == STRUCT:
+        return Column(validity=vb)
+    raise UnsupportedOperationException(f"no device decode for {f}")
 
 
 class Encoders:

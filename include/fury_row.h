@@ -113,6 +113,8 @@ typedef struct fury_schema fury_schema; /* opaque, immutable after creation, thr
  *   STRING/BINARY: offsets = n+1 int32, values = payload bytes
  *   DECIMAL     : values = n * 16 bytes (decimal128 little-endian)
  *   LIST        : offsets = n+1 int32 element offsets, child = element column (flattened)
+ *   STRUCT      : child = array of the struct's field columns (entry-aligned with the parent)
+ *   MAP         : offsets = n+1 int32 entry offsets, child = [keys column, values column]
  * validity: encode input NULL = all valid; decode output NULL = do not write validity.
  * capacity: decode output only — bytes available in `values` for STRING/BINARY payloads. */
 typedef struct fury_column {
@@ -174,6 +176,24 @@ int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* 
  * zero-length entries (ListVector fillHoles, ArrowWriter.java:539,223-225). */
 int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* columns, void* stream);
+
+/* ---- nested schemas: two-step decode --------------------------------------------------- */
+/* Schemas with STRUCT / MAP / LIST-of-variable-length fields produce a TREE of Arrow columns whose
+ * sizes depend on the data.  Nodes are the schema's fields at every level, numbered breadth-first:
+ * top-level fields 0..n-1 first, then each node's children contiguously (LIST: element; STRUCT:
+ * its fields; MAP: key, value).  fury_decode_prepare counts, for every node, the Arrow entries
+ * (node_entries) and STRING/BINARY payload bytes (node_bytes) the batch produces and returns a
+ * plan; the caller allocates every node's buffers (validity and BOOL value bitmaps ZEROED, offsets
+ * entries+1, values entries*width / node_bytes / 16*entries) and runs fury_decode_execute on
+ * the column tree (fury_column.child: LIST -> element column; STRUCT -> its field columns; MAP ->
+ * [keys, values]).  Flat schemas may use it too.  Synchronises `stream` once (prepare). */
+typedef struct fury_decode_plan fury_decode_plan;
+int32_t fury_schema_num_nodes(const fury_schema* schema);
+int fury_decode_prepare(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                        int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
+                        fury_decode_plan** plan, void* stream);
+int fury_decode_execute(fury_decode_plan* plan, fury_column* columns, int32_t arrow, void* stream);
+void fury_decode_plan_destroy(fury_decode_plan* plan);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
 /* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,

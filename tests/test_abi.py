@@ -109,11 +109,16 @@ def test_device_calls_reject_bad_arguments_without_touching_gpu():
     from fury_amd.encoder import Schema
     L = N.lib()
     assert L.fury_row_encode(None, None, 1, None, None, None) == 1
-    s = Schema(SCHEMAS["foo"])       # nested struct + map: no device kernel yet
+    s = Schema(SCHEMAS["foo"])       # nested struct + map: generic engine; rows is null
     cols = (N.FuryColumn * 5)()
-    assert L.fury_row_encode(s.handle, cols, 1, None, None, None) == 2
-    assert "nested struct" in N.last_error() or "map" in N.last_error() or \
-        "variable-length" in N.last_error()
+    assert L.fury_row_encode(s.handle, cols, 1, None, None, None) == 1
+    deep = T.field("x", T.INT32)
+    for d in range(9):               # 10 levels of nesting: beyond the generic engine
+        deep = T.struct_field(f"s{d}", [deep])
+    s3 = Schema([deep])
+    assert L.fury_row_encode(s3.handle, cols, 1, None, None, None) == 2
+    assert "nested" in N.last_error()
+    assert L.fury_schema_num_nodes(s.handle) == 5 + 1 + 2 + 2
     s2 = Schema(SCHEMAS["struct100"])
     cols2 = (N.FuryColumn * 100)()
     assert L.fury_row_encode(s2.handle, cols2, 4, None, None, None) == 1   # rows is null
