@@ -53,8 +53,12 @@ def column_to_array(f: Field, c: Column, n: int) -> pa.Array:
         m = int(np.asarray(c.offsets)[n])
         k = column_to_array(f.children[0], c.child[0], m)
         v = column_to_array(f.children[1], c.child[1], m)
-        entries = pa.StructArray.from_arrays([k, v], fields=[t.key_field, t.item_field])
-        return pa.Array.from_buffers(t, n, [vb, _buf(c.offsets)], children=[entries])
+        offs = pa.Array.from_buffers(pa.int32(), n + 1, [None, _buf(c.offsets)])
+        mask = None
+        if c.validity is not None:
+            valid = np.unpackbits(np.asarray(c.validity).view(np.uint8), bitorder="little")[:n]
+            mask = pa.array(valid == 0)
+        return pa.MapArray.from_arrays(offs, k, v, type=t, mask=mask)
     return pa.Array.from_buffers(t, n, [vb, _buf(c.values)])
 
 
