@@ -107,6 +107,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
         v.values = static_cast<const uint8_t*>(c.values);
         v.offsets = c.offsets;
         v.var_slot = nvar++;
+        v.capacity = c.values ? c.capacity : 0;
         if (nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
         break;
       case kDecimal:
@@ -126,6 +127,10 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
         } else {
           v.values = static_cast<const uint8_t*>(c.child->values);
           v.elem_validity = c.child->validity;
+          // child capacity is in bytes of values; the kernels bound element indices by it
+          v.capacity = !c.child->values ? 0
+                       : v.width == 0   ? c.child->capacity * 8
+                                        : c.child->capacity / v.width;
           if (decode && (misaligned(c.child->validity, 4) ||
                          (v.width == 0 && misaligned(c.child->values, 4))))
             return set_error(FURY_ERR_INVALID_ARGUMENT,

@@ -51,6 +51,7 @@ struct VarCol {
   int32_t width;             // fixed: 1/2/4/8, 0 = bool; list: element width (0 = bool elements)
   int32_t var_slot;          // index among var fields (decode measure scratch), -1 otherwise
   int32_t nullable;
+  int64_t capacity;          // decode: payload bytes (STRING/BINARY) / child elements (LIST)
 };
 
 struct VarArgs {
@@ -74,6 +75,8 @@ int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* row
                       hipStream_t stream);
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                           hipStream_t stream);
+// Single pass: computes the Arrow offsets itself (decoupled look-back scan across workgroups)
+// and writes payloads clipped to each column's capacity.
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                       hipStream_t stream, bool arrow);
 // ---- generic (nested) schema engine: generic.hip --------------------------------------------

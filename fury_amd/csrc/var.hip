@@ -35,7 +35,7 @@ namespace {
 constexpr int kThreads = 256;                 // = rows per workgroup
 constexpr int kEncodeStage = 48 * 1024;       // LDS pool: row image + staged sources (encode)
 constexpr int kDecodeStage = 32 * 1024;       // LDS image of the group's row range (decode)
-constexpr int kStrStage = 16 * 1024;          // LDS image of one column's Arrow output range
+constexpr int kStrStage = 8 * 1024;           // LDS image of one column's Arrow payload range
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
@@ -483,13 +483,6 @@ __global__ __launch_bounds__(kThreads) void decode_measure_fix(VarArgs a,
   }
 }
 
-__device__ __forceinline__ void put_bits_atomic(uint8_t* bits, int64_t i, bool v) {
-  uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits + (i >> 3)) & ~uintptr_t(3));
-  const int sh = static_cast<int>((reinterpret_cast<uintptr_t>(bits + (i >> 3)) & 3) * 8 + (i & 7));
-  if (v) atomicOr(w, 1u << sh);
-  else atomicAnd(w, ~(1u << sh));
-}
-
 // Byte i (0 <= i < len) of an 8-byte-aligned source, read as whole aligned words.
 __device__ __forceinline__ uint32_t src_byte(const uint8_t* src, int64_t i) {
   const uint64_t w = reinterpret_cast<const uint64_t*>(src)[i >> 3];
@@ -524,31 +517,6 @@ __device__ __forceinline__ void put_bytes(uint8_t* dst, int64_t q, const uint8_t
   for (int64_t i = 4 * w1; i < end; i++) dst[i] = static_cast<uint8_t>(src_byte(src, i - q));
 }
 
-// Writes the bit range [b, e) of `img` (LDS words aligned to global word b >> 5) into the Arrow
-// bitmap `g` (4-byte aligned): whole words by plain stores, the two boundary words (shared with
-// neighbouring workgroups) by atomic and/or of exactly this range's bits.
-__device__ __forceinline__ void flush_bits(uint32_t* g, const uint32_t* img, int64_t b, int64_t e) {
-  if (e <= b) return;
-  const int64_t wb = b >> 5, we = (e - 1) >> 5;
-  for (int64_t w = wb + threadIdx.x; w <= we; w += kThreads) {
-    uint32_t mask = ~0u;
-    if (w == wb) mask &= ~0u << (b & 31);
-    if (w == we && (e & 31)) mask &= ~0u >> (32 - (e & 31));
-    const uint32_t v = img[w - wb] & mask;
-    if (mask == ~0u) {
-      g[w] = v;
-    } else {
-      atomicAnd(&g[w], ~mask);
-      atomicOr(&g[w], v);
-    }
-  }
-}
-
-__device__ __forceinline__ void or_bits(uint32_t* img, int64_t base_word, int64_t e, bool v) {
-  if (!v) return;
-  atomicOr(&img[(e >> 5) - base_word], 1u << (e & 31));
-}
-
 template <bool kToGlobal>
 __device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, int64_t p0, int64_t p1,
                                                  int64_t a0) {
@@ -563,32 +531,148 @@ __device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, i
                                 reinterpret_cast<v4*>(g + i));
 }
 
-// Decode / row->Arrow: 256 rows per workgroup.  The group's row range is staged in LDS with 16-B
-// loads; fixed fields leave as coalesced per-column stores with ballot-built validity; each
-// string column's Arrow payload range and each list column's child values/validity range are
-// assembled in an LDS image and written out as one contiguous range.
-__global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
-                                                              const uint8_t* __restrict__ rows,
-                                                              const int64_t* __restrict__ offs) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
-  __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
+// Decode / row->Arrow, single pass: 256 rows per workgroup.  Arrow offsets of STRING/BINARY and
+// LIST fields are a scan over ALL rows, so groups chain their totals with a decoupled look-back
+// (each group publishes its aggregate, then resolves its prefix from its predecessors' published
+// words; groups take logical numbers from a ticket so every group they wait on is already
+// running).  The group's row range is staged in LDS with 16-B loads; fixed fields leave as
+// coalesced per-column stores with ballot-built validity while the look-back is in flight;
+// string payloads are assembled in an LDS image of the group's output range; list elements are
+// spread one per lane over the group's flat element range (row found by binary search over the
+// group's element starts) so child values and validity bits leave coalesced.
+constexpr int kSeqChunk = 8;                          // var outputs resolved per look-back round
+constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t wave_sum(int64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// One wave: exclusive prefix of logical group b in sequence q.  Status words pack a 2-bit flag
+// (0 = not yet published, kAgg = group total, kInc = inclusive prefix) over a 62-bit value.
+__device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q) {
   const int lane = threadIdx.x & 63;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
-  const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
-  const int64_t rbeg = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - rbeg;
-  const int64_t r = r0 + threadIdx.x;
-  const bool live = r < a.nrows;
-  const bool staged = bytes <= kDecodeStage;
-  if (staged) {
-    copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
-    __syncthreads();
+  int64_t excl = 0;
+  for (int64_t j = b - 1;; j -= 64) {
+    const int64_t idx = j - lane;
+    uint64_t v;
+    for (;;) {
+      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
+      if (__ballot((v >> 62) == 0) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t inc = __ballot((v >> 62) == 2);
+    const int stop = inc ? __builtin_ctzll(inc) : 63;
+    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
+    if (inc) return excl;
   }
-  const uint8_t* row = live ? (staged ? stage + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
+}
+
+// Last t in [0, nr) with pos[t] <= idx: the row holding element idx (empty rows share their
+// successor's start and are skipped).
+__device__ __forceinline__ int find_row(const int32_t* pos, int nr, int32_t idx) {
+  int lo = 0, hi = nr;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (pos[mid] <= idx) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// 64 bits of an Arrow bitmap starting at 64-aligned bit gbit0: bits in `mask` get `val`.
+// Words wholly owned by this group are stored; words shared with a neighbouring group are
+// updated with atomic and/or of exactly these bits.
+__device__ __forceinline__ void put_bits64(uint8_t* bits, int64_t gbit0, uint64_t val,
+                                           uint64_t mask, int64_t cap) {
+  if (gbit0 + 64 > cap) mask &= cap <= gbit0 ? 0 : (~0ull >> (64 - (cap - gbit0)));
+  const int lane = threadIdx.x & 63;
+  if (lane < 2) {
+    const uint32_t m = static_cast<uint32_t>(mask >> (32 * lane));
+    const uint32_t v = static_cast<uint32_t>(val >> (32 * lane)) & m;
+    uint32_t* w = reinterpret_cast<uint32_t*>(bits) + (gbit0 >> 5) + lane;
+    if (m == ~0u) {
+      *w = v;
+    } else if (m) {
+      atomicAnd(w, ~m);
+      atomicOr(w, v);
+    }
+  }
+}
+
+struct DecodeShared {
+  int32_t pos[kSeqChunk][kThreads + 1];   // group-relative exclusive starts; [nr] = group total
+  int64_t rowoff[kThreads];                // row start relative to the group's first row
+  int64_t base[kSeqChunk];                 // global start of the group's range, per sequence
+  int64_t tmp[kThreads / 64];
+  int64_t blk;
+};
+
+__device__ __forceinline__ bool is_seq(const VarCol& c) {
+  return c.kind == kBytes || c.kind == kListFixed;
+}
+
+// Counts + in-group scans of the sequences [cbase, cbase + nchunk); publishes the aggregates.
+__device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row, DecodeShared& sh,
+                                            int cbase, int nchunk, int64_t b, uint64_t* status,
+                                            int nseq) {
+  int seq = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (!is_seq(c)) continue;
+    const int q = seq++ - cbase;
+    if (q < 0) continue;
+    if (q >= nchunk) break;
+    const int64_t cnt = row ? var_count(a, c, k, row) : 0;
+    int64_t tot;
+    const int64_t ex = block_excl_scan(cnt, &tot, sh.tmp);
+    sh.pos[q][threadIdx.x] = static_cast<int32_t>(ex);
+    if (threadIdx.x == 0) {
+      sh.pos[q][kThreads] = static_cast<int32_t>(tot);
+      st_status(status + b * nseq + cbase + q, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot));
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void chunk_resolve(DecodeShared& sh, int cbase, int nchunk, int64_t b,
+                                              uint64_t* status, int nseq) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int q = w; q < nchunk; q += kThreads / 64) {
+    const int64_t ex = b == 0 ? 0 : look_back(status, b, nseq, cbase + q);
+    if (lane == 0) {
+      sh.base[q] = ex;
+      if (b > 0)
+        st_status(status + b * nseq + cbase + q,
+                  kInc | static_cast<uint64_t>(ex + sh.pos[q][kThreads]));
+    }
+  }
+  __syncthreads();
+}
+
+template <bool kStaged>
+__device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* src, uint8_t* oimg,
+                                             DecodeShared& sh, int64_t b, int64_t nb, int nr,
+                                             uint64_t* status, int nseq) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t r0 = b * kThreads;
+  const int64_t r = r0 + tid;
+  const bool live = tid < nr;
+  const uint8_t* row = live ? src + sh.rowoff[tid] : nullptr;
   const int64_t rbase = r - lane;                               // this wave's first row
   const int64_t nvalid = a.nrows - rbase;
   const int nbytes = nvalid >= 64 ? 8 : static_cast<int>((nvalid + 7) >> 3);
 
+  if (nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
+
+  // fixed-width fields and every field's validity: no dependency on other groups
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
     const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
@@ -598,121 +682,91 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
       const uint64_t ok = __ballot(live && !isnull);
       if (lane < nbytes) c.validity[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));
     }
-    switch (c.kind) {
-      case kFixed: {
-        uint8_t* dst = const_cast<uint8_t*>(c.values);
-        if (live) {
-          switch (c.width) {
-            case 8: __builtin_nontemporal_store(slot, reinterpret_cast<uint64_t*>(dst) + r); break;
-            case 4: reinterpret_cast<uint32_t*>(dst)[r] = static_cast<uint32_t>(slot); break;
-            case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(slot); break;
-            default: dst[r] = static_cast<uint8_t>(slot); break;
-          }
+    uint8_t* dst = const_cast<uint8_t*>(c.values);
+    if (c.kind == kFixed) {
+      if (live && dst) {
+        switch (c.width) {
+          case 8: __builtin_nontemporal_store(slot, reinterpret_cast<uint64_t*>(dst) + r); break;
+          case 4: reinterpret_cast<uint32_t*>(dst)[r] = static_cast<uint32_t>(slot); break;
+          case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(slot); break;
+          default: dst[r] = static_cast<uint8_t>(slot); break;
         }
-        break;
       }
-      case kBool: {
-        const uint64_t b = __ballot(live && (slot & 0xff) != 0);
-        uint8_t* dst = const_cast<uint8_t*>(c.values);
-        if (lane < nbytes) dst[(rbase >> 3) + lane] = static_cast<uint8_t>(b >> (8 * lane));
-        break;
-      }
-      case kDecimal: {
-        if (live) {
-          uint64_t* dst = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(c.values) + 16 * r);
-          if (isnull) {
-            dst[0] = 0;
-            dst[1] = 0;
-          } else {
-            const uint8_t* s = row + static_cast<int32_t>(slot >> 32);
-            dst[0] = reinterpret_cast<const uint64_t*>(s)[0];
-            dst[1] = reinterpret_cast<const uint64_t*>(s)[1];
-          }
+    } else if (c.kind == kBool) {
+      const uint64_t bits = __ballot(live && (slot & 0xff) != 0);
+      if (lane < nbytes && dst) dst[(rbase >> 3) + lane] = static_cast<uint8_t>(bits >> (8 * lane));
+    } else if (c.kind == kDecimal) {
+      if (live && dst) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(dst + 16 * r);
+        uint64_t lo = 0, hi = 0;
+        if (!isnull) {
+          const uint8_t* s = row + static_cast<int32_t>(slot >> 32);
+          lo = reinterpret_cast<const uint64_t*>(s)[0];
+          hi = reinterpret_cast<const uint64_t*>(s)[1];
         }
-        break;
+        d[0] = lo;
+        d[1] = hi;
       }
-      case kBytes: {
-        // Arrow payload range of this group for column k: [p0, p1) of c.values.
-        uint8_t* gdst = const_cast<uint8_t*>(c.values);
-        if (!gdst) break;
-        const int64_t p0 = c.offsets[r0];
-        const int64_t p1 = c.offsets[r0 + nr];
+    }
+  }
+
+  for (int cbase = 0; cbase < nseq; cbase += kSeqChunk) {
+    const int nchunk = min(kSeqChunk, nseq - cbase);
+    if (cbase > 0) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
+    chunk_resolve(sh, cbase, nchunk, b, status, nseq);
+    int seq = 0;
+    for (int k = 0; k < a.ncols; k++) {
+      const VarCol& c = a.col[k];
+      if (!is_seq(c)) continue;
+      const int q = seq++ - cbase;
+      if (q < 0) continue;
+      if (q >= nchunk) break;
+      const int64_t gb = sh.base[q];
+      const int32_t tot = sh.pos[q][kThreads];
+      if (live) c.offsets[r] = static_cast<int32_t>(gb + sh.pos[q][tid]);
+      if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot);
+      uint8_t* dst = const_cast<uint8_t*>(c.values);
+      if (tot == 0 || !dst) continue;
+      const int64_t cap = c.capacity;
+      if (c.kind == kBytes) {
+        const int64_t p0 = gb, p1 = gb + tot;
+        const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
+        const uint64_t slot =
+            (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
         const int64_t len = (live && !isnull) ? static_cast<uint32_t>(slot) : 0;
-        const uint8_t* src = row ? row + static_cast<int32_t>(slot >> 32) : nullptr;
-        const int64_t pos = live ? c.offsets[r] : 0;
+        const uint8_t* s = live ? row + static_cast<int32_t>(slot >> 32) : nullptr;
+        const int64_t pos = p0 + sh.pos[q][tid];
         // LDS byte i <-> global byte a0 + i, a0 = 16-aligned address of payload byte p0
-        const int64_t a0 = p0 - static_cast<int64_t>(reinterpret_cast<uintptr_t>(gdst + p0) & 15);
+        const int64_t a0 = p0 - static_cast<int64_t>(reinterpret_cast<uintptr_t>(dst + p0) & 15);
         if (p1 - a0 <= kStrStage) {
-          put_bytes(oimg, pos - a0, src, len);
+          put_bytes(oimg, pos - a0, s, len);
           __syncthreads();
-          copy_bytes_range<true>(gdst, oimg, p0, p1, a0);
+          if (cap > p0) copy_bytes_range<true>(dst, oimg, p0, min<int64_t>(p1, cap), a0);
           __syncthreads();
         } else {
-          put_bytes(gdst, pos, src, len);
+          put_bytes(dst, pos, s, max<int64_t>(0, min<int64_t>(len, cap - pos)));
         }
-        break;
+        continue;
       }
-      default: {   // kListFixed -> Arrow list child (values + element validity)
-        uint8_t* dst = const_cast<uint8_t*>(c.values);
-        const int ew = c.width == 0 ? 1 : c.width;
-        const int64_t e_b = c.offsets[r0], e_e = c.offsets[r0 + nr];
-        const uint8_t* arr = (live && !isnull) ? row + static_cast<int32_t>(slot >> 32) : nullptr;
-        const int64_t n = arr ? static_cast<int32_t>(*reinterpret_cast<const int64_t*>(arr)) : 0;
-        const int64_t hb = 8 + bm_bytes(n);
-        const int64_t e0 = live ? c.offsets[r] : 0;
-        // images: element values (bytes; bool elements as bits) and element validity bits
-        const int64_t vwb = e_b >> 5;                              // first global bit word
-        const int64_t nvw = e_e > e_b ? ((e_e - 1) >> 5) - vwb + 1 : 0;
-        const bool bits_vals = c.width == 0;
-        int64_t a0 = 0, vbytes = 0;
-        if (!bits_vals) {
-          a0 = e_b * ew - static_cast<int64_t>(reinterpret_cast<uintptr_t>(dst + e_b * ew) & 15);
-          vbytes = e_e * ew - a0;
-        }
-        const int64_t need = (bits_vals ? 4 * nvw : ((vbytes + 15) & ~int64_t(15))) +
-                             (c.elem_validity ? 4 * nvw : 0);
-        if (need <= kStrStage && dst) {
-          uint32_t* vimg = reinterpret_cast<uint32_t*>(
-              oimg + (bits_vals ? 0 : ((vbytes + 15) & ~int64_t(15))));
-          uint32_t* bimg = reinterpret_cast<uint32_t*>(oimg);    // bool element values
-          if (bits_vals)
-            vimg = reinterpret_cast<uint32_t*>(oimg + 4 * nvw);
-          const int64_t zero_words = bits_vals ? 2 * nvw : (c.elem_validity ? nvw : 0);
-          uint32_t* zbase = bits_vals ? bimg : vimg;
-          for (int64_t i = threadIdx.x; i < zero_words; i += kThreads) zbase[i] = 0;
-          __syncthreads();
-          for (int64_t j = 0; j < n; j++) {
-            const bool enull = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
-            const int64_t e = e0 + j;
-            if (c.elem_validity) or_bits(vimg, vwb, e, !enull);
-            const uint8_t* p = arr + hb + j * ew;
-            if (bits_vals) {
-              or_bits(bimg, vwb, e, !enull && *p != 0);
-              continue;
-            }
-            uint8_t* q = oimg + (e * ew - a0);
-            switch (ew) {
-              case 8: *reinterpret_cast<uint64_t*>(q) = enull ? 0 : *reinterpret_cast<const uint64_t*>(p); break;
-              case 4: *reinterpret_cast<uint32_t*>(q) = enull ? 0 : *reinterpret_cast<const uint32_t*>(p); break;
-              case 2: *reinterpret_cast<uint16_t*>(q) = enull ? 0 : *reinterpret_cast<const uint16_t*>(p); break;
-              default: *q = enull ? 0 : *p; break;
-            }
-          }
-          __syncthreads();
-          if (bits_vals) flush_bits(reinterpret_cast<uint32_t*>(dst), bimg, e_b, e_e);
-          else copy_bytes_range<true>(dst, oimg, e_b * ew, e_e * ew, a0);
-          if (c.elem_validity)
-            flush_bits(reinterpret_cast<uint32_t*>(c.elem_validity), vimg, e_b, e_e);
-          __syncthreads();
-          break;
-        }
-        if (!arr || !dst) break;
-        for (int64_t j = 0; j < n; j++) {                          // oversized: direct path
-          const bool enull = (arr[8 + (j >> 3)] >> (j & 7)) & 1;
-          if (c.elem_validity) put_bits_atomic(c.elem_validity, e0 + j, !enull);
-          uint64_t v = 0;
-          if (!enull) {
-            const uint8_t* p = arr + hb + j * ew;
+      // LIST of fixed-width elements -> Arrow child values + element validity
+      const int ew = c.width == 0 ? 1 : c.width;
+      const int sh0 = static_cast<int>(gb & 63);
+      const int64_t span = sh0 + tot;
+      for (int64_t u0 = 0; u0 < span; u0 += kThreads) {
+        const int64_t i = u0 + tid - sh0;                       // element index in the group
+        const bool act = i >= 0 && i < tot;
+        bool valid = false;
+        uint64_t v = 0;
+        if (act) {
+          const int t = find_row(sh.pos[q], nr, static_cast<int32_t>(i));
+          const uint8_t* rw = src + sh.rowoff[t];
+          const uint64_t sl = *reinterpret_cast<const uint64_t*>(rw + a.bitmap_bytes + 8 * k);
+          const uint8_t* arr = rw + static_cast<int32_t>(sl >> 32);
+          const int64_t n = *reinterpret_cast<const int64_t*>(arr);
+          const int64_t j = i - sh.pos[q][t];
+          valid = !((arr[8 + (j >> 3)] >> (j & 7)) & 1);
+          if (valid) {
+            const uint8_t* p = arr + 8 + bm_bytes(n) + j * ew;
             switch (ew) {
               case 8: v = *reinterpret_cast<const uint64_t*>(p); break;
               case 4: v = *reinterpret_cast<const uint32_t*>(p); break;
@@ -720,18 +774,50 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
               default: v = *p; break;
             }
           }
-          const int64_t e = e0 + j;
-          switch (c.width) {
-            case 8: reinterpret_cast<uint64_t*>(dst)[e] = v; break;
-            case 4: reinterpret_cast<uint32_t*>(dst)[e] = static_cast<uint32_t>(v); break;
-            case 2: reinterpret_cast<uint16_t*>(dst)[e] = static_cast<uint16_t>(v); break;
-            case 1: dst[e] = static_cast<uint8_t>(v); break;
-            default: put_bits_atomic(dst, e, v != 0); break;   // bool elements, bit-packed
+          const int64_t e = gb + i;
+          if (e < cap) {
+            switch (c.width) {
+              case 8: __builtin_nontemporal_store(v, reinterpret_cast<uint64_t*>(dst) + e); break;
+              case 4: reinterpret_cast<uint32_t*>(dst)[e] = static_cast<uint32_t>(v); break;
+              case 2: reinterpret_cast<uint16_t*>(dst)[e] = static_cast<uint16_t>(v); break;
+              case 1: dst[e] = static_cast<uint8_t>(v); break;
+              default: break;                                 // bool elements: bits below
+            }
           }
         }
-        break;
+        const uint64_t am = __ballot(act);
+        const int64_t gbit0 = gb - sh0 + (u0 + tid - lane);     // 64-aligned
+        if (c.elem_validity) put_bits64(c.elem_validity, gbit0, __ballot(act && valid), am, cap);
+        if (c.width == 0) put_bits64(dst, gbit0, __ballot(act && valid && v != 0), am, cap);
       }
     }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
+                                                              const uint8_t* __restrict__ rows,
+                                                              const int64_t* __restrict__ offs,
+                                                              uint64_t* __restrict__ status,
+                                                              uint32_t* __restrict__ ticket,
+                                                              int nseq) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
+  __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
+  __shared__ DecodeShared sh;
+  if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t b = sh.blk;
+  const int64_t r0 = b * kThreads;
+  const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
+  const int64_t rbeg = offs[r0];
+  const int64_t bytes = offs[r0 + nr] - rbeg;
+  if (threadIdx.x < nr) sh.rowoff[threadIdx.x] = offs[r0 + threadIdx.x] - rbeg;
+  if (bytes <= kDecodeStage) {
+    copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
+    __syncthreads();
+    decode_group<true>(a, stage, oimg, sh, b, gridDim.x, nr, status, nseq);
+  } else {
+    __syncthreads();
+    decode_group<false>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
   }
 }
 
@@ -876,9 +962,23 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
                       hipStream_t stream, bool arrow) {
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
   if (a.nrows == 0) return FURY_OK;
-  hipLaunchKernelGGL(decode_var_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a, rows,
-                     offs);
-  return check_hip(hipGetLastError(), "decode_var launch");
+  int nseq = 0;
+  for (int k = 0; k < a.ncols; k++)
+    if (a.col[k].kind == kBytes || a.col[k].kind == kListFixed) nseq++;
+  const int64_t nb = nblocks(a.nrows);
+  // look-back status words (nb x nseq) + the group ticket, zeroed per launch
+  const size_t wsb = (nb * nseq + 1) * 8;
+  uint64_t* ws = nullptr;
+  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
+  if (st) return st;
+  st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+  if (!st) {
+    hipLaunchKernelGGL(decode_var_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
+                       ws + 1, reinterpret_cast<uint32_t*>(ws), nseq);
+    st = check_hip(hipGetLastError(), "decode_var launch");
+  }
+  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
+  return st ? st : st2;
 }
 
 int launch_frame_rows(const uint8_t* rows, const int64_t* offs, int64_t n, int64_t fixed,

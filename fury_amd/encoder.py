@@ -349,18 +349,34 @@ class RowEncoder:
 
     def decode_into(self, batch: RowBatch, cols: List[Column], stream=None,
                     arrow: bool = False) -> None:
-        """Decode into preallocated columns (variable-length buffers must already be large
-        enough, e.g. from a previous decode of the same batch shape): no host synchronisation,
-        so the call can be captured/timed back to back."""
+        """Decode into preallocated columns in one device pass (the kernel computes the Arrow
+        offsets itself): no host synchronisation, so the call can be captured/timed back to
+        back.  Payloads past a buffer's capacity are not written; ``offsets[nrows]`` always holds
+        the size the column needs (see ``check_capacity``)."""
         keep: list = []
         sh = _stream_handle(stream)
-        if not self._schema.is_fixed:
-            _check(N.lib().fury_row_decode_measure(self._schema.handle, _ptr(batch.rows),
-                                                   _ptr(batch.row_offsets), batch.nrows,
-                                                   _c_columns(cols, keep), sh))
         fn = N.lib().fury_rows_to_arrow if arrow else N.lib().fury_row_decode
         _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), batch.nrows,
                   _c_columns(cols, keep), sh))
+
+    def check_capacity(self, cols: List[Column], nrows: int) -> None:
+        """Raises CapacityError when a decode into preallocated ``cols`` needed more payload
+        (STRING/BINARY bytes, LIST child elements) than the buffers hold (synchronises)."""
+        if self._schema.is_fixed or self.nested or nrows == 0:
+            return
+        for f, c in zip(self._schema.fields, cols):
+            if f.type_id not in (STRING, BINARY, LIST) or c.offsets is None:
+                continue
+            need = int(c.offsets[nrows].item())
+            if f.type_id == LIST:
+                e = f.children[0]
+                v = c.child[0].values if c.child else None
+                have = 0 if v is None else v.numel() * v.element_size()
+                have = have * 8 if e.type_id == BOOL else have // type_width(e.type_id)
+            else:
+                have = 0 if c.values is None else c.values.numel() * c.values.element_size()
+            if need > have:
+                raise CapacityError(f"column {f.name}: decode needs {need}, buffer holds {have}")
 
     def decode_batch(self, batch: RowBatch, validity: bool = True, stream=None,
                      out: Optional[List[Column]] = None) -> List[Column]:

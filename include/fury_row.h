@@ -116,7 +116,10 @@ typedef struct fury_schema fury_schema; /* opaque, immutable after creation, thr
  *   STRUCT      : child = array of the struct's field columns (entry-aligned with the parent)
  *   MAP         : offsets = n+1 int32 entry offsets, child = [keys column, values column]
  * validity: encode input NULL = all valid; decode output NULL = do not write validity.
- * capacity: decode output only — bytes available in `values` for STRING/BINARY payloads. */
+ * capacity: decode output only — bytes available in `values` (STRING/BINARY payload; for a LIST,
+ *   the child column's capacity bounds its element values).  Decode never writes past it.
+ * Decode output bitmaps (validity, BOOL values) are written as 32-bit words: 4-byte aligned,
+ *   padded to a multiple of 4 bytes. */
 typedef struct fury_column {
   void* values;
   uint8_t* validity;
@@ -168,7 +171,10 @@ int fury_row_decode_measure(const fury_schema* schema, const void* rows,
                             const int64_t* row_offsets, int64_t nrows, fury_column* columns,
                             void* stream);
 /* Decode rows into columns (RowEncoder.fromRow semantics: a null field leaves 0 bytes and,
- * when validity != NULL, a cleared validity bit). */
+ * when validity != NULL, a cleared validity bit).  One device pass: the STRING/BINARY/LIST
+ * offsets are computed here (fury_row_decode_measure is only needed to size the buffers); when
+ * offsets[nrows] exceeds a column's capacity the payload past the capacity is not written —
+ * grow the buffer and decode again. */
 int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, fury_column* columns, void* stream);
 /* ArrowWriter.write(row) for every row + finishAsRecordBatch: as fury_row_decode but every

@@ -334,3 +334,64 @@ def test_nested_rows_to_arrow(dev):
     for k, f in enumerate(fields):
         ref = pa.array([bb[f.name] for bb in beans], type=pa_type(f))
         assert rb.column(k).equals(ref), f.name
+
+
+# ---- single-pass decode (look-back scan of the Arrow offsets) --------------------------------
+def test_many_var_columns_multi_chunk(oracle, dev):
+    """13 STRING/LIST outputs: more than one look-back round per workgroup."""
+    fields = ([T.field(f"s{i:02d}", T.STRING) for i in range(10)] +
+              [T.array_field("la", T.INT64), T.array_field("lb", T.BOOL),
+               T.array_field("lc", T.INT16, elem_nullable=False), T.field("x", T.INT32)])
+    _roundtrip(oracle, None, 5000, dev, fields=fields,
+               cols=gen_columns("many", fields, 5000, seed=21, null_pct=10, str_max=24,
+                                list_max=9, elem_null_pct=10))
+
+
+@pytest.mark.parametrize("name,n", [("mixed", 70_000), ("nested", 70_000), ("narrow", 20_000)])
+def test_decode_into_scrubbed_buffers(oracle, dev, name, n):
+    """decode_into over reused buffers holding garbage (offsets included) == oracle fromRow."""
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=5)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(_dev_cols(host, dev), n)
+    out = enc.decode_batch(batch)
+
+    def scrub(c):
+        for t in (c.values, c.offsets, c.validity):
+            if t is not None:
+                t.view(torch.uint8).fill_(0x5A)
+        for x in c.child or []:
+            scrub(x)
+    for c in out:
+        scrub(c)
+    enc.decode_into(batch, out)
+    enc.check_capacity(out, n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert_columns_equal(fields, [column_to_host(c) for c in out],
+                         oracle.decode(fields, want, want_offs, n), n)
+
+
+def test_decode_respects_capacity(dev):
+    """Undersized payload buffers: nothing is written past them, offsets still complete."""
+    from fury_amd.encoder import CapacityError, Encoders
+    fields = [T.field("s", T.STRING), T.array_field("l", T.INT64)]
+    n = 3000
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(_dev_cols(gen_columns("cap", fields, n, seed=9, null_pct=5), dev), n)
+    ref = enc.decode_batch(batch)
+    ns = int(ref[0].offsets[n]); nl = int(ref[1].offsets[n])
+    sbuf = torch.full((ns + 4096,), 0xAB, dtype=torch.uint8, device=dev)
+    lbuf = torch.full((nl * 8 + 4096,), 0xCD, dtype=torch.uint8, device=dev)
+    out = enc.decode_batch(batch)
+    out[0].values = sbuf[: ns // 2]
+    out[1].child[0].values = lbuf[: (nl // 3) * 8]
+    enc.decode_into(batch, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0].offsets, ref[0].offsets) and torch.equal(out[1].offsets, ref[1].offsets)
+    assert torch.equal(sbuf[: ns // 2], ref[0].values[: ns // 2])
+    assert bool((sbuf[ns // 2:] == 0xAB).all())
+    assert torch.equal(lbuf[: (nl // 3) * 8], ref[1].child[0].values[: (nl // 3) * 8])
+    assert bool((lbuf[(nl // 3) * 8:] == 0xCD).all())
+    with pytest.raises(CapacityError):
+        enc.check_capacity(out, n)
