@@ -144,9 +144,10 @@ def main():
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        if offs is not None:       # variable-length rows: sizes + scan are part of encode
-            enc.measure_into(cols, n, offs, stream=stream)
-        enc.encode_into(cols, n, batch.rows, batch.row_offsets, stream=stream)
+        if offs is not None:       # variable-length rows: one pass computes sizes + rows
+            enc.encode_measured_into(cols, n, batch.rows, offs, stream=stream)
+        else:
+            enc.encode_into(cols, n, batch.rows, None, stream=stream)
         if ev is not None:
             ev[1].record(stream)
         if out_cols is not None:
@@ -178,6 +179,8 @@ def main():
         for c, d in zip(cols[:4], out_cols[:4]):
             assert torch.equal(c.values.view(torch.uint8), d.values), "decode mismatch"
     else:
+        assert int(offs[n].item()) == total_row_bytes, "row buffer overflow"
+        enc.check_capacity(var_out, n)
         for c, d in zip(cols, var_out):
             if c.offsets is not None and c.child is None:
                 assert torch.equal(c.offsets, d.offsets), "decode offsets mismatch"

@@ -59,6 +59,8 @@ SIGNATURES = {
     "fury_schema_get_info": (ctypes.c_int, [_P, ctypes.POINTER(FurySchemaInfo)]),
     "fury_row_measure": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _P]),
     "fury_row_encode": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _P, _P]),
+    "fury_row_encode_measured": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _P, _I64,
+                                                _P]),
     "fury_row_decode_measure": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(FuryColumn),
                                                _P]),
     "fury_row_decode": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(FuryColumn), _P]),

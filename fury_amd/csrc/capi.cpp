@@ -266,12 +266,46 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
     GenArgs g;
     st = gen_args(s, cols, nrows, false, false, &g);
     if (st) return st;
-    return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), hs);
+    return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), INT64_MAX, hs);
   }
   VarArgs a;
   st = var_args(s, cols, nrows, false, false, &a);
   if (st) return st;
   return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), hs);
+}
+
+int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int64_t nrows,
+                             int64_t* row_offsets, void* rows, int64_t capacity, void* stream) {
+  int st = common_checks(s, cols, nrows, "fury_row_encode_measured");
+  if (st) return st;
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (capacity < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "capacity < 0");
+  if (nrows > 0 && !rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
+  if (misaligned(rows, 16)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 16-byte aligned");
+  if (s->is_fixed) {
+    if (nrows > 0 && nrows > capacity / s->fixed_size)
+      return set_error(FURY_ERR_CAPACITY, "rows need " + std::to_string(nrows * s->fixed_size) +
+                                              " bytes, capacity is " + std::to_string(capacity));
+    if (row_offsets) {
+      st = fury_row_measure(s, cols, nrows, row_offsets, stream);
+      if (st) return st;
+    }
+    return fury_row_encode(s, cols, nrows, nullptr, rows, stream);
+  }
+  if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
+  if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
+  if (s->generic) {
+    st = gen_measure(s, cols, nrows, row_offsets, hs);
+    if (st || nrows == 0) return st;
+    GenArgs g;
+    st = gen_args(s, cols, nrows, false, false, &g);
+    if (st) return st;
+    return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
+  }
+  VarArgs a;
+  st = var_args(s, cols, nrows, false, false, &a);
+  if (st) return st;
+  return launch_encode_var_measured(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
 }
 
 int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_t* row_offsets,

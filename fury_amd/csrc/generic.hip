@@ -225,11 +225,12 @@ __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int
 
 __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
-                                                                 uint8_t* __restrict__ rows) {
+                                                                 uint8_t* __restrict__ rows,
+                                                                 int64_t cap) {
   __shared__ GenNode sn[kGenMaxNodes];
   const GenNode* nodes = stage_nodes(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows) put_row<true>(nodes, g.ntop, r, rows + offs[r]);
+  if (r < g.nrows && offs[r + 1] <= cap) put_row<true>(nodes, g.ntop, r, rows + offs[r]);
 }
 
 // ---- decode ----------------------------------------------------------------------------------
@@ -423,9 +424,11 @@ int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
   return check_hip(hipGetLastError(), "gen_measure launch");
 }
 
-int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
+                      hipStream_t stream) {
   const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  hipLaunchKernelGGL(gen_encode_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, offs, rows);
+  hipLaunchKernelGGL(gen_encode_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, offs, rows,
+                     cap);
   return check_hip(hipGetLastError(), "gen_encode launch");
 }
 

@@ -73,6 +73,10 @@ int workspace_reserve(size_t bytes, void** out);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows,
                       hipStream_t stream);
+// Measure + encode in one pass (row sizes chained across workgroups by a decoupled look-back);
+// writes row_offsets[0..nrows], never writes row bytes at or past `cap`.
+int launch_encode_var_measured(const VarArgs& a, int64_t* row_offsets, uint8_t* rows, int64_t cap,
+                               hipStream_t stream);
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                           hipStream_t stream);
 // Single pass: computes the Arrow offsets itself (decoupled look-back scan across workgroups)
@@ -102,7 +106,8 @@ struct GenArgs {
 };
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
-int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, hipStream_t stream);
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
+                      hipStream_t stream);
 int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
                      hipStream_t stream);
 int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,

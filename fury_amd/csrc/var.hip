@@ -22,6 +22,7 @@
 // ranges larger than the LDS budget fall back to direct 8-byte global accesses.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <cstring>
 #include <string>
 
@@ -339,84 +340,163 @@ __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict
   if (r == n - 1) offs[n] = *total;
 }
 
-// Plans the LDS staging of one workgroup's source ranges (uniform across the group; computed by
-// thread 0).  Returns the staged byte total after the row image (`base`).
-__device__ uint32_t plan_sources(const VarArgs& a, int64_t r0, int64_t nr, uint32_t base,
-                                 StagePlan& sp) {
-  uint32_t at = base;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    sp.len[2 * k] = sp.len[2 * k + 1] = 0;
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
-    if (e <= b) continue;
-    uint64_t lo, hi;
-    if (c.kind == kBytes) {
-      lo = reinterpret_cast<uint64_t>(c.values + b);
-      hi = reinterpret_cast<uint64_t>(c.values + e);
-    } else if (c.width == 0) {
-      lo = reinterpret_cast<uint64_t>(c.values + (b >> 3));
-      hi = reinterpret_cast<uint64_t>(c.values + ((e + 7) >> 3));
-    } else {
-      lo = reinterpret_cast<uint64_t>(c.values + b * c.width);
-      hi = reinterpret_cast<uint64_t>(c.values + e * c.width);
-    }
-    lo &= ~uint64_t(15);
-    hi = (hi + 15) & ~uint64_t(15);
-    sp.glo[2 * k] = lo;
-    sp.lds[2 * k] = at;
-    sp.len[2 * k] = static_cast<uint32_t>(min<uint64_t>(hi - lo, 0xffffffffull));
-    at += sp.len[2 * k];
-    if (c.kind == kListFixed && c.elem_validity) {
-      lo = reinterpret_cast<uint64_t>(c.elem_validity + (b >> 3)) & ~uint64_t(15);
-      hi = (reinterpret_cast<uint64_t>(c.elem_validity + ((e + 7) >> 3)) + 15) & ~uint64_t(15);
-      sp.glo[2 * k + 1] = lo;
-      sp.lds[2 * k + 1] = at;
-      sp.len[2 * k + 1] = static_cast<uint32_t>(hi - lo);
-      at += sp.len[2 * k + 1];
-    }
-  }
-  return at;
+// --- cross-workgroup scan (decoupled look-back) ---------------------------------------------
+constexpr int kSeqChunk = 8;                          // var outputs resolved per look-back round
+constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t wave_sum(int64_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
 }
 
-// Encode: 256 rows per workgroup.  Mode 2 stages every source range the group reads (string
-// payloads, list values/validity: each a contiguous range) in LDS with 16-B loads and builds the
-// rows in an LDS image of the group's contiguous output range; mode 1 stages only the output
-// image; mode 0 (oversized rows) builds rows straight in HBM.
-__global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a,
-                                                              const int64_t* __restrict__ offs,
-                                                              uint8_t* __restrict__ rows) {
+// One wave: exclusive prefix of logical group b in sequence q.  Status words pack a 2-bit flag
+// (0 = not yet published, kAgg = group total, kInc = inclusive prefix) over a 62-bit value.
+__device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q) {
+  const int lane = threadIdx.x & 63;
+  int64_t excl = 0;
+  for (int64_t j = b - 1;; j -= 64) {
+    const int64_t idx = j - lane;
+    uint64_t v;
+    for (;;) {
+      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
+      if (__ballot((v >> 62) == 0) == 0) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t inc = __ballot((v >> 62) == 2);
+    const int stop = inc ? __builtin_ctzll(inc) : 63;
+    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
+    if (inc) return excl;
+  }
+}
+
+// Plans the LDS staging of column k's source ranges for rows [r0, r0 + nr) (one thread per
+// column; offsets in LDS are assigned afterwards by assign_stage).
+__device__ __forceinline__ void plan_column(const VarArgs& a, int k, int64_t r0, int64_t nr,
+                                            StagePlan& sp) {
+  const VarCol& c = a.col[k];
+  sp.len[2 * k] = sp.len[2 * k + 1] = 0;
+  if (c.kind != kBytes && c.kind != kListFixed) return;
+  const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
+  if (e <= b) return;
+  uint64_t lo, hi;
+  if (c.kind == kBytes) {
+    lo = reinterpret_cast<uint64_t>(c.values + b);
+    hi = reinterpret_cast<uint64_t>(c.values + e);
+  } else if (c.width == 0) {
+    lo = reinterpret_cast<uint64_t>(c.values + (b >> 3));
+    hi = reinterpret_cast<uint64_t>(c.values + ((e + 7) >> 3));
+  } else {
+    lo = reinterpret_cast<uint64_t>(c.values + b * c.width);
+    hi = reinterpret_cast<uint64_t>(c.values + e * c.width);
+  }
+  lo &= ~uint64_t(15);
+  hi = (hi + 15) & ~uint64_t(15);
+  sp.glo[2 * k] = lo;
+  sp.len[2 * k] = static_cast<uint32_t>(min<uint64_t>(hi - lo, 0xffffffffull));
+  if (c.kind == kListFixed && c.elem_validity) {
+    lo = reinterpret_cast<uint64_t>(c.elem_validity + (b >> 3)) & ~uint64_t(15);
+    hi = (reinterpret_cast<uint64_t>(c.elem_validity + ((e + 7) >> 3)) + 15) & ~uint64_t(15);
+    sp.glo[2 * k + 1] = lo;
+    sp.len[2 * k + 1] = static_cast<uint32_t>(hi - lo);
+  }
+}
+
+// LDS offsets of the planned regions after the row image (`base` bytes); returns the total.
+__device__ __forceinline__ uint32_t assign_stage(int ncols, uint32_t base, StagePlan& sp) {
+  uint64_t at = base;
+  for (int k = 0; k < 2 * ncols; k++) {
+    sp.lds[k] = static_cast<uint32_t>(min<uint64_t>(at, 0xffffffffull));
+    at += sp.len[k];
+  }
+  return static_cast<uint32_t>(min<uint64_t>(at, 0xffffffffull));
+}
+
+// Encode: 256 rows per workgroup = one contiguous byte range of the row buffer.
+//   kMeasure: the row sizes are computed here and chained across groups with the decoupled
+//   look-back (fury_row_encode_measured: one pass, writes row_offsets); otherwise the offsets
+//   come from fury_row_measure.
+// Mode 2 stages every source range the group reads (string payloads, list values/validity: each
+// a contiguous range) in LDS with 16-B loads and builds the rows in an LDS image of the group's
+// output range; mode 1 stages only the output image; mode 0 (oversized rows) builds rows straight
+// in HBM.  Bytes at or past `cap` are never written.
+template <bool kMeasure>
+__global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a, int64_t* __restrict__ offs,
+                                                              uint8_t* __restrict__ rows,
+                                                              int64_t cap,
+                                                              uint64_t* __restrict__ status,
+                                                              uint32_t* __restrict__ ticket) {
   __shared__ __attribute__((aligned(16))) uint8_t pool[kEncodeStage];
   __shared__ StagePlan sp;
+  __shared__ int64_t tmp[kThreads / 64];
+  __shared__ int64_t blk, gbase;
   __shared__ uint32_t need;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
+  const int tid = threadIdx.x;
+  int64_t b = blockIdx.x;
+  if (kMeasure) {
+    if (tid == 0) blk = atomicAdd(ticket, 1u);
+    __syncthreads();
+    b = blk;
+  }
+  const int64_t r0 = b * kThreads;
   const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
-  const int64_t rbeg = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - rbeg;
-  const int64_t r = r0 + threadIdx.x;
+  const int64_t r = r0 + tid;
+  const bool live = tid < nr;
+  int64_t ex, bytes;
+  if (kMeasure) {
+    ex = block_excl_scan(live ? row_size_of(a, r) : 0, &bytes, tmp);
+    if (tid == 0)
+      st_status(status + b, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(bytes));
+  } else {
+    const int64_t rb = offs[r0];
+    bytes = offs[r0 + nr] - rb;
+    ex = live ? offs[r] - rb : 0;
+    if (tid == 0) gbase = rb;
+  }
   const uint32_t img = static_cast<uint32_t>((bytes + 15) & ~int64_t(15));
-  if (bytes <= kEncodeStage && threadIdx.x == 0) need = plan_sources(a, r0, nr, img, sp);
+  const bool fits = bytes <= kEncodeStage;
+  if (fits && tid < a.ncols) plan_column(a, tid, r0, nr, sp);
   __syncthreads();
-  if (bytes <= kEncodeStage && need <= kEncodeStage) {
+  if (fits && tid == 0) need = assign_stage(a.ncols, img, sp);
+  if (kMeasure && tid < 64) {
+    const int64_t e = b == 0 ? 0 : look_back(status, b, 1, 0);
+    if (tid == 0) {
+      gbase = e;
+      if (b > 0) st_status(status + b, kInc | static_cast<uint64_t>(e + bytes));
+    }
+  }
+  __syncthreads();
+  const int64_t base = gbase;
+  if (kMeasure) {
+    if (live) offs[r] = base + ex;
+    if (r == a.nrows - 1) offs[a.nrows] = base + bytes;   // last row closes its group
+  }
+  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
+  if (fits && need <= kEncodeStage) {
     using v4 = __attribute__((ext_vector_type(4))) uint32_t;
     for (int k = 0; k < 2 * a.ncols; k++) {
       const uint32_t len = sp.len[k];
       if (!len) continue;
       const v4* g = reinterpret_cast<const v4*>(sp.glo[k]);
       v4* l = reinterpret_cast<v4*>(pool + sp.lds[k]);
-      for (uint32_t i = threadIdx.x; i < (len >> 4); i += kThreads)
-        l[i] = __builtin_nontemporal_load(g + i);
+      for (uint32_t i = tid; i < (len >> 4); i += kThreads) l[i] = __builtin_nontemporal_load(g + i);
     }
     __syncthreads();
-    if (r < a.nrows) build_row<true>(a, r, pool + (offs[r] - rbeg), pool, sp);
+    if (live) build_row<true>(a, r, pool + ex, pool, sp);
     __syncthreads();
-    copy_range<true>(rows + rbeg, pool, bytes);
-  } else if (bytes <= kEncodeStage) {
-    if (r < a.nrows) build_row<false>(a, r, pool + (offs[r] - rbeg), pool, sp);
+    copy_range<true>(rows + base, pool, room);
+  } else if (fits) {
+    if (live) build_row<false>(a, r, pool + ex, pool, sp);
     __syncthreads();
-    copy_range<true>(rows + rbeg, pool, bytes);
-  } else {
-    if (r < a.nrows) build_row<false>(a, r, rows + offs[r], pool, sp);
+    copy_range<true>(rows + base, pool, room);
+  } else if (live && ex + row_size_of(a, r) <= room) {
+    build_row<false>(a, r, rows + base + ex, pool, sp);
   }
 }
 
@@ -540,41 +620,6 @@ __device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, i
 // string payloads are assembled in an LDS image of the group's output range; list elements are
 // spread one per lane over the group's flat element range (row found by binary search over the
 // group's element starts) so child values and validity bits leave coalesced.
-constexpr int kSeqChunk = 8;                          // var outputs resolved per look-back round
-constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
-
-__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int64_t wave_sum(int64_t x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
-}
-
-// One wave: exclusive prefix of logical group b in sequence q.  Status words pack a 2-bit flag
-// (0 = not yet published, kAgg = group total, kInc = inclusive prefix) over a 62-bit value.
-__device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q) {
-  const int lane = threadIdx.x & 63;
-  int64_t excl = 0;
-  for (int64_t j = b - 1;; j -= 64) {
-    const int64_t idx = j - lane;
-    uint64_t v;
-    for (;;) {
-      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
-      if (__ballot((v >> 62) == 0) == 0) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint64_t inc = __ballot((v >> 62) == 2);
-    const int stop = inc ? __builtin_ctzll(inc) : 63;
-    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
-    if (inc) return excl;
-  }
-}
-
 // Last t in [0, nr) with pos[t] <= idx: the row holding element idx (empty rows share their
 // successor's start and are skipped).
 __device__ __forceinline__ int find_row(const int32_t* pos, int nr, int32_t idx) {
@@ -931,9 +976,27 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
 
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
-  hipLaunchKernelGGL(encode_var_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a, offs,
-                     rows);
+  hipLaunchKernelGGL(encode_var_kernel<false>, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream,
+                     a, const_cast<int64_t*>(offs), rows, INT64_MAX, nullptr, nullptr);
   return check_hip(hipGetLastError(), "encode_var launch");
+}
+
+int launch_encode_var_measured(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
+                               hipStream_t stream) {
+  if (a.nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
+  const int64_t nb = nblocks(a.nrows);
+  const size_t wsb = (nb + 1) * 8;          // status word per group + the group ticket
+  uint64_t* ws = nullptr;
+  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
+  if (st) return st;
+  st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+  if (!st) {
+    hipLaunchKernelGGL(encode_var_kernel<true>, dim3(nb), dim3(kThreads), 0, stream, a, offs, rows,
+                       cap, ws + 1, reinterpret_cast<uint32_t*>(ws));
+    st = check_hip(hipGetLastError(), "encode_var launch");
+  }
+  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
+  return st ? st : st2;
 }
 
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* offs,

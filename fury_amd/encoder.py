@@ -240,6 +240,16 @@ class RowEncoder:
         _check(N.lib().fury_row_encode(self._schema.handle, _c_columns(columns, keep), nrows,
                                        _ptr(row_offsets), _ptr(rows), _stream_handle(stream)))
 
+    def encode_measured_into(self, columns: Sequence[Column], nrows: int, rows: torch.Tensor,
+                             row_offsets: Optional[torch.Tensor], stream=None) -> None:
+        """Measure + encode in one device pass into a reused buffer (``rows`` capacity =
+        its size): writes ``row_offsets``; when ``row_offsets[nrows]`` exceeds the capacity the
+        rows did not fit (nothing past the capacity is written) — grow and call again."""
+        keep: list = []
+        _check(N.lib().fury_row_encode_measured(
+            self._schema.handle, _c_columns(columns, keep), nrows, _ptr(row_offsets), _ptr(rows),
+            rows.numel() * rows.element_size(), _stream_handle(stream)))
+
     def encode_batch(self, columns: Sequence[Column], nrows: int, stream=None) -> RowBatch:
         offs = self.measure(columns, nrows, stream)
         if offs is None:

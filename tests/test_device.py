@@ -395,3 +395,52 @@ def test_decode_respects_capacity(dev):
     assert bool((lbuf[(nl // 3) * 8:] == 0xCD).all())
     with pytest.raises(CapacityError):
         enc.check_capacity(out, n)
+
+
+# ---- single-pass encode (fury_row_encode_measured) -------------------------------------------
+@pytest.mark.parametrize("name,n", [("mixed", 1), ("mixed", 300_001), ("nested", 90_000),
+                                    ("narrow", 5000), ("foo", 700)])
+def test_encode_measured_matches_two_pass(dev, name, n):
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS[name]
+    if name == "foo":
+        from fury_amd.beans import beans_to_columns
+        cols = _dev_cols(beans_to_columns(fields, [{"f1": i, "f2": str(i) * (i % 5),
+                                                    "f3": [str(j) for j in range(i % 4)],
+                                                    "f4": [(str(i), i)], "f5": {"f1": i, "f2": None}}
+                                                   for i in range(n)]), dev)
+    else:
+        cols = _dev_cols(gen_columns(name, fields, n, seed=17), dev)
+    enc = Encoders.bean(fields, device=dev)
+    ref = enc.encode_batch(cols, n)
+    total = ref.rows.numel()
+    rows = torch.full((total + 4096,), 0xEE, dtype=torch.uint8, device=dev)
+    offs = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    enc.encode_measured_into(cols, n, rows[:total], offs)
+    torch.cuda.synchronize()
+    assert torch.equal(offs, ref.row_offsets)
+    assert torch.equal(rows[:total], ref.rows)
+    assert bool((rows[total:] == 0xEE).all())
+    # undersized buffer: offsets still complete, nothing written past the capacity
+    rows.fill_(0xEE)
+    cap = (total // 3) & ~15
+    enc.encode_measured_into(cols, n, rows[:cap], offs)
+    torch.cuda.synchronize()
+    assert torch.equal(offs, ref.row_offsets)
+    assert bool((rows[cap:] == 0xEE).all())
+    o = ref.row_offsets.cpu().numpy()
+    end = int(o[int(np.searchsorted(o, cap, side="right")) - 1])   # rows ending by cap
+    assert torch.equal(rows[:end], ref.rows[:end])
+
+
+def test_encode_measured_fixed_capacity_error(dev):
+    from fury_amd.encoder import CapacityError, Encoders
+    fields = SCHEMAS["struct100"]
+    enc = Encoders.bean(fields, device=dev)
+    cols = _dev_cols(gen_columns("struct100", fields, 100), dev)
+    rows = torch.empty(816 * 100, dtype=torch.uint8, device=dev)
+    enc.encode_measured_into(cols, 100, rows, None)
+    ref = enc.encode_batch(cols, 100)
+    assert torch.equal(rows, ref.rows)
+    with pytest.raises(CapacityError):
+        enc.encode_measured_into(cols, 100, rows[:816 * 99], None)
