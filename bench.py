@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "row-format encode+decode GB/s (device-resident), Struct-100, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+DEFAULT_ROWS = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}
 
 
 def _parse():
@@ -40,7 +41,7 @@ def _parse():
     p.add_argument("--no-e2e", action="store_true")
     a = p.parse_args()
     if a.rows is None:
-        a.rows = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}[a.workload]
+        a.rows = DEFAULT_ROWS[a.workload]
     return a
 
 

@@ -437,11 +437,17 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_fixed_variant(value);
     return FURY_OK;
   }
+  if (std::string(key) == "var_decode") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..1");
+    set_var_decode_mode(value);
+    return FURY_OK;
+  }
   return set_error(FURY_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "fixed_variant") return fixed_variant();
+  if (key && std::string(key) == "var_decode") return var_decode_mode();
   return -1;
 }
 

@@ -70,6 +70,8 @@ struct Workspace {
 };
 int workspace_reserve(size_t bytes, void** out);
 
+int var_decode_mode();
+void set_var_decode_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows,
                       hipStream_t stream);

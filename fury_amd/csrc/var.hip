@@ -681,15 +681,31 @@ __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row
     sh.pos[q][threadIdx.x] = static_cast<int32_t>(ex);
     if (threadIdx.x == 0) {
       sh.pos[q][kThreads] = static_cast<int32_t>(tot);
-      st_status(status + b * nseq + cbase + q, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot));
+      if (status)
+        st_status(status + b * nseq + cbase + q, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot));
     }
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void chunk_resolve(DecodeShared& sh, int cbase, int nchunk, int64_t b,
-                                              uint64_t* status, int nseq) {
+template <bool kLookBack>
+__device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh, int cbase,
+                                              int nchunk, int64_t b, uint64_t* status, int nseq) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (!kLookBack) {     // offsets precomputed by the sizing pass (fury_row_decode_measure)
+    if (threadIdx.x < nchunk) {
+      int seq = 0;
+      for (int k = 0; k < a.ncols; k++) {
+        if (!is_seq(a.col[k])) continue;
+        if (seq++ == cbase + static_cast<int>(threadIdx.x)) {
+          sh.base[threadIdx.x] = a.col[k].offsets[b * kThreads];
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    return;
+  }
   for (int q = w; q < nchunk; q += kThreads / 64) {
     const int64_t ex = b == 0 ? 0 : look_back(status, b, nseq, cbase + q);
     if (lane == 0) {
@@ -702,7 +718,7 @@ __device__ __forceinline__ void chunk_resolve(DecodeShared& sh, int cbase, int n
   __syncthreads();
 }
 
-template <bool kStaged>
+template <bool kStaged, bool kLookBack>
 __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* src, uint8_t* oimg,
                                              DecodeShared& sh, int64_t b, int64_t nb, int nr,
                                              uint64_t* status, int nseq) {
@@ -715,7 +731,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
   const int64_t nvalid = a.nrows - rbase;
   const int nbytes = nvalid >= 64 ? 8 : static_cast<int>((nvalid + 7) >> 3);
 
-  if (nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
+  if (kLookBack && nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
 
   // fixed-width fields and every field's validity: no dependency on other groups
   for (int k = 0; k < a.ncols; k++) {
@@ -757,8 +773,8 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
 
   for (int cbase = 0; cbase < nseq; cbase += kSeqChunk) {
     const int nchunk = min(kSeqChunk, nseq - cbase);
-    if (cbase > 0) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
-    chunk_resolve(sh, cbase, nchunk, b, status, nseq);
+    if (cbase > 0 || !kLookBack) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
+    chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq);
     int seq = 0;
     for (int k = 0; k < a.ncols; k++) {
       const VarCol& c = a.col[k];
@@ -839,6 +855,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
   }
 }
 
+template <bool kLookBack>
 __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
                                                               const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
@@ -848,9 +865,11 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
   __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
   __shared__ DecodeShared sh;
-  if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const int64_t b = sh.blk;
+  if (kLookBack) {
+    if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
+    __syncthreads();
+  }
+  const int64_t b = kLookBack ? sh.blk : blockIdx.x;
   const int64_t r0 = b * kThreads;
   const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
   const int64_t rbeg = offs[r0];
@@ -859,10 +878,10 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   if (bytes <= kDecodeStage) {
     copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
     __syncthreads();
-    decode_group<true>(a, stage, oimg, sh, b, gridDim.x, nr, status, nseq);
+    decode_group<true, kLookBack>(a, stage, oimg, sh, b, gridDim.x, nr, status, nseq);
   } else {
     __syncthreads();
-    decode_group<false>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
+    decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
   }
 }
 
@@ -932,6 +951,8 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
 
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
+int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back, 1 sizing pass + decode
+
 }  // namespace
 
 // Device exclusive scan of s[0..n) (int64) with the total written to *total; `ws` needs
@@ -973,6 +994,9 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
 }
+
+int var_decode_mode() { return g_var_decode; }
+void set_var_decode_mode(int v) { g_var_decode = v; }
 
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
@@ -1029,6 +1053,13 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   for (int k = 0; k < a.ncols; k++)
     if (a.col[k].kind == kBytes || a.col[k].kind == kListFixed) nseq++;
   const int64_t nb = nblocks(a.nrows);
+  if (g_var_decode == 1) {       // sizing pass, then the decode kernel reads those offsets
+    int st = launch_decode_measure(a, rows, offs, stream);
+    if (st) return st;
+    hipLaunchKernelGGL(decode_var_kernel<false>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
+                       nullptr, nullptr, nseq);
+    return check_hip(hipGetLastError(), "decode_var launch");
+  }
   // look-back status words (nb x nseq) + the group ticket, zeroed per launch
   const size_t wsb = (nb * nseq + 1) * 8;
   uint64_t* ws = nullptr;
@@ -1036,7 +1067,7 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   if (st) return st;
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
   if (!st) {
-    hipLaunchKernelGGL(decode_var_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
+    hipLaunchKernelGGL(decode_var_kernel<true>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
                        ws + 1, reinterpret_cast<uint32_t*>(ws), nseq);
     st = check_hip(hipGetLastError(), "decode_var launch");
   }
