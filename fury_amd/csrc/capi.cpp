@@ -148,6 +148,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     }
   }
   a->nvar = nvar;
+  a->tile_rows = encode_tile_rows(*a);
   return FURY_OK;
 }
 

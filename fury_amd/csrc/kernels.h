@@ -61,6 +61,8 @@ struct VarArgs {
   int32_t fixed_size;
   int32_t nvar;
   int64_t nrows;
+  int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
+  int32_t pad_;
 };
 
 // Device scratch for scans; grown on demand (hipMalloc outside graph capture only).
@@ -70,6 +72,8 @@ struct Workspace {
 };
 int workspace_reserve(size_t bytes, void** out);
 
+// Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
+int encode_tile_rows(const VarArgs& a);
 int var_decode_mode();
 void set_var_decode_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);

@@ -34,7 +34,6 @@ namespace fury {
 namespace {
 
 constexpr int kThreads = 256;                 // = rows per workgroup
-constexpr int kEncodeStage = 48 * 1024;       // LDS pool: row image + staged sources (encode)
 constexpr int kDecodeStage = 32 * 1024;       // LDS image of the group's row range (decode)
 constexpr int kStrStage = 8 * 1024;           // LDS image of one column's Arrow payload range
 
@@ -65,7 +64,8 @@ __device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
   return x;
 }
 
-// Exclusive scan over the 256 threads of the block; *total gets the block sum.
+// Exclusive scan over the NT threads of the block; *total gets the block sum.
+template <int NT = kThreads>
 __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total, int64_t* tmp) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t x = wave_incl_scan(v);
@@ -73,7 +73,7 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total, in
   __syncthreads();
   int64_t pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kThreads / 64; w++) {
+  for (int w = 0; w < NT / 64; w++) {
     const int64_t s = tmp[w];
     pre += (w < wid) ? s : 0;
     tot += s;
@@ -84,26 +84,6 @@ __device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total, in
 }
 
 // --- encode side -------------------------------------------------------------------------------
-
-// Row size = fixed part + sum of appended var sections (writerIndex growth of toRow).
-__device__ int64_t row_size_of(const VarArgs& a, int64_t r) {
-  int64_t sz = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind < kBytes) continue;
-    if (c.validity && !bit_at(c.validity, r)) continue;          // null: setNullAt only
-    if (c.kind == kBytes) {
-      sz += rnd8(c.offsets[r + 1] - c.offsets[r]);
-    } else if (c.kind == kDecimal) {
-      sz += 16;
-    } else {                                                       // kListFixed
-      const int64_t n = c.offsets[r + 1] - c.offsets[r];
-      const int ew = c.width == 0 ? 1 : c.width;
-      sz += 8 + bm_bytes(n) + rnd8(n * ew);
-    }
-  }
-  return sz;
-}
 
 // Copies len bytes from an unaligned source to an 8-byte aligned destination as whole 8-byte
 // words, zero-filling the pad (writeUnaligned + zeroOutPaddingBytes).  Source words are read
@@ -178,81 +158,9 @@ __device__ int64_t write_array(uint8_t* dst, int width, const uint8_t* vals, con
   return hb + fp;
 }
 
-// Staged source regions of one workgroup (LDS copies of the contiguous global byte ranges its
-// rows read): per var column, region 2k = payload/values bytes, 2k+1 = list element validity.
-struct StagePlan {
-  uint32_t lds[2 * kMaxVarCols];
-  uint64_t glo[2 * kMaxVarCols];   // 16-byte aligned global base of the region
-  uint32_t len[2 * kMaxVarCols];   // bytes (multiple of 16), 0 = not staged
-};
-
-template <bool kSrcLds>
-__device__ __forceinline__ const uint8_t* src_at(const uint8_t* pool, const StagePlan& sp, int reg,
-                                                 const uint8_t* g) {
-  if (!kSrcLds) return g;
-  return pool + sp.lds[reg] + static_cast<uint32_t>(reinterpret_cast<uint64_t>(g) - sp.glo[reg]);
-}
-
-// Builds row r at dst (8-byte aligned, row_size_of(r) bytes) exactly as toRow does.  kSrcLds:
-// string payloads and list values/validity come from the workgroup's LDS staging copies.
-template <bool kSrcLds>
-__device__ __forceinline__ void build_row(const VarArgs& a, int64_t r, uint8_t* dst,
-                                          const uint8_t* pool, const StagePlan& sp) {
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    uint64_t slot = 0;
-    if (c.validity && !bit_at(c.validity, r)) {
-      nullbits |= 1ull << k;
-    } else {
-      switch (c.kind) {
-        case kFixed:
-        case kBool:
-          slot = load_fixed(c.values, r, c.width);
-          break;
-        case kBytes: {
-          const int64_t b = c.offsets[r];
-          const int64_t len = c.offsets[r + 1] - b;
-          copy_to_aligned(d64 + (cursor >> 3), src_at<kSrcLds>(pool, sp, 2 * k, c.values + b), len);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-          cursor += rnd8(len);
-          break;
-        }
-        case kDecimal: {
-          const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values + 16 * r);
-          d64[cursor >> 3] = s[0];
-          d64[(cursor >> 3) + 1] = s[1];
-          slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
-          cursor += 16;
-          break;
-        }
-        default: {   // kListFixed
-          const int64_t b = c.offsets[r];
-          const int64_t n = c.offsets[r + 1] - b;
-          const uint8_t* vals;
-          if (c.width == 0) vals = src_at<kSrcLds>(pool, sp, 2 * k, c.values + (b >> 3));
-          else vals = src_at<kSrcLds>(pool, sp, 2 * k, c.values + b * c.width);
-          const uint8_t* vb = c.elem_validity
-                                  ? src_at<kSrcLds>(pool, sp, 2 * k + 1, c.elem_validity + (b >> 3))
-                                  : nullptr;
-          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, b & 7, n);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
-          cursor += sz;
-          break;
-        }
-      }
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
-}
-
 // Cooperative 8-byte-aligned copy of [0, bytes) between LDS and global (16 B per lane when the
 // global side is 16-byte aligned).
-template <bool kToGlobal>
+template <bool kToGlobal, int NT = kThreads>
 __device__ __forceinline__ void copy_range(uint8_t* g, uint8_t* l, int64_t bytes) {
   using v4 = __attribute__((ext_vector_type(4))) uint32_t;
   int64_t head = 0;
@@ -263,7 +171,7 @@ __device__ __forceinline__ void copy_range(uint8_t* g, uint8_t* l, int64_t bytes
   }
   const int64_t body = (bytes - head) >> 4;
   // LDS side may be only 8-aligned at g+head: move 2 x 8 bytes per lane on the LDS side.
-  for (int64_t i = threadIdx.x; i < body; i += kThreads) {
+  for (int64_t i = threadIdx.x; i < body; i += NT) {
     uint8_t* gp = g + head + 16 * i;
     uint8_t* lp = l + head + 16 * i;
     if (kToGlobal) {
@@ -279,21 +187,10 @@ __device__ __forceinline__ void copy_range(uint8_t* g, uint8_t* l, int64_t bytes
     }
   }
   const int64_t done = head + 16 * body;
-  if (done < bytes && threadIdx.x == kThreads - 1) {    // one trailing 8-byte word
+  if (done < bytes && threadIdx.x == NT - 1) {    // one trailing 8-byte word
     if (kToGlobal) *reinterpret_cast<uint64_t*>(g + done) = *reinterpret_cast<uint64_t*>(l + done);
     else *reinterpret_cast<uint64_t*>(l + done) = *reinterpret_cast<uint64_t*>(g + done);
   }
-}
-
-__global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
-                                                           int64_t* __restrict__ block_sums) {
-  __shared__ int64_t tmp[kThreads / 64];
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  const int64_t sz = r < a.nrows ? row_size_of(a, r) : 0;
-  int64_t total;
-  const int64_t ex = block_excl_scan(sz, &total, tmp);
-  if (r < a.nrows) offs[r] = ex;
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
 // Exclusive scan of small arrays (<= kSmallScan entries): one workgroup, a few block scans.
@@ -332,11 +229,13 @@ __global__ __launch_bounds__(kThreads) void add_groups(int64_t* __restrict__ s, 
   if (i < n) s[i] += gpre[blockIdx.x];
 }
 
+// offs[r] += prefix[r / tile] (tile = rows per measure workgroup)
 __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict__ offs, int64_t n,
                                                              const int64_t* __restrict__ prefix,
-                                                             const int64_t* __restrict__ total) {
+                                                             const int64_t* __restrict__ total,
+                                                             int tile) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r < n) offs[r] += prefix[blockIdx.x];
+  if (r < n) offs[r] += prefix[r / tile];
   if (r == n - 1) offs[n] = *total;
 }
 
@@ -376,67 +275,236 @@ __device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q)
   }
 }
 
-// Plans the LDS staging of column k's source ranges for rows [r0, r0 + nr) (one thread per
-// column; offsets in LDS are assigned afterwards by assign_stage).
-__device__ __forceinline__ void plan_column(const VarArgs& a, int k, int64_t r0, int64_t nr,
-                                            StagePlan& sp) {
-  const VarCol& c = a.col[k];
-  sp.len[2 * k] = sp.len[2 * k + 1] = 0;
-  if (c.kind != kBytes && c.kind != kListFixed) return;
-  const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
-  if (e <= b) return;
-  uint64_t lo, hi;
-  if (c.kind == kBytes) {
-    lo = reinterpret_cast<uint64_t>(c.values + b);
-    hi = reinterpret_cast<uint64_t>(c.values + e);
-  } else if (c.width == 0) {
-    lo = reinterpret_cast<uint64_t>(c.values + (b >> 3));
-    hi = reinterpret_cast<uint64_t>(c.values + ((e + 7) >> 3));
-  } else {
-    lo = reinterpret_cast<uint64_t>(c.values + b * c.width);
-    hi = reinterpret_cast<uint64_t>(c.values + e * c.width);
+// ---- tile-staged encode ------------------------------------------------------------------------
+// One workgroup of kEncRows threads owns kEncRows consecutive rows.  Every input the tile reads
+// is a contiguous global range (a column's values / validity bytes / offsets for the tile, then
+// each string column's payload bytes and each list column's element values + validity between
+// the tile's first and last offsets), so the tile is staged in LDS by LDS-DMA
+// (global_load_lds_dwordx4: 16-B pieces, no register round trip, all pieces of a phase in flight
+// together): two dependent round trips to HBM per tile (meta, then payloads).  Each thread then
+// builds its row from LDS into an LDS image of the tile's contiguous output range, which leaves
+// with 16-B stores.
+constexpr int kEncRows = 128;                 // threads per encode workgroup = max rows per tile
+constexpr int kEncPool = 36 * 1024;           // LDS: staged inputs + row image
+constexpr int kMetaPool = 16 * 1024;          // bound on a tile's staged per-row inputs
+constexpr uint32_t kNone = 0xffffffffu;
+
+// LDS byte offsets of one tile's staged inputs, per column (kNone = not present / not staged).
+struct MetaMap {
+  uint32_t fix[kMaxVarCols];   // fixed values (row r0) / bool bits (byte r0/8) / decimal values
+  uint32_t val[kMaxVarCols];   // validity bits, byte r0/8
+  uint32_t off[kMaxVarCols];   // int32 offsets, entry r0
+  uint32_t pay[kMaxVarCols];   // payload bytes at offsets[r0] (bool elements: byte offsets[r0]/8)
+  uint32_t pvb[kMaxVarCols];   // list element validity, byte offsets[r0]/8
+};
+
+// Issues LDS-DMA copies of the 16-B-aligned pieces covering [gb, ge) into pool[at...]; returns
+// the LDS offset of byte gb and advances `at` (kept 16-aligned).  Reading whole aligned pieces
+// never leaves the pages holding the range.
+template <int NT>
+__device__ __forceinline__ uint32_t stage_range(uint8_t* pool, uint32_t& at, const uint8_t* gb,
+                                                const uint8_t* ge) {
+  const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
+  const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
+  const uint32_t nch = static_cast<uint32_t>((hi - lo) >> 4);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t i0 = wave * 64; i0 < nch; i0 += NT) {
+    if (i0 + lane < nch)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * (i0 + lane)),
+                                       pool + at + 16 * i0, 16, 0, 0);
   }
-  lo &= ~uint64_t(15);
-  hi = (hi + 15) & ~uint64_t(15);
-  sp.glo[2 * k] = lo;
-  sp.len[2 * k] = static_cast<uint32_t>(min<uint64_t>(hi - lo, 0xffffffffull));
-  if (c.kind == kListFixed && c.elem_validity) {
-    lo = reinterpret_cast<uint64_t>(c.elem_validity + (b >> 3)) & ~uint64_t(15);
-    hi = (reinterpret_cast<uint64_t>(c.elem_validity + ((e + 7) >> 3)) + 15) & ~uint64_t(15);
-    sp.glo[2 * k + 1] = lo;
-    sp.len[2 * k + 1] = static_cast<uint32_t>(hi - lo);
+  const uint32_t r = at + static_cast<uint32_t>(reinterpret_cast<uint64_t>(gb) - lo);
+  at += nch * 16;
+  return r;
+}
+
+__device__ __forceinline__ int32_t lds_i32(const uint8_t* pool, uint32_t off) {
+  return *reinterpret_cast<const int32_t*>(pool + off);
+}
+__device__ __forceinline__ bool lds_bit(const uint8_t* pool, uint32_t off, int64_t i) {
+  return (pool[off + (i >> 3)] >> (i & 7)) & 1;
+}
+
+// Phase A: stage every column's per-row inputs of rows [r0, r0 + nr).
+template <int NT>
+__device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int64_t nr,
+                                               uint8_t* pool, MetaMap& mm) {
+  uint32_t at = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    uint32_t fix = kNone, val = kNone, off = kNone;
+    if (c.validity) val = stage_range<NT>(pool, at, c.validity + (r0 >> 3), c.validity + ((r0 + nr + 7) >> 3));
+    switch (c.kind) {
+      case kFixed:
+        fix = stage_range<NT>(pool, at, c.values + r0 * c.width, c.values + (r0 + nr) * c.width);
+        break;
+      case kBool:
+        fix = stage_range<NT>(pool, at, c.values + (r0 >> 3), c.values + ((r0 + nr + 7) >> 3));
+        break;
+      case kDecimal:
+        fix = stage_range<NT>(pool, at, c.values + 16 * r0, c.values + 16 * (r0 + nr));
+        break;
+      default:      // kBytes, kListFixed
+        off = stage_range<NT>(pool, at, reinterpret_cast<const uint8_t*>(c.offsets + r0),
+                              reinterpret_cast<const uint8_t*>(c.offsets + r0 + nr + 1));
+        break;
+    }
+    if (threadIdx.x == 0) {
+      mm.fix[k] = fix;
+      mm.val[k] = val;
+      mm.off[k] = off;
+      mm.pay[k] = kNone;
+      mm.pvb[k] = kNone;
+    }
+  }
+  return at;
+}
+
+// Row size of tile row t from the staged inputs (writerIndex growth of toRow).
+__device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MetaMap& mm,
+                                                 const uint8_t* pool, int t) {
+  int64_t sz = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind < kBytes) continue;
+    if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) continue;
+    if (c.kind == kDecimal) {
+      sz += 16;
+      continue;
+    }
+    const int64_t n = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - lds_i32(pool, mm.off[k] + 4 * t);
+    if (c.kind == kBytes) sz += rnd8(n);
+    else sz += 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+  }
+  return sz;
+}
+
+// Bytes the payload staging of the tile needs (uniform; from the staged offsets).
+__device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MetaMap& mm,
+                                                 const uint8_t* pool, int nr) {
+  uint64_t need = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
+    if (e <= b) continue;
+    int64_t bytes;
+    if (c.kind == kBytes) bytes = e - b;
+    else if (c.width == 0) bytes = ((e + 7) >> 3) - (b >> 3);
+    else bytes = (e - b) * c.width;
+    need += static_cast<uint64_t>(bytes) + 32;
+    if (c.kind == kListFixed && c.elem_validity) need += static_cast<uint64_t>(((e + 7) >> 3) - (b >> 3)) + 32;
+  }
+  return need;
+}
+
+// Phase C: stage the payload ranges.
+template <int NT>
+__device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, uint8_t* pool,
+                                               uint32_t at, int nr) {
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
+    uint32_t pay = kNone, pvb = kNone;
+    if (e > b) {
+      if (c.kind == kBytes) pay = stage_range<NT>(pool, at, c.values + b, c.values + e);
+      else if (c.width == 0) pay = stage_range<NT>(pool, at, c.values + (b >> 3), c.values + ((e + 7) >> 3));
+      else pay = stage_range<NT>(pool, at, c.values + b * c.width, c.values + e * c.width);
+      if (c.kind == kListFixed && c.elem_validity)
+        pvb = stage_range<NT>(pool, at, c.elem_validity + (b >> 3), c.elem_validity + ((e + 7) >> 3));
+    }
+    if (threadIdx.x == 0) {
+      mm.pay[k] = pay;
+      mm.pvb[k] = pvb;
+    }
   }
 }
 
-// LDS offsets of the planned regions after the row image (`base` bytes); returns the total.
-__device__ __forceinline__ uint32_t assign_stage(int ncols, uint32_t base, StagePlan& sp) {
-  uint64_t at = base;
-  for (int k = 0; k < 2 * ncols; k++) {
-    sp.lds[k] = static_cast<uint32_t>(min<uint64_t>(at, 0xffffffffull));
-    at += sp.len[k];
+// Builds tile row t at dst (8-byte aligned) exactly as toRow does.  Per-row inputs come from the
+// staged meta; payloads from LDS when kPayLds, else straight from global memory.
+template <bool kPayLds>
+__device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& mm,
+                                               const uint8_t* pool, int t, uint8_t* dst) {
+  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
+  const int nslot0 = a.bitmap_bytes >> 3;
+  int64_t cursor = a.fixed_size;
+  uint64_t nullbits = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    uint64_t slot = 0;
+    if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) {
+      nullbits |= 1ull << k;
+    } else {
+      switch (c.kind) {
+        case kFixed: {
+          const uint8_t* p = pool + mm.fix[k] + t * c.width;
+          switch (c.width) {
+            case 8: slot = *reinterpret_cast<const uint64_t*>(p); break;
+            case 4: slot = *reinterpret_cast<const uint32_t*>(p); break;
+            case 2: slot = *reinterpret_cast<const uint16_t*>(p); break;
+            default: slot = *p; break;
+          }
+          break;
+        }
+        case kBool:
+          slot = lds_bit(pool, mm.fix[k], t);
+          break;
+        case kBytes: {
+          const int64_t ob = lds_i32(pool, mm.off[k]);
+          const int64_t o0 = lds_i32(pool, mm.off[k] + 4 * t);
+          const int64_t len = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - o0;
+          const uint8_t* src = kPayLds ? pool + mm.pay[k] + (o0 - ob) : c.values + o0;
+          copy_to_aligned(d64 + (cursor >> 3), src, len);
+          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
+          cursor += rnd8(len);
+          break;
+        }
+        case kDecimal: {
+          const uint64_t* s = reinterpret_cast<const uint64_t*>(pool + mm.fix[k] + 16 * t);
+          d64[cursor >> 3] = s[0];
+          d64[(cursor >> 3) + 1] = s[1];
+          slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
+          cursor += 16;
+          break;
+        }
+        default: {   // kListFixed
+          const int64_t ob = lds_i32(pool, mm.off[k]);
+          const int64_t o0 = lds_i32(pool, mm.off[k] + 4 * t);
+          const int64_t n = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - o0;
+          const uint8_t* vals;
+          const uint8_t* vb = nullptr;
+          if (c.width == 0)
+            vals = kPayLds ? pool + mm.pay[k] + ((o0 >> 3) - (ob >> 3)) : c.values + (o0 >> 3);
+          else
+            vals = kPayLds ? pool + mm.pay[k] + (o0 - ob) * c.width : c.values + o0 * c.width;
+          if (c.elem_validity)
+            vb = kPayLds ? pool + mm.pvb[k] + ((o0 >> 3) - (ob >> 3)) : c.elem_validity + (o0 >> 3);
+          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, o0 & 7, n);
+          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
+          cursor += sz;
+          break;
+        }
+      }
+    }
+    d64[nslot0 + k] = slot;
   }
-  return static_cast<uint32_t>(min<uint64_t>(at, 0xffffffffull));
+  d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
 }
 
-// Encode: 256 rows per workgroup = one contiguous byte range of the row buffer.
-//   kMeasure: the row sizes are computed here and chained across groups with the decoupled
-//   look-back (fury_row_encode_measured: one pass, writes row_offsets); otherwise the offsets
-//   come from fury_row_measure.
-// Mode 2 stages every source range the group reads (string payloads, list values/validity: each
-// a contiguous range) in LDS with 16-B loads and builds the rows in an LDS image of the group's
-// output range; mode 1 stages only the output image; mode 0 (oversized rows) builds rows straight
-// in HBM.  Bytes at or past `cap` are never written.
+// Encode workgroup.  kMeasure: row sizes computed here and chained across workgroups by the
+// decoupled look-back (fury_row_encode_measured; writes row_offsets); else the offsets come from
+// fury_row_measure.  Bytes at or past `cap` are never written.
 template <bool kMeasure>
-__global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a, int64_t* __restrict__ offs,
+__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a, int64_t* __restrict__ offs,
                                                               uint8_t* __restrict__ rows,
                                                               int64_t cap,
                                                               uint64_t* __restrict__ status,
                                                               uint32_t* __restrict__ ticket) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncodeStage];
-  __shared__ StagePlan sp;
-  __shared__ int64_t tmp[kThreads / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
+  __shared__ MetaMap mm;
+  __shared__ int64_t tmp[kEncRows / 64];
   __shared__ int64_t blk, gbase;
-  __shared__ uint32_t need;
   const int tid = threadIdx.x;
   int64_t b = blockIdx.x;
   if (kMeasure) {
@@ -444,26 +512,30 @@ __global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a, int64_t
     __syncthreads();
     b = blk;
   }
-  const int64_t r0 = b * kThreads;
-  const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
-  const int64_t r = r0 + tid;
+  const int R = a.tile_rows;                 // rows per tile (host-chosen so the meta fits)
+  const int64_t r0 = b * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
   const bool live = tid < nr;
+  const int64_t r = r0 + tid;
   int64_t ex, bytes;
-  if (kMeasure) {
-    ex = block_excl_scan(live ? row_size_of(a, r) : 0, &bytes, tmp);
-    if (tid == 0)
-      st_status(status + b, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(bytes));
-  } else {
+  uint32_t at;
+  if (!kMeasure) {                      // issue the offset loads with the meta DMA
     const int64_t rb = offs[r0];
     bytes = offs[r0 + nr] - rb;
     ex = live ? offs[r] - rb : 0;
     if (tid == 0) gbase = rb;
   }
-  const uint32_t img = static_cast<uint32_t>((bytes + 15) & ~int64_t(15));
-  const bool fits = bytes <= kEncodeStage;
-  if (fits && tid < a.ncols) plan_column(a, tid, r0, nr, sp);
+  at = stage_meta<kEncRows>(a, r0, nr, pool, mm);
   __syncthreads();
-  if (fits && tid == 0) need = assign_stage(a.ncols, img, sp);
+  if (kMeasure) {
+    ex = block_excl_scan<kEncRows>(live ? tile_row_size(a, mm, pool, tid) : 0, &bytes, tmp);
+    if (tid == 0) st_status(status + b, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(bytes));
+  }
+  const uint32_t img_at = at;
+  const uint64_t img = static_cast<uint64_t>((bytes + 15) & ~int64_t(15));
+  const bool img_fits = img_at + img <= kEncPool;
+  const bool pay_fits = img_fits && img_at + img + payload_need(a, mm, pool, nr) <= kEncPool;
+  if (pay_fits) stage_payloads<kEncRows>(a, mm, pool, static_cast<uint32_t>(img_at + img), nr);
   if (kMeasure && tid < 64) {
     const int64_t e = b == 0 ? 0 : look_back(status, b, 1, 0);
     if (tid == 0) {
@@ -478,26 +550,33 @@ __global__ __launch_bounds__(kThreads) void encode_var_kernel(VarArgs a, int64_t
     if (r == a.nrows - 1) offs[a.nrows] = base + bytes;   // last row closes its group
   }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (fits && need <= kEncodeStage) {
-    using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-    for (int k = 0; k < 2 * a.ncols; k++) {
-      const uint32_t len = sp.len[k];
-      if (!len) continue;
-      const v4* g = reinterpret_cast<const v4*>(sp.glo[k]);
-      v4* l = reinterpret_cast<v4*>(pool + sp.lds[k]);
-      for (uint32_t i = tid; i < (len >> 4); i += kThreads) l[i] = __builtin_nontemporal_load(g + i);
+  if (img_fits) {
+    uint8_t* image = pool + img_at;
+    if (live) {
+      if (pay_fits) build_tile_row<true>(a, mm, pool, tid, image + ex);
+      else build_tile_row<false>(a, mm, pool, tid, image + ex);
     }
     __syncthreads();
-    if (live) build_row<true>(a, r, pool + ex, pool, sp);
-    __syncthreads();
-    copy_range<true>(rows + base, pool, room);
-  } else if (fits) {
-    if (live) build_row<false>(a, r, pool + ex, pool, sp);
-    __syncthreads();
-    copy_range<true>(rows + base, pool, room);
-  } else if (live && ex + row_size_of(a, r) <= room) {
-    build_row<false>(a, r, rows + base + ex, pool, sp);
+    copy_range<true, kEncRows>(rows + base, image, room);
+  } else if (live && ex + tile_row_size(a, mm, pool, tid) <= room) {
+    build_tile_row<false>(a, mm, pool, tid, rows + base + ex);   // oversized tile: straight to HBM
   }
+}
+
+__global__ __launch_bounds__(kEncRows) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
+                                                           int64_t* __restrict__ block_sums) {
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kMetaPool];
+  __shared__ MetaMap mm;
+  __shared__ int64_t tmp[kEncRows / 64];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile_rows;
+  const int nr = static_cast<int>(min<int64_t>(a.tile_rows, a.nrows - r0));
+  stage_meta<kEncRows>(a, r0, nr, pool, mm);
+  __syncthreads();
+  int64_t total;
+  const int64_t ex = block_excl_scan<kEncRows>(
+      static_cast<int>(threadIdx.x) < nr ? tile_row_size(a, mm, pool, threadIdx.x) : 0, &total, tmp);
+  if (static_cast<int>(threadIdx.x) < nr) offs[r0 + threadIdx.x] = ex;
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
 // --- decode side -------------------------------------------------------------------------------
@@ -981,15 +1060,16 @@ void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t
 int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t n = a.nrows;
   if (n == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  const int64_t nb = nblocks(n);
+  const int64_t nb = (n + a.tile_rows - 1) / a.tile_rows;
   int64_t* ws = nullptr;
   const int64_t wsn = nb + 1 + scan_workspace(nb);
   int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
                      "hipMallocAsync");
   if (st) return st;
-  hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
+  hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, ws);
   device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
-  hipLaunchKernelGGL(add_block_prefix, dim3(nb), dim3(kThreads), 0, stream, offs, n, ws, ws + nb);
+  hipLaunchKernelGGL(add_block_prefix, dim3(nblocks(n)), dim3(kThreads), 0, stream, offs, n, ws,
+                     ws + nb, a.tile_rows);
   st = check_hip(hipGetLastError(), "measure launch");
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
@@ -1000,27 +1080,46 @@ void set_var_decode_mode(int v) { g_var_decode = v; }
 
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
-  hipLaunchKernelGGL(encode_var_kernel<false>, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream,
-                     a, const_cast<int64_t*>(offs), rows, INT64_MAX, nullptr, nullptr);
+  const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
+  hipLaunchKernelGGL(encode_var_kernel<false>, dim3(nb), dim3(kEncRows), 0, stream, a,
+                     const_cast<int64_t*>(offs), rows, INT64_MAX, nullptr, nullptr);
   return check_hip(hipGetLastError(), "encode_var launch");
 }
 
 int launch_encode_var_measured(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
                                hipStream_t stream) {
   if (a.nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  const int64_t nb = nblocks(a.nrows);
-  const size_t wsb = (nb + 1) * 8;          // status word per group + the group ticket
+  const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
+  const size_t wsb = (nb + 1) * 8;          // status word per tile + the tile ticket
   uint64_t* ws = nullptr;
   int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
   if (st) return st;
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
   if (!st) {
-    hipLaunchKernelGGL(encode_var_kernel<true>, dim3(nb), dim3(kThreads), 0, stream, a, offs, rows,
+    hipLaunchKernelGGL(encode_var_kernel<true>, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows,
                        cap, ws + 1, reinterpret_cast<uint32_t*>(ws));
     st = check_hip(hipGetLastError(), "encode_var launch");
   }
   const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
+}
+
+// Rows per encode tile so that the staged per-row inputs of a tile fit kMetaPool (always true at
+// 8 rows: <= 64 columns x (validity + 16-B decimal) pieces).
+int encode_tile_rows(const VarArgs& a) {
+  for (int R = kEncRows; R >= 8; R >>= 1) {
+    int64_t meta = 0;
+    for (int k = 0; k < a.ncols; k++) {
+      const VarCol& c = a.col[k];
+      if (c.validity) meta += R / 8 + 32;
+      if (c.kind == kFixed) meta += int64_t(R) * c.width + 32;
+      else if (c.kind == kBool) meta += R / 8 + 32;
+      else if (c.kind == kDecimal) meta += 16 * int64_t(R) + 32;
+      else meta += 4 * int64_t(R + 1) + 32;
+    }
+    if (meta <= kMetaPool) return R;
+  }
+  return 8;
 }
 
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
