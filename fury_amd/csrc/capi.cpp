@@ -438,6 +438,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_fixed_variant(value);
     return FURY_OK;
   }
+  if (std::string(key) == "var_encode") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_encode: 0..1");
+    set_var_encode_mode(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "var_decode") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..1");
     set_var_decode_mode(value);
@@ -449,6 +454,7 @@ int fury_set_tuning(const char* key, int32_t value) {
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "fixed_variant") return fixed_variant();
   if (key && std::string(key) == "var_decode") return var_decode_mode();
+  if (key && std::string(key) == "var_encode") return var_encode_mode();
   return -1;
 }
 

@@ -75,6 +75,8 @@ int workspace_reserve(size_t bytes, void** out);
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
 int var_decode_mode();
+int var_encode_mode();
+void set_var_encode_mode(int v);
 void set_var_decode_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows,

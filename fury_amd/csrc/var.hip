@@ -579,6 +579,93 @@ __global__ __launch_bounds__(kEncRows) void measure_kernel(VarArgs a, int64_t* _
   if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
 }
 
+// ---- direct encode (no LDS): one thread per row, every access straight to global memory; relies
+// on occupancy (no LDS, few VGPRs) instead of staging.  Tuning "var_encode" = 1.
+__device__ __forceinline__ int64_t row_size_direct(const VarArgs& a, int64_t r) {
+  int64_t sz = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind < kBytes) continue;
+    if (c.validity && !bit_at(c.validity, r)) continue;          // null: setNullAt only
+    if (c.kind == kDecimal) {
+      sz += 16;
+      continue;
+    }
+    const int64_t n = c.offsets[r + 1] - c.offsets[r];
+    if (c.kind == kBytes) sz += rnd8(n);
+    else sz += 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+  }
+  return sz;
+}
+
+__device__ __forceinline__ void build_row_direct(const VarArgs& a, int64_t r, uint8_t* dst) {
+  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
+  const int nslot0 = a.bitmap_bytes >> 3;
+  int64_t cursor = a.fixed_size;
+  uint64_t nullbits = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    uint64_t slot = 0;
+    if (c.validity && !bit_at(c.validity, r)) {
+      nullbits |= 1ull << k;
+    } else {
+      switch (c.kind) {
+        case kFixed:
+        case kBool:
+          slot = load_fixed(c.values, r, c.width);
+          break;
+        case kBytes: {
+          const int64_t o0 = c.offsets[r];
+          const int64_t len = c.offsets[r + 1] - o0;
+          copy_to_aligned(d64 + (cursor >> 3), c.values + o0, len);
+          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
+          cursor += rnd8(len);
+          break;
+        }
+        case kDecimal: {
+          const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values + 16 * r);
+          d64[cursor >> 3] = s[0];
+          d64[(cursor >> 3) + 1] = s[1];
+          slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
+          cursor += 16;
+          break;
+        }
+        default: {   // kListFixed
+          const int64_t o0 = c.offsets[r];
+          const int64_t n = c.offsets[r + 1] - o0;
+          const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + o0 * c.width;
+          const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
+          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, o0 & 7, n);
+          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
+          cursor += sz;
+          break;
+        }
+      }
+    }
+    d64[nslot0 + k] = slot;
+  }
+  d64[0] = nullbits;
+}
+
+__global__ __launch_bounds__(kThreads) void measure_direct_kernel(VarArgs a,
+                                                                  int64_t* __restrict__ offs,
+                                                                  int64_t* __restrict__ block_sums) {
+  __shared__ int64_t tmp[kThreads / 64];
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  int64_t total;
+  const int64_t ex = block_excl_scan(r < a.nrows ? row_size_direct(a, r) : 0, &total, tmp);
+  if (r < a.nrows) offs[r] = ex;
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kThreads) void encode_direct_kernel(VarArgs a,
+                                                                 const int64_t* __restrict__ offs,
+                                                                 uint8_t* __restrict__ rows,
+                                                                 int64_t cap) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (r < a.nrows && offs[r + 1] <= cap) build_row_direct(a, r, rows + offs[r]);
+}
+
 // --- decode side -------------------------------------------------------------------------------
 
 // Per row and var field: STRING/BINARY -> unpadded size; LIST -> numElements; else 0.
@@ -1031,6 +1118,7 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back, 1 sizing pass + decode
+int g_var_encode = 0;     // tuning "var_encode": 0 LDS-staged tiles, 1 direct (no LDS)
 
 }  // namespace
 
@@ -1060,16 +1148,20 @@ void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t
 int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t n = a.nrows;
   if (n == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  const int64_t nb = (n + a.tile_rows - 1) / a.tile_rows;
+  const int tile = g_var_encode == 1 ? kThreads : a.tile_rows;
+  const int64_t nb = (n + tile - 1) / tile;
   int64_t* ws = nullptr;
   const int64_t wsn = nb + 1 + scan_workspace(nb);
   int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
                      "hipMallocAsync");
   if (st) return st;
-  hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, ws);
+  if (g_var_encode == 1)
+    hipLaunchKernelGGL(measure_direct_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
+  else
+    hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, ws);
   device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
   hipLaunchKernelGGL(add_block_prefix, dim3(nblocks(n)), dim3(kThreads), 0, stream, offs, n, ws,
-                     ws + nb, a.tile_rows);
+                     ws + nb, tile);
   st = check_hip(hipGetLastError(), "measure launch");
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
@@ -1077,9 +1169,16 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
 
 int var_decode_mode() { return g_var_decode; }
 void set_var_decode_mode(int v) { g_var_decode = v; }
+int var_encode_mode() { return g_var_encode; }
+void set_var_encode_mode(int v) { g_var_encode = v; }
 
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
+  if (g_var_encode == 1) {
+    hipLaunchKernelGGL(encode_direct_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a,
+                       offs, rows, INT64_MAX);
+    return check_hip(hipGetLastError(), "encode_var launch");
+  }
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
   hipLaunchKernelGGL(encode_var_kernel<false>, dim3(nb), dim3(kEncRows), 0, stream, a,
                      const_cast<int64_t*>(offs), rows, INT64_MAX, nullptr, nullptr);
@@ -1089,6 +1188,13 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipS
 int launch_encode_var_measured(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
                                hipStream_t stream) {
   if (a.nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
+  if (g_var_encode == 1) {
+    int st = launch_measure_rows(a, offs, stream);
+    if (st) return st;
+    hipLaunchKernelGGL(encode_direct_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a,
+                       offs, rows, cap);
+    return check_hip(hipGetLastError(), "encode_var launch");
+  }
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
   const size_t wsb = (nb + 1) * 8;          // status word per tile + the tile ticket
   uint64_t* ws = nullptr;

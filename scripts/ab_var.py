@@ -44,11 +44,16 @@ def main():
     sh = _stream_handle(None)
     ccols = _c_columns(out, keep)
     L = N.lib()
+    def mode(v):
+        L.fury_set_tuning(b"var_encode", v)
     legs = {
-        "measure": lambda: enc.measure_into(cols, n, offs),
-        "encode_2pass": lambda: (enc.measure_into(cols, n, offs),
+        "measure": lambda: (mode(0), enc.measure_into(cols, n, offs)),
+        "measure_direct": lambda: (mode(1), enc.measure_into(cols, n, offs)),
+        "encode_2pass": lambda: (mode(0), enc.measure_into(cols, n, offs),
                                  enc.encode_into(cols, n, rows, offs)),
-        "encode_1pass": lambda: enc.encode_measured_into(cols, n, rows, offs),
+        "encode_2pass_direct": lambda: (mode(1), enc.measure_into(cols, n, offs),
+                                        enc.encode_into(cols, n, rows, offs)),
+        "encode_1pass": lambda: (mode(0), enc.encode_measured_into(cols, n, rows, offs)),
         "decode_1pass": lambda: (L.fury_set_tuning(b"var_decode", 0),
                                  enc.decode_into(batch, out)),
         "decode_2pass": lambda: (L.fury_set_tuning(b"var_decode", 1),
@@ -73,12 +78,21 @@ def main():
             times[k].append(a.elapsed_time(b) / args.iters)
     enc.check_capacity(out, n)
     L.fury_set_tuning(b"var_decode", 0)
+    mode(0)
+    ref = rows.clone()
+    mode(1)
+    enc.measure_into(cols, n, offs)
+    enc.encode_into(cols, n, rows, offs)
+    torch.cuda.synchronize()
+    assert torch.equal(rows, ref), "direct encode differs from the tile encode"
+    mode(0)
     col_bytes = _nbytes(cols)
     row_bytes = rows.numel() + offs.numel() * 8
     med = {k: round(statistics.median(v), 4) for k, v in times.items()}
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
-                    for k in ("encode_2pass", "encode_1pass", "decode_1pass", "decode_2pass")}}
+                    for k in ("encode_2pass", "encode_2pass_direct", "encode_1pass", "decode_1pass",
+                              "decode_2pass")}}
     print(json.dumps(res), flush=True)
 
 
