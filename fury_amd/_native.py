@@ -14,7 +14,8 @@ import os
 import torch  # noqa: F401
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfury_row.so")
+# FURY_ROW_LIB: alternative in-tree build of the same library (kernel-variant A/B experiments)
+LIB_PATH = os.environ.get("FURY_ROW_LIB") or os.path.join(HERE, "libfury_row.so")
 
 
 class FuryField(ctypes.Structure):

@@ -272,7 +272,7 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
   VarArgs a;
   st = var_args(s, cols, nrows, false, false, &a);
   if (st) return st;
-  return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), hs);
+  return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), INT64_MAX, hs);
 }
 
 int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int64_t nrows,
@@ -306,7 +306,9 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
   VarArgs a;
   st = var_args(s, cols, nrows, false, false, &a);
   if (st) return st;
-  return launch_encode_var_measured(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
+  st = launch_measure_rows(a, row_offsets, hs);
+  if (st || nrows == 0) return st;
+  return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
 }
 
 int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_t* row_offsets,
@@ -438,11 +440,6 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_fixed_variant(value);
     return FURY_OK;
   }
-  if (std::string(key) == "var_encode") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_encode: 0..1");
-    set_var_encode_mode(value);
-    return FURY_OK;
-  }
   if (std::string(key) == "var_decode") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..1");
     set_var_decode_mode(value);
@@ -454,7 +451,6 @@ int fury_set_tuning(const char* key, int32_t value) {
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "fixed_variant") return fixed_variant();
   if (key && std::string(key) == "var_decode") return var_decode_mode();
-  if (key && std::string(key) == "var_encode") return var_encode_mode();
   return -1;
 }
 

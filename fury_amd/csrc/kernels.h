@@ -75,16 +75,11 @@ int workspace_reserve(size_t bytes, void** out);
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
 int var_decode_mode();
-int var_encode_mode();
-void set_var_encode_mode(int v);
 void set_var_decode_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
-int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows,
+// Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.
+int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
-// Measure + encode in one pass (row sizes chained across workgroups by a decoupled look-back);
-// writes row_offsets[0..nrows], never writes row bytes at or past `cap`.
-int launch_encode_var_measured(const VarArgs& a, int64_t* row_offsets, uint8_t* rows, int64_t cap,
-                               hipStream_t stream);
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                           hipStream_t stream);
 // Single pass: computes the Arrow offsets itself (decoupled look-back scan across workgroups)

@@ -229,13 +229,11 @@ __global__ __launch_bounds__(kThreads) void add_groups(int64_t* __restrict__ s, 
   if (i < n) s[i] += gpre[blockIdx.x];
 }
 
-// offs[r] += prefix[r / tile] (tile = rows per measure workgroup)
 __global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict__ offs, int64_t n,
                                                              const int64_t* __restrict__ prefix,
-                                                             const int64_t* __restrict__ total,
-                                                             int tile) {
+                                                             const int64_t* __restrict__ total) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r < n) offs[r] += prefix[r / tile];
+  if (r < n) offs[r] += prefix[blockIdx.x];
   if (r == n - 1) offs[n] = *total;
 }
 
@@ -284,8 +282,8 @@ __device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q)
 // together): two dependent round trips to HBM per tile (meta, then payloads).  Each thread then
 // builds its row from LDS into an LDS image of the tile's contiguous output range, which leaves
 // with 16-B stores.
-constexpr int kEncRows = 128;                 // threads per encode workgroup = max rows per tile
-constexpr int kEncPool = 36 * 1024;           // LDS: staged inputs + row image
+constexpr int kEncRows = 256;                 // threads per encode workgroup = max rows per tile
+constexpr int kEncPool = 50 * 1024;           // LDS: staged inputs + row image (3 groups per CU)
 constexpr int kMetaPool = 16 * 1024;          // bound on a tile's staged per-row inputs
 constexpr uint32_t kNone = 0xffffffffu;
 
@@ -492,63 +490,30 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
   d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
 }
 
-// Encode workgroup.  kMeasure: row sizes computed here and chained across workgroups by the
-// decoupled look-back (fury_row_encode_measured; writes row_offsets); else the offsets come from
-// fury_row_measure.  Bytes at or past `cap` are never written.
-template <bool kMeasure>
-__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a, int64_t* __restrict__ offs,
+// Encode workgroup: rows [r0, r0 + R) at the offsets fury_row_measure produced.  Bytes at or
+// past `cap` are never written.
+__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
+                                                              const int64_t* __restrict__ offs,
                                                               uint8_t* __restrict__ rows,
-                                                              int64_t cap,
-                                                              uint64_t* __restrict__ status,
-                                                              uint32_t* __restrict__ ticket) {
+                                                              int64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
   __shared__ MetaMap mm;
-  __shared__ int64_t tmp[kEncRows / 64];
-  __shared__ int64_t blk, gbase;
   const int tid = threadIdx.x;
-  int64_t b = blockIdx.x;
-  if (kMeasure) {
-    if (tid == 0) blk = atomicAdd(ticket, 1u);
-    __syncthreads();
-    b = blk;
-  }
   const int R = a.tile_rows;                 // rows per tile (host-chosen so the meta fits)
-  const int64_t r0 = b * R;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
   const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
   const bool live = tid < nr;
-  const int64_t r = r0 + tid;
-  int64_t ex, bytes;
-  uint32_t at;
-  if (!kMeasure) {                      // issue the offset loads with the meta DMA
-    const int64_t rb = offs[r0];
-    bytes = offs[r0 + nr] - rb;
-    ex = live ? offs[r] - rb : 0;
-    if (tid == 0) gbase = rb;
-  }
-  at = stage_meta<kEncRows>(a, r0, nr, pool, mm);
+  // the offset loads go out together with the meta DMA
+  const int64_t base = offs[r0];
+  const int64_t bytes = offs[r0 + nr] - base;
+  const int64_t ex = live ? offs[r0 + tid] - base : 0;
+  const uint32_t img_at = stage_meta<kEncRows>(a, r0, nr, pool, mm);
   __syncthreads();
-  if (kMeasure) {
-    ex = block_excl_scan<kEncRows>(live ? tile_row_size(a, mm, pool, tid) : 0, &bytes, tmp);
-    if (tid == 0) st_status(status + b, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(bytes));
-  }
-  const uint32_t img_at = at;
   const uint64_t img = static_cast<uint64_t>((bytes + 15) & ~int64_t(15));
   const bool img_fits = img_at + img <= kEncPool;
   const bool pay_fits = img_fits && img_at + img + payload_need(a, mm, pool, nr) <= kEncPool;
   if (pay_fits) stage_payloads<kEncRows>(a, mm, pool, static_cast<uint32_t>(img_at + img), nr);
-  if (kMeasure && tid < 64) {
-    const int64_t e = b == 0 ? 0 : look_back(status, b, 1, 0);
-    if (tid == 0) {
-      gbase = e;
-      if (b > 0) st_status(status + b, kInc | static_cast<uint64_t>(e + bytes));
-    }
-  }
   __syncthreads();
-  const int64_t base = gbase;
-  if (kMeasure) {
-    if (live) offs[r] = base + ex;
-    if (r == a.nrows - 1) offs[a.nrows] = base + bytes;   // last row closes its group
-  }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (img_fits) {
     uint8_t* image = pool + img_at;
@@ -563,25 +528,10 @@ __global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a, int64_t
   }
 }
 
-__global__ __launch_bounds__(kEncRows) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
-                                                           int64_t* __restrict__ block_sums) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kMetaPool];
-  __shared__ MetaMap mm;
-  __shared__ int64_t tmp[kEncRows / 64];
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile_rows;
-  const int nr = static_cast<int>(min<int64_t>(a.tile_rows, a.nrows - r0));
-  stage_meta<kEncRows>(a, r0, nr, pool, mm);
-  __syncthreads();
-  int64_t total;
-  const int64_t ex = block_excl_scan<kEncRows>(
-      static_cast<int>(threadIdx.x) < nr ? tile_row_size(a, mm, pool, threadIdx.x) : 0, &total, tmp);
-  if (static_cast<int>(threadIdx.x) < nr) offs[r0 + threadIdx.x] = ex;
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
-}
-
-// ---- direct encode (no LDS): one thread per row, every access straight to global memory; relies
-// on occupancy (no LDS, few VGPRs) instead of staging.  Tuning "var_encode" = 1.
-__device__ __forceinline__ int64_t row_size_direct(const VarArgs& a, int64_t r) {
+// ---- measure: row sizes (writerIndex growth of toRow) + block scan, one thread per row.  Reads
+// only validity bits and offsets; plain loads at full occupancy (no LDS) measured faster here than
+// LDS-DMA staging of the same inputs.
+__device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
@@ -598,72 +548,15 @@ __device__ __forceinline__ int64_t row_size_direct(const VarArgs& a, int64_t r) 
   return sz;
 }
 
-__device__ __forceinline__ void build_row_direct(const VarArgs& a, int64_t r, uint8_t* dst) {
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    uint64_t slot = 0;
-    if (c.validity && !bit_at(c.validity, r)) {
-      nullbits |= 1ull << k;
-    } else {
-      switch (c.kind) {
-        case kFixed:
-        case kBool:
-          slot = load_fixed(c.values, r, c.width);
-          break;
-        case kBytes: {
-          const int64_t o0 = c.offsets[r];
-          const int64_t len = c.offsets[r + 1] - o0;
-          copy_to_aligned(d64 + (cursor >> 3), c.values + o0, len);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-          cursor += rnd8(len);
-          break;
-        }
-        case kDecimal: {
-          const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values + 16 * r);
-          d64[cursor >> 3] = s[0];
-          d64[(cursor >> 3) + 1] = s[1];
-          slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
-          cursor += 16;
-          break;
-        }
-        default: {   // kListFixed
-          const int64_t o0 = c.offsets[r];
-          const int64_t n = c.offsets[r + 1] - o0;
-          const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + o0 * c.width;
-          const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
-          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, o0 & 7, n);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
-          cursor += sz;
-          break;
-        }
-      }
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;
-}
-
-__global__ __launch_bounds__(kThreads) void measure_direct_kernel(VarArgs a,
+__global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a,
                                                                   int64_t* __restrict__ offs,
                                                                   int64_t* __restrict__ block_sums) {
   __shared__ int64_t tmp[kThreads / 64];
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   int64_t total;
-  const int64_t ex = block_excl_scan(r < a.nrows ? row_size_direct(a, r) : 0, &total, tmp);
+  const int64_t ex = block_excl_scan(r < a.nrows ? row_size_of(a, r) : 0, &total, tmp);
   if (r < a.nrows) offs[r] = ex;
   if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
-}
-
-__global__ __launch_bounds__(kThreads) void encode_direct_kernel(VarArgs a,
-                                                                 const int64_t* __restrict__ offs,
-                                                                 uint8_t* __restrict__ rows,
-                                                                 int64_t cap) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r < a.nrows && offs[r + 1] <= cap) build_row_direct(a, r, rows + offs[r]);
 }
 
 // --- decode side -------------------------------------------------------------------------------
@@ -1118,7 +1011,6 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back, 1 sizing pass + decode
-int g_var_encode = 0;     // tuning "var_encode": 0 LDS-staged tiles, 1 direct (no LDS)
 
 }  // namespace
 
@@ -1148,20 +1040,15 @@ void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t
 int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t n = a.nrows;
   if (n == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  const int tile = g_var_encode == 1 ? kThreads : a.tile_rows;
-  const int64_t nb = (n + tile - 1) / tile;
+  const int64_t nb = nblocks(n);
   int64_t* ws = nullptr;
   const int64_t wsn = nb + 1 + scan_workspace(nb);
   int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
                      "hipMallocAsync");
   if (st) return st;
-  if (g_var_encode == 1)
-    hipLaunchKernelGGL(measure_direct_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
-  else
-    hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, ws);
+  hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
   device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
-  hipLaunchKernelGGL(add_block_prefix, dim3(nblocks(n)), dim3(kThreads), 0, stream, offs, n, ws,
-                     ws + nb, tile);
+  hipLaunchKernelGGL(add_block_prefix, dim3(nb), dim3(kThreads), 0, stream, offs, n, ws, ws + nb);
   st = check_hip(hipGetLastError(), "measure launch");
   int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
@@ -1169,45 +1056,12 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
 
 int var_decode_mode() { return g_var_decode; }
 void set_var_decode_mode(int v) { g_var_decode = v; }
-int var_encode_mode() { return g_var_encode; }
-void set_var_encode_mode(int v) { g_var_encode = v; }
-
-int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, hipStream_t stream) {
+int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
+                      hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
-  if (g_var_encode == 1) {
-    hipLaunchKernelGGL(encode_direct_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a,
-                       offs, rows, INT64_MAX);
-    return check_hip(hipGetLastError(), "encode_var launch");
-  }
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
-  hipLaunchKernelGGL(encode_var_kernel<false>, dim3(nb), dim3(kEncRows), 0, stream, a,
-                     const_cast<int64_t*>(offs), rows, INT64_MAX, nullptr, nullptr);
+  hipLaunchKernelGGL(encode_var_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
   return check_hip(hipGetLastError(), "encode_var launch");
-}
-
-int launch_encode_var_measured(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
-                               hipStream_t stream) {
-  if (a.nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  if (g_var_encode == 1) {
-    int st = launch_measure_rows(a, offs, stream);
-    if (st) return st;
-    hipLaunchKernelGGL(encode_direct_kernel, dim3(nblocks(a.nrows)), dim3(kThreads), 0, stream, a,
-                       offs, rows, cap);
-    return check_hip(hipGetLastError(), "encode_var launch");
-  }
-  const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
-  const size_t wsb = (nb + 1) * 8;          // status word per tile + the tile ticket
-  uint64_t* ws = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
-  if (st) return st;
-  st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-  if (!st) {
-    hipLaunchKernelGGL(encode_var_kernel<true>, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows,
-                       cap, ws + 1, reinterpret_cast<uint32_t*>(ws));
-    st = check_hip(hipGetLastError(), "encode_var launch");
-  }
-  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-  return st ? st : st2;
 }
 
 // Rows per encode tile so that the staged per-row inputs of a tile fit kMetaPool (always true at

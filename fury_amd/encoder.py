@@ -242,7 +242,7 @@ class RowEncoder:
 
     def encode_measured_into(self, columns: Sequence[Column], nrows: int, rows: torch.Tensor,
                              row_offsets: Optional[torch.Tensor], stream=None) -> None:
-        """Measure + encode in one device pass into a reused buffer (``rows`` capacity =
+        """Measure + encode in one call (no host sync) into a reused buffer (``rows`` capacity =
         its size): writes ``row_offsets``; when ``row_offsets[nrows]`` exceeds the capacity the
         rows did not fit (nothing past the capacity is written) — grow and call again."""
         keep: list = []

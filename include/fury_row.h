@@ -23,7 +23,7 @@
  *                           FMT/row/binary/writer/BinaryWriter.java:106-194,
  *                           FMT/row/binary/writer/BinaryRowWriter.java:76-124,
  *                           FMT/row/binary/writer/BinaryArrayWriter.java:77-118)
- *   fury_row_encode_measured both in one pass (toRow into a growable buffer, Encoders.java:88-93)
+ *   fury_row_encode_measured both in one call (toRow into a growable buffer, Encoders.java:88-93)
  *   fury_row_decode_measure the Arrow offsets fromRow/ArrowWriter would produce
  *   fury_row_decode         RowEncoder.fromRow over a batch: BinaryRow getters
  *                           (FMT/encoder/RowEncoderBuilder.java:185-217,
@@ -166,8 +166,9 @@ int fury_row_measure(const fury_schema* schema, const fury_column* columns, int6
  * nrows * fixed_size when row_offsets is NULL and the schema is fixed). */
 int fury_row_encode(const fury_schema* schema, const fury_column* columns, int64_t nrows,
                     const int64_t* row_offsets, void* rows, void* stream);
-/* Measure + encode in ONE device pass — the batch form of toRow writing into a growable
- * buffer: writes row_offsets[0..nrows] exactly as fury_row_measure and the rows into `rows`
+/* Measure + encode in one call with no host synchronisation — the batch form of toRow writing
+ * into a growable buffer: writes row_offsets[0..nrows] exactly as fury_row_measure and the rows
+ * into `rows`
  * (capacity bytes).  Bytes at or past `capacity` are never written: when row_offsets[nrows] >
  * capacity, grow the buffer and call again.  Fixed schemas know their size up front and return
  * FURY_ERR_CAPACITY instead (row_offsets may be NULL for them). */

@@ -2,9 +2,9 @@
 
     python scripts/ab_var.py [--workload mixed|nested|narrow] [--rows N] [--rounds 5] [--iters 10]
 
-Legs: measure (fury_row_measure), two-pass encode (measure + fury_row_encode), one-pass encode
-(fury_row_encode_measured), decode one-pass (look-back) and two-pass (tuning var_decode=1),
-decode_measure (sizing pass only).  Prints a
+Legs: measure (fury_row_measure), encode (fury_row_encode at known offsets), encode_measured
+(fury_row_encode_measured = measure + encode), decode one-pass (look-back) and two-pass (tuning
+var_decode=1), decode_measure (sizing pass only).  Prints a
 JSON line with the median ms of each leg and the algorithmic GB/s of the encode/decode legs.
 """
 import argparse
@@ -44,16 +44,10 @@ def main():
     sh = _stream_handle(None)
     ccols = _c_columns(out, keep)
     L = N.lib()
-    def mode(v):
-        L.fury_set_tuning(b"var_encode", v)
     legs = {
-        "measure": lambda: (mode(0), enc.measure_into(cols, n, offs)),
-        "measure_direct": lambda: (mode(1), enc.measure_into(cols, n, offs)),
-        "encode_2pass": lambda: (mode(0), enc.measure_into(cols, n, offs),
-                                 enc.encode_into(cols, n, rows, offs)),
-        "encode_2pass_direct": lambda: (mode(1), enc.measure_into(cols, n, offs),
-                                        enc.encode_into(cols, n, rows, offs)),
-        "encode_1pass": lambda: (mode(0), enc.encode_measured_into(cols, n, rows, offs)),
+        "measure": lambda: enc.measure_into(cols, n, offs),
+        "encode": lambda: enc.encode_into(cols, n, rows, offs),
+        "encode_measured": lambda: enc.encode_measured_into(cols, n, rows, offs),
         "decode_1pass": lambda: (L.fury_set_tuning(b"var_decode", 0),
                                  enc.decode_into(batch, out)),
         "decode_2pass": lambda: (L.fury_set_tuning(b"var_decode", 1),
@@ -78,21 +72,13 @@ def main():
             times[k].append(a.elapsed_time(b) / args.iters)
     enc.check_capacity(out, n)
     L.fury_set_tuning(b"var_decode", 0)
-    mode(0)
-    ref = rows.clone()
-    mode(1)
-    enc.measure_into(cols, n, offs)
-    enc.encode_into(cols, n, rows, offs)
-    torch.cuda.synchronize()
-    assert torch.equal(rows, ref), "direct encode differs from the tile encode"
-    mode(0)
+
     col_bytes = _nbytes(cols)
     row_bytes = rows.numel() + offs.numel() * 8
     med = {k: round(statistics.median(v), 4) for k, v in times.items()}
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
-                    for k in ("encode_2pass", "encode_2pass_direct", "encode_1pass", "decode_1pass",
-                              "decode_2pass")}}
+                    for k in ("encode", "encode_measured", "decode_1pass", "decode_2pass")}}
     print(json.dumps(res), flush=True)
 
 
