@@ -586,14 +586,17 @@ __global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
   const int64_t rbeg = offs[r0];
   const int64_t bytes = offs[r0 + nr] - rbeg;
   const int64_t r = r0 + threadIdx.x;
-  // stage the group's contiguous row range (16-B coalesced loads) so the per-row slot reads
+  // stage the group's contiguous row range (LDS-DMA, 16-B pieces) so the per-row slot reads
   // below hit LDS instead of scattered HBM lines
-  const bool staged = bytes <= kDecodeStage;
+  const bool staged = bytes + 32 <= kDecodeStage;
+  uint32_t d0 = 0;
   if (staged) {
-    copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
+    uint32_t at = 0;
+    d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
     __syncthreads();
   }
-  const uint8_t* row = r < a.nrows ? (staged ? stage + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
+  const uint8_t* row =
+      r < a.nrows ? (staged ? stage + d0 + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
@@ -934,10 +937,11 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   const int64_t rbeg = offs[r0];
   const int64_t bytes = offs[r0 + nr] - rbeg;
   if (threadIdx.x < nr) sh.rowoff[threadIdx.x] = offs[r0 + threadIdx.x] - rbeg;
-  if (bytes <= kDecodeStage) {
-    copy_range<false>(const_cast<uint8_t*>(rows + rbeg), stage, bytes);
+  if (bytes + 32 <= kDecodeStage) {          // LDS-DMA: every piece in flight at once
+    uint32_t at = 0;
+    const uint32_t d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
     __syncthreads();
-    decode_group<true, kLookBack>(a, stage, oimg, sh, b, gridDim.x, nr, status, nseq);
+    decode_group<true, kLookBack>(a, stage + d0, oimg, sh, b, gridDim.x, nr, status, nseq);
   } else {
     __syncthreads();
     decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
