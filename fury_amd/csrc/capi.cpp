@@ -149,6 +149,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   }
   a->nvar = nvar;
   a->tile_rows = encode_tile_rows(*a);
+  if (const char* e = getenv("FURY_VAR_DBG")) a->dbg = atoi(e);
   return FURY_OK;
 }
 

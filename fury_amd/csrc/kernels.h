@@ -62,7 +62,7 @@ struct VarArgs {
   int32_t nvar;
   int64_t nrows;
   int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
-  int32_t pad_;
+  int32_t dbg;               // DIAGNOSTIC phase-skip bits (FURY_VAR_DBG), 0 in production
 };
 
 // Device scratch for scans; grown on demand (hipMalloc outside graph capture only).

@@ -92,6 +92,25 @@ __device__ __forceinline__ void copy_to_aligned(uint64_t* dst, const uint8_t* sr
   if (len <= 0) return;
   const uintptr_t s = reinterpret_cast<uintptr_t>(src) & 7;
   const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s);
+  if (len <= 32) {
+    // short string: every source word is requested before any is used (one memory latency
+    // instead of one per word); words past the last source byte are not read
+    const int nsrc = static_cast<int>((s + len + 7) >> 3);       // <= 5
+    uint64_t w[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) w[j] = j < nsrc ? ap[j] : 0;
+    const int nw = static_cast<int>((len + 7) >> 3);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      if (k < nw) {
+        uint64_t x = s ? (w[k] >> (8 * s)) | (w[k + 1] << (64 - 8 * s)) : w[k];
+        const int64_t rem = len - 8 * k;
+        if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
+        dst[k] = x;
+      }
+    }
+    return;
+  }
   const int64_t nw = (len + 7) >> 3;
   const int64_t last_src_word = (static_cast<int64_t>(s) + len - 1) >> 3;
   uint64_t lo = ap[0];
@@ -229,14 +248,6 @@ __global__ __launch_bounds__(kThreads) void add_groups(int64_t* __restrict__ s, 
   if (i < n) s[i] += gpre[blockIdx.x];
 }
 
-__global__ __launch_bounds__(kThreads) void add_block_prefix(int64_t* __restrict__ offs, int64_t n,
-                                                             const int64_t* __restrict__ prefix,
-                                                             const int64_t* __restrict__ total) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r < n) offs[r] += prefix[blockIdx.x];
-  if (r == n - 1) offs[n] = *total;
-}
-
 // --- cross-workgroup scan (decoupled look-back) ---------------------------------------------
 constexpr int kSeqChunk = 8;                          // var outputs resolved per look-back round
 constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
@@ -287,6 +298,11 @@ constexpr int kEncPool = 50 * 1024;           // LDS: staged inputs + row image 
 constexpr int kMetaPool = 16 * 1024;          // bound on a tile's staged per-row inputs
 constexpr uint32_t kNone = 0xffffffffu;
 
+struct PipeLayout {
+  int rows;                   // rows per tile
+  uint32_t msz, psz, isz;     // LDS bytes: meta slot, payload slot, row image
+};
+
 // LDS byte offsets of one tile's staged inputs, per column (kNone = not present / not staged).
 struct MetaMap {
   uint32_t fix[kMaxVarCols];   // fixed values (row r0) / bool bits (byte r0/8) / decimal values
@@ -301,12 +317,12 @@ struct MetaMap {
 // never leaves the pages holding the range.
 template <int NT>
 __device__ __forceinline__ uint32_t stage_range(uint8_t* pool, uint32_t& at, const uint8_t* gb,
-                                                const uint8_t* ge) {
+                                                const uint8_t* ge, bool issue = true) {
   const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
   const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
   const uint32_t nch = static_cast<uint32_t>((hi - lo) >> 4);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t i0 = wave * 64; i0 < nch; i0 += NT) {
+  for (uint32_t i0 = wave * 64; issue && i0 < nch; i0 += NT) {
     if (i0 + lane < nch)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * (i0 + lane)),
                                        pool + at + 16 * i0, 16, 0, 0);
@@ -326,8 +342,7 @@ __device__ __forceinline__ bool lds_bit(const uint8_t* pool, uint32_t off, int64
 // Phase A: stage every column's per-row inputs of rows [r0, r0 + nr).
 template <int NT>
 __device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int64_t nr,
-                                               uint8_t* pool, MetaMap& mm) {
-  uint32_t at = 0;
+                                               uint8_t* pool, MetaMap& mm, uint32_t at = 0) {
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
     uint32_t fix = kNone, val = kNone, off = kNone;
@@ -400,17 +415,18 @@ __device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MetaMap
 template <int NT>
 __device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, uint8_t* pool,
                                                uint32_t at, int nr) {
+  const bool iss = !(a.dbg & 1);
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = a.col[k];
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
     uint32_t pay = kNone, pvb = kNone;
     if (e > b) {
-      if (c.kind == kBytes) pay = stage_range<NT>(pool, at, c.values + b, c.values + e);
-      else if (c.width == 0) pay = stage_range<NT>(pool, at, c.values + (b >> 3), c.values + ((e + 7) >> 3));
-      else pay = stage_range<NT>(pool, at, c.values + b * c.width, c.values + e * c.width);
+      if (c.kind == kBytes) pay = stage_range<NT>(pool, at, c.values + b, c.values + e, iss);
+      else if (c.width == 0) pay = stage_range<NT>(pool, at, c.values + (b >> 3), c.values + ((e + 7) >> 3), iss);
+      else pay = stage_range<NT>(pool, at, c.values + b * c.width, c.values + e * c.width, iss);
       if (c.kind == kListFixed && c.elem_validity)
-        pvb = stage_range<NT>(pool, at, c.elem_validity + (b >> 3), c.elem_validity + ((e + 7) >> 3));
+        pvb = stage_range<NT>(pool, at, c.elem_validity + (b >> 3), c.elem_validity + ((e + 7) >> 3), iss);
     }
     if (threadIdx.x == 0) {
       mm.pay[k] = pay;
@@ -420,10 +436,11 @@ __device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, ui
 }
 
 // Builds tile row t at dst (8-byte aligned) exactly as toRow does.  Per-row inputs come from the
-// staged meta; payloads from LDS when kPayLds, else straight from global memory.
-template <bool kPayLds>
+// staged meta in `pool`; a column's payload from `pay` when it was staged (mm.pay[k] != kNone),
+// else straight from global memory.
 __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& mm,
-                                               const uint8_t* pool, int t, uint8_t* dst) {
+                                               const uint8_t* pool, const uint8_t* pay, int t,
+                                               uint8_t* dst) {
   uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
   const int nslot0 = a.bitmap_bytes >> 3;
   int64_t cursor = a.fixed_size;
@@ -452,7 +469,7 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
           const int64_t ob = lds_i32(pool, mm.off[k]);
           const int64_t o0 = lds_i32(pool, mm.off[k] + 4 * t);
           const int64_t len = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - o0;
-          const uint8_t* src = kPayLds ? pool + mm.pay[k] + (o0 - ob) : c.values + o0;
+          const uint8_t* src = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0 - ob) : c.values + o0;
           copy_to_aligned(d64 + (cursor >> 3), src, len);
           slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
           cursor += rnd8(len);
@@ -473,11 +490,11 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
           const uint8_t* vals;
           const uint8_t* vb = nullptr;
           if (c.width == 0)
-            vals = kPayLds ? pool + mm.pay[k] + ((o0 >> 3) - (ob >> 3)) : c.values + (o0 >> 3);
+            vals = mm.pay[k] != kNone ? pay + mm.pay[k] + ((o0 >> 3) - (ob >> 3)) : c.values + (o0 >> 3);
           else
-            vals = kPayLds ? pool + mm.pay[k] + (o0 - ob) * c.width : c.values + o0 * c.width;
+            vals = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0 - ob) * c.width : c.values + o0 * c.width;
           if (c.elem_validity)
-            vb = kPayLds ? pool + mm.pvb[k] + ((o0 >> 3) - (ob >> 3)) : c.elem_validity + (o0 >> 3);
+            vb = mm.pvb[k] != kNone ? pay + mm.pvb[k] + ((o0 >> 3) - (ob >> 3)) : c.elem_validity + (o0 >> 3);
           const int64_t sz = write_array(dst + cursor, c.width, vals, vb, o0 & 7, n);
           slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
           cursor += sz;
@@ -490,17 +507,66 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
   d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
 }
 
+// DIAGNOSTIC: build_tile_row with the column kinds known at compile time (experiment on the
+// cost of interpreting the schema at run time).
+struct SpecMixed {
+  static constexpr int n = 6;
+  static constexpr int kind[6] = {kFixed, kFixed, kFixed, kBytes, kBytes, kBytes};
+  static constexpr int width[6] = {4, 8, 8, 1, 1, 1};
+};
+template <class S>
+__device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MetaMap& mm,
+                                                    const uint8_t* pool, const uint8_t* pay, int t,
+                                                    uint8_t* dst) {
+  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
+  const int nslot0 = a.bitmap_bytes >> 3;
+  int64_t cursor = a.fixed_size;
+  uint64_t nullbits = 0;
+  bool ok[S::n];
+  uint64_t fixv[S::n];
+  int32_t o0[S::n], o1[S::n], ob[S::n];
+#pragma unroll
+  for (int k = 0; k < S::n; k++) {
+    ok[k] = mm.val[k] == kNone || lds_bit(pool, mm.val[k], t);
+    if (S::kind[k] == kFixed) {
+      const uint8_t* p = pool + mm.fix[k] + t * S::width[k];
+      fixv[k] = S::width[k] == 8 ? *reinterpret_cast<const uint64_t*>(p)
+                                 : *reinterpret_cast<const uint32_t*>(p);
+    } else {
+      ob[k] = lds_i32(pool, mm.off[k]);
+      o0[k] = lds_i32(pool, mm.off[k] + 4 * t);
+      o1[k] = lds_i32(pool, mm.off[k] + 4 * (t + 1));
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < S::n; k++) {
+    const VarCol& c = a.col[k];
+    uint64_t slot = 0;
+    if (!ok[k]) {
+      nullbits |= 1ull << k;
+    } else if (S::kind[k] == kFixed) {
+      slot = fixv[k];
+    } else {
+      const int64_t len = o1[k] - o0[k];
+      const uint8_t* src = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0[k] - ob[k]) : c.values + o0[k];
+      copy_to_aligned(d64 + (cursor >> 3), src, len);
+      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
+      cursor += rnd8(len);
+    }
+    d64[nslot0 + k] = slot;
+  }
+  d64[0] = nullbits;
+}
+
 // Encode workgroup: rows [r0, r0 + R) at the offsets fury_row_measure produced.  Bytes at or
 // past `cap` are never written.
-__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
-                                                              const int64_t* __restrict__ offs,
-                                                              uint8_t* __restrict__ rows,
-                                                              int64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
-  __shared__ MetaMap mm;
+template <int POOL, bool kStagePay>
+__device__ __forceinline__ void encode_tile(const VarArgs& a, const int64_t* __restrict__ offs,
+                                            uint8_t* __restrict__ rows, int64_t cap, int64_t tile,
+                                            uint8_t* pool, MetaMap& mm) {
   const int tid = threadIdx.x;
   const int R = a.tile_rows;                 // rows per tile (host-chosen so the meta fits)
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t r0 = tile * R;
   const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
   const bool live = tid < nr;
   // the offset loads go out together with the meta DMA
@@ -510,27 +576,405 @@ __global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
   const uint32_t img_at = stage_meta<kEncRows>(a, r0, nr, pool, mm);
   __syncthreads();
   const uint64_t img = static_cast<uint64_t>((bytes + 15) & ~int64_t(15));
-  const bool img_fits = img_at + img <= kEncPool;
-  const bool pay_fits = img_fits && img_at + img + payload_need(a, mm, pool, nr) <= kEncPool;
-  if (pay_fits) stage_payloads<kEncRows>(a, mm, pool, static_cast<uint32_t>(img_at + img), nr);
-  __syncthreads();
+  const bool img_fits = img_at + img <= POOL;
+  const bool pay_fits =
+      kStagePay && img_fits && img_at + img + payload_need(a, mm, pool, nr) <= POOL;
+  if (pay_fits) {
+    stage_payloads<kEncRows>(a, mm, pool, static_cast<uint32_t>(img_at + img), nr);
+    __syncthreads();
+  }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (img_fits) {
     uint8_t* image = pool + img_at;
-    if (live) {
-      if (pay_fits) build_tile_row<true>(a, mm, pool, tid, image + ex);
-      else build_tile_row<false>(a, mm, pool, tid, image + ex);
+    if (live && (a.dbg & 256)) {
+      build_tile_row_spec<SpecMixed>(a, mm, pool, pool, tid, image + ex);
+    } else if (live && !(a.dbg & 2)) {
+      build_tile_row(a, mm, pool, pool, tid, image + ex);
     }
     __syncthreads();
-    copy_range<true, kEncRows>(rows + base, image, room);
+    if (!(a.dbg & 4)) copy_range<true, kEncRows>(rows + base, image, room);
   } else if (live && ex + tile_row_size(a, mm, pool, tid) <= room) {
-    build_tile_row<false>(a, mm, pool, tid, rows + base + ex);   // oversized tile: straight to HBM
+    build_tile_row(a, mm, pool, pool, tid, rows + base + ex);    // oversized tile: straight to HBM
   }
 }
 
-// ---- measure: row sizes (writerIndex growth of toRow) + block scan, one thread per row.  Reads
-// only validity bits and offsets; plain loads at full occupancy (no LDS) measured faster here than
-// LDS-DMA staging of the same inputs.
+__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
+                                                              const int64_t* __restrict__ offs,
+                                                              uint8_t* __restrict__ rows,
+                                                              int64_t cap) {
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
+  __shared__ MetaMap mm;
+  encode_tile<kEncPool, true>(a, offs, rows, cap, blockIdx.x, pool, mm);
+}
+
+// Payloads read straight from global memory (no payload staging): a smaller LDS pool, so more
+// workgroups share a CU.
+constexpr int kEncPoolDirect = 38 * 1024;
+__global__ __launch_bounds__(kEncRows) void encode_var_kernel_d(VarArgs a,
+                                                                const int64_t* __restrict__ offs,
+                                                                uint8_t* __restrict__ rows,
+                                                                int64_t cap) {
+  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPoolDirect];
+  __shared__ MetaMap mm;
+  encode_tile<kEncPoolDirect, false>(a, offs, rows, cap, blockIdx.x, pool, mm);
+}
+
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Waits until at most n of this wave's vector-memory operations are outstanding (n uniform).
+// The n youngest are the image stores just issued, so every older operation — the next tile's
+// LDS-DMA — has landed, while the stores keep draining.
+__device__ __forceinline__ void wait_vm_le(int n) {
+  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
+#define FURY_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    FURY_VMW(0) FURY_VMW(1) FURY_VMW(2) FURY_VMW(3) FURY_VMW(4) FURY_VMW(5) FURY_VMW(6)
+    FURY_VMW(7) FURY_VMW(8) FURY_VMW(9) FURY_VMW(10) FURY_VMW(11) FURY_VMW(12) FURY_VMW(13)
+    FURY_VMW(14) FURY_VMW(15)
+#undef FURY_VMW
+  }
+}
+
+// Stores img[0, bytes) to g (any alignment): each wave writes a contiguous quarter of the 16-byte
+// aligned body with 16-B non-temporal stores, wave 0 the unaligned head and wave 3 the tail by
+// single-byte lanes.  Returns the number of store instructions this wave issued (uniform).
+__device__ __forceinline__ int store_image(uint8_t* g, const uint8_t* img, int64_t bytes) {
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (bytes <= 0) return 0;
+  const int64_t head = min<int64_t>(bytes, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
+  const int64_t body = (bytes - head) >> 4;
+  const int64_t tail = bytes - head - 16 * body;
+  int cnt = 0;
+  if (head > 0 && wave == 0) {
+    if (lane < head) g[lane] = img[lane];
+    cnt++;
+  }
+  const int64_t q = (body + 3) >> 2;
+  const int64_t j0 = wave * q, j1 = min<int64_t>(body, j0 + q);
+  for (int64_t j = j0; j < j1; j += 64) {
+    const int64_t i = j + lane;
+    if (i < j1) {
+      const uint8_t* lp = img + head + 16 * i;
+      const uint64_t x = reinterpret_cast<const uint64_t*>(lp)[0];
+      const uint64_t y = reinterpret_cast<const uint64_t*>(lp)[1];
+      v4 v;
+      v.x = static_cast<uint32_t>(x); v.y = static_cast<uint32_t>(x >> 32);
+      v.z = static_cast<uint32_t>(y); v.w = static_cast<uint32_t>(y >> 32);
+      __builtin_nontemporal_store(v, reinterpret_cast<v4*>(g + head + 16 * i));
+    }
+    cnt++;
+  }
+  if (tail > 0 && wave == 3) {
+    const int64_t t0 = head + 16 * body;
+    if (lane < tail) g[t0 + lane] = img[t0 + lane];
+    cnt++;
+  }
+  return cnt;
+}
+
+// ---- register-staged encode (schemas of <= kRegCols fields) -----------------------------------
+// One workgroup builds one tile of R rows (thread = row) into an LDS image of the tile's
+// contiguous output range, then stores it with 16-B stores.  The per-row inputs of every column
+// are loaded straight into registers (the column count is a template parameter, so the per-column
+// values live in VGPRs and all the loads are issued together: one HBM round trip), and the
+// string / decimal / list bytes are then read from global memory by their row's thread (a second
+// round trip, issued for all columns at once).  LDS holds only the image, so five workgroups
+// share a CU.
+constexpr int kRegCols = 16;
+constexpr int kRegImg = 30 * 1024;
+
+// Copies len bytes at global src to 8-byte aligned dst (LDS or global) as whole words, zero pad.
+template <typename D>
+__device__ __forceinline__ void put_string(D* dst, const uint8_t* src, int64_t len) {
+  if (len <= 0) return;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src) & 7;
+  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s);
+  const int64_t nw = (len + 7) >> 3;
+  const int64_t nsrc = (static_cast<int64_t>(s) + len + 7) >> 3;
+  for (int64_t k0 = 0; k0 < nw; k0 += 4) {
+    uint64_t w[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) w[j] = k0 + j < nsrc ? ap[k0 + j] : 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int64_t k = k0 + j;
+      if (k < nw) {
+        uint64_t x = s ? (w[j] >> (8 * s)) | (w[j + 1] << (64 - 8 * s)) : w[j];
+        const int64_t rem = len - 8 * k;
+        if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
+        dst[k] = x;
+      }
+    }
+  }
+}
+
+// 64 bits of a bitmap starting at bit i, reading only the aligned words that hold wanted bits
+// (bits past `lim` are garbage).
+__device__ __forceinline__ uint64_t load_bits64(const uint8_t* bits, int64_t i, int lim) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(bits) + (i >> 3);
+  const uint64_t* a = reinterpret_cast<const uint64_t*>(addr & ~uintptr_t(7));
+  const int sh = static_cast<int>((addr & 7) * 8 + (i & 7));
+  const uint64_t lo = a[0];
+  if (sh == 0) return lo;
+  const uint64_t hi = sh + lim > 64 ? a[1] : 0;
+  return (lo >> sh) | (hi << (64 - sh));
+}
+
+// BinaryArrayWriter image of n elements read from global memory (register-staged encode):
+// element values and validity words are fetched in batches so their loads overlap.
+template <typename D>
+__device__ __forceinline__ int64_t put_array(D* d64, int width, const uint8_t* vals,
+                                             const uint8_t* vbits, int64_t vbit0, int64_t n) {
+  const int ew = width == 0 ? 1 : width;
+  const int64_t nbw = (n + 63) >> 6;
+  d64[0] = static_cast<uint64_t>(n);
+  for (int64_t w = 0; w < nbw; w++) {
+    const int lim = static_cast<int>(min<int64_t>(64, n - 64 * w));
+    const uint64_t valid = vbits ? load_bits64(vbits, vbit0 + 64 * w, lim) : ~0ull;
+    const uint64_t m = lim == 64 ? ~0ull : ((1ull << lim) - 1);
+    d64[1 + w] = ~valid & m;                            // bit = 1 null
+  }
+  D* out = d64 + 1 + nbw;
+  if (ew == 8) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(vals);
+    for (int64_t j0 = 0; j0 < n; j0 += 8) {
+      const int lim = static_cast<int>(min<int64_t>(8, n - j0));
+      const uint64_t vm = vbits ? load_bits64(vbits, vbit0 + j0, lim) : ~0ull;
+      uint64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) x[u] = u < lim ? src[j0 + u] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        if (u < lim) out[j0 + u] = ((vm >> u) & 1) ? x[u] : 0;
+    }
+    return 8 * (1 + nbw + n);
+  }
+  const int per = 8 / ew;
+  const int64_t nw = (n * ew + 7) >> 3;
+  for (int64_t q = 0; q < nw; q++) {
+    const int lim = static_cast<int>(min<int64_t>(per, n - q * per));
+    const uint64_t vm = vbits ? load_bits64(vbits, vbit0 + q * per, lim) : ~0ull;
+    uint64_t word = 0;
+    for (int t = 0; t < lim; t++) {
+      const int64_t j = q * per + t;
+      if (!((vm >> t) & 1)) continue;                  // null element stays 0
+      uint64_t x;
+      switch (width) {
+        case 4: x = reinterpret_cast<const uint32_t*>(vals)[j]; break;
+        case 2: x = reinterpret_cast<const uint16_t*>(vals)[j]; break;
+        case 1: x = vals[j]; break;
+        default: x = bit_at(vals, vbit0 + j); break;   // bool: bit-packed, same bit origin
+      }
+      word |= x << (8 * ew * t);
+    }
+    out[q] = word;
+  }
+  return 8 * (1 + nbw + nw);
+}
+
+// Builds row r (tile thread t) at d64 from the register-staged inputs.
+template <int K, typename D>
+__device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const uint64_t* v,
+                                              uint64_t valid, D* d64) {
+  const int nslot0 = a.bitmap_bytes >> 3;
+  int64_t cursor = a.fixed_size;
+  uint64_t nullbits = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    uint64_t slot = 0;
+    if (!((valid >> k) & 1)) {
+      nullbits |= 1ull << k;
+    } else if (c.kind == kFixed || c.kind == kBool) {
+      slot = v[k];
+    } else if (c.kind == kBytes) {
+      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
+      const int64_t len = o1 - o0;
+      put_string(d64 + (cursor >> 3), c.values + o0, len);
+      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
+      cursor += rnd8(len);
+    } else if (c.kind == kDecimal) {
+      const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values) + 2 * r;
+      d64[cursor >> 3] = s[0];
+      d64[(cursor >> 3) + 1] = s[1];
+      slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
+      cursor += 16;
+    } else {   // kListFixed
+      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
+      const int64_t n = o1 - o0;
+      const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + int64_t(o0) * c.width;
+      const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
+      const int64_t sz = put_array(d64 + (cursor >> 3), c.width, vals, vb, o0 & 7, n);
+      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
+      cursor += sz;
+    }
+    d64[nslot0 + k] = slot;
+  }
+  d64[0] = nullbits;
+}
+
+template <int K>
+__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
+                                                           const int64_t* __restrict__ offs,
+                                                           uint8_t* __restrict__ rows, int64_t cap) {
+  __shared__ __attribute__((aligned(16))) uint64_t img[kRegImg / 8];
+  const int tid = threadIdx.x;
+  const int R = a.tile_rows;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t r = live ? r0 + tid : r0;
+  const int64_t base = offs[r0];
+  const int64_t bytes = offs[r0 + nr] - base;
+  const int64_t ex = offs[r] - base;
+  // per-row inputs of every column: one batch of independent loads
+  uint64_t v[K];
+  uint64_t valid = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    const bool ok = !c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1);
+    valid |= static_cast<uint64_t>(ok) << k;
+    uint64_t x = 0;
+    switch (c.kind) {
+      case kFixed: x = load_fixed(c.values, r, c.width); break;
+      case kBool: x = bit_at(c.values, r); break;
+      case kBytes:
+      case kListFixed:
+        x = static_cast<uint32_t>(c.offsets[r]) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(c.offsets[r + 1])) << 32);
+        break;
+      default: break;
+    }
+    v[k] = x;
+  }
+  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
+  if (bytes <= kRegImg) {
+    if (live) reg_build_row<K>(a, r, v, valid, img + (ex >> 3));
+    __syncthreads();
+    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
+  } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
+    const int64_t sz = offs[r + 1] - offs[r];
+    if (ex + sz <= room) reg_build_row<K>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
+  }
+}
+
+// ---- pipelined encode ------------------------------------------------------------------------
+// A fixed grid of resident workgroups (2 per CU) walks the tiles t = blockIdx.x + i * gridDim.x.
+// Each workgroup double-buffers its inputs: while tile t is built from slot s and stored, the
+// LDS-DMA of tile t + gridDim.x (its row offsets, per-row inputs and payload ranges) is already in
+// flight into slot s ^ 1, so one HBM round trip per tile is overlapped with the build instead of
+// two being waited for.  The payload ranges of the next tile come from scalar loads of the two
+// bounding string/list offsets, so they do not wait for that tile's meta to land.
+struct PipeSlot {
+  MetaMap mm;
+  uint32_t offs_at;          // LDS offset (in the meta slot) of the staged offs[r0]
+  uint32_t pad_;
+};
+
+template <int NT>
+__device__ __forceinline__ void pipe_issue(const VarArgs& a, const int64_t* __restrict__ offs,
+                                           int64_t t, uint8_t* meta, uint8_t* pay, uint32_t psz,
+                                           PipeSlot& ps) {
+  const int R = a.tile_rows;
+  const int64_t r0 = t * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
+  uint32_t at = 0;
+  const uint32_t oa = stage_range<NT>(meta, at, reinterpret_cast<const uint8_t*>(offs + r0),
+                                      reinterpret_cast<const uint8_t*>(offs + r0 + nr + 1));
+  stage_meta<NT>(a, r0, nr, meta, ps.mm, at);        // sets every mm.pay / mm.pvb to kNone
+  uint32_t pat = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
+    if (e <= b) continue;
+    const uint8_t *gb, *ge;
+    if (c.kind == kBytes) { gb = c.values + b; ge = c.values + e; }
+    else if (c.width == 0) { gb = c.values + (b >> 3); ge = c.values + ((e + 7) >> 3); }
+    else { gb = c.values + b * c.width; ge = c.values + e * c.width; }
+    const bool vb = c.kind == kListFixed && c.elem_validity;
+    const uint8_t* vgb = vb ? c.elem_validity + (b >> 3) : nullptr;
+    const uint8_t* vge = vb ? c.elem_validity + ((e + 7) >> 3) : nullptr;
+    auto span = [](const uint8_t* x, const uint8_t* y) -> uint64_t {
+      return ((reinterpret_cast<uint64_t>(y) + 15) & ~uint64_t(15)) -
+             (reinterpret_cast<uint64_t>(x) & ~uint64_t(15));
+    };
+    const uint64_t need = span(gb, ge) + (vb ? span(vgb, vge) : 0);
+    if (pat + need > psz) continue;                   // this column reads global memory
+    const uint32_t pa = stage_range<NT>(pay, pat, gb, ge);
+    const uint32_t pv = vb ? stage_range<NT>(pay, pat, vgb, vge) : kNone;
+    if (threadIdx.x == 0) {
+      ps.mm.pay[k] = pa;
+      ps.mm.pvb[k] = pv;
+    }
+  }
+  if (threadIdx.x == 0) ps.offs_at = oa;
+}
+
+__device__ __forceinline__ int pipe_build_store(const VarArgs& a, uint8_t* __restrict__ rows,
+                                                 int64_t cap, int64_t t, const uint8_t* meta,
+                                                 const uint8_t* pay, uint8_t* img, uint32_t isz,
+                                                 const PipeSlot& ps) {
+  const int tid = threadIdx.x;
+  const int R = a.tile_rows;
+  const int64_t r0 = t * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t* so = reinterpret_cast<const int64_t*>(meta + ps.offs_at);
+  const int64_t base = so[0];
+  const int64_t bytes = so[nr] - base;
+  const int64_t ex = live ? so[tid] - base : 0;
+  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
+  if (bytes + 16 <= isz) {
+    if (live) build_tile_row(a, ps.mm, meta, pay, tid, img + ex);
+    __syncthreads();
+    return store_image(rows + base, img, room);
+  }
+  if (live && ex + tile_row_size(a, ps.mm, meta, tid) <= room)
+    build_tile_row(a, ps.mm, meta, pay, tid, rows + base + ex);   // oversized tile: straight to HBM
+  return 0;                                                       // wait for everything
+}
+
+__global__ __launch_bounds__(kEncRows) void encode_var_pipe(VarArgs a,
+                                                            const int64_t* __restrict__ offs,
+                                                            uint8_t* __restrict__ rows,
+                                                            int64_t cap, int64_t ntiles,
+                                                            uint32_t msz, uint32_t psz,
+                                                            uint32_t isz) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  __shared__ PipeSlot ps[2];
+  uint8_t* img = lds + 2 * msz + 2 * psz;
+  int64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  int s = 0;
+  pipe_issue<kEncRows>(a, offs, t, lds, lds + 2 * msz, psz, ps[0]);
+  wait_dma();
+  __syncthreads();
+  for (;;) {
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles)
+      pipe_issue<kEncRows>(a, offs, tn, lds + (s ^ 1) * msz, lds + 2 * msz + (s ^ 1) * psz, psz,
+                           ps[s ^ 1]);
+    const int nst =
+        pipe_build_store(a, rows, cap, t, lds + s * msz, lds + 2 * msz + s * psz, img, isz, ps[s]);
+    wait_vm_le(nst);
+    __syncthreads();
+    if (tn >= ntiles) break;
+    t = tn;
+    s ^= 1;
+  }
+}
+
+// ---- measure: row sizes (writerIndex growth of toRow) and their exclusive scan.  Each thread
+// sizes 4 consecutive rows (one validity nibble and 5 consecutive offsets per column), so a
+// 256-thread workgroup covers 1,024 rows and writes their group-relative exclusive offsets and its
+// total; a device scan of the (few) group totals and one add pass finish the scan.  (A single
+// pass with a decoupled look-back was measured slower: the ticket atomic that orders the
+// workgroups serialises at this workgroup count.)
+constexpr int kMeasRows = 4;                                   // rows per thread
+constexpr int kMeasTile = kThreads * kMeasRows;                // rows per workgroup
+
 __device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
@@ -548,15 +992,60 @@ __device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   return sz;
 }
 
-__global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a,
-                                                                  int64_t* __restrict__ offs,
-                                                                  int64_t* __restrict__ block_sums) {
+__global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
+                                                           int64_t* __restrict__ gsum) {
   __shared__ int64_t tmp[kThreads / 64];
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t r = b * kMeasTile + kMeasRows * threadIdx.x;   // first of this thread's rows
+  int64_t sz[kMeasRows];
+  if (r + kMeasRows <= a.nrows) {                 // whole quad: vector-friendly straight line
+#pragma unroll
+    for (int j = 0; j < kMeasRows; j++) sz[j] = a.fixed_size;
+    for (int k = 0; k < a.ncols; k++) {
+      const VarCol& c = a.col[k];
+      if (c.kind < kBytes) continue;
+      const uint32_t vb = c.validity ? (c.validity[r >> 3] >> (r & 7)) : 0xffu;
+      if (c.kind == kDecimal) {
+#pragma unroll
+        for (int j = 0; j < kMeasRows; j++) sz[j] += ((vb >> j) & 1) ? 16 : 0;
+        continue;
+      }
+      int32_t o[kMeasRows + 1];
+#pragma unroll
+      for (int j = 0; j <= kMeasRows; j++) o[j] = c.offsets[r + j];
+#pragma unroll
+      for (int j = 0; j < kMeasRows; j++) {
+        const int64_t n = o[j + 1] - o[j];
+        const int64_t add = c.kind == kBytes ? rnd8(n)
+                                             : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+        sz[j] += ((vb >> j) & 1) ? add : 0;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kMeasRows; j++) sz[j] = r + j < a.nrows ? row_size_of(a, r + j) : 0;
+  }
+  int64_t loc[kMeasRows], run = 0;
+#pragma unroll
+  for (int j = 0; j < kMeasRows; j++) {
+    loc[j] = run;
+    run += sz[j];
+  }
   int64_t total;
-  const int64_t ex = block_excl_scan(r < a.nrows ? row_size_of(a, r) : 0, &total, tmp);
-  if (r < a.nrows) offs[r] = ex;
-  if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+  const int64_t ex = block_excl_scan(run, &total, tmp);
+#pragma unroll
+  for (int j = 0; j < kMeasRows; j++)
+    if (r + j < a.nrows) offs[r + j] = ex + loc[j];
+  if (threadIdx.x == 0) gsum[b] = total;
+}
+
+// offs[r] += prefix of r's measure group; offs[n] = total.
+__global__ __launch_bounds__(kThreads) void add_group_prefix(int64_t* __restrict__ offs, int64_t n,
+                                                             const int64_t* __restrict__ prefix,
+                                                             const int64_t* __restrict__ total) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (r < n) offs[r] += prefix[r / kMeasTile];
+  if (r == n - 1) offs[n] = *total;
 }
 
 // --- decode side -------------------------------------------------------------------------------
@@ -769,7 +1258,7 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
     return;
   }
   for (int q = w; q < nchunk; q += kThreads / 64) {
-    const int64_t ex = b == 0 ? 0 : look_back(status, b, nseq, cbase + q);
+    const int64_t ex = (b == 0 || (a.dbg & 32)) ? 0 : look_back(status, b, nseq, cbase + q);
     if (lane == 0) {
       sh.base[q] = ex;
       if (b > 0)
@@ -796,7 +1285,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
   if (kLookBack && nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
 
   // fixed-width fields and every field's validity: no dependency on other groups
-  for (int k = 0; k < a.ncols; k++) {
+  for (int k = 0; k < ((a.dbg & 8) ? 0 : a.ncols); k++) {
     const VarCol& c = a.col[k];
     const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
     const uint64_t slot =
@@ -849,7 +1338,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
       if (live) c.offsets[r] = static_cast<int32_t>(gb + sh.pos[q][tid]);
       if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot);
       uint8_t* dst = const_cast<uint8_t*>(c.values);
-      if (tot == 0 || !dst) continue;
+      if (tot == 0 || !dst || (a.dbg & 16)) continue;
       const int64_t cap = c.capacity;
       if (c.kind == kBytes) {
         const int64_t p0 = gb, p1 = gb + tot;
@@ -927,11 +1416,11 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
   __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
   __shared__ DecodeShared sh;
-  if (kLookBack) {
+  if (kLookBack && !(a.dbg & 64)) {
     if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
     __syncthreads();
   }
-  const int64_t b = kLookBack ? sh.blk : blockIdx.x;
+  const int64_t b = (kLookBack && !(a.dbg & 64)) ? sh.blk : blockIdx.x;
   const int64_t r0 = b * kThreads;
   const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
   const int64_t rbeg = offs[r0];
@@ -1044,27 +1533,129 @@ void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t
 int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t n = a.nrows;
   if (n == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
-  const int64_t nb = nblocks(n);
-  int64_t* ws = nullptr;
+  const int64_t nb = (n + kMeasTile - 1) / kMeasTile;
+  int64_t* ws = nullptr;          // [group sums x nb][total][scan scratch]
   const int64_t wsn = nb + 1 + scan_workspace(nb);
   int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
                      "hipMallocAsync");
   if (st) return st;
   hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
   device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
-  hipLaunchKernelGGL(add_block_prefix, dim3(nb), dim3(kThreads), 0, stream, offs, n, ws, ws + nb);
+  hipLaunchKernelGGL(add_group_prefix, dim3(nblocks(n)), dim3(kThreads), 0, stream, offs, n, ws,
+                     ws + nb);
   st = check_hip(hipGetLastError(), "measure launch");
-  int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
+  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
 }
 
 int var_decode_mode() { return g_var_decode; }
 void set_var_decode_mode(int v) { g_var_decode = v; }
+// LDS plan of the pipelined encode: per workgroup 2 meta slots + 2 payload slots + 1 row image
+// within kPipeLds, so kPipeGroupsPerCU workgroups share a CU.  Payload and row sizes are
+// estimated from the input buffers' byte counts (fury_column.capacity; 32 B per string when
+// unknown) with headroom; a tile whose payload or image does not fit reads / writes global
+// memory directly for that part, so the plan affects speed only.
+constexpr int kPipeGroupsPerCU = 2;
+constexpr int64_t kPipeLds = 77 * 1024;
+
+static int64_t r16(int64_t x) { return (x + 15) & ~int64_t(15); }
+
+bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
+  if (a.nrows <= 0) return false;
+  double pay_row = 0, img_row = a.fixed_size;
+  int nvarc = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind == kDecimal) img_row += 16;
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    nvarc++;
+    const double per = c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
+    if (c.kind == kBytes) {
+      pay_row += per;
+      img_row += per + 7;
+    } else {
+      const double ew = c.width == 0 ? 0.125 : c.width;
+      pay_row += per * ew + (c.elem_validity ? per / 8 : 0);
+      img_row += 16 + per * (c.width == 0 ? 1 : c.width) + 7;
+    }
+  }
+  for (int R = kEncRows; R >= 32; R -= 32) {
+    int64_t meta = 8 * int64_t(R + 1) + 32;
+    for (int k = 0; k < a.ncols; k++) {
+      const VarCol& c = a.col[k];
+      if (c.validity) meta += R / 8 + 32;
+      if (c.kind == kFixed) meta += int64_t(R) * c.width + 32;
+      else if (c.kind == kBool) meta += R / 8 + 32;
+      else if (c.kind == kDecimal) meta += 16 * int64_t(R) + 32;
+      else meta += 4 * int64_t(R + 1) + 32;
+    }
+    const int64_t msz = r16(meta);
+    const int64_t psz = r16(static_cast<int64_t>(R * pay_row * 1.15) + 64 * nvarc);
+    const int64_t isz = r16(static_cast<int64_t>(R * img_row * 1.10) + 64);
+    if (2 * msz + 2 * psz + isz <= kPipeLds) {
+      L->rows = R;
+      L->msz = static_cast<uint32_t>(msz);
+      L->psz = static_cast<uint32_t>(psz);
+      L->isz = static_cast<uint32_t>(isz);
+      return true;
+    }
+  }
+  return false;
+}
+
+// Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
+// counts, as plan_encode_pipe) fit the LDS image with headroom.
+int reg_tile_rows(const VarArgs& a) {
+  double img_row = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind == kDecimal) img_row += 16;
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const double per = c.capacity > 0 && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
+    img_row += c.kind == kBytes ? per + 7 : 16 + per * (c.width == 0 ? 1 : c.width) + 7;
+  }
+  for (int R = kEncRows; R > 64; R -= 64)
+    if (R * img_row * 1.08 <= kRegImg) return R;
+  return 64;
+}
+
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
-  hipLaunchKernelGGL(encode_var_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
+  PipeLayout L;
+  if ((a.dbg & 2048) && plan_encode_pipe(a, &L)) {
+    VarArgs b = a;
+    b.tile_rows = L.rows;
+    const int64_t nt = (a.nrows + L.rows - 1) / L.rows;
+    const size_t lds = 2 * static_cast<size_t>(L.msz) + 2 * L.psz + L.isz;
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(encode_var_pipe),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       static_cast<int>(lds));
+    if (e != hipSuccess) return check_hip(e, "hipFuncSetAttribute");
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t g = nt < int64_t(cus) * kPipeGroupsPerCU ? nt : int64_t(cus) * kPipeGroupsPerCU;
+    hipLaunchKernelGGL(encode_var_pipe, dim3(static_cast<unsigned>(g)), dim3(kEncRows), lds, stream,
+                       b, offs, rows, cap, nt, L.msz, L.psz, L.isz);
+  } else if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
+    VarArgs b = a;
+    b.tile_rows = reg_tile_rows(a);
+    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
+    switch (a.ncols) {
+#define FURY_REG(KK) case KK: hipLaunchKernelGGL(encode_var_reg<KK>, dim3(nt), dim3(kEncRows), 0, stream, b, offs, rows, cap); break;
+      FURY_REG(1) FURY_REG(2) FURY_REG(3) FURY_REG(4) FURY_REG(5) FURY_REG(6) FURY_REG(7)
+      FURY_REG(8) FURY_REG(9) FURY_REG(10) FURY_REG(11) FURY_REG(12) FURY_REG(13) FURY_REG(14)
+      FURY_REG(15) FURY_REG(16)
+#undef FURY_REG
+      default: break;
+    }
+  } else if (a.dbg & 512) {
+    hipLaunchKernelGGL(encode_var_kernel_d, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
+  } else {
+    hipLaunchKernelGGL(encode_var_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
+  }
   return check_hip(hipGetLastError(), "encode_var launch");
 }
 

@@ -48,6 +48,9 @@ def main():
         "measure": lambda: enc.measure_into(cols, n, offs),
         "encode": lambda: enc.encode_into(cols, n, rows, offs),
         "encode_measured": lambda: enc.encode_measured_into(cols, n, rows, offs),
+        "encode_tile": lambda: (os.environ.__setitem__("FURY_VAR_DBG", "1024"),
+                                enc.encode_into(cols, n, rows, offs),
+                                os.environ.__setitem__("FURY_VAR_DBG", "0")),
         "decode_1pass": lambda: (L.fury_set_tuning(b"var_decode", 0),
                                  enc.decode_into(batch, out)),
         "decode_2pass": lambda: (L.fury_set_tuning(b"var_decode", 1),
@@ -78,7 +81,7 @@ def main():
     med = {k: round(statistics.median(v), 4) for k, v in times.items()}
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
-                    for k in ("encode", "encode_measured", "decode_1pass", "decode_2pass")}}
+                    for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass")}}
     print(json.dumps(res), flush=True)
 
 
