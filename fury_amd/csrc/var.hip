@@ -41,6 +41,7 @@ __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
 }
 __device__ __forceinline__ int64_t rnd8(int64_t n) { return (n + 7) & ~int64_t(7); }
+__host__ __device__ __forceinline__ int64_t r16(int64_t x) { return (x + 15) & ~int64_t(15); }
 __device__ __forceinline__ int64_t bm_bytes(int64_t n) { return ((n + 63) >> 6) << 3; }
 
 __device__ __forceinline__ uint64_t load_fixed(const uint8_t* p, int64_t i, int w) {
@@ -1162,6 +1163,397 @@ __device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, i
                                 reinterpret_cast<v4*>(g + i));
 }
 
+__device__ __forceinline__ bool is_seq(const VarCol& c) {
+  return c.kind == kBytes || c.kind == kListFixed;
+}
+
+// ---- register-staged decode (schemas of <= kRegCols fields) -----------------------------------
+// One workgroup decodes 256 rows (thread = row).  Each thread loads its row's null word and slots
+// straight into registers (one batch of loads; the L2 serves the neighbouring lanes' lines), so
+// LDS holds only the output assembly images.  STRING/BINARY/LIST counts are scanned in the
+// workgroup and chained across workgroups by a decoupled look-back in launch order; fixed-width
+// fields leave as coalesced column stores while predecessors publish.  Each variable-length
+// column's Arrow range for the tile is assembled in LDS (string bytes OR-ed at byte offsets into a
+// zeroed image — rows keep strings 8-byte aligned, so every source word is one aligned load; list
+// elements at their element slots; validity / bool bits OR-ed into a bit image) and leaves with
+// 16-B stores, byte-exact at the two ends and with atomic and/or on bitmap words shared with the
+// neighbouring tiles.
+constexpr int kDecImg = 24 * 1024;
+
+}  // namespace
+__device__ unsigned int g_lookback_timeouts = 0;     // spins abandoned (never expected)
+namespace {
+
+// look_back with a bounded spin: a predecessor that never publishes (only possible if workgroups
+// were not dispatched in launch order) is counted in g_lookback_timeouts instead of hanging.
+__device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q) {
+  const int lane = threadIdx.x & 63;
+  int64_t excl = 0;
+  uint32_t spins = 0;
+  for (int64_t j = b - 1;; j -= 64) {
+    const int64_t idx = j - lane;
+    uint64_t v;
+    for (;;) {
+      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
+      if (__ballot((v >> 62) == 0) == 0) break;
+      if (++spins > (1u << 24)) {
+        if (lane == 0) atomicAdd(&g_lookback_timeouts, 1u);
+        return 0;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint64_t inc = __ballot((v >> 62) == 2);
+    const int stop = inc ? __builtin_ctzll(inc) : 63;
+    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
+    if (inc) return excl;
+  }
+}
+
+// Stores image bytes img[0, n) to g[0, n) (g any alignment, img 16-aligned LDS with >= 16 bytes
+// of readable padding past n): byte stores up to g's 16-byte boundary, then 16-B non-temporal
+// stores whose data is funnel-shifted out of aligned image words, then the byte tail.
+__device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, int64_t n) {
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  if (n <= 0) return;
+  const int64_t head = min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
+  const int64_t body = (n - head) >> 4;
+  const int64_t t0 = head + 16 * body;
+  if (threadIdx.x < head) g[threadIdx.x] = img[threadIdx.x];
+  if (threadIdx.x < n - t0) g[t0 + threadIdx.x] = img[t0 + threadIdx.x];
+  const uint64_t* i64 = reinterpret_cast<const uint64_t*>(img);
+  const int sh = static_cast<int>(head & 7) * 8;
+  for (int64_t m = threadIdx.x; m < body; m += kThreads) {
+    const int64_t off = head + 16 * m;
+    const int64_t q = off >> 3;
+    uint64_t x, y;
+    if (sh == 0) {
+      x = i64[q];
+      y = i64[q + 1];
+    } else {
+      const uint64_t w0 = i64[q], w1 = i64[q + 1], w2 = i64[q + 2];
+      x = (w0 >> sh) | (w1 << (64 - sh));
+      y = (w1 >> sh) | (w2 << (64 - sh));
+    }
+    v4 vv;
+    vv.x = static_cast<uint32_t>(x); vv.y = static_cast<uint32_t>(x >> 32);
+    vv.z = static_cast<uint32_t>(y); vv.w = static_cast<uint32_t>(y >> 32);
+    __builtin_nontemporal_store(vv, reinterpret_cast<v4*>(g + head + 16 * m));
+  }
+}
+
+// Stores a bit image (image bit i = global bit gbit0 + i, >= 1 word of padding) to the global
+// bitmap bits [gbit0, gbit0 + n): whole words plainly, the words shared with neighbouring tiles
+// with atomic and/or of exactly these bits.
+__device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t* img, int64_t gbit0,
+                                                   int64_t n) {
+  if (n <= 0) return;
+  const int64_t end = gbit0 + n;
+  const int64_t w0 = gbit0 >> 5, w1 = (end + 31) >> 5;
+  uint32_t* g = reinterpret_cast<uint32_t*>(bits);
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += kThreads) {
+    const int64_t i0 = 32 * w - gbit0;
+    uint32_t x;
+    if (i0 < 0) {
+      x = img[0] << (-i0);
+    } else {
+      const int64_t q = i0 >> 5;
+      const int s = static_cast<int>(i0 & 31);
+      x = s ? (img[q] >> s) | (img[q + 1] << (32 - s)) : img[q];
+    }
+    uint32_t m = ~0u;
+    if (w == w0) m &= ~0u << (gbit0 & 31);
+    if (w == w1 - 1 && (end & 31)) m &= (1u << (end & 31)) - 1;
+    if (m == ~0u) {
+      g[w] = x;
+    } else {
+      atomicAnd(g + w, ~m);
+      atomicOr(g + w, x & m);
+    }
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
+                                                           const int64_t* __restrict__ offs,
+                                                           uint64_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) uint64_t oimg[kDecImg / 8];
+  __shared__ int64_t tmp[kThreads / 64];
+  __shared__ int64_t sbase[K];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  const int64_t r0 = b * kThreads;
+  const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t r = live ? r0 + tid : r0;
+  const uint8_t* row = rows + offs[r];
+  const uint64_t* row64 = reinterpret_cast<const uint64_t*>(row);
+  // null word + slots: one batch of loads
+  const uint64_t nullw = live ? row64[0] : ~0ull;
+  uint64_t slot[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) slot[k] = row64[1 + k];
+  // element counts of LIST fields (dependent load of the array header)
+  uint32_t cnt[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    const bool isnull = (nullw >> k) & 1;
+    cnt[k] = 0;
+    if (!isnull && c.kind == kBytes) cnt[k] = static_cast<uint32_t>(slot[k]);
+    if (!isnull && c.kind == kListFixed)
+      cnt[k] = static_cast<uint32_t>(*reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot[k] >> 32)));
+  }
+  // in-tile exclusive scans, two columns per 64-bit scan (tile totals < 2^32)
+  uint32_t ex[K], tot[K];
+#pragma unroll
+  for (int k = 0; k < K; k += 2) {
+    const bool s0 = is_seq(a.col[k]);
+    const bool s1 = k + 1 < K && is_seq(a.col[k + 1]);
+    ex[k] = tot[k] = 0;
+    if (k + 1 < K) ex[k + 1] = tot[k + 1] = 0;
+    if (!s0 && !s1) continue;
+    const uint64_t pk = cnt[k] | (k + 1 < K ? static_cast<uint64_t>(cnt[k + 1]) << 32 : 0);
+    int64_t t64;
+    const uint64_t e64 = static_cast<uint64_t>(block_excl_scan(static_cast<int64_t>(pk), &t64, tmp));
+    ex[k] = static_cast<uint32_t>(e64);
+    tot[k] = static_cast<uint32_t>(t64);
+    if (k + 1 < K) {
+      ex[k + 1] = static_cast<uint32_t>(e64 >> 32);
+      tot[k + 1] = static_cast<uint32_t>(static_cast<uint64_t>(t64) >> 32);
+    }
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if (is_seq(a.col[k]))
+        st_status(status + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
+  }
+  // tile-relative LDS images of every variable-length column (image byte / bit i = the tile's
+  // i-th output byte / element); laid out from the tile totals alone, so the rows are scattered
+  // into them while the predecessors' prefixes are still being resolved
+  uint32_t img_at[K];
+  uint32_t used = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    img_at[k] = kNone;
+    if (!is_seq(c) || !c.values || tot[k] == 0) continue;
+    int64_t need;
+    if (c.kind == kBytes) need = r16(tot[k] + 16);
+    else if (c.width == 0) need = r16((((tot[k] + 31) >> 5) + 1) * 4);
+    else need = r16(int64_t(tot[k]) * c.width + 16);
+    if (c.kind == kListFixed && c.elem_validity) need += r16((((tot[k] + 31) >> 5) + 1) * 4);
+    if (used + need <= kDecImg) {
+      img_at[k] = used;
+      used += static_cast<uint32_t>(need);
+    }
+  }
+  for (uint32_t i = 16 * tid; i < used; i += 16 * kThreads)
+    *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    if (img_at[k] == kNone || !live || cnt[k] == 0 || (a.dbg & 16)) continue;
+    const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
+    uint8_t* im = reinterpret_cast<uint8_t*>(oimg) + img_at[k];
+    if (c.kind == kBytes) {
+      const int64_t len = cnt[k];
+      const int64_t d = ex[k];
+      uint64_t* iw = reinterpret_cast<uint64_t*>(im) + (d >> 3);
+      const int sh = static_cast<int>(d & 7) * 8;
+      const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
+      const int64_t nw = (len + 7) >> 3;
+      for (int64_t j0 = 0; j0 < nw; j0 += 4) {
+        uint64_t w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) w[u] = j0 + u < nw ? s64[j0 + u] : 0;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int64_t j = j0 + u;
+          if (j >= nw) break;
+          uint64_t x = w[u];
+          const int64_t rem = len - 8 * j;
+          if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
+          atomicOr(reinterpret_cast<unsigned long long*>(iw + j), x << sh);
+          if (sh && (x >> (64 - sh))) atomicOr(reinterpret_cast<unsigned long long*>(iw + j + 1), x >> (64 - sh));
+        }
+      }
+      continue;
+    }
+    // LIST of fixed-width elements: values at element slots, bits by OR
+    const int64_t n = cnt[k];
+    const int ew = c.width == 0 ? 1 : c.width;
+    const uint8_t* ev = src + 8 + bm_bytes(n);
+    const int64_t vb = c.width == 0 ? r16((((tot[k] + 31) >> 5) + 1) * 4) : r16(int64_t(tot[k]) * c.width + 16);
+    uint32_t* bimg = reinterpret_cast<uint32_t*>(im + vb);
+    for (int64_t j0 = 0; j0 < n; j0 += 8) {
+      const int lim = static_cast<int>(min<int64_t>(8, n - j0));
+      const uint64_t nulls = load_bits64(src + 8, j0, lim);
+      uint64_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        x[u] = 0;
+        if (u < lim) {
+          switch (ew) {
+            case 8: x[u] = reinterpret_cast<const uint64_t*>(ev)[j0 + u]; break;
+            case 4: x[u] = reinterpret_cast<const uint32_t*>(ev)[j0 + u]; break;
+            case 2: x[u] = reinterpret_cast<const uint16_t*>(ev)[j0 + u]; break;
+            default: x[u] = ev[j0 + u]; break;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (u >= lim) break;
+        const bool valid = !((nulls >> u) & 1);
+        const int64_t e = ex[k] + j0 + u;                     // tile-relative element
+        const uint64_t val = valid ? x[u] : 0;
+        if (c.width == 8) {
+          reinterpret_cast<uint64_t*>(im)[e] = val;
+        } else if (c.width == 0) {
+          if (val & 0xff) atomicOr(reinterpret_cast<uint32_t*>(im) + (e >> 5), 1u << (e & 31));
+        } else if (val) {
+          const int64_t bo = e * ew;
+          atomicOr(reinterpret_cast<uint32_t*>(im) + (bo >> 2), static_cast<uint32_t>(val << (8 * (bo & 3))));
+        }
+        if (c.elem_validity && valid) atomicOr(bimg + (e >> 5), 1u << (e & 31));
+      }
+    }
+  }
+  // fixed-width fields, decimals and every field's validity (no dependency on other tiles)
+  const int64_t rbase = r0 + 64 * wave;
+  const int64_t nvalid = a.nrows - rbase;
+  const int nwords = nvalid >= 64 ? 2 : nvalid <= 0 ? 0 : static_cast<int>((nvalid + 31) >> 5);
+#pragma unroll
+  for (int k = 0; k < ((a.dbg & 8) ? 0 : K); k++) {
+    const VarCol& c = a.col[k];
+    const bool isnull = (nullw >> k) & 1;
+    if (c.validity) {
+      const uint64_t ok = __ballot(live && !isnull);
+      if (lane < nwords)
+        reinterpret_cast<uint32_t*>(c.validity)[(rbase >> 5) + lane] = static_cast<uint32_t>(ok >> (32 * lane));
+    }
+    uint8_t* dst = const_cast<uint8_t*>(c.values);
+    if (!dst) continue;
+    const uint64_t x = isnull ? 0 : slot[k];
+    if (c.kind == kFixed) {
+      if (live) {
+        switch (c.width) {
+          case 8: __builtin_nontemporal_store(x, reinterpret_cast<uint64_t*>(dst) + r); break;
+          case 4: __builtin_nontemporal_store(static_cast<uint32_t>(x), reinterpret_cast<uint32_t*>(dst) + r); break;
+          case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(x); break;
+          default: dst[r] = static_cast<uint8_t>(x); break;
+        }
+      }
+    } else if (c.kind == kBool) {
+      const uint64_t bits = __ballot(live && (x & 0xff) != 0);
+      if (lane < nwords)
+        reinterpret_cast<uint32_t*>(dst)[(rbase >> 5) + lane] = static_cast<uint32_t>(bits >> (32 * lane));
+    } else if (c.kind == kDecimal && live) {
+      uint64_t lo = 0, hi = 0;
+      if (!isnull) {
+        const uint64_t* s = reinterpret_cast<const uint64_t*>(row + static_cast<int32_t>(x >> 32));
+        lo = s[0];
+        hi = s[1];
+      }
+      uint64_t* d = reinterpret_cast<uint64_t*>(dst + 16 * r);
+      d[0] = lo;
+      d[1] = hi;
+    }
+  }
+  // prefixes of the variable-length columns: one wave per column (round robin)
+  {
+    int q = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      if (!is_seq(a.col[k])) continue;
+      if ((q++ & 3) != wave) continue;
+      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k);
+      if (lane == 0) {
+        sbase[k] = pre;
+        if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
+      }
+    }
+  }
+  __syncthreads();
+  // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    if (!is_seq(c)) continue;
+    const int64_t gb = sbase[k];
+    if (live) c.offsets[r] = static_cast<int32_t>(gb + ex[k]);
+    if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot[k]);
+    if (img_at[k] != kNone || !c.values || !live || cnt[k] == 0) continue;
+    uint8_t* dst = const_cast<uint8_t*>(c.values);
+    const int64_t cap = c.capacity;
+    const int64_t pos = gb + ex[k];
+    const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
+    if (c.kind == kBytes) {
+      put_bytes(dst, pos, src, max<int64_t>(0, min<int64_t>(cnt[k], cap - pos)));
+      continue;
+    }
+    const int64_t n = cnt[k];
+    const int ew = c.width == 0 ? 1 : c.width;
+    const uint8_t* ev = src + 8 + bm_bytes(n);
+    for (int64_t j = 0; j < n; j++) {
+      const int64_t e = pos + j;
+      if (e >= cap) break;
+      const bool valid = !((src[8 + (j >> 3)] >> (j & 7)) & 1);
+      uint64_t x = 0;
+      if (valid) {
+        switch (ew) {
+          case 8: x = reinterpret_cast<const uint64_t*>(ev)[j]; break;
+          case 4: x = reinterpret_cast<const uint32_t*>(ev)[j]; break;
+          case 2: x = reinterpret_cast<const uint16_t*>(ev)[j]; break;
+          default: x = ev[j]; break;
+        }
+      }
+      switch (c.width) {
+        case 8: reinterpret_cast<uint64_t*>(dst)[e] = x; break;
+        case 4: reinterpret_cast<uint32_t*>(dst)[e] = static_cast<uint32_t>(x); break;
+        case 2: reinterpret_cast<uint16_t*>(dst)[e] = static_cast<uint16_t>(x); break;
+        case 1: dst[e] = static_cast<uint8_t>(x); break;
+        default: {
+          uint32_t* wd = reinterpret_cast<uint32_t*>(dst) + (e >> 5);
+          const uint32_t m = 1u << (e & 31);
+          if (valid && x) atomicOr(wd, m); else atomicAnd(wd, ~m);
+        }
+      }
+      if (c.elem_validity) {
+        uint32_t* wd = reinterpret_cast<uint32_t*>(c.elem_validity) + (e >> 5);
+        const uint32_t m = 1u << (e & 31);
+        if (valid) atomicOr(wd, m); else atomicAnd(wd, ~m);
+      }
+    }
+  }
+  // images -> HBM at the resolved positions
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const VarCol& c = a.col[k];
+    if (img_at[k] == kNone) continue;
+    const int64_t gb = sbase[k];
+    uint8_t* dst = const_cast<uint8_t*>(c.values);
+    const uint8_t* im = reinterpret_cast<const uint8_t*>(oimg) + img_at[k];
+    const int64_t n = max<int64_t>(0, min<int64_t>(tot[k], c.capacity - gb));
+    if (c.kind == kBytes) {
+      store_shifted(dst + gb, im, n);
+      continue;
+    }
+    int64_t vb;
+    if (c.width == 0) {
+      vb = r16((((tot[k] + 31) >> 5) + 1) * 4);
+      store_bits_shifted(dst, reinterpret_cast<const uint32_t*>(im), gb, n);
+    } else {
+      vb = r16(int64_t(tot[k]) * c.width + 16);
+      store_shifted(dst + gb * c.width, im, n * c.width);
+    }
+    if (c.elem_validity)
+      store_bits_shifted(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
+  }
+}
+
 // Decode / row->Arrow, single pass: 256 rows per workgroup.  Arrow offsets of STRING/BINARY and
 // LIST fields are a scan over ALL rows, so groups chain their totals with a decoupled look-back
 // (each group publishes its aggregate, then resolves its prefix from its predecessors' published
@@ -1211,9 +1603,6 @@ struct DecodeShared {
   int64_t blk;
 };
 
-__device__ __forceinline__ bool is_seq(const VarCol& c) {
-  return c.kind == kBytes || c.kind == kListFixed;
-}
 
 // Counts + in-group scans of the sequences [cbase, cbase + nchunk); publishes the aggregates.
 __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row, DecodeShared& sh,
@@ -1558,7 +1947,6 @@ void set_var_decode_mode(int v) { g_var_decode = v; }
 constexpr int kPipeGroupsPerCU = 2;
 constexpr int64_t kPipeLds = 77 * 1024;
 
-static int64_t r16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
 bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
   if (a.nrows <= 0) return false;
@@ -1713,6 +2101,26 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     hipLaunchKernelGGL(decode_var_kernel<false>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
                        nullptr, nullptr, nseq);
     return check_hip(hipGetLastError(), "decode_var launch");
+  }
+  if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
+    const size_t wsb = static_cast<size_t>(nb) * a.ncols * 8;
+    uint64_t* ws = nullptr;
+    int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
+    if (st) return st;
+    st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+    if (!st) {
+      switch (a.ncols) {
+#define FURY_DREG(KK) case KK: hipLaunchKernelGGL(decode_var_reg<KK>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs, ws); break;
+        FURY_DREG(1) FURY_DREG(2) FURY_DREG(3) FURY_DREG(4) FURY_DREG(5) FURY_DREG(6) FURY_DREG(7)
+        FURY_DREG(8) FURY_DREG(9) FURY_DREG(10) FURY_DREG(11) FURY_DREG(12) FURY_DREG(13)
+        FURY_DREG(14) FURY_DREG(15) FURY_DREG(16)
+#undef FURY_DREG
+        default: break;
+      }
+      st = check_hip(hipGetLastError(), "decode_var_reg launch");
+    }
+    const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
+    return st ? st : st2;
   }
   // look-back status words (nb x nseq) + the group ticket, zeroed per launch
   const size_t wsb = (nb * nseq + 1) * 8;
