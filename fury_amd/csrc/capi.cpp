@@ -437,7 +437,8 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
 int fury_set_tuning(const char* key, int32_t value) {
   if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
   if (std::string(key) == "fixed_variant") {
-    if (value < 0 || value > 7) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..7");
+    if (value < 0 || value > 255)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..255");
     set_fixed_variant(value);
     return FURY_OK;
   }
@@ -446,12 +447,20 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_decode_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "unframe") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "unframe: 0..1");
+    set_unframe_mode(value);
+    return FURY_OK;
+  }
   return set_error(FURY_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "fixed_variant") return fixed_variant();
   if (key && std::string(key) == "var_decode") return var_decode_mode();
+  if (key && std::string(key) == "unframe") return unframe_mode();
+  if (key && std::string(key) == "unframe_walks")
+    return static_cast<int32_t>(unframe_walk_count());
   return -1;
 }
 

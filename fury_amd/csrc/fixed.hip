@@ -52,6 +52,30 @@ __device__ __forceinline__ void store_value(uint8_t* p, int64_t row, int width, 
   }
 }
 
+// Column of work item idx (= c * R + r).  R >= 64: a wave covers 64 rows of ONE column (wave
+// uniform, scalar column record).  R == 32 (short tiles): lanes 0-31 take column c0 and lanes 32-63
+// column c0 + 1 of the same wave.
+template <int R>
+__device__ __forceinline__ int col_of(int idx, int total, int lane) {
+  if constexpr (R >= 64) {
+    return __builtin_amdgcn_readfirstlane(min(idx, total - 1) / R);
+  } else {
+    static_assert(R == 32, "short tiles are 32 rows");
+    return __builtin_amdgcn_readfirstlane(min(idx - lane, total - 1) / R) + (lane >> 5);
+  }
+}
+template <int R>
+__device__ __forceinline__ uint8_t* values_of(const FixedArgs& a, int c, int lane) {
+  if constexpr (R >= 64) {
+    return const_cast<uint8_t*>(a.col[c].values);
+  } else {
+    const int c0 = __builtin_amdgcn_readfirstlane(c);
+    uint8_t* p0 = const_cast<uint8_t*>(a.col[c0].values);
+    uint8_t* p1 = const_cast<uint8_t*>(a.col[min(c0 + 1, kMaxFixedCols - 1)].values);
+    return lane >= 32 ? p1 : p0;
+  }
+}
+
 // Global access helpers; NT bit 0 = non-temporal loads, bit 1 = non-temporal stores (streamed
 // bytes are touched once, so keeping them out of L2/MALL leaves room for the other stream).
 using v4u = __attribute__((ext_vector_type(4))) uint32_t;
@@ -80,29 +104,39 @@ __device__ __forceinline__ void st16(uint8_t* p, const v4u& v) {
   else *q = v;
 }
 
-// Copies `bytes` (multiple of 8) between LDS and global, 16 B per lane where possible.
-template <bool kToGlobal, int NT>
+// Copies `bytes` (multiple of 8) between LDS and global, 16 B per lane where possible, with D
+// 16-B accesses per lane in flight before the LDS side is touched (loads) / issued back to back
+// (stores).
+template <bool kToGlobal, int NT, int D = 4>
 __device__ __forceinline__ void copy_tile(uint8_t* __restrict__ g, uint8_t* __restrict__ lds,
                                           int64_t bytes) {
   const int64_t n16 = bytes >> 4;
   v4u* l16 = reinterpret_cast<v4u*>(lds);
   int64_t i = threadIdx.x;
-  for (; i + 3 * kThreads < n16; i += 4 * kThreads) {
+  for (; i + (D - 1) * kThreads < n16; i += D * kThreads) {
+    v4u t[D];
     if (kToGlobal) {
-      v4u a = l16[i], b = l16[i + kThreads], c = l16[i + 2 * kThreads], d = l16[i + 3 * kThreads];
-      st16<NT>(g + 16 * i, a);
-      st16<NT>(g + 16 * (i + kThreads), b);
-      st16<NT>(g + 16 * (i + 2 * kThreads), c);
-      st16<NT>(g + 16 * (i + 3 * kThreads), d);
+#pragma unroll
+      for (int k = 0; k < D; k++) t[k] = l16[i + k * kThreads];
+#pragma unroll
+      for (int k = 0; k < D; k++) st16<NT>(g + 16 * (i + k * kThreads), t[k]);
     } else {
-      v4u a = ld16<NT>(g + 16 * i), b = ld16<NT>(g + 16 * (i + kThreads));
-      v4u c = ld16<NT>(g + 16 * (i + 2 * kThreads)), d = ld16<NT>(g + 16 * (i + 3 * kThreads));
-      l16[i] = a; l16[i + kThreads] = b; l16[i + 2 * kThreads] = c; l16[i + 3 * kThreads] = d;
+#pragma unroll
+      for (int k = 0; k < D; k++) t[k] = ld16<NT>(g + 16 * (i + k * kThreads));
+#pragma unroll
+      for (int k = 0; k < D; k++) l16[i + k * kThreads] = t[k];
     }
   }
-  for (; i < n16; i += kThreads) {
-    if (kToGlobal) st16<NT>(g + 16 * i, l16[i]);
-    else l16[i] = ld16<NT>(g + 16 * i);
+  if (!kToGlobal) {     // remainder: all of this lane's loads first, then the LDS writes
+    v4u t[D];
+#pragma unroll
+    for (int k = 0; k < D; k++)
+      if (i + k * kThreads < n16) t[k] = ld16<NT>(g + 16 * (i + k * kThreads));
+#pragma unroll
+    for (int k = 0; k < D; k++)
+      if (i + k * kThreads < n16) l16[i + k * kThreads] = t[k];
+  } else {
+    for (; i < n16; i += kThreads) st16<NT>(g + 16 * i, l16[i]);
   }
   if ((bytes & 15) && threadIdx.x == 0) {
     uint64_t* g8 = reinterpret_cast<uint64_t*>(g + (n16 << 4));
@@ -112,8 +146,53 @@ __device__ __forceinline__ void copy_tile(uint8_t* __restrict__ g, uint8_t* __re
   }
 }
 
+// LDS row stride of the padded encode: an odd number of 8-B words.
+__host__ __device__ __forceinline__ int lds_row_stride(int rs) { return ((rs >> 3) & 1) ? rs : rs + 8; }
+
+// Row tile LDS -> global.  Unpadded: one contiguous copy.  Padded (LDS row stride ls != rs):
+// each lane's 16-B output chunk is read as two 8-B words from their padded LDS rows; the chunk's
+// (row, offset) advances incrementally by the loop stride, so there is no division per chunk.
+template <int NT, int DS, bool PAD>
+__device__ __forceinline__ void store_tile(uint8_t* __restrict__ g, uint8_t* __restrict__ lds,
+                                           int nr, int rs, int ls) {
+  const int64_t bytes = static_cast<int64_t>(nr) * rs;
+  if (!PAD || ls == rs) {
+    copy_tile<true, NT, DS>(g, lds, bytes);
+    return;
+  }
+  const int n16 = static_cast<int>(bytes >> 4);
+  constexpr int kStep = 16 * kThreads;
+  const int q = kStep / rs, rm = kStep - q * rs;
+  int o = 16 * threadIdx.x;
+  int row = o / rs, w = o - row * rs;
+  for (int i = threadIdx.x; i < n16; i += kThreads) {
+    const uint64_t lo = *reinterpret_cast<const uint64_t*>(lds + row * ls + w);
+    int row2 = row, w2 = w + 8;
+    if (w2 >= rs) { w2 -= rs; row2++; }
+    const uint64_t hi = *reinterpret_cast<const uint64_t*>(lds + row2 * ls + w2);
+    st16<NT>(g + 16 * static_cast<int64_t>(i),
+             v4u{static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32),
+                 static_cast<uint32_t>(hi), static_cast<uint32_t>(hi >> 32)});
+    row += q;
+    w += rm;
+    if (w >= rs) { w -= rs; row++; }
+  }
+  if ((bytes & 15) && threadIdx.x == 0) {       // a last 8-B word (rs % 16 == 8, nr odd)
+    const int64_t o8 = static_cast<int64_t>(n16) << 4;
+    const int r8 = static_cast<int>(o8 / rs);
+    *reinterpret_cast<uint64_t*>(g + o8) =
+        *reinterpret_cast<const uint64_t*>(lds + r8 * ls + (o8 - static_cast<int64_t>(r8) * rs));
+  }
+}
+
 // kFast: every column is 8 bytes wide and no column carries validity.
-template <int R, bool kFast, int NT>
+// U = column loads per lane in flight in the gather (8 default, 16 "deep"); P = pair mode
+// (fast path only): a lane moves rows 2q and 2q + 1 of one column with ONE 16-B load, so a
+// wave-instruction covers 128 rows (R >= 128) or two columns x 64 rows (R = 64).
+// PAD: LDS rows are laid out with an odd number of 8-B words (row size + 8 when row_size / 8 is
+// even) so the 64 lanes of a column write hit 64 distinct LDS banks; the copy-out then maps
+// each 16-B output chunk back to its padded LDS address.
+template <int R, bool kFast, int NT, int U = kUnroll, int DS = 4, bool P = false, bool PAD = false>
 __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
                                                                  uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -122,30 +201,73 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
   const int bw = bm >> 3;
+  const int ls = PAD ? lds_row_stride(rs) : rs;     // LDS bytes per row
 
   // BinaryRowWriter.reset(): zero the bitmap words of every row of the tile.
   for (int i = threadIdx.x; i < R * bw; i += kThreads) {
     const int r = i / bw, w = i - r * bw;
-    *reinterpret_cast<uint64_t*>(lds + r * rs + 8 * w) = 0;
+    *reinterpret_cast<uint64_t*>(lds + r * ls + 8 * w) = 0;
   }
   if (!kFast) __syncthreads();   // the null bits below are OR-ed into these words
 
+  const int lane = threadIdx.x & 63;
+  if constexpr (P) {
+    static_assert(kFast, "pair mode is fast-path only");
+    constexpr int H = R / 2;                       // row pairs per column of the tile
+    const int total2 = a.ncols * H;
+    for (int base = threadIdx.x; base < total2; base += kThreads * U) {
+      v4u v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int idx = base + u * kThreads;
+        const int c = col_of<H>(idx, total2, lane);
+        const int r = 2 * (idx - c * H);
+        if (idx < total2 && r < nr) {
+          const uint8_t* src = values_of<H>(a, c, lane) + (r0 + r) * 8;
+          if (r + 1 < nr) {
+            v[u] = ld16<NT>(src);
+          } else {
+            const uint64_t x = ld8<NT>(src);
+            v[u] = v4u{static_cast<uint32_t>(x), static_cast<uint32_t>(x >> 32), 0u, 0u};
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int idx = base + u * kThreads;
+        const int c = col_of<H>(idx, total2, lane);
+        const int r = 2 * (idx - c * H);
+        if (idx < total2 && r < nr) {
+          uint8_t* p = lds + r * ls + bm + 8 * c;
+          *reinterpret_cast<uint64_t*>(p) = static_cast<uint64_t>(v[u].x) |
+                                            (static_cast<uint64_t>(v[u].y) << 32);
+          if (r + 1 < nr)
+            *reinterpret_cast<uint64_t*>(p + ls) = static_cast<uint64_t>(v[u].z) |
+                                                   (static_cast<uint64_t>(v[u].w) << 32);
+        }
+      }
+    }
+    __syncthreads();
+    store_tile<NT, DS, PAD>(rows + r0 * rs, lds, nr, rs, ls);
+    return;
+  }
+
   // Gather: item = c * R + r; a wave covers 64 consecutive rows of ONE column (R % 64 == 0).
   const int total = a.ncols * R;
-  for (int base = threadIdx.x; base < total; base += kThreads * kUnroll) {
-    uint64_t v[kUnroll];
-    bool isnull[kUnroll];
+  for (int base = threadIdx.x; base < total; base += kThreads * U) {
+    uint64_t v[U];
+    bool isnull[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
+    for (int u = 0; u < U; u++) {
       const int idx = base + u * kThreads;
-      const int c = __builtin_amdgcn_readfirstlane(min(idx, total - 1) / R);
+      const int c = col_of<R>(idx, total, lane);
       const int r = idx - c * R;
       v[u] = 0;
       isnull[u] = false;
       if (idx < total && r < nr) {
         const int64_t row = r0 + r;
         if (kFast) {
-          v[u] = ld8<NT>(a.col[c].values + row * 8);
+          v[u] = ld8<NT>(values_of<R>(a, c, lane) + row * 8);
         } else {
           const uint8_t* vb = a.col[c].validity;
           if (vb && !((vb[row >> 3] >> (row & 7)) & 1)) {
@@ -157,12 +279,12 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
       }
     }
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
+    for (int u = 0; u < U; u++) {
       const int idx = base + u * kThreads;
-      const int c = __builtin_amdgcn_readfirstlane(min(idx, total - 1) / R);
+      const int c = col_of<R>(idx, total, lane);
       const int r = idx - c * R;
       if (idx < total && r < nr) {
-        uint8_t* rowp = lds + r * rs;
+        uint8_t* rowp = lds + r * ls;
         *reinterpret_cast<uint64_t*>(rowp + bm + 8 * c) = v[u];
         if (!kFast && isnull[u]) {
           atomicOr(reinterpret_cast<uint32_t*>(rowp) + (c >> 5), 1u << (c & 31));
@@ -171,10 +293,12 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
     }
   }
   __syncthreads();
-  copy_tile<true, NT>(rows + r0 * rs, lds, static_cast<int64_t>(nr) * rs);
+  store_tile<NT, DS, PAD>(rows + r0 * rs, lds, nr, rs, ls);
 }
 
-template <int R, bool kFast, int NT>
+// D = 16-B row-tile loads per lane in flight (4 default, 16 "deep": the whole 64-row Struct-100
+// tile in one round trip); P = pair mode (16-B column stores of rows 2q, 2q + 1).
+template <int R, bool kFast, int NT, int D = 4, bool P = false>
 __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
                                                                  const uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -183,25 +307,52 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
 
-  copy_tile<false, NT>(const_cast<uint8_t*>(rows + r0 * rs), lds, static_cast<int64_t>(nr) * rs);
+  copy_tile<false, NT, D>(const_cast<uint8_t*>(rows + r0 * rs), lds, static_cast<int64_t>(nr) * rs);
   __syncthreads();
 
-  const int total = a.ncols * R;
   const int lane = threadIdx.x & 63;
+  if constexpr (P) {
+    static_assert(kFast, "pair mode is fast-path only");
+    constexpr int H = R / 2;
+    const int total2 = a.ncols * H;
+    for (int base = threadIdx.x; base < total2; base += kThreads * kUnroll) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const int idx = base + u * kThreads;
+        if (__builtin_amdgcn_readfirstlane(idx - lane) >= total2) break;
+        const int c = col_of<H>(idx, total2, lane);
+        const int r = 2 * (idx - c * H);
+        if (idx < total2 && r < nr) {
+          const uint8_t* p = lds + r * rs + bm + 8 * c;
+          const uint64_t x0 = *reinterpret_cast<const uint64_t*>(p);
+          uint8_t* dst = values_of<H>(a, c, lane) + (r0 + r) * 8;
+          if (r + 1 < nr) {
+            const uint64_t x1 = *reinterpret_cast<const uint64_t*>(p + rs);
+            st16<NT>(dst, v4u{static_cast<uint32_t>(x0), static_cast<uint32_t>(x0 >> 32),
+                              static_cast<uint32_t>(x1), static_cast<uint32_t>(x1 >> 32)});
+          } else {
+            st8<NT>(dst, x0);
+          }
+        }
+      }
+    }
+    return;
+  }
+  const int total = a.ncols * R;
   for (int base = threadIdx.x; base < total; base += kThreads * kUnroll) {
 #pragma unroll
     for (int u = 0; u < kUnroll; u++) {
       const int idx = base + u * kThreads;
       if (__builtin_amdgcn_readfirstlane(idx - lane) >= total) break;   // wave-uniform exit
-      const int c = __builtin_amdgcn_readfirstlane(idx / R);
+      const int c = col_of<R>(idx, total, lane);
       const int r = idx - c * R;
-      const bool live = r < nr;
+      const bool live = r < nr && idx < total;
       const uint8_t* rowp = lds + r * rs;
       const int64_t row = r0 + r;
       if (kFast) {
         if (live) {
           uint64_t v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-          st8<NT>(const_cast<uint8_t*>(a.col[c].values) + row * 8, v);
+          st8<NT>(values_of<R>(a, c, lane) + row * 8, v);
         }
         continue;
       }
@@ -366,7 +517,8 @@ static int g_variant = -1;
 int fixed_variant() {
   if (g_variant < 0) {
     const char* e = getenv("FURY_FIXED_VARIANT");
-    g_variant = e ? atoi(e) : 6;   // tile kernel + nt loads + nt stores (A/B: profiles/r01_ab_fixed.json)
+    // tile kernel + nt loads + nt stores + pair-mode deep decode (A/B: profiles/r01_ab_fixed*.json)
+    g_variant = e ? atoi(e) : 54;
   }
   return g_variant;
 }
@@ -407,8 +559,8 @@ int pick_rows_per_tile(int row_size) {
 
 template <typename K>
 int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t stream,
-                       const FixedArgs& a, uint8_t* rows) {
-  const size_t lds = static_cast<size_t>(R) * row_size;
+                       const FixedArgs& a, uint8_t* rows, int lds_row = 0) {
+  const size_t lds = static_cast<size_t>(R) * (lds_row ? lds_row : row_size);
   static_assert(sizeof(FixedArgs) < 4096, "kernel argument block too large");
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
@@ -423,10 +575,56 @@ int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t
   return check_hip(hipGetLastError(), "fixed kernel launch");
 }
 
+// Fast-path tile kernels (nt loads + stores) with the variant bits 3 (deep encode gather: 16
+// column loads per lane in flight), 4 (pair mode: 16-B column accesses) and 5 (deep decode:
+// 16 tile loads per lane in flight).
+template <int R, bool kEnc, bool P>
+int launch_fast_tile(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool deep, bool pad) {
+  const int ls = lds_row_stride(a.row_size);
+  if (kEnc) {
+    if (pad)
+      return deep ? launch_tile_kernel(encode_fixed_kernel<R, true, 3, 16, 4, P, true>, R,
+                                       a.row_size, a.nrows, stream, a, rows, ls)
+                  : launch_tile_kernel(encode_fixed_kernel<R, true, 3, 8, 4, P, true>, R,
+                                       a.row_size, a.nrows, stream, a, rows, ls);
+    return deep ? launch_tile_kernel(encode_fixed_kernel<R, true, 3, 16, 4, P>, R, a.row_size,
+                                     a.nrows, stream, a, rows)
+                : launch_tile_kernel(encode_fixed_kernel<R, true, 3, 8, 4, P>, R, a.row_size,
+                                     a.nrows, stream, a, rows);
+  }
+  return deep ? launch_tile_kernel(decode_fixed_kernel<R, true, 3, 16, P>, R, a.row_size, a.nrows,
+                                   stream, a, rows)
+              : launch_tile_kernel(decode_fixed_kernel<R, true, 3, 4, P>, R, a.row_size, a.nrows,
+                                   stream, a, rows);
+}
+
+template <bool kEnc>
+int launch_fast_tile_variant(const FixedArgs& a, uint8_t* rows, hipStream_t stream, int var) {
+  const int R = pick_rows_per_tile(a.row_size);
+  const bool deep = (var & (kEnc ? 8 : 32)) != 0;
+  const bool pad = kEnc && (var & 128) != 0;
+  // pad only where it fits the LDS budget of the unpadded tile's occupancy class
+  const bool pad_ok = pad && static_cast<int64_t>(R) * lds_row_stride(a.row_size) <= 64 * 1024;
+  bool pair = (var & (kEnc ? 64 : 16)) != 0;
+  for (int c = 0; c < a.ncols && pair; c++)       // 16-B column accesses need 16-B aligned columns
+    pair = (reinterpret_cast<uintptr_t>(a.col[c].values) & 15) == 0;
+#define FURY_FT(RR)                                                              \
+  if (R == RR)                                                                   \
+    return pair ? launch_fast_tile<RR, kEnc, true>(a, rows, stream, deep, pad_ok) \
+                : launch_fast_tile<RR, kEnc, false>(a, rows, stream, deep, pad_ok);
+  FURY_FT(256)
+  FURY_FT(128)
+  FURY_FT(64)
+#undef FURY_FT
+  return set_error(FURY_ERR_UNSUPPORTED, "row size");
+}
+
 }  // namespace
 
 // Variant bits (fury_set_tuning("fixed_variant")): bit 0 = pipelined persistent kernel,
-// bit 1 = non-temporal stores, bit 2 = non-temporal loads.  Only the fast path (8-byte columns,
+// bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode gather, bit 4 =
+// pair-mode decode, bit 5 = deep decode loads, bit 6 = pair-mode encode, bit 7 = padded LDS rows
+// in the encode (bits 3-7 with nt loads + stores only).  Only the fast path (8-byte columns,
 // no validity) has variants; the general path always runs the tile kernel.
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
@@ -440,6 +638,7 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
       default: return launch_pipe(encode_fixed_pipe<32, 0>, a.row_size, a.nrows, stream, a, rows);
     }
   }
+  if (fast && (var & 248) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                          \
   if (R == RR) {                                                                              \
@@ -486,6 +685,7 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
       default: return launch_pipe(decode_fixed_pipe<17, 0>, a.row_size, a.nrows, stream, a, r);
     }
   }
+  if (fast && (var & 248) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_DEC(RR)                                                                          \
   if (R == RR) {                                                                              \

@@ -122,6 +122,11 @@ void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t
 int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t nrows,
                       int64_t fixed_size, int64_t schema_hash, uint8_t* out,
                       int64_t* frame_offsets, hipStream_t stream);
+// Unframe mode (tuning "unframe"): 0 speculative parallel parse (sequential walk on failure),
+// 1 always the sequential walk; unframe_walk_count() = streams the walk has parsed.
+int unframe_mode();
+void set_unframe_mode(int v);
+int64_t unframe_walk_count();
 int launch_unframe_rows(const uint8_t* in, int64_t in_len, int64_t nrows, int64_t schema_hash,
                         uint8_t* rows_out, int64_t* row_offsets, hipStream_t stream);
 

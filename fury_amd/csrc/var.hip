@@ -1826,70 +1826,6 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   }
 }
 
-// --- framing -----------------------------------------------------------------------------------
-// RowEncoder.encode(MemoryBuffer, T): [int32 len = 8 + size][int64 schemaHash][row]
-// (FMT/encoder/Encoders.java:201-213).  Frame i starts at rowOffset(i) + 12 * i, which is
-// 4-byte aligned, so the copy runs in 4-byte words.
-__global__ __launch_bounds__(kThreads) void frame_kernel(const uint8_t* __restrict__ rows,
-                                                         const int64_t* __restrict__ offs,
-                                                         int64_t n, int64_t fixed,
-                                                         int64_t hash, uint8_t* __restrict__ out,
-                                                         int64_t* __restrict__ fo) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  const int64_t b = offs ? offs[i] : i * fixed;
-  const int64_t e = offs ? offs[i + 1] : (i + 1) * fixed;
-  const int64_t start = b + 12 * i;
-  uint32_t* o = reinterpret_cast<uint32_t*>(out + start);
-  if (lane == 0) {
-    o[0] = static_cast<uint32_t>(8 + (e - b));
-    o[1] = static_cast<uint32_t>(hash);
-    o[2] = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
-    if (fo) {
-      fo[i] = start;
-      if (i == n - 1) fo[n] = start + 12 + (e - b);
-    }
-  }
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(rows + b);
-  for (int64_t w = lane; w < ((e - b) >> 2); w += 64) o[3 + w] = s[w];
-}
-
-// Sequential frame walk (frame i's position depends on every earlier length): one lane.
-__global__ void unframe_walk(const uint8_t* __restrict__ in, int64_t len, int64_t n, int64_t hash,
-                             int64_t* __restrict__ frame_pos, int64_t* __restrict__ row_offs,
-                             int32_t* __restrict__ err) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  int64_t pos = 0, out = 0;
-  for (int64_t i = 0; i < n; i++) {
-    if (pos + 12 > len) { *err = 2; return; }
-    int32_t l;
-    int64_t h;
-    memcpy(&l, in + pos, 4);
-    memcpy(&h, in + pos + 4, 8);
-    if (h != hash) { *err = 1; return; }
-    if (l < 8 || pos + 4 + l > len) { *err = 2; return; }
-    frame_pos[i] = pos;
-    row_offs[i] = out;
-    out += l - 8;
-    pos += 4 + l;
-  }
-  row_offs[n] = out;
-}
-
-__global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restrict__ in,
-                                                         const int64_t* __restrict__ frame_pos,
-                                                         const int64_t* __restrict__ row_offs,
-                                                         int64_t n, uint8_t* __restrict__ out) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(in + frame_pos[i] + 12);
-  uint32_t* d = reinterpret_cast<uint32_t*>(out + row_offs[i]);
-  const int64_t words = (row_offs[i + 1] - row_offs[i]) >> 2;
-  for (int64_t w = lane; w < words; w += 64) d[w] = s[w];
-}
-
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back, 1 sizing pass + decode
@@ -2135,43 +2071,6 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   }
   const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
   return st ? st : st2;
-}
-
-int launch_frame_rows(const uint8_t* rows, const int64_t* offs, int64_t n, int64_t fixed,
-                      int64_t hash, uint8_t* out, int64_t* fo, hipStream_t stream) {
-  const int64_t blocks = (n + (kThreads / 64) - 1) / (kThreads / 64);
-  hipLaunchKernelGGL(frame_kernel, dim3(blocks), dim3(kThreads), 0, stream, rows, offs, n, fixed,
-                     hash, out, fo);
-  return check_hip(hipGetLastError(), "frame launch");
-}
-
-int launch_unframe_rows(const uint8_t* in, int64_t len, int64_t n, int64_t hash, uint8_t* rows_out,
-                        int64_t* row_offs, hipStream_t stream) {
-  int64_t* fp = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&fp), n * 8 + 8, stream),
-                     "hipMallocAsync");
-  if (st) return st;
-  int32_t* err = reinterpret_cast<int32_t*>(fp + n);
-  (void)hipMemsetAsync(err, 0, 4, stream);
-  hipLaunchKernelGGL(unframe_walk, dim3(1), dim3(64), 0, stream, in, len, n, hash, fp, row_offs,
-                     err);
-  int32_t herr = 0;
-  (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
-  st = check_hip(hipStreamSynchronize(stream), "unframe sync");
-  if (!st && herr == 0) {
-    const int64_t blocks = (n + (kThreads / 64) - 1) / (kThreads / 64);
-    hipLaunchKernelGGL(unframe_copy, dim3(blocks), dim3(kThreads), 0, stream, in, fp, row_offs, n,
-                       rows_out);
-    st = check_hip(hipGetLastError(), "unframe copy launch");
-  }
-  (void)hipFreeAsync(fp, stream);
-  if (st) return st;
-  if (herr == 1)
-    return set_error(FURY_ERR_CLASS_NOT_COMPATIBLE,
-                     "Schema is not consistent: peer schema hash differs from " +
-                         std::to_string(hash));
-  if (herr == 2) return set_error(FURY_ERR_OUT_OF_BOUNDS, "frame runs past the end of the stream");
-  return FURY_OK;
 }
 
 }  // namespace fury

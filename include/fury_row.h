@@ -213,8 +213,14 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
 /* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,
  * 8-byte, no-null schemas) is a bit set: bit 0 = pipelined persistent kernel (else one tile per
- * workgroup), bit 1 = non-temporal stores, bit 2 = non-temporal loads.  Results are
- * bit-identical across variants.  Default 6 (tile + nt loads + nt stores). */
+ * workgroup), bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode
+ * gather (16 column loads per lane in flight), bit 4 = pair-mode decode (16-B column stores),
+ * bit 5 = deep decode (16 tile loads per lane in flight), bit 6 = pair-mode encode, bit 7 =
+ * padded LDS rows in the encode.  Results are bit-identical across variants.  Default 54
+ * (tile + nt loads/stores + pair-mode deep decode).
+ * Key "var_decode": 0 one-pass look-back decode, 1 sizing pass + decode.
+ * Key "unframe": 0 speculative parallel stream parse (sequential walk when it does not verify),
+ * 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk parsed. */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 

@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--variants", default="0,1,2,3,6,7")
+    ap.add_argument("--layout", default="separate",
+                    help="separate: one allocation per column; arrow: one contiguous body, "
+                         "columns back to back (an Arrow RecordBatch body)")
     args = ap.parse_args()
     import torch
     from fury_amd import _native as N
@@ -31,11 +34,19 @@ def main():
     fields = SCHEMAS["struct100"]
     n = args.rows
     g = torch.Generator(device=dev).manual_seed(1)
-    cols = [Column(values=torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device=dev,
-                                        generator=g)) for _ in fields]
+    if args.layout == "arrow":
+        body = torch.randint(-2**63, 2**63 - 1, (len(fields) * n,), dtype=torch.int64, device=dev,
+                             generator=g)
+        cols = [Column(values=body[i * n:(i + 1) * n]) for i in range(len(fields))]
+    else:
+        cols = [Column(values=torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64,
+                                            device=dev, generator=g)) for _ in fields]
     enc = Encoders.bean(fields, device=dev)
     rows = torch.empty(n * 816, dtype=torch.uint8, device=dev)
     out = enc.alloc_columns(n, validity=False)
+    if args.layout == "arrow":
+        obody = torch.empty(len(fields) * n * 8, dtype=torch.uint8, device=dev)
+        out = [Column(values=obody[i * n * 8:(i + 1) * n * 8]) for i in range(len(fields))]
     batch = RowBatch(rows, None, n, enc.schema_hash)
     variants = [int(v) for v in args.variants.split(",")]
     ref_rows = None

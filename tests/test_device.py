@@ -189,6 +189,114 @@ def test_frame_unframe_roundtrip(oracle, dev):
             other.unframe(stream, n)
 
 
+@pytest.mark.parametrize("variant", [6, 14, 22, 38, 54, 62, 118, 134, 182, 254, 7, 0])
+def test_fixed_variants_bit_exact(oracle, dev, variant):
+    """Every fixed-width kernel variant (tuning 'fixed_variant') writes the oracle's rows and
+    decodes them back, including ragged last tiles (odd row counts for the pair mode)."""
+    from fury_amd import _native as N
+    old = N.lib().fury_get_tuning(b"fixed_variant")
+    assert N.lib().fury_set_tuning(b"fixed_variant", variant) == 0
+    try:
+        for n in (1, 3, 63, 65, 129, 1001):
+            _roundtrip(oracle, "struct100", n, dev, seed=n)
+    finally:
+        N.lib().fury_set_tuning(b"fixed_variant", old)
+
+
+def _walks():
+    from fury_amd import _native as N
+    return N.lib().fury_get_tuning(b"unframe_walks")
+
+
+def _unframe_both(enc, stream, n):
+    """unframe by the speculative parallel parse and by the sequential walk (tuning 'unframe')."""
+    from fury_amd import _native as N
+    assert N.lib().fury_set_tuning(b"unframe", 1) == 0
+    try:
+        walked = enc.unframe(stream, n)
+    finally:
+        N.lib().fury_set_tuning(b"unframe", 0)
+    return enc.unframe(stream, n), walked
+
+
+@pytest.mark.parametrize("name,n", [("mixed", 5000), ("struct100", 3000), ("nested", 4097),
+                                    ("narrow", 1), ("mixed", 257)])
+def test_unframe_parallel_equals_walk(oracle, dev, name, n):
+    """Speculative parallel parse == sequential walk == oracle rows, without falling back."""
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=31)
+    enc = Encoders.bean(fields, device=dev)
+    stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    w0 = _walks()
+    fast, walked = _unframe_both(enc, stream, n)
+    assert _walks() == w0 + 1, "a clean stream must verify without the sequential walk"
+    rows, offs = oracle.encode(fields, host, n)
+    assert np.array_equal(fast.rows.cpu().numpy(), rows)
+    assert np.array_equal(walked.rows.cpu().numpy(), rows)
+    if fast.row_offsets is not None:
+        assert np.array_equal(fast.row_offsets.cpu().numpy(), offs)
+
+
+def test_unframe_fake_header_in_payload(oracle, dev):
+    """A row whose slots spell a plausible frame header ([len 16][schema hash]) is a false
+    candidate: verification fails, the walk re-parses, results are still the oracle's."""
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS["struct100"]
+    n = 600
+    host = gen_columns("struct100", fields, n, seed=5)
+    enc = Encoders.bean(fields, device=dev)
+    h = enc.schema_hash & (2**64 - 1)
+    f0 = host[0].values.view(np.uint64)
+    f1 = host[1].values.view(np.uint64)
+    for r in (0, 5, 599):
+        f0[r] = np.uint64(16 | ((h & 0xFFFFFFFF) << 32))
+        f1[r] = np.uint64(h >> 32)
+    stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    w0 = _walks()
+    got = enc.unframe(stream, n)
+    assert _walks() == w0 + 1, "fake headers must send the stream to the sequential walk"
+    rows, _ = oracle.encode(fields, host, n)
+    assert np.array_equal(got.rows.cpu().numpy(), rows)
+
+
+def test_unframe_unaligned_and_truncated(oracle, dev):
+    from fury_amd.encoder import Encoders, FuryError
+    fields = SCHEMAS["mixed"]
+    n = 777
+    host = gen_columns("mixed", fields, n, seed=6)
+    enc = Encoders.bean(fields, device=dev)
+    stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    rows, offs = oracle.encode(fields, host, n)
+    buf = torch.zeros(stream.numel() + 4, dtype=torch.uint8, device=dev)
+    buf[4:] = stream
+    got = enc.unframe(buf[4:], n)          # 4-byte aligned base: the walk parses it
+    assert np.array_equal(got.rows.cpu().numpy(), rows)
+    with pytest.raises(FuryError):
+        enc.unframe(stream[:-8], n)        # last frame runs past the end
+    short = enc.unframe(stream, n - 1)     # fewer frames than the stream holds: a prefix
+    assert np.array_equal(short.rows.cpu().numpy(), rows[:offs[n - 1]])
+
+
+def test_unframe_large_fast_path(dev):
+    """400k Struct-100 frames (331 MB stream): parallel parse round trip, no fallback."""
+    from fury_amd.encoder import Encoders
+    from fury_amd.workloads import Column as C
+    fields = SCHEMAS["struct100"]
+    n = 400_000
+    g = torch.Generator(device=dev).manual_seed(9)
+    cols = [C(values=torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device=dev,
+                                   generator=g)) for _ in fields]
+    enc = Encoders.bean(fields, device=dev)
+    b = enc.encode_batch(cols, n)
+    stream, _ = enc.frame(b)
+    w0 = _walks()
+    got = enc.unframe(stream, n)
+    assert _walks() == w0
+    assert torch.equal(got.rows, b.rows)
+    del stream, got, b
+
+
 def test_rows_to_arrow_matches_pyarrow(oracle, dev):
     """ArrowWriter path: device Arrow buffers == pyarrow arrays built from the same values."""
     import pyarrow as pa
