@@ -7,11 +7,12 @@
 // Parsing a stream back is inherently a chain (frame i's position depends on every earlier
 // length); walking it with one lane costs one dependent HBM round trip per frame.  The device
 // parse instead speculates and verifies:
-//   mark    every 4-aligned stream position is tested as a frame header (schema hash at +4, length
-//           >= 8, a multiple of 8, inside the stream): one coalesced read of the stream, one
-//           candidate bit per word and a candidate count per workgroup;
-//   scan    device exclusive scan of the counts;
-//   emit    the first nrows candidate positions in stream order;
+//   scan    every 4-aligned stream position is tested as a frame header (schema hash at +4,
+//           length >= 8, a multiple of 8, inside the stream): one coalesced read of the stream.
+//           Each workgroup counts its candidates, takes its place among them by a decoupled
+//           look-back over the workgroups before it (launch order, bounded spin), and writes the
+//           positions and lengths of the first nrows candidates,
+//           staged through LDS so the writes are coalesced;
 //   verify  candidate 0 is at 0 and candidate k + 1 is exactly where frame k ends, for all k
 //           (then candidate k IS frame k, by induction); row offset k = position k - 12 k;
 //   copy    rows, 8 B per lane, into the contiguous row buffer (skips itself unless verified).
@@ -38,30 +39,48 @@ constexpr int kMarkWords = 8;                       // stream words (4 B) per la
 constexpr int kMarkSpan = kThreads * kMarkWords;    // words per workgroup
 constexpr int kCopyFrames = 256;                    // frames per workgroup in the copy pass
 
-// Encoders.encode(MemoryBuffer, T) for each row: a wave per row, 4-byte word copy.
+// Encoders.encode(MemoryBuffer, T) for each row.  A workgroup owns kCopyFrames consecutive rows
+// = one contiguous range of the row buffer and of the stream: lane q moves the row buffer's 8-B
+// word q (its row found by binary search over the range's row offsets in LDS) to stream
+// position rowOffset + 12 * (row + 1) (4-byte aligned: two dword stores); lane f < rows writes
+// frame f's 12-B header.
 __global__ __launch_bounds__(kThreads) void frame_kernel(const uint8_t* __restrict__ rows,
                                                          const int64_t* __restrict__ offs,
                                                          int64_t n, int64_t fixed,
                                                          int64_t hash, uint8_t* __restrict__ out,
                                                          int64_t* __restrict__ fo) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  const int64_t b = offs ? offs[i] : i * fixed;
-  const int64_t e = offs ? offs[i + 1] : (i + 1) * fixed;
-  const int64_t start = b + 12 * i;
-  uint32_t* o = reinterpret_cast<uint32_t*>(out + start);
-  if (lane == 0) {
-    o[0] = static_cast<uint32_t>(8 + (e - b));
+  __shared__ int64_t ro[kCopyFrames + 1];
+  const int64_t k0 = static_cast<int64_t>(blockIdx.x) * kCopyFrames;
+  const int kn = static_cast<int>(min(static_cast<int64_t>(kCopyFrames), n - k0));
+  for (int f = threadIdx.x; f <= kn; f += kThreads) ro[f] = offs ? offs[k0 + f] : (k0 + f) * fixed;
+  __syncthreads();
+  if (threadIdx.x < kn) {
+    const int f = threadIdx.x;
+    const int64_t start = ro[f] + 12 * (k0 + f);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + start);
+    o[0] = static_cast<uint32_t>(8 + (ro[f + 1] - ro[f]));
     o[1] = static_cast<uint32_t>(hash);
     o[2] = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
     if (fo) {
-      fo[i] = start;
-      if (i == n - 1) fo[n] = start + 12 + (e - b);
+      fo[k0 + f] = start;
+      if (k0 + f == n - 1) fo[n] = start + 12 + (ro[f + 1] - ro[f]);
     }
   }
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(rows + b);
-  for (int64_t w = lane; w < ((e - b) >> 2); w += 64) o[3 + w] = s[w];
+  const int64_t base = ro[0];
+  const int64_t words = (ro[kn] - base) >> 3;
+  for (int64_t q = threadIdx.x; q < words; q += kThreads) {
+    const int64_t d = base + 8 * q;
+    int lo = 0, hi = kn - 1;
+    while (lo < hi) {                 // last row that starts at or before d
+      const int mid = (lo + hi + 1) >> 1;
+      if (ro[mid] <= d) lo = mid;
+      else hi = mid - 1;
+    }
+    const uint64_t v = *reinterpret_cast<const uint64_t*>(rows + d);
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + d + 12 * (k0 + lo + 1));
+    o[0] = static_cast<uint32_t>(v);
+    o[1] = static_cast<uint32_t>(v >> 32);
+  }
 }
 
 // ---- sequential walk (reference semantics, fallback) -------------------------------------------
@@ -102,92 +121,211 @@ __global__ __launch_bounds__(kThreads) void unframe_copy_walked(const uint8_t* _
 }
 
 // ---- speculative parallel parse -----------------------------------------------------------------
-__device__ __forceinline__ int block_sum(int x) {
-  __shared__ int part[kThreads / 64];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
-  __syncthreads();
-  int s = 0;
-#pragma unroll
-  for (int w = 0; w < kThreads / 64; w++) s += part[w];
-  return s;
-}
-
-// Exclusive prefix of x over the workgroup (thread order).
-__device__ __forceinline__ int block_excl_scan(int x) {
-  __shared__ int part[kThreads / 64];
+// Exclusive prefix of x over the workgroup (thread order) and the workgroup total, for packed
+// 16-bit counters (no field overflows: at most kThreads * kMarkWords per field).
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t x, uint64_t* total) {
+  __shared__ uint64_t part[kThreads / 64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int inc = x;
+  uint64_t inc = x;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(inc, o);
+    const uint64_t y = __shfl_up(inc, o);
     if (lane >= o) inc += y;
   }
   if (lane == 63) part[wid] = inc;
   __syncthreads();
-  int before = 0;
-  for (int w = 0; w < wid; w++) before += part[w];
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; w++) {
+    before += w < wid ? part[w] : 0;
+    all += part[w];
+  }
+  *total = all;
   return before + inc - x;
 }
 
-// Candidate bits: bit j of mask[g] = stream word kMarkWords * g + j starts a plausible header.
-// The stream base is 16-byte aligned (checked on the host).
-__global__ __launch_bounds__(kThreads) void unframe_mark(const uint32_t* __restrict__ in,
-                                                         int64_t len, int64_t hash,
-                                                         uint8_t* __restrict__ mask,
-                                                         int64_t* __restrict__ counts) {
-  const int64_t W = len >> 2;
-  const int64_t g = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  const int64_t w0 = g * kMarkWords;
-  uint32_t x[kMarkWords + 2];
-  if (w0 + kMarkWords + 2 <= W) {
-    using v4u = __attribute__((ext_vector_type(4))) uint32_t;
-    const v4u a = *reinterpret_cast<const v4u*>(in + w0);
-    const v4u b = *reinterpret_cast<const v4u*>(in + w0 + 4);
-    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-    x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
-    x[8] = in[w0 + 8];
-    x[9] = in[w0 + 9];
-  } else {
-#pragma unroll
-    for (int j = 0; j < kMarkWords + 2; j++) x[j] = w0 + j < W ? in[w0 + j] : 0u;
-  }
-  const uint32_t hlo = static_cast<uint32_t>(hash);
-  const uint32_t hhi = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
-  uint32_t bits = 0;
-#pragma unroll
-  for (int j = 0; j < kMarkWords; j++) {
-    const int64_t p = 4 * (w0 + j);
-    const uint32_t l = x[j];
-    const bool hdr = (w0 + j + 3 <= W) && x[j + 1] == hlo && x[j + 2] == hhi &&
-                     static_cast<int32_t>(l) >= 8 && (l & 7) == 0 &&
-                     p + 4 + static_cast<int64_t>(l) <= len;
-    bits |= hdr ? (1u << j) : 0u;
-  }
-  mask[g] = static_cast<uint8_t>(bits);
-  const int total = block_sum(__popc(bits));
-  if (threadIdx.x == 0) counts[blockIdx.x] = total;
+// Decoupled look-back status words: 2-bit flag (0 = not yet published, kAgg = the workgroup's
+// own count, kInc = inclusive prefix) over a 62-bit value.
+constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The first n candidates' stream positions, in stream order (counts = exclusive prefix).
-__global__ __launch_bounds__(kThreads) void unframe_emit(const uint8_t* __restrict__ mask,
-                                                         const int64_t* __restrict__ counts,
-                                                         int64_t n, int64_t* __restrict__ cand) {
-  const int64_t g = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  uint32_t bits = mask[g];
-  int64_t k = counts[blockIdx.x] + block_excl_scan(__popc(bits));
-  const int64_t w0 = g * kMarkWords;
-  while (bits && k < n) {
-    const int j = __builtin_ctz(bits);
-    cand[k++] = 4 * (w0 + j);
-    bits &= bits - 1;
+// One wave: exclusive prefix of workgroup b.  Workgroups are dispatched in blockIdx order, so
+// every predecessor is running or done; the spin is bounded all the same (a ticket atomic per
+// workgroup would serialise the whole launch on one address), and a workgroup that gives up
+// flags the parse as failed, which sends the stream to the sequential walk.
+// kWin predecessors per step; 64 measured faster than 256 (the polling traffic costs more than
+// the shorter chain saves).
+template <int kWin>
+__device__ int64_t look_back(const uint64_t* status, int64_t b, int32_t* err) {
+  constexpr int U = kWin / 64;            // predecessors per lane per step
+  const int lane = threadIdx.x & 63;
+  int64_t excl = 0;
+  uint32_t spins = 0;
+  for (int64_t j = b - 1;; j -= kWin) {
+    uint64_t v[U];
+    for (;;) {
+      bool pend = false;
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int64_t idx = j - 64 * u - lane;
+        v[u] = idx >= 0 ? ld_status(status + idx) : kInc;
+        pend |= (v[u] >> 62) == 0;
+      }
+      if (__ballot(pend) == 0) break;
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicOr(err, 8);
+        return 0;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    int stop = kWin;                      // nearest inclusive predecessor (distance - 1)
+#pragma unroll
+    for (int u = U - 1; u >= 0; u--) {
+      const uint64_t inc = __ballot((v[u] >> 62) == 2);
+      if (inc) stop = 64 * u + __builtin_ctzll(inc);
+    }
+    int64_t x = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x += (64 * u + lane <= stop) ? static_cast<int64_t>(v[u] & kValMask) : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    excl += x;
+    if (stop < kWin) return excl;
   }
+}
+
+// Candidates of the stream in order: position and length of candidate k < n go to cand[k] /
+// clen[k]; *total = the number of candidates in the whole stream.  A workgroup covers kRounds
+// consecutive 8-KB pieces (lane t of round r reads words r * kMarkSpan + 8 t .. + 8: coalesced),
+// so the look-back chain has one link per 64 KB of stream.  Candidates are staged in LDS in
+// stream order (at most kStage per workgroup: real frames are >= 20 B, so only a stream full of
+// false candidates overflows; it is flagged and goes to the walk).  The stream base is 16-byte
+// aligned (checked on the host); status (nb words) and err are zero at launch.
+constexpr int kRounds = 8;
+constexpr int kStage = 4096;
+template <int kWin>
+__global__ __launch_bounds__(kThreads) void unframe_scan(const uint32_t* __restrict__ in,
+                                                         int64_t len, int64_t hash, int64_t n,
+                                                         uint64_t* __restrict__ status,
+                                                         int64_t* __restrict__ cand,
+                                                         int32_t* __restrict__ clen,
+                                                         int64_t* __restrict__ total,
+                                                         int32_t* __restrict__ err) {
+  __shared__ int64_t spre;
+  __shared__ int32_t spos[kStage];        // candidate word index within the workgroup's span
+  __shared__ int32_t slen[kStage];
+  const int64_t b = blockIdx.x;
+  const int64_t W = len >> 2;
+  const uint32_t hlo = static_cast<uint32_t>(hash);
+  const uint32_t hhi = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
+  int tot = 0;                             // candidates staged so far (workgroup-uniform)
+  bool overflow = false;
+  // every round's words are loaded before any is tested: 64 KB per workgroup in flight
+  uint32_t xs[kRounds][kMarkWords + 2];
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    const int64_t w0 = b * kRounds * kMarkSpan + r * kMarkSpan + threadIdx.x * kMarkWords;
+    uint32_t* x = xs[r];
+    if (w0 + kMarkWords + 2 <= W) {
+      using v4u = __attribute__((ext_vector_type(4))) uint32_t;
+      const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0));
+      const v4u c = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0 + 4));
+      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+      x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
+      x[8] = in[w0 + 8];
+      x[9] = in[w0 + 9];
+    } else {
+#pragma unroll
+      for (int j = 0; j < kMarkWords + 2; j++) x[j] = w0 + j < W ? in[w0 + j] : 0u;
+    }
+  }
+  // candidate bits of every round, then ONE packed scan of the per-round counts (4 rounds of
+  // 16-bit fields per 64-bit word) instead of a workgroup scan per round
+  static_assert(kRounds == 8, "two packed words of four 16-bit round counters");
+  uint32_t bits[kRounds];
+  uint64_t packed[2] = {0, 0};
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    const int64_t w0 = b * kRounds * kMarkSpan + r * kMarkSpan + threadIdx.x * kMarkWords;
+    const uint32_t* x = xs[r];
+    uint32_t bb = 0;
+#pragma unroll
+    for (int j = 0; j < kMarkWords; j++) {
+      const int64_t p = 4 * (w0 + j);
+      const uint32_t l = x[j];
+      const bool hdr = (w0 + j + 3 <= W) && x[j + 1] == hlo && x[j + 2] == hhi &&
+                       static_cast<int32_t>(l) >= 8 && (l & 7) == 0 &&
+                       p + 4 + static_cast<int64_t>(l) <= len;
+      bb |= hdr ? (1u << j) : 0u;
+    }
+    bits[r] = bb;
+    packed[r >> 2] |= static_cast<uint64_t>(__popc(bb)) << (16 * (r & 3));
+  }
+  uint64_t tlo, thi;
+  const uint64_t elo = block_excl_scan64(packed[0], &tlo);
+  __syncthreads();                         // block_excl_scan64's LDS reused
+  const uint64_t ehi = block_excl_scan64(packed[1], &thi);
+  int base = 0;                            // candidates of the earlier rounds (all threads)
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) {
+    const uint64_t e = r < 4 ? elo : ehi, t = r < 4 ? tlo : thi;
+    const int sh = 16 * (r & 3);
+    int local = base + static_cast<int>((e >> sh) & 0xffff);
+    const int rel = r * kMarkSpan + threadIdx.x * kMarkWords;
+#pragma unroll
+    for (int j = 0; j < kMarkWords; j++) {
+      if (bits[r] & (1u << j)) {
+        if (local < kStage) {
+          spos[local] = rel + j;
+          slen[local] = static_cast<int32_t>(xs[r][j]);
+        }
+        local++;
+      }
+    }
+    base += static_cast<int>((t >> sh) & 0xffff);
+  }
+  tot = base;
+  overflow = tot > kStage;
+  __syncthreads();
+  if (overflow) {
+    if (threadIdx.x == 0) atomicOr(err, 16);
+    tot = kStage;                          // keep the chain consistent; the parse is discarded
+  }
+  if (threadIdx.x == 0 && b == 0) {
+    st_status(status, kInc | static_cast<uint64_t>(tot));
+    spre = 0;
+  } else if (threadIdx.x == 0) {
+    st_status(status + b, kAgg | static_cast<uint64_t>(tot));
+  }
+  if (b > 0 && threadIdx.x < 64) {
+    const int64_t pre = look_back<kWin>(status, b, err);
+    if (threadIdx.x == 0) {
+      st_status(status + b, kInc | static_cast<uint64_t>(pre + tot));
+      spre = pre;
+    }
+  }
+  __syncthreads();
+  const int64_t pre = spre;
+  for (int i = threadIdx.x; i < tot; i += kThreads) {
+    const int64_t k = pre + i;
+    if (k < n) {
+      cand[k] = 4 * (b * kRounds * kMarkSpan + spos[i]);
+      clen[k] = slen[i];
+    }
+  }
+  if (threadIdx.x == 0 && b == gridDim.x - 1) *total = pre + tot;
 }
 
 // Candidate k is frame k iff candidate 0 is at 0 and each candidate ends where the next begins.
-__global__ __launch_bounds__(kThreads) void unframe_verify(const uint8_t* __restrict__ in,
-                                                           const int64_t* __restrict__ cand,
+__global__ __launch_bounds__(kThreads) void unframe_verify(const int64_t* __restrict__ cand,
+                                                           const int32_t* __restrict__ clen,
                                                            const int64_t* __restrict__ total,
                                                            int64_t n, int64_t* __restrict__ row_offs,
                                                            int32_t* __restrict__ err) {
@@ -198,7 +336,7 @@ __global__ __launch_bounds__(kThreads) void unframe_verify(const uint8_t* __rest
     return;
   }
   const int64_t p = cand[k];
-  const int64_t end = p + 4 + *reinterpret_cast<const int32_t*>(in + p);
+  const int64_t end = p + 4 + clen[k];
   bool ok = k != 0 || p == 0;
   if (k + 1 < n) ok = ok && cand[k + 1] == end;
   row_offs[k] = p - 12 * k;
@@ -241,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
 }
 
 std::atomic<int64_t> g_unframe_walks{0};   // streams parsed by the sequential walk
-int g_unframe_mode = 0;                     // tuning "unframe": 0 speculative, 1 always walk
+int g_unframe_mode = 0;   // tuning "unframe": 0 speculative, 1 always walk
 
 int unframe_walked(const uint8_t* in, int64_t len, int64_t n, int64_t hash, uint8_t* rows_out,
                    int64_t* row_offs, hipStream_t stream) {
@@ -282,7 +420,7 @@ int64_t unframe_walk_count() { return g_unframe_walks.load(); }
 int launch_frame_rows(const uint8_t* rows, const int64_t* offs, int64_t n, int64_t fixed,
                       int64_t hash, uint8_t* out, int64_t* fo, hipStream_t stream) {
   if (n == 0) return FURY_OK;
-  const int64_t blocks = (n + (kThreads / 64) - 1) / (kThreads / 64);
+  const int64_t blocks = (n + kCopyFrames - 1) / kCopyFrames;
   hipLaunchKernelGGL(frame_kernel, dim3(blocks), dim3(kThreads), 0, stream, rows, offs, n, fixed,
                      hash, out, fo);
   return check_hip(hipGetLastError(), "frame launch");
@@ -294,28 +432,26 @@ int launch_unframe_rows(const uint8_t* in, int64_t len, int64_t n, int64_t hash,
   if (n == 0 || len < 12 || !aligned || g_unframe_mode == 1)
     return unframe_walked(in, len, n, hash, rows_out, row_offs, stream);
   const int64_t W = len >> 2;
-  const int64_t nb = (W + kMarkSpan - 1) / kMarkSpan;
+  const int64_t nb = (W + kRounds * kMarkSpan - 1) / (kRounds * kMarkSpan);
   if (nb > 0x7fffffff) return set_error(FURY_ERR_INVALID_ARGUMENT, "stream too large");
-  // workspace: [cand n][counts nb][total][scan ws][err (8 B)][mask nb * kThreads bytes]
-  const int64_t ws_n = scan_workspace(nb);
-  const int64_t words = n + nb + 1 + ws_n + 1;
+  // workspace: [cand n][status nb][total][err (8 B)][clen n x 4 B]
+  const int64_t words = n + nb + 2;
   uint8_t* buf = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&buf), words * 8 + nb * kThreads,
-                                    stream), "hipMallocAsync");
+  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&buf), words * 8 + n * 4, stream),
+                     "hipMallocAsync");
   if (st) return st;
   int64_t* cand = reinterpret_cast<int64_t*>(buf);
-  int64_t* counts = cand + n;
-  int64_t* total = counts + nb;
-  int64_t* ws = total + 1;
-  int32_t* err = reinterpret_cast<int32_t*>(ws + ws_n);
-  uint8_t* mask = buf + words * 8;
-  (void)hipMemsetAsync(err, 0, 4, stream);
-  hipLaunchKernelGGL(unframe_mark, dim3(nb), dim3(kThreads), 0, stream,
-                     reinterpret_cast<const uint32_t*>(in), len, hash, mask, counts);
-  device_scan(counts, nb, total, ws, stream);
-  hipLaunchKernelGGL(unframe_emit, dim3(nb), dim3(kThreads), 0, stream, mask, counts, n, cand);
+  uint64_t* status = reinterpret_cast<uint64_t*>(cand + n);
+  int64_t* total = reinterpret_cast<int64_t*>(status + nb);
+  int32_t* err = reinterpret_cast<int32_t*>(total + 1);
+  int32_t* clen = reinterpret_cast<int32_t*>(buf + words * 8);
+  (void)hipMemsetAsync(status, 0, (nb + 2) * 8, stream);
+  hipLaunchKernelGGL(unframe_scan<64>, dim3(nb),
+                     dim3(kThreads), 0, stream,
+                     reinterpret_cast<const uint32_t*>(in), len, hash, n, status, cand, clen,
+                     total, err);
   const int64_t vb = (n + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(unframe_verify, dim3(vb), dim3(kThreads), 0, stream, in, cand, total, n,
+  hipLaunchKernelGGL(unframe_verify, dim3(vb), dim3(kThreads), 0, stream, cand, clen, total, n,
                      row_offs, err);
   const int64_t cb = (n + kCopyFrames - 1) / kCopyFrames;
   hipLaunchKernelGGL(unframe_copy, dim3(cb), dim3(kThreads), 0, stream, in, cand, row_offs, n,
