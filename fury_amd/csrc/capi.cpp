@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -487,6 +488,28 @@ int fury_unframe_rows(const fury_schema* s, const void* stream_bytes, int64_t st
   return launch_unframe_rows(static_cast<const uint8_t*>(stream_bytes), stream_len, nrows,
                              s->schema_hash, static_cast<uint8_t*>(rows_out), row_offsets,
                              static_cast<hipStream_t>(stream));
+}
+
+int fury_arrow_ipc_schema(const fury_schema* s, uint8_t* out, int64_t cap, int64_t* len) {
+  if (!s || !len) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema/len is null");
+  std::vector<uint8_t> msg;
+  const int st = ipc_schema_message(s, &msg);
+  if (st) return st;
+  *len = static_cast<int64_t>(msg.size());
+  if (!out) return FURY_OK;
+  if (cap < *len) return set_error(FURY_ERR_CAPACITY, "IPC schema message needs " +
+                                                          std::to_string(*len) + " bytes");
+  std::memcpy(out, msg.data(), msg.size());
+  return FURY_OK;
+}
+
+int fury_arrow_ipc_record_batch(const fury_schema* s, const fury_column* columns, int64_t nrows,
+                                void* out, int64_t cap, int64_t* len, void* stream) {
+  if (!s || !len) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema/len is null");
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (!columns && s->num_fields > 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "columns is null");
+  return ipc_record_batch(s, columns, nrows, static_cast<uint8_t*>(out), cap, len,
+                          static_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -130,4 +130,11 @@ int64_t unframe_walk_count();
 int launch_unframe_rows(const uint8_t* in, int64_t in_len, int64_t nrows, int64_t schema_hash,
                         uint8_t* rows_out, int64_t* row_offsets, hipStream_t stream);
 
+// Arrow IPC (ipc.hip): encapsulated Schema message (host bytes) and RecordBatch message of
+// device columns written to device memory (out == NULL: *len only).
+int type_width_of(int32_t type_id);
+int ipc_schema_message(const fury_schema* s, std::vector<uint8_t>* out);
+int ipc_record_batch(const fury_schema* s, const fury_column* cols, int64_t n, uint8_t* out,
+                     int64_t cap, int64_t* len, hipStream_t stream);
+
 }  // namespace fury

@@ -522,6 +522,49 @@ class ArrowWriter:
         return columns_to_record_batch(self._enc.schema().fields,
                                        [column_to_host(c) for c in self.finish()], self._n)
 
+    # -- Arrow IPC (ArrowUtils.serializeRecordBatch / ArrowSerializers, ArrowUtils.java:63-72,
+    #    ArrowSerializers.java:128-167) ---------------------------------------------------------
+    def ipc_schema(self) -> bytes:
+        """Encapsulated IPC Schema message (host bytes)."""
+        return ipc_schema_message(self._enc)
+
+    def finish_as_ipc_message(self, stream=None) -> torch.Tensor:
+        """The written batch as ONE encapsulated IPC RecordBatch message in device memory
+        (``serializeRecordBatch`` of ``finishAsRecordBatch()``)."""
+        return ipc_record_batch_message(self._enc, self.finish(), self._n, stream)
+
+    def finish_as_ipc_stream(self, stream=None) -> bytes:
+        """Schema message + the batch + end-of-stream marker, on the host: the bytes
+        ``ArrowStreamWriter`` writes for the batch (ArrowSerializers.java:128-134)."""
+        body = self.finish_as_ipc_message(stream).cpu().numpy().tobytes()
+        return self.ipc_schema() + body + IPC_EOS
+
     def reset(self) -> None:
         self._cols = None
         self._n = 0
+
+
+IPC_EOS = b"\xff\xff\xff\xff\x00\x00\x00\x00"
+
+
+def ipc_schema_message(enc: "RowEncoder") -> bytes:
+    n = ctypes.c_int64(0)
+    _check(N.lib().fury_arrow_ipc_schema(enc._schema.handle, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value)
+    _check(N.lib().fury_arrow_ipc_schema(enc._schema.handle, buf, n.value, ctypes.byref(n)))
+    return buf.raw[:n.value]
+
+
+def ipc_record_batch_message(enc: "RowEncoder", cols: List[Column], nrows: int,
+                             stream=None) -> torch.Tensor:
+    """Encapsulated IPC RecordBatch message of device columns, gathered on the device."""
+    keep: list = []
+    cc = _c_columns(cols, keep)
+    n = ctypes.c_int64(0)
+    sh = _stream_handle(stream)
+    _check(N.lib().fury_arrow_ipc_record_batch(enc._schema.handle, cc, nrows, None, 0,
+                                               ctypes.byref(n), sh))
+    out = torch.empty(max(n.value, 16), dtype=torch.uint8, device=enc.device)
+    _check(N.lib().fury_arrow_ipc_record_batch(enc._schema.handle, cc, nrows, _ptr(out), n.value,
+                                               ctypes.byref(n), sh))
+    return out[:n.value]

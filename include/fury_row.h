@@ -236,6 +236,24 @@ int fury_frame_rows(const fury_schema* schema, const void* rows, const int64_t* 
 int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64_t stream_len,
                       int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream);
 
+/* ---- Arrow IPC (ArrowUtils.serializeRecordBatch, FMT/vectorized/ArrowUtils.java:63-72;
+ *      ArrowSerializers stream writers, FMT/vectorized/ArrowSerializers.java:128-167) --------- */
+/* Encapsulated IPC Schema message of the schema, in HOST memory:
+ * [0xFFFFFFFF][int32 metadata size][flatbuffer Message<Schema>][padding to 8].  *len receives
+ * the size; out == NULL only sets *len, a too small cap returns FURY_ERR_CAPACITY.  An IPC
+ * stream is this message, then record batch messages, then the 8-byte end-of-stream marker
+ * [0xFFFFFFFF][0x00000000] (ArrowStreamWriter.writeEndOfStream). */
+int fury_arrow_ipc_schema(const fury_schema* schema, uint8_t* out, int64_t cap, int64_t* len);
+/* Encapsulated IPC RecordBatch message of device columns (fury_rows_to_arrow output, or any
+ * columns in that layout) written to DEVICE memory `out` (16-byte aligned): flatbuffer metadata,
+ * then the body = every Arrow buffer in pre-order (validity, offsets, values; children after
+ * their parent; a MAP's "entries" struct node in between), each padded to 64 bytes.  Null
+ * counts are computed on the device from the validity bitmaps.  The lengths of variable-size
+ * buffers are read back from the device offsets, so the call is synchronous on `stream`.
+ * out == NULL only sets *len. */
+int fury_arrow_ipc_record_batch(const fury_schema* schema, const fury_column* columns,
+                                int64_t nrows, void* out, int64_t cap, int64_t* len, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,9 @@ Legs: frame (Encoders.encode(MemoryBuffer, T) for every row), unframe by the spe
 parse (tuning unframe=0), and — on a bounded prefix, since it is one dependent HBM round trip
 per frame — by the sequential walk (unframe=1).  Algorithmic bytes: frame reads the rows (+ row
 offsets) and writes rows + 12 B per frame; unframe reads the stream and writes rows + row offsets.
-Prints one JSON line with median ms and GB/s per leg.
+Also times the Arrow IPC RecordBatch message of the decoded columns (leg "ipc": body gathered on
+the device, reads the columns and writes the message).  Prints one JSON line with median ms
+and GB/s per leg.
 """
 import argparse
 import json
@@ -28,7 +30,7 @@ def main():
     args = ap.parse_args()
     import torch
     from fury_amd import _native as N
-    from fury_amd.encoder import Encoders
+    from fury_amd.encoder import ArrowWriter, Encoders, ipc_record_batch_message
     from bench import DEFAULT_ROWS, make_device_columns
     from fury_amd.workloads import SCHEMAS
     dev = torch.device("cuda:0")
@@ -47,7 +49,12 @@ def main():
         else stream[:(batch.rows.numel() // n) * nw + 12 * nw]
     row_bytes = batch.rows.numel()
     offs_bytes = 0 if batch.row_offsets is None else 8 * (n + 1)
+    aw = ArrowWriter(enc)
+    aw.write(batch)
+    dcols = aw.finish()
+    ipc_len = ipc_record_batch_message(enc, dcols, n).numel()
     legs = {
+        "ipc": (lambda: ipc_record_batch_message(enc, dcols, n), 2 * ipc_len),
         "frame": (lambda: enc.frame(batch), row_bytes + offs_bytes + stream.numel() + 8 * (n + 1)),
         "unframe": (lambda: enc.unframe(stream, n), stream.numel() + row_bytes + 8 * (n + 1)),
     }
