@@ -236,35 +236,29 @@ def main():
 
 
 def end_to_end(enc, cols, n, dev, stream):
-    """Host(pinned) columns -> H2D -> encode -> D2H rows, then back: the PCIe-inclusive rate
-    (reported in DESIGN.md, never `value`)."""
+    """Host (pinned) columns -> rows in host memory -> columns in host memory through the
+    host-memory batch path a JVM caller uses (fury_row_encode_host / fury_row_decode_host:
+    chunked H2D, kernel and D2H on three streams, overlapped): the PCIe-inclusive rate reported
+    in DESIGN.md, never `value`."""
     import torch
-    from fury_amd.encoder import RowBatch
-    host_cols = [c.values.to("cpu").pin_memory() for c in cols]
+    from fury_amd.workloads import Column
+    host_cols = [Column(values=c.values.view(torch.uint8).to("cpu").pin_memory()) for c in cols]
     fixed = enc.schema().fixed_size
     host_rows = torch.empty(n * fixed, dtype=torch.uint8).pin_memory()
-    dev_rows = torch.empty(n * fixed, dtype=torch.uint8, device=dev)
-    from fury_amd.workloads import Column
-    dcols = [Column(values=torch.empty_like(c.values)) for c in cols]
-    out = enc.alloc_columns(n, validity=False)
+    out = [Column(values=torch.empty(n * 8, dtype=torch.uint8).pin_memory()) for _ in cols]
+    enc.encode_host(host_cols, n, rows=host_rows)          # warm-up (device buffers, streams)
     reps = 3
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        for h, d in zip(host_cols, dcols):
-            d.values.copy_(h, non_blocking=True)
-        enc.encode_into(dcols, n, dev_rows, None, stream=stream)
-        host_rows.copy_(dev_rows, non_blocking=True)
-        dev_rows.copy_(host_rows, non_blocking=True)
-        enc.decode_batch(RowBatch(dev_rows, None, n, enc.schema_hash), validity=False,
-                         stream=stream, out=out)
-        for h, o in zip(host_cols, out):
-            h.view(torch.uint8).copy_(o.values, non_blocking=True)
-    torch.cuda.synchronize()
+        enc.encode_host(host_cols, n, rows=host_rows)
+        enc.decode_host(host_rows, None, n, out=out)
     dt = (time.perf_counter() - t0) / reps
+    for k in (0, len(cols) // 2, len(cols) - 1):
+        assert torch.equal(out[k].values, host_cols[k].values), "host-path round trip"
     alg = 2 * (n * 800 + n * fixed)
     return {"GBps_algorithmic": round(alg / dt / 1e9, 2), "ms_per_step": round(dt * 1e3, 2),
-            "what": "pinned host columns -> H2D -> encode -> D2H rows -> H2D -> decode -> D2H"}
+            "what": "pinned host columns -> fury_row_encode_host -> host rows -> "
+                    "fury_row_decode_host -> host columns (chunked H2D/kernel/D2H on 3 streams)"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,437 @@
+// hostpath.cpp — the host-memory batch path: columns and rows that live in host memory (a JVM's
+// off-heap DirectByteBuffers, read from a socket or a file — the north-star boundary) go
+// through HBM and back inside one call.  This is what the JNI glue calls with
+// GetDirectBufferAddress pointers; the device entry points of capi.cpp do the work.
+//
+// Fixed-width schemas (Struct-100) are streamed in 64-row-aligned chunks on three HIP streams:
+// chunk k's H2D copies, chunk k-1's kernel and chunk k-2's D2H copies overlap, so the call runs
+// at the PCIe rate (both directions of the link busy) rather than at the sum of the three
+// phases.  Variable-length schemas are staged whole: their row offsets are a scan over the
+// whole batch.  Pinning (hipHostRegister) is the caller's choice (fury_host_register): pinned
+// buffers DMA at the link rate, pageable ones are bounced through the runtime's staging buffers.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "kernels.h"
+
+namespace fury {
+namespace {
+
+constexpr int kStages = 3;
+
+struct DeviceArena {                            // frees everything it handed out
+  std::vector<void*> ptrs;
+  ~DeviceArena() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  int alloc(int64_t bytes, void** out) {
+    *out = nullptr;
+    if (bytes <= 0) bytes = 16;
+    const int st = check_hip(hipMalloc(out, static_cast<size_t>(bytes)), "hipMalloc");
+    if (!st) ptrs.push_back(*out);
+    return st;
+  }
+};
+
+struct Streams {
+  hipStream_t s[kStages] = {};
+  ~Streams() {
+    for (auto& x : s)
+      if (x) (void)hipStreamDestroy(x);
+  }
+  int create() {
+    for (auto& x : s) {
+      const int st = check_hip(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate");
+      if (st) return st;
+    }
+    return FURY_OK;
+  }
+  int sync() {
+    int st = FURY_OK;
+    for (auto& x : s) {
+      const int e = check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
+      if (!st) st = e;
+    }
+    return st;
+  }
+};
+
+// Bytes of a fixed-width column's values for rows [0, n).
+int64_t fixed_bytes(const FieldPlan& p, int64_t n) {
+  return p.kind == kBool ? (n + 7) / 8 : n * p.width;
+}
+// Device bitmap buffers are written as 32-bit words (fury_row.h): pad to 4 bytes.
+int64_t bitmap_alloc(int64_t n) { return ((n + 31) / 32) * 4 + 4; }
+
+// Bytes one row occupies in a stage (row image + its column values + validity bits, rounded up).
+int64_t stage_bytes_per_row(const fury_schema* s) {
+  int64_t per_row = s->fixed_size;
+  for (const auto& p : s->plan) per_row += p.width > 0 ? p.width : 1;
+  return per_row + s->num_fields;             // validity bits, generously
+}
+
+// Rows per chunk: kTargetChunks chunks (env FURY_HOST_CHUNKS), 64-row aligned (bitmaps slice on
+// 32-bit words), at most kMaxStageBytes of HBM per stage.  Measured on the MI355X box
+// (scripts/ab_host.py, profiles/r01_host_path.json): the H2D and D2H copies of different
+// streams did not overlap there, and every extra chunk adds one copy per column, so more chunks
+// were slower (1: 42.6 GB/s, 3: 41.8, 6: 31.5, 12: 22.2 GB/s encode); the default is one chunk
+// (whole batch staged), the pipeline stays for hosts whose copy engines do overlap.
+constexpr int64_t kTargetChunks = 1;
+constexpr int64_t kMaxStageBytes = 1ll << 30;
+int64_t rows_per_chunk(const fury_schema* s, int64_t n) {
+  const int64_t per_row = stage_bytes_per_row(s);
+  int64_t chunks = kTargetChunks;
+  if (const char* e = getenv("FURY_HOST_CHUNKS")) chunks = atoll(e) > 0 ? atoll(e) : chunks;
+  int64_t c = (n + chunks - 1) / chunks;
+  if (c * per_row > kMaxStageBytes) c = kMaxStageBytes / per_row;
+  c = ((c + 63) / 64) * 64;
+  return c < 64 ? 64 : c;
+}
+
+int fixed_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows, bool decode,
+               int32_t device) {
+  if (n == 0) return FURY_OK;
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  const int64_t C = rows_per_chunk(s, n);
+  const int nf = s->num_fields;
+  Streams ss;
+  if ((st = ss.create())) return st;
+  // one stream-ordered workspace for all stages (pooled by the runtime across calls)
+  std::vector<int64_t> col_off(nf), val_off(nf);
+  int64_t stage = ((C * s->fixed_size + 255) / 256) * 256;
+  for (int k = 0; k < nf; k++) {
+    col_off[k] = stage;
+    stage += ((fixed_bytes(s->plan[k], C) + 16 + 255) / 256) * 256;
+    val_off[k] = -1;
+    if (host[k].validity) {
+      val_off[k] = stage;
+      stage += ((bitmap_alloc(C) + 255) / 256) * 256;
+    }
+  }
+  static bool pool_kept = false;             // keep the workspace pooled between calls
+  if (!pool_kept) {
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+      uint64_t keep = UINT64_MAX;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    pool_kept = true;
+  }
+  uint8_t* ws = nullptr;
+  if ((st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), stage * kStages, ss.s[0]),
+                      "hipMallocAsync")))
+    return st;
+  hipEvent_t ready;
+  (void)hipEventCreateWithFlags(&ready, hipEventDisableTiming);
+  (void)hipEventRecord(ready, ss.s[0]);
+  for (int g = 1; g < kStages; g++) (void)hipStreamWaitEvent(ss.s[g], ready, 0);
+  std::vector<std::vector<fury_column>> dcols(kStages, std::vector<fury_column>(nf));
+  std::vector<void*> drows(kStages);
+  for (int g = 0; g < kStages; g++) {
+    uint8_t* base = ws + g * stage;
+    drows[g] = base;
+    for (int k = 0; k < nf; k++) {
+      dcols[g][k] = fury_column{};
+      dcols[g][k].values = base + col_off[k];
+      if (val_off[k] >= 0) dcols[g][k].validity = base + val_off[k];
+    }
+  }
+  for (int64_t r0 = 0, k = 0; r0 < n && !st; r0 += C, k++) {
+    const int g = static_cast<int>(k % kStages);
+    hipStream_t hs = ss.s[g];
+    const int64_t nr = n - r0 < C ? n - r0 : C;
+    uint8_t* hrows = rows + r0 * s->fixed_size;
+    if (!decode) {
+      for (int j = 0; j < nf; j++) {
+        const FieldPlan& p = s->plan[j];
+        const uint8_t* hv = static_cast<const uint8_t*>(host[j].values) +
+                            (p.kind == kBool ? r0 / 8 : r0 * p.width);
+        (void)hipMemcpyAsync(dcols[g][j].values, hv, fixed_bytes(p, nr), hipMemcpyHostToDevice, hs);
+        if (host[j].validity)
+          (void)hipMemcpyAsync(dcols[g][j].validity, host[j].validity + r0 / 8, (nr + 7) / 8,
+                               hipMemcpyHostToDevice, hs);
+      }
+      st = fury_row_encode(s, dcols[g].data(), nr, nullptr, drows[g], hs);
+      if (!st)
+        st = check_hip(hipMemcpyAsync(hrows, drows[g], nr * s->fixed_size, hipMemcpyDeviceToHost,
+                                      hs), "hipMemcpyAsync D2H rows");
+    } else {
+      (void)hipMemcpyAsync(drows[g], hrows, nr * s->fixed_size, hipMemcpyHostToDevice, hs);
+      st = fury_row_decode(s, drows[g], nullptr, nr, dcols[g].data(), hs);
+      for (int j = 0; j < nf && !st; j++) {
+        const FieldPlan& p = s->plan[j];
+        uint8_t* hv = static_cast<uint8_t*>(host[j].values) +
+                      (p.kind == kBool ? r0 / 8 : r0 * p.width);
+        (void)hipMemcpyAsync(hv, dcols[g][j].values, fixed_bytes(p, nr), hipMemcpyDeviceToHost, hs);
+        if (host[j].validity)
+          (void)hipMemcpyAsync(host[j].validity + r0 / 8, dcols[g][j].validity, (nr + 7) / 8,
+                               hipMemcpyDeviceToHost, hs);
+      }
+      if (!st) st = check_hip(hipGetLastError(), "hipMemcpyAsync D2H columns");
+    }
+  }
+  const int st2 = ss.sync();                  // every stage done before the workspace goes
+  (void)hipFreeAsync(ws, ss.s[0]);
+  const int st3 = check_hip(hipStreamSynchronize(ss.s[0]), "hipStreamSynchronize");
+  (void)hipEventDestroy(ready);
+  return st ? st : st2 ? st2 : st3;
+}
+
+// ---- variable-length schemas: stage the whole batch ----------------------------------------
+int host_offset(const int32_t* offs, int64_t i) { return offs ? offs[i] : 0; }
+
+// Copies a host column tree (Arrow layout of fury_row.h) of `n` entries to the device.
+int stage_column(const OwnedField& f, const fury_column& h, int64_t n, DeviceArena& arena,
+                 std::deque<std::vector<fury_column>>& kids, fury_column* d, hipStream_t hs) {
+  *d = fury_column{};
+  auto copy = [&](const void* src, int64_t bytes, void** dst) {
+    int st = arena.alloc(bytes + 16, dst);
+    if (!st && bytes > 0 && src)
+      st = check_hip(hipMemcpyAsync(*dst, src, bytes, hipMemcpyHostToDevice, hs), "H2D column");
+    return st;
+  };
+  int st = FURY_OK;
+  if (h.validity) {
+    void* v = nullptr;
+    if ((st = copy(h.validity, (n + 7) / 8, &v))) return st;
+    d->validity = static_cast<uint8_t*>(v);
+  }
+  const int t = f.type_id;
+  if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST || t == FURY_TYPE_MAP) {
+    if (n > 0 && !h.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, f.name + ": offsets is null");
+    void* o = nullptr;
+    if ((st = copy(h.offsets, n > 0 ? (n + 1) * 4 : 0, &o))) return st;
+    d->offsets = static_cast<int32_t*>(o);
+  }
+  const int64_t m = n > 0 ? host_offset(h.offsets, n) : 0;
+  switch (t) {
+    case FURY_TYPE_STRING: case FURY_TYPE_BINARY:
+      return copy(h.values, m, &d->values);
+    case FURY_TYPE_LIST: case FURY_TYPE_MAP: case FURY_TYPE_STRUCT: {
+      const int64_t len = t == FURY_TYPE_STRUCT ? n : m;
+      if (!h.child && len > 0) return set_error(FURY_ERR_INVALID_ARGUMENT, f.name + ": child is null");
+      kids.emplace_back(f.children.size());
+      std::vector<fury_column>& kc = kids.back();
+      for (size_t i = 0; i < f.children.size(); i++) {
+        static const fury_column empty{};
+        if ((st = stage_column(f.children[i], h.child ? h.child[i] : empty, len, arena, kids,
+                               &kc[i], hs)))
+          return st;
+      }
+      d->child = kc.data();
+      return FURY_OK;
+    }
+    case FURY_TYPE_BOOL:
+      return copy(h.values, (n + 7) / 8, &d->values);
+    default:
+      return copy(h.values, n * type_width_of(t), &d->values);
+  }
+}
+
+int var_encode_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
+                    int64_t cap, int64_t* row_offsets, int64_t* row_bytes, int32_t device) {
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  Streams ss;
+  if ((st = ss.create())) return st;
+  hipStream_t hs = ss.s[0];
+  DeviceArena arena;
+  std::deque<std::vector<fury_column>> kids;     // stable addresses: children point into it
+  std::vector<fury_column> dcols(s->num_fields);
+  for (int k = 0; k < s->num_fields; k++)
+    if ((st = stage_column(s->fields[k], host[k], n, arena, kids, &dcols[k], hs))) return st;
+  void* doffs = nullptr;
+  if ((st = arena.alloc((n + 1) * 8, &doffs))) return st;
+  int64_t* dof = static_cast<int64_t*>(doffs);
+  if ((st = fury_row_measure(s, dcols.data(), n, dof, hs))) return st;
+  int64_t total = 0;
+  if ((st = check_hip(hipMemcpyAsync(&total, dof + n, 8, hipMemcpyDeviceToHost, hs), "D2H total")))
+    return st;
+  if ((st = ss.sync())) return st;
+  *row_bytes = total;
+  if (total > cap)
+    return set_error(FURY_ERR_CAPACITY, "rows need " + std::to_string(total) +
+                                            " bytes, capacity is " + std::to_string(cap));
+  void* drows = nullptr;
+  if ((st = arena.alloc(total, &drows))) return st;
+  if ((st = fury_row_encode(s, dcols.data(), n, dof, drows, hs))) return st;
+  (void)hipMemcpyAsync(rows, drows, total, hipMemcpyDeviceToHost, hs);
+  (void)hipMemcpyAsync(row_offsets, dof, (n + 1) * 8, hipMemcpyDeviceToHost, hs);
+  return ss.sync();
+}
+
+// Flat variable-length schemas: size the outputs on the device (decode measure), check them
+// against the host buffers' capacities, decode, copy back.
+int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* row_offsets,
+                    int64_t n, fury_column* host, int32_t device) {
+  if (s->generic)
+    return set_error(FURY_ERR_UNSUPPORTED,
+                     "host-memory decode of nested schemas: use the device API (fury_decode_prepare)");
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  Streams ss;
+  if ((st = ss.create())) return st;
+  hipStream_t hs = ss.s[0];
+  DeviceArena arena;
+  const int64_t total = row_offsets[n];
+  void *drows = nullptr, *doffs = nullptr;
+  if ((st = arena.alloc(total, &drows)) || (st = arena.alloc((n + 1) * 8, &doffs))) return st;
+  (void)hipMemcpyAsync(drows, rows, total, hipMemcpyHostToDevice, hs);
+  (void)hipMemcpyAsync(doffs, row_offsets, (n + 1) * 8, hipMemcpyHostToDevice, hs);
+  const int nf = s->num_fields;
+  std::vector<fury_column> d(nf);
+  std::vector<fury_column> dchild(nf);
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    fury_column& c = d[k];
+    c = fury_column{};
+    void* v = nullptr;
+    if (host[k].validity) {
+      if ((st = arena.alloc(bitmap_alloc(n), &v))) return st;
+      c.validity = static_cast<uint8_t*>(v);
+    }
+    if (p.kind == kBytes || p.kind == kListFixed) {
+      if (!host[k].offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "output offsets is null");
+      if ((st = arena.alloc((n + 1) * 4, &v))) return st;
+      c.offsets = static_cast<int32_t*>(v);
+      if (p.kind == kListFixed) {           // element column, sized after the measure
+        dchild[k] = fury_column{};
+        c.child = &dchild[k];
+      }
+    } else {
+      const int64_t bytes = p.kind == kDecimal ? n * 16 : p.kind == kBool ? bitmap_alloc(n)
+                                                                          : n * p.width;
+      if ((st = arena.alloc(bytes, &c.values))) return st;
+    }
+  }
+  if ((st = fury_row_decode_measure(s, drows, static_cast<int64_t*>(doffs), n, d.data(), hs)))
+    return st;
+  std::vector<int32_t> need(nf, 0);
+  for (int k = 0; k < nf; k++)
+    if (d[k].offsets)
+      (void)hipMemcpyAsync(&need[k], d[k].offsets + n, 4, hipMemcpyDeviceToHost, hs);
+  if ((st = ss.sync())) return st;
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    if (!d[k].offsets) continue;
+    if (p.kind == kBytes) {
+      if (host[k].capacity < need[k])
+        return set_error(FURY_ERR_CAPACITY, "column " + s->fields[k].name + " needs " +
+                                                std::to_string(need[k]) + " payload bytes");
+      if ((st = arena.alloc(need[k], &d[k].values))) return st;
+      d[k].capacity = need[k];
+    } else {                                  // LIST of fixed-width elements
+      const int64_t m = need[k];
+      const int64_t eb = p.elem_type == FURY_TYPE_BOOL ? (m + 7) / 8 : m * type_width_of(p.elem_type);
+      fury_column& e = dchild[k];
+      e = fury_column{};
+      const fury_column* he = host[k].child;
+      if (!he || he->capacity < eb)
+        return set_error(FURY_ERR_CAPACITY, "column " + s->fields[k].name + " needs " +
+                                                std::to_string(eb) + " element bytes");
+      if ((st = arena.alloc(eb + 8, &e.values))) return st;
+      e.capacity = eb;
+      if (he->validity) {
+        void* v = nullptr;
+        if ((st = arena.alloc(bitmap_alloc(m), &v))) return st;
+        (void)hipMemsetAsync(v, 0, bitmap_alloc(m), hs);
+        e.validity = static_cast<uint8_t*>(v);
+      }
+      d[k].child = &e;
+    }
+  }
+  if ((st = fury_row_decode(s, drows, static_cast<int64_t*>(doffs), n, d.data(), hs))) return st;
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    if (host[k].validity)
+      (void)hipMemcpyAsync(host[k].validity, d[k].validity, (n + 7) / 8, hipMemcpyDeviceToHost, hs);
+    if (d[k].offsets) {
+      (void)hipMemcpyAsync(host[k].offsets, d[k].offsets, (n + 1) * 4, hipMemcpyDeviceToHost, hs);
+      if (p.kind == kBytes) {
+        (void)hipMemcpyAsync(host[k].values, d[k].values, need[k], hipMemcpyDeviceToHost, hs);
+      } else {
+        const int64_t m = need[k];
+        const int64_t eb =
+            p.elem_type == FURY_TYPE_BOOL ? (m + 7) / 8 : m * type_width_of(p.elem_type);
+        (void)hipMemcpyAsync(host[k].child->values, dchild[k].values, eb, hipMemcpyDeviceToHost, hs);
+        if (host[k].child->validity)
+          (void)hipMemcpyAsync(host[k].child->validity, dchild[k].validity, (m + 7) / 8,
+                               hipMemcpyDeviceToHost, hs);
+      }
+    } else {
+      const int64_t bytes = p.kind == kDecimal ? n * 16 : p.kind == kBool ? (n + 7) / 8 : n * p.width;
+      (void)hipMemcpyAsync(host[k].values, d[k].values, bytes, hipMemcpyDeviceToHost, hs);
+    }
+  }
+  return ss.sync();
+}
+
+}  // namespace
+}  // namespace fury
+
+using namespace fury;
+
+extern "C" {
+
+int fury_host_register(void* p, int64_t bytes) {
+  if (!p || bytes <= 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_host_register: empty range");
+  return check_hip(hipHostRegister(p, static_cast<size_t>(bytes), hipHostRegisterDefault),
+                   "hipHostRegister");
+}
+
+int fury_host_unregister(void* p) {
+  if (!p) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_host_unregister: null");
+  return check_hip(hipHostUnregister(p), "hipHostUnregister");
+}
+
+int fury_row_encode_host(const fury_schema* s, const fury_column* columns, int64_t nrows,
+                         void* rows, int64_t rows_capacity, int64_t* row_offsets,
+                         int64_t* row_bytes, int32_t device) {
+  if (!s || !row_bytes) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema/row_bytes is null");
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (nrows > 0 && s->num_fields > 0 && !columns)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "columns is null");
+  if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
+  if (s->is_fixed) {
+    *row_bytes = nrows * s->fixed_size;
+    if (*row_bytes > rows_capacity)
+      return set_error(FURY_ERR_CAPACITY, "rows need " + std::to_string(*row_bytes) + " bytes");
+    if (nrows > 0 && !rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
+    if (row_offsets)
+      for (int64_t i = 0; i <= nrows; i++) row_offsets[i] = i * s->fixed_size;
+    return fixed_host(s, columns, nrows, static_cast<uint8_t*>(rows), false, device);
+  }
+  if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
+  if (nrows == 0) {
+    row_offsets[0] = 0;
+    *row_bytes = 0;
+    return FURY_OK;
+  }
+  return var_encode_host(s, columns, nrows, static_cast<uint8_t*>(rows), rows_capacity, row_offsets,
+                         row_bytes, device);
+}
+
+int fury_row_decode_host(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                         int64_t nrows, fury_column* columns, int32_t device) {
+  if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (nrows == 0) return FURY_OK;
+  if (!rows || (s->num_fields > 0 && !columns))
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/columns is null");
+  if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
+  if (s->is_fixed)
+    return fixed_host(s, columns, nrows, static_cast<uint8_t*>(const_cast<void*>(rows)), true,
+                      device);
+  if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
+  return var_decode_host(s, static_cast<const uint8_t*>(rows), row_offsets, nrows, columns, device);
+}
+
+}  // extern "C"

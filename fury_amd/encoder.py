@@ -156,6 +156,48 @@ def _c_columns(cols: Sequence[Column], keep: list):
     return arr
 
 
+def _hptr(a) -> Optional[int]:
+    """Address of a HOST buffer: a contiguous numpy array or CPU tensor (e.g. pinned)."""
+    if a is None:
+        return None
+    if isinstance(a, torch.Tensor):
+        if a.device.type != "cpu" or not a.is_contiguous():
+            raise IllegalArgumentException("host buffers must be contiguous CPU tensors")
+        return a.data_ptr()
+    a = np.asarray(a)
+    if not a.flags["C_CONTIGUOUS"]:
+        raise IllegalArgumentException("host buffers must be contiguous")
+    return a.ctypes.data
+
+
+def _nbytes(a) -> int:
+    if a is None:
+        return 0
+    if isinstance(a, torch.Tensor):
+        return a.numel() * a.element_size()
+    return np.asarray(a).nbytes
+
+
+def _c_host_columns(cols: Sequence[Column], keep: list):
+    arr = (N.FuryColumn * max(len(cols), 1))()
+    for i, c in enumerate(cols):
+        for a in (c.values, c.validity, c.offsets):
+            if a is not None:
+                keep.append(a)
+        arr[i].values = _hptr(c.values)
+        arr[i].validity = _hptr(c.validity)
+        arr[i].offsets = _hptr(c.offsets)
+        arr[i].capacity = _nbytes(c.values)
+        arr[i].child = _c_host_columns(c.child, keep) if c.child else None
+    keep.append(arr)
+    return arr
+
+
+def _tree_bytes(cols: Sequence[Column]) -> int:
+    return sum(_nbytes(c.values) + _nbytes(c.validity) + _nbytes(c.offsets) +
+               (_tree_bytes(c.child) if c.child else 0) for c in cols)
+
+
 def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
     s = stream if stream is not None else torch.cuda.current_stream()
     return s.cuda_stream
@@ -396,6 +438,66 @@ class RowEncoder:
                 f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
                 f"hash are {self.schema_hash}/{batch.schema_hash}. Please check writer schema.")
         return self._decode(batch, validity, False, stream, out)
+
+    # -- host-memory batch path: the JNI boundary (off-heap buffers in, off-heap buffers out) --
+    def encode_host(self, columns: Sequence[Column], nrows: int, rows=None, row_offsets=None,
+                    device_index: int = 0):
+        """Host columns (numpy arrays or CPU/pinned tensors, fury_row.h layout) -> host rows,
+        through HBM inside the call (``fury_row_encode_host``).  Returns (rows, row_offsets);
+        row_offsets is None for fixed-width schemas unless a buffer was passed."""
+        keep: list = []
+        cc = _c_host_columns(columns, keep)
+        fixed = self._schema.is_fixed
+        if rows is None:
+            bound = nrows * self._schema.fixed_size
+            if not fixed:
+                bound += 2 * _tree_bytes(columns) + 64 * nrows * (len(self._schema.fields) + 1)
+            rows = np.empty(max(bound, 16), dtype=np.uint8)
+        if row_offsets is None and not fixed:
+            row_offsets = np.empty(nrows + 1, dtype=np.int64)
+        nb = ctypes.c_int64(0)
+        st = N.lib().fury_row_encode_host(self._schema.handle, cc, nrows, _hptr(rows),
+                                          _nbytes(rows), _hptr(row_offsets), ctypes.byref(nb),
+                                          device_index)
+        if st == 7:                               # FURY_ERR_CAPACITY: retry at the exact size
+            rows = np.empty(max(nb.value, 16), dtype=np.uint8)
+            st = N.lib().fury_row_encode_host(self._schema.handle, cc, nrows, _hptr(rows),
+                                              _nbytes(rows), _hptr(row_offsets),
+                                              ctypes.byref(nb), device_index)
+        _check(st)
+        return rows[:nb.value], row_offsets
+
+    def decode_host(self, rows, row_offsets, nrows: int, out: Optional[List[Column]] = None,
+                    device_index: int = 0) -> List[Column]:
+        """Host rows -> host columns through HBM (``fury_row_decode_host``).  Without ``out``,
+        numpy columns are allocated: validity for nullable fields, and payload / element
+        buffers bounded by the row bytes (a row holds every byte it decodes to)."""
+        from .workloads import Column as C
+        if out is None:
+            out = []
+            rb = max(_nbytes(rows), 16)
+            for f in self._schema.fields:
+                vb = np.zeros((nrows + 7) // 8 + 8, dtype=np.uint8) if f.nullable else None
+                if f.type_id in (STRING, BINARY):
+                    out.append(C(values=np.empty(rb, dtype=np.uint8), validity=vb,
+                                 offsets=np.empty(nrows + 1, dtype=np.int32)))
+                elif f.type_id == LIST:
+                    e = f.children[0]
+                    ev = np.zeros(rb // 8 + 8, dtype=np.uint8) if e.nullable else None
+                    out.append(C(validity=vb, offsets=np.empty(nrows + 1, dtype=np.int32),
+                                 child=[C(values=np.empty(rb, dtype=np.uint8), validity=ev)]))
+                elif f.type_id == BOOL:
+                    out.append(C(values=np.empty((nrows + 7) // 8 + 8, dtype=np.uint8),
+                                 validity=vb))
+                elif f.type_id == DECIMAL:
+                    out.append(C(values=np.empty(nrows * 16, dtype=np.uint8), validity=vb))
+                else:
+                    out.append(C(values=np.empty(max(nrows * type_width(f.type_id), 8),
+                                                 dtype=np.uint8), validity=vb))
+        keep: list = []
+        _check(N.lib().fury_row_decode_host(self._schema.handle, _hptr(rows), _hptr(row_offsets),
+                                            nrows, _c_host_columns(out, keep), device_index))
+        return out
 
     # -- framing (Encoders.java:165-182, 201-213) ------------------------------------------
     def frame(self, batch: RowBatch, stream=None):

@@ -236,6 +236,29 @@ int fury_frame_rows(const fury_schema* schema, const void* rows, const int64_t* 
 int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64_t stream_len,
                       int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream);
 
+/* ---- host-memory batch path (the JNI boundary: DirectByteBuffer addresses) ---------------- */
+/* The functions below take HOST pointers (a JVM's off-heap buffers) and run the device path
+ * inside the call (synchronous): Encoders.bean(...).encode over a batch
+ * (FMT/encoder/Encoders.java:185-213) and decode (:165-182), with the bytes crossing PCIe.
+ * Fixed-width schemas are streamed in chunks over three HIP streams (H2D, kernels and D2H of
+ * consecutive chunks overlap); variable-length schemas are staged whole.  `device` is the HIP
+ * device ordinal.  Pin long-lived buffers once with fury_host_register (hipHostRegister). */
+int fury_host_register(void* ptr, int64_t bytes);
+int fury_host_unregister(void* ptr);
+/* Host columns (fury_column layout, host pointers) -> host rows.  Fixed-width: rows are
+ * nrows * fixed_size bytes, row_offsets optional (filled with i * fixed_size when given).
+ * Variable-length: row_offsets (host, nrows + 1) is required and filled.  *row_bytes = bytes
+ * the rows need; FURY_ERR_CAPACITY (nothing written) when that exceeds rows_capacity. */
+int fury_row_encode_host(const fury_schema* schema, const fury_column* columns, int64_t nrows,
+                         void* rows, int64_t rows_capacity, int64_t* row_offsets,
+                         int64_t* row_bytes, int32_t device);
+/* Host rows -> host columns (fromRow semantics, like fury_row_decode).  Variable-length flat
+ * schemas: STRING/BINARY payload capacity in fury_column.capacity, LIST element bytes in the
+ * child's capacity (FURY_ERR_CAPACITY when short); nested schemas: FURY_ERR_UNSUPPORTED (use
+ * the device API). */
+int fury_row_decode_host(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                         int64_t nrows, fury_column* columns, int32_t device);
+
 /* ---- Arrow IPC (ArrowUtils.serializeRecordBatch, FMT/vectorized/ArrowUtils.java:63-72;
  *      ArrowSerializers stream writers, FMT/vectorized/ArrowSerializers.java:128-167) --------- */
 /* Encapsulated IPC Schema message of the schema, in HOST memory:
