@@ -600,7 +600,9 @@ int launch_fast_tile(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool
 
 template <bool kEnc>
 int launch_fast_tile_variant(const FixedArgs& a, uint8_t* rows, hipStream_t stream, int var) {
-  const int R = pick_rows_per_tile(a.row_size);
+  int R = pick_rows_per_tile(a.row_size);
+  // bit 8: tall tiles (twice the rows: longer contiguous column runs, fewer workgroups per CU)
+  if ((var & 256) && R < 256 && static_cast<int64_t>(2 * R) * a.row_size <= 160 * 1024) R *= 2;
   const bool deep = (var & (kEnc ? 8 : 32)) != 0;
   const bool pad = kEnc && (var & 128) != 0;
   // pad only where it fits the LDS budget of the unpadded tile's occupancy class
@@ -624,7 +626,7 @@ int launch_fast_tile_variant(const FixedArgs& a, uint8_t* rows, hipStream_t stre
 // Variant bits (fury_set_tuning("fixed_variant")): bit 0 = pipelined persistent kernel,
 // bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode gather, bit 4 =
 // pair-mode decode, bit 5 = deep decode loads, bit 6 = pair-mode encode, bit 7 = padded LDS rows
-// in the encode (bits 3-7 with nt loads + stores only).  Only the fast path (8-byte columns,
+// in the encode, bit 8 = tall tiles (bits 3-8 with nt loads + stores only).  Only the fast path (8-byte columns,
 // no validity) has variants; the general path always runs the tile kernel.
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
@@ -638,7 +640,7 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
       default: return launch_pipe(encode_fixed_pipe<32, 0>, a.row_size, a.nrows, stream, a, rows);
     }
   }
-  if (fast && (var & 248) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
+  if (fast && (var & 504) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                          \
   if (R == RR) {                                                                              \
@@ -685,7 +687,7 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
       default: return launch_pipe(decode_fixed_pipe<17, 0>, a.row_size, a.nrows, stream, a, r);
     }
   }
-  if (fast && (var & 248) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
+  if (fast && (var & 504) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_DEC(RR)                                                                          \
   if (R == RR) {                                                                              \

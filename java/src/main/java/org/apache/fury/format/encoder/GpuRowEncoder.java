@@ -1,0 +1,180 @@
+/*
+ * GpuRowEncoder — the Java drop-in for the MI355X row codec (libfury_row.so through
+ * libfury_row_jni.so).  NOT COMPILED IN THIS REPOSITORY: the build image has no JDK and no
+ * Maven (DESIGN.md §1); it is the binding a maintainer adds next to
+ * java/fury-format/src/main/java/org/apache/fury/format/encoder/Encoders.java.
+ *
+ * Per-object API: identical to RowEncoder<T> (RowEncoder.java:26-32, Encoder.java:31-40) — it
+ * delegates to Encoders.bean(cls), so existing callers (RowSuite.java:100-126, FMTT/*) keep their
+ * exact bytes and exceptions.
+ * Batch API: Arrow columns (a VectorSchemaRoot, as ArrowWriter produces them, ArrowWriter.java:
+ * 55-99) <-> packed rows in off-heap MemoryBuffers, through fury_row_encode_host /
+ * fury_row_decode_host (include/fury_row.h): the buffers' addresses cross JNI, the bytes cross
+ * PCIe inside the native call, the rows are bit-identical to toRow(obj) for every object.
+ */
+package org.apache.fury.format.encoder;
+
+import java.util.ArrayList;
+import java.util.List;
+import org.apache.arrow.memory.ArrowBuf;
+import org.apache.arrow.vector.BaseVariableWidthVector;
+import org.apache.arrow.vector.BitVector;
+import org.apache.arrow.vector.FieldVector;
+import org.apache.arrow.vector.VectorSchemaRoot;
+import org.apache.arrow.vector.complex.ListVector;
+import org.apache.arrow.vector.complex.MapVector;
+import org.apache.arrow.vector.complex.StructVector;
+import org.apache.arrow.vector.types.pojo.Field;
+import org.apache.arrow.vector.types.pojo.Schema;
+import org.apache.fury.format.row.binary.BinaryRow;
+import org.apache.fury.format.type.DataTypes;
+import org.apache.fury.memory.MemoryBuffer;
+
+public final class GpuRowEncoder<T> implements RowEncoder<T> {
+  static {
+    System.loadLibrary("fury_row_jni");
+  }
+
+  private final RowEncoder<T> cpu;
+  private final long schemaHandle;      // fury_schema*, freed by close()
+  private final int device;
+
+  public GpuRowEncoder(Class<T> beanClass, int device) {
+    this.cpu = Encoders.bean(beanClass);
+    this.device = device;
+    List<String> names = new ArrayList<>();
+    List<Integer> meta = new ArrayList<>();       // per node: typeId, nullable, numChildren
+    for (Field f : cpu.schema().getFields()) {
+      flattenField(f, names, meta);
+    }
+    int[] m = new int[meta.size()];
+    for (int i = 0; i < m.length; i++) {
+      m[i] = meta.get(i);
+    }
+    this.schemaHandle =
+        nativeSchemaCreate(names.toArray(new String[0]), m, cpu.schema().getFields().size());
+  }
+
+  // ---- RowEncoder<T>: the reference implementation, unchanged ----------------------------
+  @Override public Schema schema() { return cpu.schema(); }
+  @Override public BinaryRow toRow(T obj) { return cpu.toRow(obj); }
+  @Override public T fromRow(BinaryRow row) { return cpu.fromRow(row); }
+  @Override public byte[] encode(T obj) { return cpu.encode(obj); }
+  @Override public void encode(MemoryBuffer buffer, T obj) { cpu.encode(buffer, obj); }
+  @Override public T decode(byte[] bytes) { return cpu.decode(bytes); }
+  @Override public T decode(MemoryBuffer buffer) { return cpu.decode(buffer); }
+
+  // ---- batch path --------------------------------------------------------------------------
+  /**
+   * Encodes root.getRowCount() rows into the off-heap buffer `rows` (row i at
+   * rowOffsets[i], int64 little-endian, nrows + 1 entries; for all-fixed-width schemas row i is at
+   * i * fixedSize and rowOffsets may be null).  Returns the row bytes written.  Throws
+   * IndexOutOfBoundsException-family errors exactly where fury_status says.
+   */
+  public long encodeBatch(VectorSchemaRoot root, MemoryBuffer rows, MemoryBuffer rowOffsets) {
+    checkOffHeap(rows);
+    long[] desc = describe(root, false);
+    return nativeEncodeHost(schemaHandle, desc, root.getRowCount(), rows.getUnsafeAddress(),
+        rows.size(), rowOffsets == null ? 0 : addressOf(rowOffsets), device);
+  }
+
+  /** Decodes nrows rows into `out` (vectors allocated by the caller for nrows values and, for
+   * strings / lists, enough payload capacity); sets the value counts. */
+  public void decodeBatch(MemoryBuffer rows, MemoryBuffer rowOffsets, int nrows,
+                          VectorSchemaRoot out) {
+    checkOffHeap(rows);
+    long[] desc = describe(out, true);
+    nativeDecodeHost(schemaHandle, rows.getUnsafeAddress(),
+        rowOffsets == null ? 0 : addressOf(rowOffsets), nrows, desc, device);
+    out.setRowCount(nrows);
+    for (FieldVector v : out.getFieldVectors()) {
+      if (v instanceof BaseVariableWidthVector) {
+        ((BaseVariableWidthVector) v).setLastSet(nrows - 1);
+      }
+    }
+  }
+
+  public void close() {
+    nativeSchemaDestroy(schemaHandle);
+  }
+
+  // ---- column descriptors: 5 longs per node in pre-order ----------------------------------
+  // {values address, validity address, offsets address, values capacity, number of children};
+  // a MAP's children are its keys and values vectors (the "entries" struct is skipped, as in
+  // fury_row.h's fury_column).
+  private static long[] describe(VectorSchemaRoot root, boolean decode) {
+    List<Long> d = new ArrayList<>();
+    for (FieldVector v : root.getFieldVectors()) {
+      describe(v, decode, d);
+    }
+    long[] out = new long[d.size()];
+    for (int i = 0; i < out.length; i++) {
+      out[i] = d.get(i);
+    }
+    return out;
+  }
+
+  private static void describe(FieldVector v, boolean decode, List<Long> d) {
+    boolean nullable = v.getField().isNullable();
+    ArrowBuf validity = v.getValidityBuffer();
+    List<FieldVector> kids = new ArrayList<>();
+    long values = 0, offsets = 0, capacity = 0;
+    if (v instanceof MapVector) {
+      StructVector entries = (StructVector) ((MapVector) v).getDataVector();
+      kids.add((FieldVector) entries.getChildByOrdinal(0));
+      kids.add((FieldVector) entries.getChildByOrdinal(1));
+      offsets = v.getOffsetBuffer().memoryAddress();
+    } else if (v instanceof ListVector) {
+      kids.add(((ListVector) v).getDataVector());
+      offsets = v.getOffsetBuffer().memoryAddress();
+    } else if (v instanceof StructVector) {
+      kids.addAll(((StructVector) v).getChildrenFromFields());
+    } else {
+      values = v.getDataBuffer().memoryAddress();
+      capacity = v.getDataBuffer().capacity();
+      if (v instanceof BaseVariableWidthVector) {
+        offsets = v.getOffsetBuffer().memoryAddress();
+      }
+    }
+    d.add(values);
+    d.add(nullable && (decode || v.getNullCount() > 0) ? validity.memoryAddress() : 0L);
+    d.add(offsets);
+    d.add(capacity);
+    d.add((long) kids.size());
+    for (FieldVector k : kids) {
+      describe(k, decode, d);
+    }
+  }
+
+  private static void flattenField(Field f, List<String> names, List<Integer> meta) {
+    List<Field> kids = f.getChildren();
+    if (f.getType() instanceof org.apache.arrow.vector.types.pojo.ArrowType.Map) {
+      kids = kids.get(0).getChildren();          // entries struct -> (key, value)
+    }
+    names.add(f.getName());
+    meta.add((int) DataTypes.getTypeIdValue(f.getType()));
+    meta.add(f.isNullable() ? 1 : 0);
+    meta.add(kids.size());
+    for (Field k : kids) {
+      flattenField(k, names, meta);
+    }
+  }
+
+  private static long addressOf(MemoryBuffer b) {
+    checkOffHeap(b);
+    return b.getUnsafeAddress();
+  }
+
+  private static void checkOffHeap(MemoryBuffer b) {
+    if (!b.isOffHeap()) {
+      throw new IllegalArgumentException("batch buffers must be off-heap (DirectByteBuffer)");
+    }
+  }
+
+  private static native long nativeSchemaCreate(String[] names, int[] meta, int numTopFields);
+  private static native void nativeSchemaDestroy(long schema);
+  private static native long nativeEncodeHost(long schema, long[] columns, long nrows, long rows,
+                                              long rowsCapacity, long rowOffsets, int device);
+  private static native void nativeDecodeHost(long schema, long rows, long rowOffsets, long nrows,
+                                              long[] columns, int device);
+}

@@ -60,7 +60,7 @@ def main():
     for kind, fneed, wneed, fcal, wcal in (("encode", "encode_fixed", "encode_fixed", "fetch8",
                                             "write16"),
                                            ("decode", "decode_fixed", "decode_fixed", "fetch16",
-                                            "write8")):
+                                            "write16")):    # pair-mode decode: 16-B stores
         fv, fk = pick(bf, fneed)
         wv, wk = pick(bw, wneed)
         if fv is None or wv is None:
