@@ -626,7 +626,10 @@ int launch_fast_tile_variant(const FixedArgs& a, uint8_t* rows, hipStream_t stre
 // Variant bits (fury_set_tuning("fixed_variant")): bit 0 = pipelined persistent kernel,
 // bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode gather, bit 4 =
 // pair-mode decode, bit 5 = deep decode loads, bit 6 = pair-mode encode, bit 7 = padded LDS rows
-// in the encode, bit 8 = tall tiles (bits 3-8 with nt loads + stores only).  Only the fast path (8-byte columns,
+// in the encode, bit 8 = tall tiles (bits 3-8 with nt loads + stores only).  A column-strip
+// encode (a workgroup per 256 rows x 20 columns: 2 KB contiguous column reads, 160-B strided row
+// strips written) measured 2.77 vs 5.80 TB/s in one process and was removed: partial-row
+// writes cost far more than the longer reads gain.  Only the fast path (8-byte columns,
 // no validity) has variants; the general path always runs the tile kernel.
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
