@@ -187,7 +187,7 @@ def main():
                 assert torch.equal(c.offsets, d.offsets), "decode offsets mismatch"
 
     e2e = None
-    if rank == 0 and not args.no_e2e and args.workload == "struct100":
+    if world == 1 and not args.no_e2e and args.workload == "struct100":
         e2e = end_to_end(enc, cols, n, dev, stream)
 
     if rank != 0:
@@ -229,7 +229,7 @@ def main():
     }
     if e2e is not None:
         line["e2e_pcie"] = e2e
-    if not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:     # the CPU baseline is an N=1 figure
         line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds)
     print(json.dumps(line), flush=True)
     orch.close()
