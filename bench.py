@@ -30,7 +30,7 @@ DEFAULT_ROWS = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000
 def _parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rows", type=int, default=None,
                    help="rows per GPU (default: BASELINE config size: struct100 1M, mixed 10M, "
@@ -112,6 +112,9 @@ def main():
     world, rank, local = r.world, r.rank, r.local
     # orchestration only (gloo barrier + max of timings); the data path has no collective
     orch = Orchestrator(r)
+    # one process per GPU; with fewer GPUs than ranks (a rehearsal on a 1-GPU box) ranks share
+    ndev = torch.cuda.device_count()
+    local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -168,8 +171,8 @@ def main():
     for k in range(args.steps):
         step(events[k])
     torch.cuda.synchronize()
+    dt = time.perf_counter() - t0       # this rank's K steps; the max over ranks is taken below
     orch.barrier()
-    dt = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
 
