@@ -1212,6 +1212,7 @@ __device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq
 // Stores image bytes img[0, n) to g[0, n) (g any alignment, img 16-aligned LDS with >= 16 bytes
 // of readable padding past n): byte stores up to g's 16-byte boundary, then 16-B non-temporal
 // stores whose data is funnel-shifted out of aligned image words, then the byte tail.
+template <int NT = kThreads>
 __device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, int64_t n) {
   using v4 = __attribute__((ext_vector_type(4))) uint32_t;
   if (n <= 0) return;
@@ -1222,7 +1223,7 @@ __device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, in
   if (threadIdx.x < n - t0) g[t0 + threadIdx.x] = img[t0 + threadIdx.x];
   const uint64_t* i64 = reinterpret_cast<const uint64_t*>(img);
   const int sh = static_cast<int>(head & 7) * 8;
-  for (int64_t m = threadIdx.x; m < body; m += kThreads) {
+  for (int64_t m = threadIdx.x; m < body; m += NT) {
     const int64_t off = head + 16 * m;
     const int64_t q = off >> 3;
     uint64_t x, y;
@@ -1244,13 +1245,14 @@ __device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, in
 // Stores a bit image (image bit i = global bit gbit0 + i, >= 1 word of padding) to the global
 // bitmap bits [gbit0, gbit0 + n): whole words plainly, the words shared with neighbouring tiles
 // with atomic and/or of exactly these bits.
+template <int NT = kThreads>
 __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t* img, int64_t gbit0,
                                                    int64_t n) {
   if (n <= 0) return;
   const int64_t end = gbit0 + n;
   const int64_t w0 = gbit0 >> 5, w1 = (end + 31) >> 5;
   uint32_t* g = reinterpret_cast<uint32_t*>(bits);
-  for (int64_t w = w0 + threadIdx.x; w < w1; w += kThreads) {
+  for (int64_t w = w0 + threadIdx.x; w < w1; w += NT) {
     const int64_t i0 = 32 * w - gbit0;
     uint32_t x;
     if (i0 < 0) {
@@ -1272,17 +1274,17 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
   }
 }
 
-template <int K>
-__global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
+template <int K, int NT = kThreads>
+__global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                            const int64_t* __restrict__ offs,
                                                            uint64_t* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) uint64_t oimg[kDecImg / 8];
-  __shared__ int64_t tmp[kThreads / 64];
+  __shared__ __attribute__((aligned(16))) uint64_t oimg[kDecImg / 8 * (NT / kThreads)];
+  __shared__ int64_t tmp[NT / 64];
   __shared__ int64_t sbase[K];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t b = blockIdx.x, nb = gridDim.x;
-  const int64_t r0 = b * kThreads;
-  const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
+  const int64_t r0 = b * NT;
+  const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
   const int64_t r = live ? r0 + tid : r0;
   const uint8_t* row = rows + offs[r];
@@ -1314,7 +1316,7 @@ __global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint
     if (!s0 && !s1) continue;
     const uint64_t pk = cnt[k] | (k + 1 < K ? static_cast<uint64_t>(cnt[k + 1]) << 32 : 0);
     int64_t t64;
-    const uint64_t e64 = static_cast<uint64_t>(block_excl_scan(static_cast<int64_t>(pk), &t64, tmp));
+    const uint64_t e64 = static_cast<uint64_t>(block_excl_scan<NT>(static_cast<int64_t>(pk), &t64, tmp));
     ex[k] = static_cast<uint32_t>(e64);
     tot[k] = static_cast<uint32_t>(t64);
     if (k + 1 < K) {
@@ -1343,12 +1345,12 @@ __global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint
     else if (c.width == 0) need = r16((((tot[k] + 31) >> 5) + 1) * 4);
     else need = r16(int64_t(tot[k]) * c.width + 16);
     if (c.kind == kListFixed && c.elem_validity) need += r16((((tot[k] + 31) >> 5) + 1) * 4);
-    if (used + need <= kDecImg) {
+    if (used + need <= kDecImg * (NT / kThreads)) {
       img_at[k] = used;
       used += static_cast<uint32_t>(need);
     }
   }
-  for (uint32_t i = 16 * tid; i < used; i += 16 * kThreads)
+  for (uint32_t i = 16 * tid; i < used; i += 16 * NT)
     *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
   __syncthreads();
 #pragma unroll
@@ -1468,7 +1470,7 @@ __global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint
 #pragma unroll
     for (int k = 0; k < K; k++) {
       if (!is_seq(a.col[k])) continue;
-      if ((q++ & 3) != wave) continue;
+      if ((q++ % (NT / 64)) != wave) continue;
       const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k);
       if (lane == 0) {
         sbase[k] = pre;
@@ -1538,19 +1540,19 @@ __global__ __launch_bounds__(kThreads) void decode_var_reg(VarArgs a, const uint
     const uint8_t* im = reinterpret_cast<const uint8_t*>(oimg) + img_at[k];
     const int64_t n = max<int64_t>(0, min<int64_t>(tot[k], c.capacity - gb));
     if (c.kind == kBytes) {
-      store_shifted(dst + gb, im, n);
+      store_shifted<NT>(dst + gb, im, n);
       continue;
     }
     int64_t vb;
     if (c.width == 0) {
       vb = r16((((tot[k] + 31) >> 5) + 1) * 4);
-      store_bits_shifted(dst, reinterpret_cast<const uint32_t*>(im), gb, n);
+      store_bits_shifted<NT>(dst, reinterpret_cast<const uint32_t*>(im), gb, n);
     } else {
       vb = r16(int64_t(tot[k]) * c.width + 16);
-      store_shifted(dst + gb * c.width, im, n * c.width);
+      store_shifted<NT>(dst + gb * c.width, im, n * c.width);
     }
     if (c.elem_validity)
-      store_bits_shifted(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
+      store_bits_shifted<NT>(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
   }
 }
 
@@ -1828,7 +1830,8 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
-int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back, 1 sizing pass + decode
+int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back (tile rows by sequence
+                          // count), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256 rows
 
 }  // namespace
 
@@ -2039,14 +2042,27 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     return check_hip(hipGetLastError(), "decode_var launch");
   }
   if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
-    const size_t wsb = static_cast<size_t>(nb) * a.ncols * 8;
+    // 512-row tiles halve the look-back chain links: faster with several string / list
+    // sequences to chain (mixed, 3: 0.656 vs 0.737 ms), slower with one (nested: 0.287 vs
+    // 0.274 ms) — scripts/ab_var.py.  Mode 0 picks by sequence count, 2 / 3 force 512 / 256.
+    const bool wide = g_var_decode == 2 || (g_var_decode == 0 && nseq >= 2);
+    const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
+    const size_t wsb = static_cast<size_t>(nbr) * a.ncols * 8;
     uint64_t* ws = nullptr;
     int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     if (!st) {
       switch (a.ncols) {
-#define FURY_DREG(KK) case KK: hipLaunchKernelGGL(decode_var_reg<KK>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs, ws); break;
+#define FURY_DREG(KK)                                                                          \
+  case KK:                                                                                     \
+    if (wide)                                                                                  \
+      hipLaunchKernelGGL((decode_var_reg<KK, 512>), dim3(nbr), dim3(512), 0, stream, a, rows,  \
+                         offs, ws);                                                            \
+    else                                                                                       \
+      hipLaunchKernelGGL(decode_var_reg<KK>, dim3(nb), dim3(kThreads), 0, stream, a, rows,     \
+                         offs, ws);                                                            \
+    break;
         FURY_DREG(1) FURY_DREG(2) FURY_DREG(3) FURY_DREG(4) FURY_DREG(5) FURY_DREG(6) FURY_DREG(7)
         FURY_DREG(8) FURY_DREG(9) FURY_DREG(10) FURY_DREG(11) FURY_DREG(12) FURY_DREG(13)
         FURY_DREG(14) FURY_DREG(15) FURY_DREG(16)

@@ -218,7 +218,8 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
  * bit 5 = deep decode (16 tile loads per lane in flight), bit 6 = pair-mode encode, bit 7 =
  * padded LDS rows in the encode.  Results are bit-identical across variants.  Default 54
  * (tile + nt loads/stores + pair-mode deep decode).
- * Key "var_decode": 0 one-pass look-back decode, 1 sizing pass + decode.
+ * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
+ * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles.
  * Key "unframe": 0 speculative parallel stream parse (sequential walk when it does not verify),
  * 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk parsed. */
 int fury_set_tuning(const char* key, int32_t value);

@@ -1,0 +1,74 @@
+"""Timing of the nested-schema engine (generic.hip: STRUCT / MAP / LIST of var elements), on the
+tests' 7-field nested schema (struct with list + string, list<list<int>>, map<string,int>,
+list<struct>, list<string>, bool).  Columns come from beans (host, slow), repeated to --rows.
+
+    python scripts/ab_generic.py [--rows 400000]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _bytes(cols):
+    t = 0
+    for c in cols:
+        for a in (c.values, c.validity, c.offsets):
+            if a is not None:
+                t += a.numel() * a.element_size()
+        if c.child:
+            t += _bytes(c.child)
+    return t
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=400_000)
+    ap.add_argument("--iters", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    from tests.test_device import _nested_beans, _nested_fields
+    fields = _nested_fields()
+    base = _nested_beans(50_000, seed=1)
+    beans = (base * (args.rows // len(base) + 1))[:args.rows]
+    n = len(beans)
+    dev = torch.device("cuda:0")
+    cols = [column_to_device(c, dev) for c in beans_to_columns(fields, beans)]
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(cols, n)
+    out = enc.decode_batch(batch)
+    torch.cuda.synchronize()
+
+    def t(f):
+        f()
+        torch.cuda.synchronize()
+        xs = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(args.iters):
+                f()
+            b.record()
+            torch.cuda.synchronize()
+            xs.append(a.elapsed_time(b) / args.iters)
+        return statistics.median(xs)
+    enc_ms = t(lambda: enc.encode_batch(cols, n))
+    dec_ms = t(lambda: enc.decode_batch(batch))
+    cb = _bytes(cols)
+    rb = batch.rows.numel() + 8 * (n + 1)
+    print(json.dumps({"schema": "tests _nested_fields (7 fields, depth 3)", "rows": n,
+                      "column_bytes": cb, "row_bytes": rb,
+                      "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+                      "encode_GBps": round((cb + rb) / enc_ms / 1e6, 1),
+                      "decode_GBps": round((cb + rb) / dec_ms / 1e6, 1),
+                      "note": "wall per call incl. host syncs (measure + size reads)"}))
+
+
+if __name__ == "__main__":
+    main()

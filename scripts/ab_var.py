@@ -51,10 +51,12 @@ def main():
         "encode_tile": lambda: (os.environ.__setitem__("FURY_VAR_DBG", "1024"),
                                 enc.encode_into(cols, n, rows, offs),
                                 os.environ.__setitem__("FURY_VAR_DBG", "0")),
-        "decode_1pass": lambda: (L.fury_set_tuning(b"var_decode", 0),
+        "decode_1pass": lambda: (L.fury_set_tuning(b"var_decode", 3),
                                  enc.decode_into(batch, out)),
         "decode_2pass": lambda: (L.fury_set_tuning(b"var_decode", 1),
                                  enc.decode_into(batch, out)),
+        "decode_512": lambda: (L.fury_set_tuning(b"var_decode", 2),
+                               enc.decode_into(batch, out), L.fury_set_tuning(b"var_decode", 3)),
         "decode_measure": lambda: L.fury_row_decode_measure(enc._schema.handle, _ptr(rows),
                                                             _ptr(offs), n, ccols, sh),
     }
@@ -81,7 +83,8 @@ def main():
     med = {k: round(statistics.median(v), 4) for k, v in times.items()}
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
-                    for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass")}}
+                    for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass",
+                              "decode_512")}}
     print(json.dumps(res), flush=True)
 
 

@@ -203,6 +203,21 @@ def test_fixed_variants_bit_exact(oracle, dev, variant):
         N.lib().fury_set_tuning(b"fixed_variant", old)
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_var_decode_modes_bit_exact(oracle, dev, mode):
+    """Every variable-length decode mode (tuning 'var_decode': one-pass look-back with 256- or
+    512-row tiles, sizing pass + decode) decodes to the oracle's columns."""
+    from fury_amd import _native as N
+    old = N.lib().fury_get_tuning(b"var_decode")
+    assert N.lib().fury_set_tuning(b"var_decode", mode) == 0
+    try:
+        for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
+                        ("nested", 4097), ("beanb", 700)):
+            _roundtrip(oracle, name, n, dev, seed=n + mode)
+    finally:
+        N.lib().fury_set_tuning(b"var_decode", old)
+
+
 def _walks():
     from fury_amd import _native as N
     return N.lib().fury_get_tuning(b"unframe_walks")
