@@ -40,46 +40,72 @@ constexpr int kMarkSpan = kThreads * kMarkWords;    // words per workgroup
 constexpr int kCopyFrames = 256;                    // frames per workgroup in the copy pass
 
 // Encoders.encode(MemoryBuffer, T) for each row.  A workgroup owns kCopyFrames consecutive rows
-// = one contiguous range of the row buffer and of the stream: lane q moves the row buffer's 8-B
-// word q (its row found by binary search over the range's row offsets in LDS) to stream
-// position rowOffset + 12 * (row + 1) (4-byte aligned: two dword stores); lane f < rows writes
-// frame f's 12-B header.
+// = one contiguous range of the row buffer and of the stream.  The stream side is written in
+// 16-byte aligned chunks (non-temporal): a lane finds the frame under its chunk by binary search
+// over the range's frame starts in LDS and assembles the chunk's four dwords from the 12-byte
+// header and the row's 4-byte words (a chunk spans at most two frames: a frame is >= 20 bytes);
+// the unaligned head and tail of the range go out as dwords.
 __global__ __launch_bounds__(kThreads) void frame_kernel(const uint8_t* __restrict__ rows,
                                                          const int64_t* __restrict__ offs,
                                                          int64_t n, int64_t fixed,
                                                          int64_t hash, uint8_t* __restrict__ out,
                                                          int64_t* __restrict__ fo) {
-  __shared__ int64_t ro[kCopyFrames + 1];
+  __shared__ int64_t ro[kCopyFrames + 1];   // row offsets of the range's rows (+ the end)
+  __shared__ int64_t st[kCopyFrames + 1];   // their frame starts in the stream (+ the end)
   const int64_t k0 = static_cast<int64_t>(blockIdx.x) * kCopyFrames;
   const int kn = static_cast<int>(min(static_cast<int64_t>(kCopyFrames), n - k0));
-  for (int f = threadIdx.x; f <= kn; f += kThreads) ro[f] = offs ? offs[k0 + f] : (k0 + f) * fixed;
-  __syncthreads();
-  if (threadIdx.x < kn) {
-    const int f = threadIdx.x;
-    const int64_t start = ro[f] + 12 * (k0 + f);
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + start);
-    o[0] = static_cast<uint32_t>(8 + (ro[f + 1] - ro[f]));
-    o[1] = static_cast<uint32_t>(hash);
-    o[2] = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
-    if (fo) {
-      fo[k0 + f] = start;
-      if (k0 + f == n - 1) fo[n] = start + 12 + (ro[f + 1] - ro[f]);
-    }
+  for (int f = threadIdx.x; f <= kn; f += kThreads) {
+    const int64_t r = offs ? offs[k0 + f] : (k0 + f) * fixed;
+    ro[f] = r;
+    st[f] = r + 12 * (k0 + f);
   }
-  const int64_t base = ro[0];
-  const int64_t words = (ro[kn] - base) >> 3;
-  for (int64_t q = threadIdx.x; q < words; q += kThreads) {
-    const int64_t d = base + 8 * q;
+  __syncthreads();
+  if (fo && threadIdx.x < kn) {
+    fo[k0 + threadIdx.x] = st[threadIdx.x];
+    if (k0 + threadIdx.x == n - 1) fo[n] = st[kn];
+  }
+  const uint32_t hlo = static_cast<uint32_t>(hash);
+  const uint32_t hhi = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
+  // stream dword at byte position q of frame f (advanced while q is past its end)
+  auto dword_at = [&](int64_t q, int& f) -> uint32_t {
+    while (f + 1 < kn && st[f + 1] <= q) f++;
+    const int64_t rel = q - st[f];
+    if (rel < 12) {
+      return rel == 0 ? static_cast<uint32_t>(8 + (ro[f + 1] - ro[f])) : rel == 4 ? hlo : hhi;
+    }
+    return *reinterpret_cast<const uint32_t*>(rows + ro[f] + rel - 12);
+  };
+  auto find = [&](int64_t q) {                 // last frame that starts at or before q
     int lo = 0, hi = kn - 1;
-    while (lo < hi) {                 // last row that starts at or before d
+    while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (ro[mid] <= d) lo = mid;
+      if (st[mid] <= q) lo = mid;
       else hi = mid - 1;
     }
-    const uint64_t v = *reinterpret_cast<const uint64_t*>(rows + d);
-    uint32_t* o = reinterpret_cast<uint32_t*>(out + d + 12 * (k0 + lo + 1));
-    o[0] = static_cast<uint32_t>(v);
-    o[1] = static_cast<uint32_t>(v >> 32);
+    return lo;
+  };
+  const int64_t S = st[0], E = st[kn];
+  const uintptr_t ob = reinterpret_cast<uintptr_t>(out);
+  int64_t A = S + static_cast<int64_t>((16 - ((ob + S) & 15)) & 15);   // first 16-B aligned
+  int64_t B = E - static_cast<int64_t>((ob + E) & 15);                   // last 16-B boundary
+  if (A > B) A = B = E;                        // short range: dwords only
+  for (int64_t q = S + 4 * threadIdx.x; q < A; q += 4 * kThreads) {
+    int f = find(q);
+    *reinterpret_cast<uint32_t*>(out + q) = dword_at(q, f);
+  }
+  for (int64_t q = B + 4 * threadIdx.x; q < E; q += 4 * kThreads) {
+    int f = find(q);
+    *reinterpret_cast<uint32_t*>(out + q) = dword_at(q, f);
+  }
+  using v4u = __attribute__((ext_vector_type(4))) uint32_t;
+  for (int64_t q = A + 16 * threadIdx.x; q < B; q += 16 * kThreads) {
+    int f = find(q);
+    v4u v;
+    v.x = dword_at(q, f);
+    v.y = dword_at(q + 4, f);
+    v.z = dword_at(q + 8, f);
+    v.w = dword_at(q + 12, f);
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(out + q));
   }
 }
 
@@ -345,8 +371,8 @@ __global__ __launch_bounds__(kThreads) void unframe_verify(const int64_t* __rest
 }
 
 // Rows out of a verified stream: each workgroup owns kCopyFrames frames = one contiguous range of
-// the row buffer; a lane moves 8 B (its frame found by binary search over the range's row
-// offsets in LDS), so the row-buffer stores are fully coalesced.
+// the row buffer, written in 16-byte aligned chunks (a lane finds its chunk's frame by binary
+// search over the range's row offsets in LDS and reads the 4-byte aligned stream words).
 __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restrict__ in,
                                                          const int64_t* __restrict__ cand,
                                                          const int64_t* __restrict__ row_offs,
@@ -362,19 +388,43 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
     if (f < kn) src[f] = cand[k0 + f] + 12;
   }
   __syncthreads();
-  const int64_t base = ro[0];
-  const int64_t words = (ro[kn] - base) >> 3;
-  for (int64_t q = threadIdx.x; q < words; q += kThreads) {
-    const int64_t d = base + 8 * q;
+  auto find = [&](int64_t d) {        // last frame whose row starts at or before d
     int lo = 0, hi = kn - 1;
-    while (lo < hi) {                 // last frame whose row starts at or before d
+    while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
       if (ro[mid] <= d) lo = mid;
       else hi = mid - 1;
     }
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(in + src[lo] + (d - ro[lo]));
-    const uint64_t v = static_cast<uint64_t>(s[0]) | (static_cast<uint64_t>(s[1]) << 32);
-    *reinterpret_cast<uint64_t*>(out + d) = v;
+    return lo;
+  };
+  // row-buffer dword at d (rows are whole 8-byte words, so a dword never straddles two rows)
+  auto dword_at = [&](int64_t d, int& f) -> uint32_t {
+    while (f + 1 < kn && ro[f + 1] <= d) f++;
+    return *reinterpret_cast<const uint32_t*>(in + src[f] + (d - ro[f]));
+  };
+  // 16-byte aligned chunks of the row buffer (non-temporal stores), dwords at the two ends
+  const int64_t S = ro[0], E = ro[kn];
+  const uintptr_t ob = reinterpret_cast<uintptr_t>(out);
+  int64_t A = S + static_cast<int64_t>((16 - ((ob + S) & 15)) & 15);
+  int64_t B = E - static_cast<int64_t>((ob + E) & 15);
+  if (A > B) A = B = E;
+  for (int64_t d = S + 4 * threadIdx.x; d < A; d += 4 * kThreads) {
+    int f = find(d);
+    *reinterpret_cast<uint32_t*>(out + d) = dword_at(d, f);
+  }
+  for (int64_t d = B + 4 * threadIdx.x; d < E; d += 4 * kThreads) {
+    int f = find(d);
+    *reinterpret_cast<uint32_t*>(out + d) = dword_at(d, f);
+  }
+  using v4u = __attribute__((ext_vector_type(4))) uint32_t;
+  for (int64_t d = A + 16 * threadIdx.x; d < B; d += 16 * kThreads) {
+    int f = find(d);
+    v4u v;
+    v.x = dword_at(d, f);
+    v.y = dword_at(d + 4, f);
+    v.z = dword_at(d + 8, f);
+    v.w = dword_at(d + 12, f);
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(out + d));
   }
 }
 
