@@ -62,6 +62,26 @@ __device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
   return v;
 }
 
+// Copies len bytes from an 8-byte aligned source (a row's var section) to any destination:
+// bytes up to the destination's 8-byte boundary, then whole 8-byte stores of funnel-shifted
+// source words, then the tail bytes.  Only [dst, dst + len) is written (neighbouring threads
+// own the bytes around it).
+__device__ __forceinline__ void copy_to_unaligned(uint8_t* dst, const uint8_t* src, int64_t len) {
+  if (len <= 0) return;
+  const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
+  for (int64_t t = 0; t < head; t++) dst[t] = src[t];
+  const int64_t body = (len - head) >> 3;
+  const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
+  const int sh = static_cast<int>(head) * 8;           // source bit offset of the body
+  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst + head);
+  for (int64_t w = 0; w < body; w++) {
+    const uint64_t lo = s64[w];
+    const uint64_t v = sh ? (lo >> sh) | (s64[w + 1] << (64 - sh)) : lo;
+    d64[w] = v;
+  }
+  for (int64_t t = head + 8 * body; t < len; t++) dst[t] = src[t];
+}
+
 // ---- encode ----------------------------------------------------------------------------------
 
 __device__ __forceinline__ void zero_bytes(uint8_t* p, int64_t n) {
@@ -71,12 +91,20 @@ __device__ __forceinline__ void zero_bytes(uint8_t* p, int64_t n) {
 
 // Appends len bytes (unaligned source) at dst (8-aligned), zero-padding to 8.
 __device__ __forceinline__ void append_unaligned(uint8_t* dst, const uint8_t* src, int64_t len) {
+  // aligned source words funnel-shifted into place; no word past the last source byte is read
+  const uintptr_t so = reinterpret_cast<uintptr_t>(src) & 7;
+  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - so);
   const int64_t nw = (len + 7) >> 3;
+  const int64_t nsrc = (static_cast<int64_t>(so) + len + 7) >> 3;
+  const int sh = static_cast<int>(so) * 8;
+  uint64_t cur = nsrc > 0 ? ap[0] : 0;
   for (int64_t w = 0; w < nw; w++) {
-    uint64_t x = 0;
-    const int64_t lim = min<int64_t>(8, len - 8 * w);
-    for (int64_t t = 0; t < lim; t++) x |= static_cast<uint64_t>(src[8 * w + t]) << (8 * t);
+    const uint64_t nxt = w + 1 < nsrc ? ap[w + 1] : 0;
+    uint64_t x = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+    const int64_t rem = len - 8 * w;
+    if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
     st8(dst + 8 * w, x);
+    cur = nxt;
   }
 }
 
@@ -338,8 +366,7 @@ __device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni
         cur.b[ni] = pos + size;
         if (W) {
           uint8_t* dst = const_cast<uint8_t*>(n.values);
-          if (dst)
-            for (int64_t t = 0; t < size; t++) dst[pos + t] = vp[t];
+          if (dst) copy_to_unaligned(dst + pos, vp, size);
           n.offsets[e + 1] = static_cast<int32_t>(pos + size);
         }
         return;
@@ -381,18 +408,20 @@ __device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni
 
 // Pass 1 (W = false): per row, per node, Arrow entries and payload bytes -> cnt[2*node][row],
 // cnt[2*node+1][row].  Pass 2 (W = true): cursors start at the scanned positions.
+// The per-thread cursors live in dynamic LDS sized for the schema's node count (2 x 8 B x
+// nnodes per thread), so small schemas keep many workgroups per CU (a fixed kGenMaxNodes-sized
+// array held this latency-bound interpreter to 3 waves per CU).
 template <bool W>
 __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               int64_t* __restrict__ cnt) {
-  __shared__ int64_t ce[kThreads * kGenMaxNodes];
-  __shared__ int64_t cb[kThreads * kGenMaxNodes];
+  extern __shared__ int64_t cur_lds[];
   __shared__ GenNode sn[kGenMaxNodes];
   const GenNode* nodes = stage_nodes(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (r >= g.nrows) return;
-  int64_t* e = ce + threadIdx.x * kGenMaxNodes;
-  int64_t* b = cb + threadIdx.x * kGenMaxNodes;
+  int64_t* e = cur_lds + threadIdx.x * (2 * g.nnodes);
+  int64_t* b = e + g.nnodes;
   for (int i = 0; i < g.nnodes; i++) {
     e[i] = W ? cnt[(2 * i) * g.nrows + r] : 0;
     b[i] = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
@@ -408,6 +437,10 @@ __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const u
       cnt[(2 * i + 1) * g.nrows + r] = b[i];
     }
   }
+}
+
+size_t cursor_lds(const GenArgs& g) {
+  return static_cast<size_t>(kThreads) * 2 * (g.nnodes > 0 ? g.nnodes : 1) * sizeof(int64_t);
 }
 
 // Arrow offsets start at 0 for every node that has them.
@@ -435,7 +468,7 @@ int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int6
 int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
                      hipStream_t stream) {
   const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(gen_decode_kernel<false>, dim3(blocks), dim3(kThreads), 0, stream, g, rows,
+  hipLaunchKernelGGL(gen_decode_kernel<false>, dim3(blocks), dim3(kThreads), cursor_lds(g), stream, g, rows,
                      offs, cnt);
   return check_hip(hipGetLastError(), "gen_count launch");
 }
@@ -444,7 +477,7 @@ int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs
                       hipStream_t stream) {
   hipLaunchKernelGGL(gen_offsets_zero, dim3(1), dim3(kGenMaxNodes), 0, stream, g);
   const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(gen_decode_kernel<true>, dim3(blocks), dim3(kThreads), 0, stream, g, rows,
+  hipLaunchKernelGGL(gen_decode_kernel<true>, dim3(blocks), dim3(kThreads), cursor_lds(g), stream, g, rows,
                      offs, cnt);
   return check_hip(hipGetLastError(), "gen_decode launch");
 }
