@@ -400,13 +400,14 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
     const int64_t cells = 2 * static_cast<int64_t>(nn) * nrows;
     int64_t* dev = nullptr;
     int st = check_hip(hipMalloc(reinterpret_cast<void**>(&dev),
-                                 (cells + 2 * nn + scan_workspace(nrows)) * 8), "hipMalloc");
+                                 (cells + 2 * nn + scan_workspace(cells) + 2 * nn + 1) * 8),
+                       "hipMalloc");
     if (st) { delete p; return st; }
     p->cnt = dev;
     st = launch_gen_count(g, p->rows, row_offsets, dev, hs);
     int64_t* tot = dev + cells;
     int64_t* ws = tot + 2 * nn;
-    for (int q = 0; q < 2 * nn && !st; q++) device_scan(dev + q * nrows, nrows, tot + q, ws, hs);
+    if (!st) st = device_scan_batched(dev, 2 * nn, nrows, tot, ws, hs);
     if (!st) st = check_hip(hipMemcpyAsync(totals.data(), tot, 2 * nn * 8, hipMemcpyDeviceToHost, hs),
                             "hipMemcpyAsync");
     if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");

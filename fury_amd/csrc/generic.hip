@@ -109,13 +109,13 @@ __device__ __forceinline__ void append_unaligned(uint8_t* dst, const uint8_t* sr
 }
 
 template <int D, bool W>
-__device__ __attribute__((noinline)) void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+__device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
                           int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
                           int64_t& cursor);
 
 // BinaryArrayWriter image of elements [b, b + m) of node `ei` at buf + cursor.
 template <int D, bool W>
-__device__ __attribute__((noinline)) void put_array(const GenNode* nodes, int ei, int64_t b, int64_t m, uint8_t* buf,
+__device__ void put_array(const GenNode* nodes, int ei, int64_t b, int64_t m, uint8_t* buf,
                           int64_t& cursor) {
   const GenNode& e = nodes[ei];
   const int w = gwidth(e.type);
@@ -134,7 +134,7 @@ __device__ __attribute__((noinline)) void put_array(const GenNode* nodes, int ei
 }
 
 template <int D, bool W>
-__device__ __attribute__((noinline)) void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+__device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
                           int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
                           int64_t& cursor) {
   if constexpr (D >= kGenMaxDepth) {
@@ -269,13 +269,13 @@ struct Cursors {
 };
 
 template <int D, bool W>
-__device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
+__device__ void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
                           int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
                           int64_t ordinal, Cursors cur);
 
 // Elements of a BinaryArray at `arr` into node ei's Arrow column (m entries).
 template <int D, bool W>
-__device__ __attribute__((noinline)) void get_array(const GenNode* nodes, int ei, const uint8_t* arr, int64_t m, Cursors cur) {
+__device__ void get_array(const GenNode* nodes, int ei, const uint8_t* arr, int64_t m, Cursors cur) {
   const GenNode& e = nodes[ei];
   const int w = gwidth(e.type);
   const int es = w > 0 ? w : 8;
@@ -286,7 +286,7 @@ __device__ __attribute__((noinline)) void get_array(const GenNode* nodes, int ei
 
 // A null (or absent) entry for node ni and, for structs, one null entry in every child.
 template <int D, bool W>
-__device__ __attribute__((noinline)) void null_entry(const GenNode* nodes, int ni, Cursors cur) {
+__device__ void null_entry(const GenNode* nodes, int ni, Cursors cur) {
   if constexpr (D >= kGenMaxDepth) {
     return;
   } else {
@@ -318,7 +318,7 @@ __device__ __forceinline__ void set_valid_bit(uint8_t* bits, int64_t i) {
 }
 
 template <int D, bool W>
-__device__ __attribute__((noinline)) void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
+__device__ void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
                           int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
                           int64_t ordinal, Cursors cur) {
   if constexpr (D >= kGenMaxDepth) {
@@ -439,6 +439,23 @@ __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const u
   }
 }
 
+__global__ void seg_bases(const int64_t* __restrict__ s, int64_t nseq, int64_t len,
+                          const int64_t* __restrict__ grand, int64_t* __restrict__ bases,
+                          int64_t* __restrict__ totals) {
+  const int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (q >= nseq) return;
+  const int64_t b = s[q * len];
+  const int64_t e = q + 1 < nseq ? s[(q + 1) * len] : *grand;
+  bases[q] = b;
+  totals[q] = e - b;
+}
+
+__global__ void seg_unbase(int64_t* __restrict__ s, int64_t n, int64_t len,
+                           const int64_t* __restrict__ bases) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) s[i] -= bases[i / len];
+}
+
 size_t cursor_lds(const GenArgs& g) {
   return static_cast<size_t>(kThreads) * 2 * (g.nnodes > 0 ? g.nnodes : 1) * sizeof(int64_t);
 }
@@ -480,6 +497,24 @@ int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs
   hipLaunchKernelGGL(gen_decode_kernel<true>, dim3(blocks), dim3(kThreads), cursor_lds(g), stream, g, rows,
                      offs, cnt);
   return check_hip(hipGetLastError(), "gen_decode launch");
+}
+
+// nseq independent exclusive scans of len entries each (s[q * len + i]), totals[q] = sequence
+// sums: ONE scan over the concatenation, then every sequence minus its starting prefix (instead
+// of a 3-kernel scan per sequence: the nested decode has 2 x nodes sequences).
+// ws: scan_workspace(nseq * len) + 2 * nseq + 1 entries.
+int device_scan_batched(int64_t* s, int64_t nseq, int64_t len, int64_t* totals, int64_t* ws,
+                        hipStream_t stream) {
+  const int64_t n = nseq * len;
+  int64_t* grand = ws;
+  int64_t* bases = ws + 1;
+  int64_t* sws = ws + 1 + nseq;
+  device_scan(s, n, grand, sws, stream);
+  hipLaunchKernelGGL(seg_bases, dim3(static_cast<unsigned>((nseq + 255) / 256)), dim3(256), 0, stream,
+                     s, nseq, len, grand, bases, totals);
+  hipLaunchKernelGGL(seg_unbase, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
+                     s, n, len, bases);
+  return check_hip(hipGetLastError(), "batched scan launch");
 }
 
 }  // namespace fury

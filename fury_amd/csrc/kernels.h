@@ -118,6 +118,9 @@ int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);
+// nseq independent exclusive scans of len entries (ws: scan_workspace(nseq * len) + 2 nseq + 1).
+int device_scan_batched(int64_t* s, int64_t nseq, int64_t len, int64_t* totals, int64_t* ws,
+                        hipStream_t stream);
 
 int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t nrows,
                       int64_t fixed_size, int64_t schema_hash, uint8_t* out,
