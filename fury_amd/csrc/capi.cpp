@@ -181,6 +181,10 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     n.type = t.type_id;
     n.first_child = t.first_child;
     n.num_children = t.num_children;
+    // breadth-first order: a node's parent is set before it
+    if (i < static_cast<size_t>(s->num_fields)) n.row_aligned = 1;
+    if (n.row_aligned && t.type_id == FURY_TYPE_STRUCT)
+      for (int j = 0; j < t.num_children; j++) g->node[t.first_child + j].row_aligned = 1;
     if (t.num_children > 0) {
       if (!c->child) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": child columns missing");
       for (int j = 0; j < t.num_children; j++) col[t.first_child + j] = &c->child[j];

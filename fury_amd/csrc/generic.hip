@@ -266,6 +266,8 @@ __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
 struct Cursors {
   int64_t* e;   // [node]
   int64_t* b;   // [node]
+  uint64_t* vmask;   // row-aligned nodes: validity bit of this row's entry, by node index
+  uint64_t* bmask;   // row-aligned BOOL nodes: value bit of this row's entry
 };
 
 template <int D, bool W>
@@ -331,7 +333,10 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
       return;
     }
     const int64_t e = cur.e[ni]++;
-    if (W && n.validity) set_valid_bit(n.validity, e);
+    if (W && n.validity) {
+      if (n.row_aligned) *cur.vmask |= 1ull << ni;   // written by a wave ballot (entry = row)
+      else set_valid_bit(n.validity, e);
+    }
     const uint8_t* sp = base + slot_addr;
     const int w = gwidth(n.type);
     if (w > 0) {
@@ -344,7 +349,10 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
       uint8_t* dst = const_cast<uint8_t*>(n.values);
       if (!dst) return;
       if (n.type == FURY_TYPE_BOOL) {
-        if (v & 0xff) set_valid_bit(dst, e);
+        if (v & 0xff) {
+          if (n.row_aligned) *cur.bmask |= 1ull << ni;
+          else set_valid_bit(dst, e);
+        }
       } else if (w == 8) {
         st8(dst + 8 * e, v);
       } else if (w == 4) {
@@ -415,26 +423,52 @@ template <bool W>
 __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               int64_t* __restrict__ cnt) {
+  static_assert(kThreads == 64, "one wave = 64 consecutive rows (ballot bitmap words)");
   extern __shared__ int64_t cur_lds[];
   __shared__ GenNode sn[kGenMaxNodes];
   const GenNode* nodes = stage_nodes(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r >= g.nrows) return;
-  int64_t* e = cur_lds + threadIdx.x * (2 * g.nnodes);
-  int64_t* b = e + g.nnodes;
-  for (int i = 0; i < g.nnodes; i++) {
-    e[i] = W ? cnt[(2 * i) * g.nrows + r] : 0;
-    b[i] = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
-  }
-  const uint8_t* row = rows + offs[r];
-  const int64_t bmb = gbm(g.ntop);
-  Cursors cur{e, b};
-  for (int k = 0; k < g.ntop; k++)
-    get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
-  if (!W) {
+  const bool live = r < g.nrows;
+  uint64_t vmask = 0, bmask = 0;
+  if (live) {
+    int64_t* e = cur_lds + threadIdx.x * (2 * g.nnodes);
+    int64_t* b = e + g.nnodes;
     for (int i = 0; i < g.nnodes; i++) {
-      cnt[(2 * i) * g.nrows + r] = e[i];
-      cnt[(2 * i + 1) * g.nrows + r] = b[i];
+      e[i] = W ? cnt[(2 * i) * g.nrows + r] : 0;
+      b[i] = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
+    }
+    const uint8_t* row = rows + offs[r];
+    const int64_t bmb = gbm(g.ntop);
+    Cursors cur{e, b, &vmask, &bmask};
+    for (int k = 0; k < g.ntop; k++)
+      get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
+    if (!W) {
+      for (int i = 0; i < g.nnodes; i++) {
+        cnt[(2 * i) * g.nrows + r] = e[i];
+        cnt[(2 * i + 1) * g.nrows + r] = b[i];
+      }
+    }
+  }
+  if (!W) return;
+  // row-aligned nodes: the wave's 64 rows are 64 consecutive Arrow entries, so their validity /
+  // bool bits are two whole 32-bit words (no atomics; the host zeroes nothing for them)
+  const int lane = threadIdx.x;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
+  const int64_t left = g.nrows - r0;
+  const int nwords = left >= 64 ? 2 : static_cast<int>((left + 31) >> 5);
+  for (int i = 0; i < g.nnodes; i++) {
+    const GenNode& n = nodes[i];
+    if (!n.row_aligned) continue;
+    if (n.validity) {
+      const uint64_t bits = __ballot(live && ((vmask >> i) & 1));
+      if (lane < nwords)
+        reinterpret_cast<uint32_t*>(n.validity)[(r0 >> 5) + lane] = static_cast<uint32_t>(bits >> (32 * lane));
+    }
+    if (n.type == FURY_TYPE_BOOL && n.values) {
+      const uint64_t bits = __ballot(live && ((bmask >> i) & 1));
+      if (lane < nwords)
+        reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(n.values))[(r0 >> 5) + lane] =
+            static_cast<uint32_t>(bits >> (32 * lane));
     }
   }
 }

@@ -97,7 +97,7 @@ struct GenNode {
   int32_t type;            // fury_type_id
   int32_t first_child;     // node index of the first child (children are contiguous)
   int32_t num_children;
-  int32_t pad_;
+  int32_t row_aligned;     // reached from the top through STRUCTs only: Arrow entry index = row
 };
 
 struct GenArgs {
