@@ -123,3 +123,49 @@ def test_device_calls_reject_bad_arguments_without_touching_gpu():
     cols2 = (N.FuryColumn * 100)()
     assert L.fury_row_encode(s2.handle, cols2, 4, None, None, None) == 1   # rows is null
     assert L.fury_row_encode(s2.handle, cols2, -1, None, None, None) == 1  # nrows < 0
+
+
+def test_new_entry_points_reject_bad_arguments_without_touching_gpu():
+    """IPC, host-memory path, framing and tuning: argument errors are reported on the host
+    (status codes = the reference's exception types) before any HIP call."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Schema
+    L = N.lib()
+    n = ctypes.c_int64(0)
+    s = Schema(SCHEMAS["struct100"])
+    cols = (N.FuryColumn * 100)()
+    # Arrow IPC
+    assert L.fury_arrow_ipc_schema(None, None, 0, ctypes.byref(n)) == 1
+    assert L.fury_arrow_ipc_schema(s.handle, None, 0, None) == 1
+    assert L.fury_arrow_ipc_schema(s.handle, None, 0, ctypes.byref(n)) == 0 and n.value > 0
+    small = ctypes.create_string_buffer(8)
+    assert L.fury_arrow_ipc_schema(s.handle, small, 8, ctypes.byref(n)) == 7      # CAPACITY
+    assert L.fury_arrow_ipc_record_batch(None, cols, 1, None, 0, ctypes.byref(n), None) == 1
+    assert L.fury_arrow_ipc_record_batch(s.handle, cols, -1, None, 0, ctypes.byref(n), None) == 1
+    assert L.fury_arrow_ipc_record_batch(s.handle, None, 1, None, 0, ctypes.byref(n), None) == 1
+    # host-memory path
+    nb = ctypes.c_int64(0)
+    assert L.fury_row_encode_host(None, cols, 1, None, 0, None, ctypes.byref(nb), 0) == 1
+    assert L.fury_row_encode_host(s.handle, cols, -1, None, 0, None, ctypes.byref(nb), 0) == 1
+    assert L.fury_row_encode_host(s.handle, cols, 10, None, 100, None, ctypes.byref(nb), 0) == 7
+    assert nb.value == 10 * 816                                   # bytes the rows need
+    m = Schema(SCHEMAS["mixed"])
+    mcols = (N.FuryColumn * 6)()
+    assert L.fury_row_encode_host(m.handle, mcols, 3, None, 0, None, ctypes.byref(nb), 0) == 1
+    assert L.fury_row_decode_host(None, None, None, 1, cols, 0) == 1
+    assert L.fury_row_decode_host(s.handle, None, None, 1, cols, 0) == 1       # rows null
+    assert L.fury_row_decode_host(m.handle, small, None, 1, mcols, 0) == 1     # offsets null
+    assert L.fury_row_decode_host(s.handle, None, None, 0, cols, 0) == 0       # empty batch
+    assert L.fury_host_register(None, 16) == 1 and L.fury_host_unregister(None) == 1
+    # framing
+    assert L.fury_frame_rows(None, None, None, 1, None, None, None) == 1
+    assert L.fury_frame_rows(m.handle, small, None, 1, small, None, None) == 1  # offsets null
+    assert L.fury_unframe_rows(s.handle, None, 10, 1, None, None, None) == 1
+    assert L.fury_unframe_rows(s.handle, None, -1, 1, None, None, None) == 1
+    # tuning knobs: range checks, unknown keys
+    assert L.fury_set_tuning(b"fixed_variant", 512) == 1
+    assert L.fury_set_tuning(b"var_decode", 4) == 1
+    assert L.fury_set_tuning(b"unframe", 2) == 1
+    assert L.fury_set_tuning(b"no_such_knob", 0) == 1
+    assert L.fury_get_tuning(b"no_such_knob") == -1
+    assert L.fury_get_tuning(b"fixed_variant") == 54
