@@ -443,8 +443,8 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
 int fury_set_tuning(const char* key, int32_t value) {
   if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
   if (std::string(key) == "fixed_variant") {
-    if (value < 0 || value > 511)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..511");
+    if (value < 0 || value > 1023)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..1023");
     set_fixed_variant(value);
     return FURY_OK;
   }

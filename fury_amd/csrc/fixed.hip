@@ -76,6 +76,16 @@ __device__ __forceinline__ uint8_t* values_of(const FixedArgs& a, int c, int lan
   }
 }
 
+// Tile of workgroup b.  Workgroups are dealt round-robin to the 8 XCDs (b % 8); tile_order 1
+// gives each XCD one contiguous eighth of the tiles (b -> (b % 8) * (nb / 8) + b / 8 on the
+// largest multiple of 8, identity on the tail), so an XCD's L2 and TLB see one address range.
+__device__ __forceinline__ int64_t tile_of(const FixedArgs& a) {
+  const int64_t b = blockIdx.x, nb = gridDim.x;
+  if (!a.tile_order) return b;
+  const int64_t q = nb >> 3;
+  return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
+}
+
 // Global access helpers; NT bit 0 = non-temporal loads, bit 1 = non-temporal stores (streamed
 // bytes are touched once, so keeping them out of L2/MALL leaves room for the other stream).
 using v4u = __attribute__((ext_vector_type(4))) uint32_t;
@@ -196,7 +206,7 @@ template <int R, bool kFast, int NT, int U = kUnroll, int DS = 4, bool P = false
 __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
                                                                  uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t r0 = tile_of(a) * R;
   const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
@@ -302,7 +312,7 @@ template <int R, bool kFast, int NT, int D = 4, bool P = false>
 __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
                                                                  const uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t r0 = tile_of(a) * R;
   const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
@@ -599,7 +609,9 @@ int launch_fast_tile(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool
 }
 
 template <bool kEnc>
-int launch_fast_tile_variant(const FixedArgs& a, uint8_t* rows, hipStream_t stream, int var) {
+int launch_fast_tile_variant(const FixedArgs& a0, uint8_t* rows, hipStream_t stream, int var) {
+  FixedArgs a = a0;
+  a.tile_order = (var & 512) ? 1 : 0;          // bit 9: XCD-contiguous tile ranges
   int R = pick_rows_per_tile(a.row_size);
   // bit 8: tall tiles (twice the rows: longer contiguous column runs, fewer workgroups per CU)
   if ((var & 256) && R < 256 && static_cast<int64_t>(2 * R) * a.row_size <= 160 * 1024) R *= 2;
@@ -643,7 +655,7 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
       default: return launch_pipe(encode_fixed_pipe<32, 0>, a.row_size, a.nrows, stream, a, rows);
     }
   }
-  if (fast && (var & 504) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
+  if (fast && (var & 1016) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                          \
   if (R == RR) {                                                                              \
@@ -690,7 +702,7 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
       default: return launch_pipe(decode_fixed_pipe<17, 0>, a.row_size, a.nrows, stream, a, r);
     }
   }
-  if (fast && (var & 504) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
+  if (fast && (var & 1016) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_DEC(RR)                                                                          \
   if (R == RR) {                                                                              \

@@ -29,7 +29,7 @@ struct FixedArgs {
   int32_t ncols;
   int32_t bitmap_bytes;
   int32_t row_size;
-  int32_t pad_;
+  int32_t tile_order;                 // 0: tile = blockIdx; 1: XCD-contiguous tile ranges
   int64_t nrows;
 };
 

@@ -189,7 +189,7 @@ def test_frame_unframe_roundtrip(oracle, dev):
             other.unframe(stream, n)
 
 
-@pytest.mark.parametrize("variant", [6, 14, 22, 38, 54, 62, 118, 134, 182, 254, 310, 7, 0])
+@pytest.mark.parametrize("variant", [6, 14, 22, 38, 54, 62, 118, 134, 182, 254, 310, 566, 7, 0])
 def test_fixed_variants_bit_exact(oracle, dev, variant):
     """Every fixed-width kernel variant (tuning 'fixed_variant') writes the oracle's rows and
     decodes them back, including ragged last tiles (odd row counts for the pair mode)."""
