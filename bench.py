@@ -223,6 +223,10 @@ def main():
                    else round(total_row_bytes / n, 2),
                    "algorithmic_bytes_per_step_per_gpu": step_bytes,
                    "parallelism": f"{world} independent shard(s), no collective"},
+        # row bytes per second beside the algorithmic bytes (information only)
+        "rows": {"rows_per_s": round(n * world * args.steps / dt_max, 1),
+                 "row_GBps": round(2 * total_row_bytes * world * args.steps / dt_max / 1e9, 2),
+                 "what": "rows encoded+decoded per second; row bytes written+read per second"},
         "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
