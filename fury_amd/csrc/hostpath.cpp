@@ -15,6 +15,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -70,6 +72,21 @@ int64_t fixed_bytes(const FieldPlan& p, int64_t n) {
 // Device bitmap buffers are written as 32-bit words (fury_row.h): pad to 4 bytes.
 int64_t bitmap_alloc(int64_t n) { return ((n + 31) / 32) * 4 + 4; }
 
+// The stream-ordered pool of `device` keeps freed workspace memory instead of returning it at
+// every synchronisation (the default release threshold 0 re-mapped ~1.7 GB per call).  Once per
+// device, thread-safe.
+void keep_pool(int device) {
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!done.insert(device).second) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+}
+
 // Bytes one row occupies in a stage (row image + its column values + validity bits, rounded up).
 int64_t stage_bytes_per_row(const fury_schema* s) {
   int64_t per_row = s->fixed_size;
@@ -116,15 +133,7 @@ int fixed_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t
       stage += ((bitmap_alloc(C) + 255) / 256) * 256;
     }
   }
-  static bool pool_kept = false;             // keep the workspace pooled between calls
-  if (!pool_kept) {
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-      uint64_t keep = UINT64_MAX;
-      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    }
-    pool_kept = true;
-  }
+  keep_pool(device);                          // keep the workspace pooled between calls
   uint8_t* ws = nullptr;
   if ((st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), stage * kStages, ss.s[0]),
                       "hipMallocAsync")))
