@@ -185,6 +185,8 @@ def main():
     else:
         assert int(offs[n].item()) == total_row_bytes, "row buffer overflow"
         enc.check_capacity(var_out, n)
+        from fury_amd import _native as N
+        assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0, "look-back gave up"
         for c, d in zip(cols, var_out):
             if c.offsets is not None and c.child is None:
                 assert torch.equal(c.offsets, d.offsets), "decode offsets mismatch"

@@ -465,6 +465,8 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "fixed_variant") return fixed_variant();
   if (key && std::string(key) == "var_decode") return var_decode_mode();
   if (key && std::string(key) == "unframe") return unframe_mode();
+  if (key && std::string(key) == "lookback_timeouts")
+    return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")
     return static_cast<int32_t>(unframe_walk_count());
   return -1;

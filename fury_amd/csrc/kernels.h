@@ -75,6 +75,7 @@ int workspace_reserve(size_t bytes, void** out);
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
 int var_decode_mode();
+int64_t lookback_timeouts();
 void set_var_decode_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 // Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.

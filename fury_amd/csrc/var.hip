@@ -1877,6 +1877,16 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
 }
 
 int var_decode_mode() { return g_var_decode; }
+
+// Look-back spins abandoned so far (each one would have left wrong Arrow offsets behind; never
+// observed: workgroups are dispatched in launch order).  Synchronous device read.
+int64_t lookback_timeouts() {
+  unsigned int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_lookback_timeouts), sizeof(v), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return v;
+}
 void set_var_decode_mode(int v) { g_var_decode = v; }
 // LDS plan of the pipelined encode: per workgroup 2 meta slots + 2 payload slots + 1 row image
 // within kPipeLds, so kPipeGroupsPerCU workgroups share a CU.  Payload and row sizes are

@@ -221,7 +221,9 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
  * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
  * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles.
  * Key "unframe": 0 speculative parallel stream parse (sequential walk when it does not verify),
- * 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk parsed. */
+ * 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk parsed.
+ * fury_get_tuning("lookback_timeouts") = decoupled look-backs of the variable-length decode that
+ * gave up waiting (must stay 0; synchronous device read). */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 

@@ -216,6 +216,7 @@ def test_var_decode_modes_bit_exact(oracle, dev, mode):
             _roundtrip(oracle, name, n, dev, seed=n + mode)
     finally:
         N.lib().fury_set_tuning(b"var_decode", old)
+    assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
 def _walks():
