@@ -523,6 +523,19 @@ class RowEncoder:
         return RowBatch(rows[:total], None if self._schema.is_fixed else offs, nrows,
                         self.schema_hash)
 
+    def encode_stream(self, columns: Sequence[Column], nrows: int, stream=None) -> torch.Tensor:
+        """Batch ``encode(MemoryBuffer, T)`` over every row: the byte stream a Java writer loop
+        produces (``[int32 len][int64 hash][row]`` per row), in device memory."""
+        out, _ = self.frame(self.encode_batch(columns, nrows, stream=stream), stream=stream)
+        return out
+
+    def decode_stream(self, stream_bytes: torch.Tensor, nrows: int, validity: bool = True,
+                      stream=None) -> List[Column]:
+        """Batch ``decode(MemoryBuffer)`` of nrows frames: parallel stream parse, then the
+        columns (ClassNotCompatibleException on a schema-hash mismatch, like the reference)."""
+        return self.decode_batch(self.unframe(stream_bytes, nrows, stream=stream),
+                                 validity=validity, stream=stream)
+
     # -- single-object API (a bean is a dict name -> value) --------------------------------
     def to_row(self, bean: dict) -> bytes:
         """``toRow(obj).toBytes()``: canonical row bytes of one bean."""

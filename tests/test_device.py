@@ -254,6 +254,21 @@ def test_unframe_parallel_equals_walk(oracle, dev, name, n):
         assert np.array_equal(fast.row_offsets.cpu().numpy(), offs)
 
 
+@pytest.mark.parametrize("name,n", [("mixed", 3001), ("struct100", 513), ("nested", 700)])
+def test_stream_encode_decode(oracle, dev, name, n):
+    """encode_stream / decode_stream: the Java encode(MemoryBuffer, T) loop's stream and back to
+    the oracle's columns."""
+    from fury_amd.encoder import column_to_host, Encoders
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=41)
+    enc = Encoders.bean(fields, device=dev)
+    s = enc.encode_stream(_dev_cols(host, dev), n)
+    rows, offs = oracle.encode(fields, host, n)
+    assert s.numel() == rows.nbytes + 12 * n
+    dec = [column_to_host(c) for c in enc.decode_stream(s, n)]
+    assert_columns_equal(fields, dec, oracle.decode(fields, rows, offs, n), n)
+
+
 def test_unframe_fake_header_in_payload(oracle, dev):
     """A row whose slots spell a plausible frame header ([len 16][schema hash]) is a false
     candidate: verification fails, the walk re-parses, results are still the oracle's."""
