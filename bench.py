@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "row-format encode+decode GB/s (device-resident), Struct-100, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+CPU_THREADS = 16               # the GPU box's CPU share per GPU (nproc shows the whole machine)
 DEFAULT_ROWS = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}
 
 
@@ -97,10 +98,32 @@ def cpu_baseline(name, fields, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(per_pass * reps / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
-            "kind": "port",
-            "sample": f"{reps} x encode+decode of {sample} {name} rows (oracle/row_oracle.c, "
-                      f"toRow/fromRow restatement, 1 thread) in {dt:.1f} s"}
+    out = {"value": round(per_pass * reps / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
+           "kind": "port",
+           "sample": f"{reps} x encode+decode of {sample} {name} rows (oracle/row_oracle.c, "
+                     f"toRow/fromRow restatement, 1 thread) in {dt:.1f} s"}
+    # the same restatement on THREADS host threads (one encoder per thread, like the reference's
+    # thread-confined RowEncoder; ctypes releases the GIL inside the C calls)
+    from concurrent.futures import ThreadPoolExecutor
+    threads = CPU_THREADS
+    stop = time.perf_counter() + budget_s / 2
+
+    def work(_):
+        k = 0
+        while time.perf_counter() < stop:
+            r, o = O.encode(fields, host, sample)
+            O.decode(fields, r, None if name == "struct100" else o, sample, with_validity=False)
+            k += 1
+        return k
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        total = sum(ex.map(work, range(threads)))
+    dt = time.perf_counter() - t0
+    out["threads"] = {"value": round(per_pass * total / dt / 1e9, 4), "unit": "GB/s",
+                      "cores": threads,
+                      "sample": f"{total} x encode+decode of {sample} {name} rows on {threads} "
+                                f"threads in {dt:.1f} s"}
+    return out
 
 
 def main():
