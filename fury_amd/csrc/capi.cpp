@@ -150,7 +150,14 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   }
   a->nvar = nvar;
   a->tile_rows = encode_tile_rows(*a);
-  if (const char* e = getenv("FURY_VAR_DBG")) a->dbg = atoi(e);
+  // FURY_VAR_DBG selects kernel variants for A/B (bits 512 / 1024 / 2048: all correct).  Bits
+  // 1-64 switch phases OFF for timing (scripts/diag_var.py) and leave wrong outputs, so they
+  // are honoured only with FURY_DIAGNOSTIC=1.
+  if (const char* e = getenv("FURY_VAR_DBG")) {
+    a->dbg = atoi(e);
+    const char* d = getenv("FURY_DIAGNOSTIC");
+    if (!d || std::string(d) != "1") a->dbg &= ~127;
+  }
   return FURY_OK;
 }
 

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
+    os.environ["FURY_DIAGNOSTIC"] = "1"      # the phase-skipping bits are diagnostic only
     import torch
     from bench import DEFAULT_ROWS, make_device_columns
     from fury_amd.encoder import Encoders
