@@ -224,8 +224,9 @@ def main():
     dominant = ("encode", enc_ms, enc_bytes) if enc_ms >= dec_ms else ("decode", dec_ms, dec_bytes)
     achieved = dominant[2] / (dominant[1] * 1e-3) / 1e9
     traffic = None
-    pmc_file = os.path.join(ROOT, "profiles", "pmc_struct100.json")
-    if args.workload == "struct100" and os.path.exists(pmc_file) and n == 1_000_000:
+    # PMC traffic (scripts/pmc.sh, scripts/pmc_var_traffic.sh) applies to the same workload and size
+    pmc_file = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
+    if os.path.exists(pmc_file) and n == DEFAULT_ROWS[args.workload]:
         pm = json.load(open(pmc_file))
         traffic = pm.get(f"{dominant[0]}_hbm_bytes_per_launch")
     line = {
