@@ -583,3 +583,45 @@ def test_encode_measured_fixed_capacity_error(dev):
     assert torch.equal(rows, ref.rows)
     with pytest.raises(CapacityError):
         enc.encode_measured_into(cols, 100, rows[:816 * 99], None)
+
+
+def _encode_measured(enc, cols, n, dev):
+    total_guess = enc.encode_batch(cols, n).rows.numel()
+    rows = torch.full((total_guess + 64,), 0xEE, dtype=torch.uint8, device=dev)
+    offs = torch.full((n + 1,), -1, dtype=torch.int64, device=dev)
+    enc.encode_measured_into(cols, n, rows[:total_guess], offs)
+    torch.cuda.synchronize()
+    return rows, offs, total_guess
+
+
+@pytest.mark.parametrize("case", ["mixed_multi_group", "long_strings", "long_lists", "edge_strings"])
+def test_encode_measured_vs_oracle(oracle, dev, case):
+    """fury_row_encode_measured (measure + encode in one call) against the oracle directly: rows
+    and offsets bit-exact across several measure groups (1,024 rows) that straddle encode tiles,
+    for oversized tiles that take the direct-to-HBM branch, and for edge-length strings; nothing
+    is written past the rows."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders
+    if case == "mixed_multi_group":
+        fields, n = SCHEMAS["mixed"], 5 * 1024 + 77
+        host = gen_columns("mixed", fields, n, seed=29)
+    elif case == "long_strings":
+        fields, n = SCHEMAS["mixed"], 2500
+        host = gen_columns("mixed", fields, n, seed=31, str_max=600)
+    elif case == "long_lists":
+        fields, n = SCHEMAS["nested"], 1500
+        host = gen_columns("nested", fields, n, seed=37, list_max=200)
+    else:
+        fields = [T.field("a", T.STRING), T.field("b", T.BINARY)]
+        vals = ["", "x", "abcdefg", "abcdefgh", "abcdefghi", None, "z" * 300, "", "q" * 8191] * 150
+        n = len(vals)
+        host = beans_to_columns(fields, [{"a": v, "b": (v.encode() if v is not None else None)}
+                                         for v in vals])
+    want, want_offs = oracle.encode(fields, host, n)
+    enc = Encoders.bean(fields, device=dev)
+    cols = _dev_cols(host, dev)
+    rows, offs, total = _encode_measured(enc, cols, n, dev)
+    assert total == want.size
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    assert bool((rows[total:] == 0xEE).all())
