@@ -324,11 +324,24 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
   return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
 }
 
+// An empty batch still yields valid Arrow offsets (offsets[0] = 0) in every top-level column that
+// has an offsets buffer; for n > 0 the decode kernels write them, for n = 0 none is launched.
+static int zero_empty_offsets(const fury_schema* s, fury_column* cols, hipStream_t hs) {
+  if (!cols) return FURY_OK;
+  for (int k = 0; k < s->num_fields; k++) {
+    if (!cols[k].offsets) continue;
+    const int st = check_hip(hipMemsetAsync(cols[k].offsets, 0, 4, hs), "memset");
+    if (st) return st;
+  }
+  return FURY_OK;
+}
+
 int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                             int64_t nrows, fury_column* cols, void* stream) {
   int st = common_checks(s, cols, nrows, "fury_row_decode_measure");
   if (st) return st;
-  if (s->is_fixed || nrows == 0) return FURY_OK;   // nothing variable to size
+  if (nrows == 0) return zero_empty_offsets(s, cols, static_cast<hipStream_t>(stream));
+  if (s->is_fixed) return FURY_OK;   // nothing variable to size
   if (s->generic)
     return set_error(FURY_ERR_INVALID_ARGUMENT,
                      "nested schema: size outputs with fury_decode_prepare / fury_decode_execute");
@@ -345,7 +358,7 @@ static int decode_impl(const fury_schema* s, const void* rows, const int64_t* ro
                        const char* fn) {
   int st = common_checks(s, cols, nrows, fn);
   if (st) return st;
-  if (nrows == 0) return FURY_OK;
+  if (nrows == 0) return zero_empty_offsets(s, cols, static_cast<hipStream_t>(stream));
   if (!rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
   hipStream_t hs = static_cast<hipStream_t>(stream);
   if (s->is_fixed) {

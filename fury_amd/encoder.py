@@ -369,10 +369,51 @@ class RowEncoder:
             L.fury_decode_plan_destroy(plan)
         return top
 
+    def _decode_bound(self, batch: RowBatch, validity: bool, arrow: bool,
+                      stream=None) -> List[Column]:
+        """Variable-length outputs sized from a bound the rows give (a column's payload bytes and
+        list elements <= the batch's row bytes: every byte of them is inside some row), decoded
+        in one pass, then trimmed to the real sizes after ONE host read of every column's
+        offsets[n] -- no fury_row_decode_measure pass over the rows."""
+        n = batch.nrows
+        bound = int(batch.rows.numel())
+        cols = self.alloc_columns(n, validity)
+        for f, c in zip(self._schema.fields, cols):
+            if f.type_id in (STRING, BINARY):
+                c.values = torch.empty(max(bound, 1), dtype=torch.uint8, device=self.device)
+            elif f.type_id == LIST:
+                e = f.children[0]
+                nbytes = (bound + 7) // 8 if e.type_id == BOOL else bound
+                c.child = [Column(
+                    values=torch.empty(nbytes + 8, dtype=torch.uint8, device=self.device),
+                    validity=(torch.zeros((bound + 7) // 8 + 4, dtype=torch.uint8,
+                                          device=self.device) if validity else None))]
+        self.decode_into(batch, cols, stream, arrow)
+        var = [(f, c) for f, c in zip(self._schema.fields, cols)
+               if f.type_id in (STRING, BINARY, LIST)]
+        if not var or n == 0:
+            return cols
+        totals = torch.stack([c.offsets[n] for _, c in var]).cpu().tolist()
+        for (f, c), total in zip(var, totals):
+            if f.type_id == LIST:
+                e = f.children[0]
+                ch = c.child[0]
+                nbytes = (total + 7) // 8 if e.type_id == BOOL else total * type_width(e.type_id)
+                ch.values = ch.values[:nbytes + 8]
+                if ch.validity is not None:
+                    ch.validity = ch.validity[:(total + 7) // 8 + 4]
+            else:
+                c.values = c.values[:max(total, 1)]
+        return cols
+
     def _decode(self, batch: RowBatch, validity: bool, arrow: bool, stream=None,
-                out: Optional[List[Column]] = None) -> List[Column]:
+                out: Optional[List[Column]] = None, sizing: str = "measure") -> List[Column]:
         if self.nested:
             return self._decode_nested(batch, validity, arrow, stream)
+        if sizing not in ("measure", "bound"):
+            raise ValueError(f"sizing must be 'measure' or 'bound', not {sizing!r}")
+        if sizing == "bound" and out is None and not self._schema.is_fixed:
+            return self._decode_bound(batch, validity, arrow, stream)
         n = batch.nrows
         cols = out if out is not None else self.alloc_columns(n, validity)
         keep: list = []
@@ -431,13 +472,16 @@ class RowEncoder:
                 raise CapacityError(f"column {f.name}: decode needs {need}, buffer holds {have}")
 
     def decode_batch(self, batch: RowBatch, validity: bool = True, stream=None,
-                     out: Optional[List[Column]] = None) -> List[Column]:
-        """Rows -> columns (generated fromRow semantics)."""
+                     out: Optional[List[Column]] = None, sizing: str = "measure") -> List[Column]:
+        """Rows -> columns (generated fromRow semantics).  Variable-length outputs are sized by
+        ``sizing``: "measure" (default) runs fury_row_decode_measure first and allocates exactly;
+        "bound" allocates each from the batch's row bytes (HBM for speed: no sizing pass over the
+        rows) and trims after one host read."""
         if batch.schema_hash != self.schema_hash:
             raise ClassNotCompatibleException(
                 f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
                 f"hash are {self.schema_hash}/{batch.schema_hash}. Please check writer schema.")
-        return self._decode(batch, validity, False, stream, out)
+        return self._decode(batch, validity, False, stream, out, sizing)
 
     # -- host-memory batch path: the JNI boundary (off-heap buffers in, off-heap buffers out) --
     def encode_host(self, columns: Sequence[Column], nrows: int, rows=None, row_offsets=None,

@@ -625,3 +625,28 @@ def test_encode_measured_vs_oracle(oracle, dev, case):
     assert np.array_equal(offs.cpu().numpy(), want_offs)
     assert np.array_equal(rows[:total].cpu().numpy(), want)
     assert bool((rows[total:] == 0xEE).all())
+
+
+@pytest.mark.parametrize("name,n,knobs", [("mixed", 3000, {}), ("mixed", 2000, {"str_max": 600}),
+                                          ("nested", 1500, {"list_max": 200}), ("mixed", 0, {})])
+def test_decode_bound_sizing_matches_oracle(oracle, dev, name, n, knobs):
+    """decode_batch(sizing="bound"): outputs sized from the row bytes, one decode pass, trimmed
+    after -- columns equal the oracle's decode and the measured path's buffers exactly."""
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=41, **knobs)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(_dev_cols(host, dev), n)
+    got = enc.decode_batch(batch, sizing="bound")
+    ref = enc.decode_batch(batch)
+    torch.cuda.synchronize()
+    want, want_offs = oracle.encode(fields, host, n)
+    assert_columns_equal(fields, [column_to_host(c) for c in got],
+                         oracle.decode(fields, want, want_offs, n), n)
+    for a, b in zip(got, ref):
+        if a.offsets is not None:
+            assert torch.equal(a.offsets, b.offsets)
+        if a.values is not None and b.values is not None:
+            assert a.values.numel() == b.values.numel()
+    with pytest.raises(ValueError):
+        enc.decode_batch(batch, sizing="guess")
