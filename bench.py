@@ -2,9 +2,13 @@
 
 One step = encode one batch of Arrow-style columns into Fury rows (HBM -> HBM) + decode those
 rows back into columns, through the HIP kernels behind the C ABI.  Default workload is
-configs[1]: 1M rows of Struct-100 (f00..f99, int64/float64, non-null) per GPU; with --gpus N
-(torch.distributed.run, one process per GPU) every rank runs its own independent shard
-(weak scaling, no data-path collective: rows are independent).
+configs[1]: 1M rows of Struct-100 (f00..f99, int64/float64, non-null) per GPU.  With --gpus N
+there is one process per GPU: started by torch.distributed.run (RANK/WORLD_SIZE in the
+environment, which must agree with --gpus), or, when run directly, spawned by this script
+through fury_amd.shard.launch before it touches the GPU.  Every rank runs its own independent
+shard of global rows, no data-path collective (rows are independent): --rows R per GPU (weak
+scaling, default) or --total-rows T split into contiguous shards (strong scaling; C5 =
+--total-rows 100000000 --gpus 8).
 
 Prints ONE JSON line (rank 0).  `value` = total algorithmic bytes of all ranks / max-over-ranks
 time (encode reads 800 B + writes 816 B per row, decode the reverse; 3,232 B/row).
@@ -28,19 +32,26 @@ CPU_THREADS = 16               # the GPU box's CPU share per GPU (nproc shows th
 DEFAULT_ROWS = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}
 
 
-def _parse():
+def _parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--rows", type=int, default=None,
-                   help="rows per GPU (default: BASELINE config size: struct100 1M, mixed 10M, "
-                        "nested 4M)")
+                   help="rows per GPU, weak scaling (default: BASELINE config size: struct100 1M, "
+                        "mixed 10M, nested 4M)")
+    p.add_argument("--total-rows", type=int, default=None,
+                   help="strong scaling: this many rows in total, split into contiguous "
+                        "near-equal shards over the GPUs (C5: --total-rows 100000000 --gpus 8)")
+    p.add_argument("--share-gpus", action="store_true",
+                   help="rehearsal only: allow more ranks than visible GPUs (ranks share them)")
     p.add_argument("--workload", default="struct100", choices=["struct100", "mixed", "nested"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-rows", type=int, default=None,
+                   help="rows of the CPU baseline's batch (default: the bench batch, C2 = 1M)")
     p.add_argument("--no-e2e", action="store_true")
-    a = p.parse_args()
+    a = p.parse_args(argv)
     if a.rows is None:
         a.rows = DEFAULT_ROWS[a.workload]
     return a
@@ -57,86 +68,122 @@ def _nbytes(cols):
     return sum(t.numel() * t.element_size() for c in cols for t in _buffers(c))
 
 
-def make_device_columns(name, fields, rows, rank, start, dev):
-    """Synthetic columns resident in HBM.  Struct-100: random 64-bit patterns generated on the
-    device (shard-keyed seed).  Var-length workloads: SplitMix64 generator on the host (shard =
-    global row range), copied once before timing."""
-    import torch
+def make_device_columns(name, fields, rows, start, dev):
+    """Synthetic columns resident in HBM, SplitMix64 keyed by (column, GLOBAL row index), so a
+    shard holds exactly the rows a single-GPU run over the whole range would.  Struct-100 is
+    generated on the device (fury_amd.workloads.gen_columns_torch, bit-identical to the host
+    generator); variable-length workloads on the host, copied once before timing."""
     from fury_amd.encoder import column_to_device
-    from fury_amd.workloads import Column, gen_columns
+    from fury_amd.workloads import gen_columns, gen_columns_torch
     if name == "struct100":
-        g = torch.Generator(device=dev).manual_seed(1234 + rank)
-        cols = []
-        for f in fields:
-            v = torch.randint(-2**63, 2**63 - 1, (rows,), dtype=torch.int64, device=dev,
-                              generator=g)
-            cols.append(Column(values=v.view(torch.float64) if f.type_id == 12 else v))
-        return cols
+        return gen_columns_torch(name, fields, rows, seed=1234, start=start, device=dev)
     host = gen_columns(name, fields, rows, seed=1234, start=start)
     return [column_to_device(c, dev) for c in host]
 
 
-def cpu_baseline(name, fields, budget_s):
-    """Oracle C restatement (kind "port"), 1 thread, timed on this host on a bounded sample."""
-    import numpy as np
+def _host_cpus():
+    """(CPUs this process may run on, CPUs the machine has): the box's nproc shows the whole
+    machine, the affinity mask the share a GPU job gets."""
+    try:
+        mine = len(os.sched_getaffinity(0))
+    except AttributeError:
+        mine = os.cpu_count() or 1
+    return mine, os.cpu_count() or 1
+
+
+def cpu_baseline(name, fields, budget_s, sample_rows):
+    """Oracle C restatement of the Java writer/reader (kind "port") timed on this host on the
+    bench workload's own batch (``sample_rows`` rows, default = the full C2 batch of 1M rows):
+    1 thread over the whole batch, then CPU_THREADS threads each encoding + decoding a
+    contiguous slice of it (one encoder per thread, like the reference's thread-confined
+    RowEncoder; ctypes releases the GIL inside the C calls)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     from fury_amd.workloads import gen_columns
-    sample = 20_000 if name == "struct100" else 50_000
-    host = gen_columns(name, fields, sample, seed=99)
-    rows, offs = O.encode(fields, host, sample)
-    col_bytes = sum(a.nbytes for c in host for a in (c.values, c.validity, c.offsets) if a is not None)
-    col_bytes += sum(a.nbytes for c in host for ch in (c.child or []) for a in
-                     (ch.values, ch.validity, ch.offsets) if a is not None)
-    row_bytes = rows.nbytes + (0 if name == "struct100" else offs.nbytes)
-    per_pass = 2 * (col_bytes + row_bytes)
+    var = name != "struct100"
+    host = gen_columns(name, fields, sample_rows, seed=99)
+
+    def nbytes(cols):
+        return sum(a.nbytes for c in cols for a in (c.values, c.validity, c.offsets)
+                   if a is not None) + sum(nbytes(c.child) for c in cols if c.child)
+
+    rows, offs = O.encode(fields, host, sample_rows)
+    per_pass = 2 * (nbytes(host) + rows.nbytes + (offs.nbytes if var else 0))
+    del rows, offs
     t0 = time.perf_counter()
     reps = 0
     while True:
-        r, o = O.encode(fields, host, sample)
-        O.decode(fields, r, None if name == "struct100" else o, sample, with_validity=False)
+        r, o = O.encode(fields, host, sample_rows)
+        O.decode(fields, r, o if var else None, sample_rows, with_validity=False)
+        del r, o
         reps += 1
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
+    mine, machine = _host_cpus()
     out = {"value": round(per_pass * reps / dt / 1e9, 4), "unit": "GB/s", "cores": 1,
            "kind": "port",
-           "sample": f"{reps} x encode+decode of {sample} {name} rows (oracle/row_oracle.c, "
-                     f"toRow/fromRow restatement, 1 thread) in {dt:.1f} s"}
-    # the same restatement on THREADS host threads (one encoder per thread, like the reference's
-    # thread-confined RowEncoder; ctypes releases the GIL inside the C calls)
-    from concurrent.futures import ThreadPoolExecutor
+           "sample": f"{reps} x encode+decode of the {sample_rows}-row {name} batch "
+                     f"(oracle/row_oracle.c, toRow/fromRow restatement, 1 thread) in {dt:.1f} s",
+           "host_cpus": {"affinity": mine, "nproc": machine}}
+    if var:
+        return out     # slicing variable-length columns per thread is not implemented
     threads = CPU_THREADS
+    bounds = [(sample_rows * t // threads, sample_rows * (t + 1) // threads) for t in range(threads)]
+    from fury_amd.workloads import Column
+    parts = [[Column(values=c.values[b:e]) for c in host] for b, e in bounds]
     stop = time.perf_counter() + budget_s / 2
 
-    def work(_):
-        k = 0
+    def work(t):
+        k, m = 0, bounds[t][1] - bounds[t][0]
         while time.perf_counter() < stop:
-            r, o = O.encode(fields, host, sample)
-            O.decode(fields, r, None if name == "struct100" else o, sample, with_validity=False)
+            r, _ = O.encode(fields, parts[t], m)
+            O.decode(fields, r, None, m, with_validity=False)
             k += 1
         return k
     t0 = time.perf_counter()
     with ThreadPoolExecutor(threads) as ex:
-        total = sum(ex.map(work, range(threads)))
+        laps = list(ex.map(work, range(threads)))
     dt = time.perf_counter() - t0
-    out["threads"] = {"value": round(per_pass * total / dt / 1e9, 4), "unit": "GB/s",
+    done = sum(laps) / threads            # whole-batch passes (every slice the same size +-1)
+    out["threads"] = {"value": round(per_pass * done / dt / 1e9, 4), "unit": "GB/s",
                       "cores": threads,
-                      "sample": f"{total} x encode+decode of {sample} {name} rows on {threads} "
-                                f"threads in {dt:.1f} s"}
+                      "sample": f"{sum(laps)} x encode+decode of 1/{threads} slices of the "
+                                f"{sample_rows}-row batch on {threads} threads in {dt:.1f} s"}
     return out
+
+
+def _worker(argv):
+    """One rank of a `bench.py --gpus N` run started by fury_amd.shard.launch."""
+    run(_parse(argv))
 
 
 def main():
     args = _parse()
+    if "RANK" not in os.environ and args.gpus > 1:
+        # started directly with --gpus N: one worker process per GPU (spawned before this
+        # process touches the GPU), rank 0 prints the JSON line
+        from fury_amd.shard import launch
+        launch(args.gpus, _worker, (sys.argv[1:],))
+        return
+    run(args)
+
+
+def run(args):
     import torch
 
-    from fury_amd.shard import Orchestrator, from_env, weak_shard
+    from fury_amd.shard import Orchestrator, from_env, strong_shard, weak_shard
     r = from_env()
     world, rank, local = r.world, r.rank, r.local
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     # orchestration only (gloo barrier + max of timings); the data path has no collective
     orch = Orchestrator(r)
-    # one process per GPU; with fewer GPUs than ranks (a rehearsal on a 1-GPU box) ranks share
+    # one process per GPU; sharing a GPU between ranks only as an explicit rehearsal
     ndev = torch.cuda.device_count()
+    if ndev < world and not args.share_gpus:
+        raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPUs "
+                         "(--share-gpus for a rehearsal)")
     local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -145,9 +192,13 @@ def main():
     from fury_amd.workloads import SCHEMAS
     fields = SCHEMAS[args.workload]
     enc = Encoders.bean(fields, device=dev)
-    n = args.rows
-    start, n = weak_shard(args.rows, rank)
-    cols = make_device_columns(args.workload, fields, n, rank, start, dev)
+    if args.total_rows is not None:
+        start, n = strong_shard(args.total_rows, world, rank)
+        scaling = "strong"
+    else:
+        start, n = weak_shard(args.rows, rank)
+        scaling = "weak"
+    cols = make_device_columns(args.workload, fields, n, start, dev)
     out_cols = enc.alloc_columns(n, validity=False) if enc.schema().is_fixed else None
     stream = torch.cuda.current_stream()
 
@@ -218,6 +269,10 @@ def main():
     if world == 1 and not args.no_e2e and args.workload == "struct100":
         e2e = end_to_end(enc, cols, n, dev, stream)
 
+    # every rank's bytes and rows (shards may differ by one row under strong scaling)
+    all_bytes = sum(orch.gather_ints(int(step_bytes)))
+    all_rows = sum(orch.gather_ints(int(n)))
+    all_row_bytes = sum(orch.gather_ints(int(total_row_bytes)))
     if rank != 0:
         orch.close()
         return
@@ -229,29 +284,39 @@ def main():
     if os.path.exists(pmc_file) and n == DEFAULT_ROWS[args.workload]:
         pm = json.load(open(pmc_file))
         traffic = pm.get(f"{dominant[0]}_hbm_bytes_per_launch")
+    data = ("synthetic SplitMix64 values keyed by (column, global row) generated in HBM; "
+            "no dataset") if args.workload == "struct100" else \
+        "synthetic SplitMix64 columns keyed by (column, global row), copied to HBM once; no dataset"
+    config = {"workload": {"struct100": "Struct-100 encode+decode (configs[1])",
+                           "mixed": "mixed int32/int64/double + 3 utf8 + nulls (configs[2])",
+                           "nested": "id/score + list<int64> encode + decode (configs[3])"
+                           }[args.workload],
+              "rows_per_gpu": n, "row_bytes": enc.schema().fixed_size if offs is None
+              else round(total_row_bytes / max(n, 1), 2),
+              "algorithmic_bytes_per_step_per_gpu": step_bytes,
+              "parallelism": f"{world} independent shard(s), no collective"}
+    if args.total_rows is not None:
+        config["total_rows"] = args.total_rows
+        if args.workload == "struct100" and args.total_rows == 100_000_000:
+            config["workload"] = "Struct-100 encode+decode, 100M rows sharded over the GPUs " \
+                                 "(configs[4])"
     line = {
         "metric": METRIC,
-        "value": round(step_bytes * world * args.steps / dt_max / 1e9, 2),
+        "value": round(all_bytes * args.steps / dt_max / 1e9, 2),
         "unit": "GB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt_max * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "int64" if args.workload == "struct100" else "u8",
-        "data": "synthetic (random 64-bit patterns in HBM; no dataset)",
-        "config": {"workload": {"struct100": "Struct-100 encode+decode (configs[1])",
-                                "mixed": "mixed int32/int64/double + 3 utf8 + nulls (configs[2])",
-                                "nested": "id/score + list<int64> (configs[3])"}[args.workload],
-                   "rows_per_gpu": n, "row_bytes": enc.schema().fixed_size if offs is None
-                   else round(total_row_bytes / n, 2),
-                   "algorithmic_bytes_per_step_per_gpu": step_bytes,
-                   "parallelism": f"{world} independent shard(s), no collective"},
+        "data": data,
+        "config": config,
         # row bytes per second beside the algorithmic bytes (information only)
-        "rows": {"rows_per_s": round(n * world * args.steps / dt_max, 1),
-                 "row_GBps": round(2 * total_row_bytes * world * args.steps / dt_max / 1e9, 2),
+        "rows": {"rows_per_s": round(all_rows * args.steps / dt_max, 1),
+                 "row_GBps": round(2 * all_row_bytes * args.steps / dt_max / 1e9, 2),
                  "what": "rows encoded+decoded per second; row bytes written+read per second"},
         "roofline": {"bound": "hbm", "kernel": dominant[0], "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -263,7 +328,8 @@ def main():
     if e2e is not None:
         line["e2e_pcie"] = e2e
     if world == 1 and not args.no_cpu_baseline:     # the CPU baseline is an N=1 figure
-        line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds)
+        line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds,
+                                            args.cpu_rows or n)
     print(json.dumps(line), flush=True)
     orch.close()
 

@@ -432,7 +432,11 @@ int fury_row_decode_host(const fury_schema* s, const void* rows, const int64_t* 
                          int64_t nrows, fury_column* columns, int32_t device) {
   if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
   if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
-  if (nrows == 0) return FURY_OK;
+  if (nrows == 0) {            // an empty batch still yields valid Arrow offsets (offsets[0] = 0)
+    for (int k = 0; columns && k < s->num_fields; k++)
+      if (columns[k].offsets) columns[k].offsets[0] = 0;
+    return FURY_OK;
+  }
   if (!rows || (s->num_fields > 0 && !columns))
     return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/columns is null");
   if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);

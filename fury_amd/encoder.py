@@ -16,6 +16,7 @@ Errors raise the Python counterparts of the reference's exceptions (see ``errors
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import struct
 from dataclasses import dataclass
@@ -203,6 +204,13 @@ def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
     return s.cuda_stream
 
 
+def _on(stream: Optional[torch.cuda.Stream]):
+    """Makes ``stream`` torch's current stream for the body: output allocations belong to it (the
+    caching allocator does not hand them to other streams while the kernels run) and host reads
+    (``.item()``, ``.cpu()``) wait for the kernels launched on it."""
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+
+
 def column_to_device(c: Column, device) -> Column:
     def t(a):
         if a is None:
@@ -264,7 +272,8 @@ class RowEncoder:
         """Row offsets (int64[nrows+1], device) for variable-length schemas; None if fixed."""
         if self._schema.is_fixed:
             return None
-        offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
+        with _on(stream):
+            offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
         keep: list = []
         _check(N.lib().fury_row_measure(self._schema.handle, _c_columns(columns, keep), nrows,
                                         offs.data_ptr(), _stream_handle(stream)))
@@ -294,11 +303,12 @@ class RowEncoder:
 
     def encode_batch(self, columns: Sequence[Column], nrows: int, stream=None) -> RowBatch:
         offs = self.measure(columns, nrows, stream)
-        if offs is None:
-            total = nrows * self._schema.fixed_size
-        else:
-            total = int(offs[nrows].item())
-        rows = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
+        with _on(stream):
+            if offs is None:
+                total = nrows * self._schema.fixed_size
+            else:
+                total = int(offs[nrows].item())
+            rows = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
         self.encode_into(columns, nrows, rows, offs, stream)
         return RowBatch(rows[:total] if total else rows[:0], offs, nrows, self.schema_hash)
 
@@ -356,9 +366,10 @@ class RowEncoder:
         try:
             order = _bfs(self._schema.fields)
             cols: List[Column] = []
-            for i, (f, first) in enumerate(order):
-                cols.append(_alloc_node(f, int(entries[i]), int(nbytes[i]), validity or arrow,
-                                        self.device))
+            with _on(stream):
+                for i, (f, first) in enumerate(order):
+                    cols.append(_alloc_node(f, int(entries[i]), int(nbytes[i]), validity or arrow,
+                                            self.device))
             for i, (f, first) in enumerate(order):
                 if f.children:
                     cols[i].child = [cols[first + j] for j in range(len(f.children))]
@@ -374,35 +385,43 @@ class RowEncoder:
         """Variable-length outputs sized from a bound the rows give (a column's payload bytes and
         list elements <= the batch's row bytes: every byte of them is inside some row), decoded
         in one pass, then trimmed to the real sizes after ONE host read of every column's
-        offsets[n] -- no fury_row_decode_measure pass over the rows."""
+        offsets[n] -- no fury_row_decode_measure pass over the rows.  Rows that break the bound
+        (a slot pointing outside its row) fall back to the exact-size ("measure") decode."""
         n = batch.nrows
-        bound = int(batch.rows.numel())
-        cols = self.alloc_columns(n, validity)
-        for f, c in zip(self._schema.fields, cols):
-            if f.type_id in (STRING, BINARY):
-                c.values = torch.empty(max(bound, 1), dtype=torch.uint8, device=self.device)
-            elif f.type_id == LIST:
-                e = f.children[0]
-                nbytes = (bound + 7) // 8 if e.type_id == BOOL else bound
-                c.child = [Column(
-                    values=torch.empty(nbytes + 8, dtype=torch.uint8, device=self.device),
-                    validity=(torch.zeros((bound + 7) // 8 + 4, dtype=torch.uint8,
-                                          device=self.device) if validity else None))]
+        bound = int(batch.rows.numel() * batch.rows.element_size())
+        with _on(stream):
+            cols = self.alloc_columns(n, validity)
+            for f, c in zip(self._schema.fields, cols):
+                if f.type_id in (STRING, BINARY):
+                    c.values = torch.empty(max(bound, 1), dtype=torch.uint8, device=self.device)
+                elif f.type_id == LIST:
+                    e = f.children[0]
+                    nbytes = (bound + 7) // 8 if e.type_id == BOOL else bound
+                    c.child = [Column(
+                        values=torch.empty(nbytes + 8, dtype=torch.uint8, device=self.device),
+                        validity=(torch.zeros((bound + 7) // 8 + 4, dtype=torch.uint8,
+                                              device=self.device) if validity else None))]
         self.decode_into(batch, cols, stream, arrow)
         var = [(f, c) for f, c in zip(self._schema.fields, cols)
                if f.type_id in (STRING, BINARY, LIST)]
         if not var or n == 0:
             return cols
-        totals = torch.stack([c.offsets[n] for _, c in var]).cpu().tolist()
+        with _on(stream):
+            totals = torch.stack([c.offsets[n] for _, c in var]).cpu().tolist()
         for (f, c), total in zip(var, totals):
             if f.type_id == LIST:
                 e = f.children[0]
                 ch = c.child[0]
                 nbytes = (total + 7) // 8 if e.type_id == BOOL else total * type_width(e.type_id)
+                have = ch.values.numel() - 8
+                if total < 0 or nbytes > have:
+                    return self._decode(batch, validity, arrow, stream, None, "measure")
                 ch.values = ch.values[:nbytes + 8]
                 if ch.validity is not None:
                     ch.validity = ch.validity[:(total + 7) // 8 + 4]
             else:
+                if total < 0 or total > c.values.numel():
+                    return self._decode(batch, validity, arrow, stream, None, "measure")
                 c.values = c.values[:max(total, 1)]
         return cols
 
@@ -415,13 +434,28 @@ class RowEncoder:
         if sizing == "bound" and out is None and not self._schema.is_fixed:
             return self._decode_bound(batch, validity, arrow, stream)
         n = batch.nrows
-        cols = out if out is not None else self.alloc_columns(n, validity)
+        if out is not None:
+            cols = out
+        else:
+            with _on(stream):
+                cols = self.alloc_columns(n, validity)
         keep: list = []
         sh = _stream_handle(stream)
         if not self._schema.is_fixed:
             _check(N.lib().fury_row_decode_measure(self._schema.handle, _ptr(batch.rows),
                                                    _ptr(batch.row_offsets), n,
                                                    _c_columns(cols, keep), sh))
+            self._size_var_outputs(cols, n, validity, stream)
+            keep = []
+        fn = N.lib().fury_rows_to_arrow if arrow else N.lib().fury_row_decode
+        _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), n,
+                  _c_columns(cols, keep), sh))
+        return cols
+
+    def _size_var_outputs(self, cols: List[Column], n: int, validity: bool, stream) -> None:
+        """Allocates the payload / element buffers of the variable-length outputs from the
+        offsets fury_row_decode_measure wrote (host read on ``stream``)."""
+        with _on(stream):
             for f, c in zip(self._schema.fields, cols):
                 if f.type_id in (STRING, BINARY):
                     total = int(c.offsets[n].item()) if n else 0
@@ -434,11 +468,6 @@ class RowEncoder:
                         values=torch.empty(nbytes + 8, dtype=torch.uint8, device=self.device),
                         validity=(torch.zeros((total + 7) // 8 + 4, dtype=torch.uint8,
                                               device=self.device) if validity else None))]
-            keep = []
-        fn = N.lib().fury_rows_to_arrow if arrow else N.lib().fury_row_decode
-        _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), n,
-                  _c_columns(cols, keep), sh))
-        return cols
 
     def decode_into(self, batch: RowBatch, cols: List[Column], stream=None,
                     arrow: bool = False) -> None:
@@ -476,7 +505,10 @@ class RowEncoder:
         """Rows -> columns (generated fromRow semantics).  Variable-length outputs are sized by
         ``sizing``: "measure" (default) runs fury_row_decode_measure first and allocates exactly;
         "bound" allocates each from the batch's row bytes (HBM for speed: no sizing pass over the
-        rows) and trims after one host read."""
+        rows) and trims after one host read.  Memory cost of "bound": the returned columns are
+        views of those row-sized buffers, so while they live every STRING / BINARY / LIST output
+        holds about the batch's row bytes of HBM (K variable-length columns: ~K x row bytes).
+        ``stream``: every kernel, output allocation and host read of the call runs on it."""
         if batch.schema_hash != self.schema_hash:
             raise ClassNotCompatibleException(
                 f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
@@ -548,8 +580,9 @@ class RowEncoder:
         """Java ``encode(MemoryBuffer, T)`` stream for every row: returns (bytes, frame_offsets)."""
         n = batch.nrows
         total = batch.rows.numel() + 12 * n
-        out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
-        fo = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        with _on(stream):
+            out = torch.empty(max(total, 16), dtype=torch.uint8, device=self.device)
+            fo = torch.empty(n + 1, dtype=torch.int64, device=self.device)
         _check(N.lib().fury_frame_rows(self._schema.handle, _ptr(batch.rows),
                                        _ptr(batch.row_offsets), n, _ptr(out), _ptr(fo),
                                        _stream_handle(stream)))
@@ -558,12 +591,15 @@ class RowEncoder:
     def unframe(self, stream_bytes: torch.Tensor, nrows: int, stream=None) -> RowBatch:
         """Parses a ``decode(MemoryBuffer)`` stream; raises ClassNotCompatibleException on a
         schema-hash mismatch."""
-        rows = torch.empty(max(stream_bytes.numel(), 16), dtype=torch.uint8, device=self.device)
-        offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
+        with _on(stream):
+            rows = torch.empty(max(stream_bytes.numel(), 16), dtype=torch.uint8,
+                               device=self.device)
+            offs = torch.empty(nrows + 1, dtype=torch.int64, device=self.device)
         _check(N.lib().fury_unframe_rows(self._schema.handle, _ptr(stream_bytes),
                                          stream_bytes.numel(), nrows, _ptr(rows), _ptr(offs),
                                          _stream_handle(stream)))
-        total = int(offs[nrows].item()) if nrows else 0
+        with _on(stream):
+            total = int(offs[nrows].item()) if nrows else 0
         return RowBatch(rows[:total], None if self._schema.is_fixed else offs, nrows,
                         self.schema_hash)
 

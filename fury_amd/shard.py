@@ -9,8 +9,9 @@ exclusive scan of per-shard byte totals (``global_row_base``).
 from __future__ import annotations
 
 import os
+import socket
 from dataclasses import dataclass
-from typing import List, Tuple
+from typing import Callable, List, Sequence, Tuple
 
 
 @dataclass
@@ -23,6 +24,36 @@ class Rank:
 def from_env() -> Rank:
     return Rank(int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
                 int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker_entry(index: int, world: int, port: int, target: Callable, args: Sequence) -> None:
+    os.environ.update(RANK=str(index), LOCAL_RANK=str(index), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    target(*args)
+
+
+def launch(world: int, target: Callable, args: Sequence = ()) -> None:
+    """Starts `world` worker processes (one per GPU), each with the torch.distributed.run
+    environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), and runs
+    ``target(*args)`` in every one; raises if any worker fails.
+
+    Workers are spawned (fresh interpreters), so the caller must not have initialised the GPU:
+    the parent only waits for its children.  ``bench.py --gpus N`` and the CPU gloo tests go
+    through this same launcher."""
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker_entry, args=(world, free_port(), target, tuple(args)),
+                       nprocs=world, join=True, start_method="spawn")
 
 
 def weak_shard(rows_per_rank: int, rank: int) -> Tuple[int, int]:

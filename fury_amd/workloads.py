@@ -217,6 +217,62 @@ def gen_columns(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
     return [gen_column(f, seed, k, start, n, **knobs) for k, f in enumerate(fields)]
 
 
+def _u64_const(c: int):
+    """A uint64 constant as the int64 with the same bits (torch has no uint64 arithmetic)."""
+    c &= 0xFFFFFFFFFFFFFFFF
+    return c - (1 << 64) if c >= 1 << 63 else c
+
+
+def _t_shr(x, s: int):
+    """Logical right shift of int64 tensors holding uint64 bits."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def _t_splitmix64(x):
+    z = x + _u64_const(0x9E3779B97F4A7C15)
+    z = (z ^ _t_shr(z, 30)) * _u64_const(0xBF58476D1CE4E5B9)
+    z = (z ^ _t_shr(z, 27)) * _u64_const(0x94D049BB133111EB)
+    return z ^ _t_shr(z, 31)
+
+
+def gen_columns_torch(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
+                      start: int = 0, device=None) -> List[Column]:
+    """``gen_columns`` for all-fixed-width, non-null schemas (Struct-100) computed with torch on
+    ``device`` (the GPU for the bench, so 12.5M-row shards need no host copy): the same SplitMix64
+    values keyed by (seed, column, GLOBAL row index), bit for bit."""
+    import torch
+    if _KNOBS.get(name, {}).get("null_pct", 10) != 0:
+        raise ValueError(f"{name}: the torch generator covers non-null schemas only")
+    rows = torch.arange(start, start + n, dtype=torch.int64, device=device)
+    out = []
+    for col, f in enumerate(fields):
+        k = (seed * 0x9E3779B97F4A7C15 + (col + 1) * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+        h = _t_splitmix64(rows ^ _u64_const(k))
+        t = f.type_id
+        if t == FLOAT64:
+            v = _t_shr(h, 11).to(torch.float64) * (1.0 / (1 << 53))
+        elif t == FLOAT32:
+            v = _t_shr(h, 40).to(torch.float32) * (1.0 / (1 << 24))
+        elif t in (INT64, TIMESTAMP):
+            v = h
+        elif t in (INT32, DATE32):
+            v = _t_trunc(h, 32, torch.int32)
+        elif t == INT16:
+            v = _t_trunc(h, 16, torch.int16)
+        elif t == INT8:
+            v = _t_trunc(h, 8, torch.int8)
+        else:
+            raise ValueError(f"{name}: no torch generator for type {t}")
+        out.append(Column(values=v.contiguous()))
+    return out
+
+
+def _t_trunc(h, bits: int, dtype):
+    """Two's-complement truncation of int64 bits to a narrower signed type (numpy astype)."""
+    low = h & ((1 << bits) - 1)
+    return (low - ((low >> (bits - 1)) << bits)).to(dtype)
+
+
 def algorithmic_bytes_fixed(fields: Sequence[Field], nrows: int) -> dict:
     """SURVEY §8(d) / BASELINE.md §4 accounting for fixed-width schemas: encode reads the value
     columns and writes rows; decode the reverse."""

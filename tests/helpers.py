@@ -53,6 +53,11 @@ def assert_columns_equal(fields: Sequence[Field], got, want, n: int, path: str =
             assert_columns_equal(f.children, g.child, w.child, int(wo[n]), p + ".")
         elif t == STRUCT:
             assert_columns_equal(f.children, g.child, w.child, n, p + ".")
+        elif t == MAP:
+            go = as_u8(g.offsets).view(np.int32)[:n + 1]
+            wo = as_u8(w.offsets).view(np.int32)[:n + 1]
+            assert np.array_equal(go, wo), f"{p}: map offsets"
+            assert_columns_equal(f.children, g.child, w.child, int(wo[n]), p + ".")
         else:
             raise ValueError(t)
 

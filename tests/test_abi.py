@@ -169,3 +169,21 @@ def test_new_entry_points_reject_bad_arguments_without_touching_gpu():
     assert L.fury_set_tuning(b"no_such_knob", 0) == 1
     assert L.fury_get_tuning(b"no_such_knob") == -1
     assert L.fury_get_tuning(b"fixed_variant") == 54
+
+
+def test_host_decode_empty_batch_writes_arrow_offsets():
+    """fury_row_decode_host with nrows = 0 (the JNI path) leaves valid Arrow offsets
+    (offsets[0] = 0) in every top-level column that has an offsets buffer, like the device
+    decode; it touches no GPU."""
+    import numpy as np
+    from fury_amd import _native as N
+    from fury_amd.encoder import Schema
+    L = N.lib()
+    m = Schema(SCHEMAS["mixed"])
+    cols = (N.FuryColumn * 6)()
+    offs = [np.full(4, 77, np.int32) for _ in range(6)]
+    for k in range(3, 6):                      # s1..s3: STRING
+        cols[k].offsets = offs[k].ctypes.data
+    assert L.fury_row_decode_host(m.handle, None, None, 0, cols, 0) == 0
+    for k in range(3, 6):
+        assert offs[k][0] == 0 and offs[k][1] == 77

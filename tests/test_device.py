@@ -650,3 +650,192 @@ def test_decode_bound_sizing_matches_oracle(oracle, dev, name, n, knobs):
             assert a.values.numel() == b.values.numel()
     with pytest.raises(ValueError):
         enc.decode_batch(batch, sizing="guess")
+
+
+# ---- round 2: wide flat schemas (> 16 fields: the LDS-DMA encode / ticketed decode kernels) ----
+def _wide_fields(ncols):
+    """ncols fields cycling int32 / int64 / double / String / List<Long> / boolean / String,
+    all nullable (boxed Java types), named so Descriptor order = index order."""
+    kinds = [T.INT32, T.INT64, T.FLOAT64, T.STRING, "list", T.BOOL, T.STRING]
+    out = []
+    for i in range(ncols):
+        k = kinds[i % len(kinds)]
+        name = f"f{i:03d}"
+        out.append(T.array_field(name, T.INT64) if k == "list" else T.field(name, k))
+    return out
+
+
+@pytest.mark.parametrize("ncols,n,str_max", [(17, 3001, 40), (33, 2049, 64), (64, 1500, 24),
+                                             (17, 700, 600), (64, 257, 300)])
+def test_wide_var_schemas_bit_exact(oracle, dev, ncols, n, str_max):
+    """17 / 33 / 64-field flat schemas with strings, lists and 10 % nulls (long strings in the
+    str_max = 300 / 600 cases overflow the LDS tiles): encode (measure + encode), encode_measured,
+    decode, rows_to_arrow, and the sizing-pass decode mode — all oracle-exact."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import ArrowWriter, Encoders, column_to_host
+    fields = _wide_fields(ncols)
+    host = gen_columns("wide", fields, n, seed=ncols + n, null_pct=10, str_max=str_max,
+                       list_max=12, list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    cols = _dev_cols(host, dev)
+    rows, offs, total = _encode_measured(enc, cols, n, dev)
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    assert bool((rows[total:] == 0xEE).all())
+    ref = oracle.decode(fields, want, want_offs, n)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
+    old = N.lib().fury_get_tuning(b"var_decode")
+    assert N.lib().fury_set_tuning(b"var_decode", 1) == 0
+    try:
+        dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    finally:
+        N.lib().fury_set_tuning(b"var_decode", old)
+    assert_columns_equal(fields, dec, ref, n)
+    assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
+
+
+def test_wide_var_schema_large_batch(oracle, dev):
+    """A 40-field schema over 300k rows (>1,000 workgroups chained by the ticketed look-back)."""
+    fields = _wide_fields(40)
+    n = 300_000
+    host = gen_columns("wide", fields, n, seed=4, null_pct=10, str_max=20, list_max=6)
+    _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+
+
+# ---- round 2: rows as Java's RowEncoder.encode(obj) writes them (reused buffer) ---------------
+def _nullable_fixed_fields():
+    return [T.field("a", T.INT32), T.field("b", T.INT64), T.field("c", T.FLOAT64),
+            T.field("d", T.BOOL), T.field("e", T.INT16), T.field("f", T.FLOAT32)]
+
+
+@pytest.mark.parametrize("name,n", [("mixed", 3000), ("narrow", 1200), ("beanb", 900),
+                                    ("nullable_fixed", 2000), ("wide33", 800), ("nested_deep", 400)])
+def test_decode_java_encode_rows_with_stale_null_slots(oracle, dev, name, n):
+    """RowEncoder.encode(obj) reuses one buffer (Encoders.java:146,191-198), so a null field's slot
+    keeps the previous row's value (for a string or list: an offset/size that may point past this
+    row).  The device must decode such rows exactly like the reference's fromRow, which never
+    looks at a null field's slot: equal to oracle.decode of the same rows and to the decode of
+    the canonical (toRow) rows."""
+    from fury_amd.encoder import Encoders, RowBatch, column_to_host
+    if name == "nullable_fixed":
+        fields = _nullable_fixed_fields()
+        host = gen_columns("nf", fields, n, seed=n, null_pct=30)
+    elif name == "wide33":
+        fields = _wide_fields(33)
+        host = gen_columns("wide", fields, n, seed=n, null_pct=30, str_max=40)
+    elif name == "nested_deep":
+        from fury_amd.beans import beans_to_columns
+        fields = _nested_fields()
+        host = beans_to_columns(fields, _nested_beans(n, seed=11))
+    else:
+        fields = SCHEMAS[name]
+        host = gen_columns(name, fields, n, seed=n, null_pct=30)
+    canon, offs = oracle.encode(fields, host, n)
+    java, joffs = oracle.encode(fields, host, n, reuse=True)
+    assert np.array_equal(offs, joffs)
+    assert not np.array_equal(canon, java), "the case must contain stale null slots"
+    enc = Encoders.bean(fields, device=dev)
+    rows = torch.from_numpy(java.copy()).to(dev)
+    roffs = None if enc.schema().is_fixed else torch.from_numpy(joffs).to(dev)
+    dec = [column_to_host(c) for c in enc.decode_batch(RowBatch(rows, roffs, n, enc.schema_hash))]
+    want = oracle.decode(fields, java, joffs, n)
+    assert_columns_equal(fields, dec, want, n)
+    assert_columns_equal(fields, dec, oracle.decode(fields, canon, offs, n), n)
+    if not enc.nested:
+        from fury_amd.encoder import ArrowWriter
+        w = ArrowWriter(enc)
+        w.write(RowBatch(rows, roffs, n, enc.schema_hash))
+        assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], want, n)
+
+
+# ---- round 2: explicit side streams, malformed rows under bound sizing ----------------------
+@pytest.mark.parametrize("sizing", ["measure", "bound"])
+def test_side_stream_encode_decode(oracle, dev, sizing):
+    """encode_batch / decode_batch / unframe on a torch.cuda.Stream() that is not the current
+    stream, held back by a spin kernel: output allocations and host reads wait for that stream,
+    so sizes and bytes are still the oracle's."""
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = SCHEMAS["mixed"]
+    n = 20_000
+    host = gen_columns("mixed", fields, n, seed=12)
+    enc = Encoders.bean(fields, device=dev)
+    cols = _dev_cols(host, dev)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    if hasattr(torch.cuda, "_sleep"):
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(50_000_000)
+    batch = enc.encode_batch(cols, n, stream=s)
+    dec = enc.decode_batch(batch, stream=s, sizing=sizing)
+    s.synchronize()
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    assert_columns_equal(fields, [column_to_host(c) for c in dec],
+                         oracle.decode(fields, want, want_offs, n), n)
+
+
+def test_bound_decode_falls_back_on_slot_outside_row(dev):
+    """A string slot whose size runs far past its row (malformed rows) makes the column's payload
+    larger than the row-byte bound: decode_batch(sizing="bound") must not hand back offsets that
+    point past the values buffer -- it re-decodes with exact sizes.  (The bytes read past the row
+    stay inside a zero-padded allocation here.)"""
+    from fury_amd.encoder import Encoders, RowBatch
+    fields = SCHEMAS["mixed"]
+    n = 1000
+    host = gen_columns("mixed", fields, n, seed=2)
+    enc = Encoders.bean(fields, device=dev)
+    b = enc.encode_batch(_dev_cols(host, dev), n)
+    total = b.rows.numel()
+    big = torch.zeros(total + (1 << 20), dtype=torch.uint8, device=dev)
+    big[:total] = b.rows
+    offs = b.row_offsets.cpu().numpy()
+    r = 500
+    row = big[int(offs[r]):int(offs[r + 1])].cpu().numpy().copy()
+    slot_at = 8 + 8 * 3                               # s1's slot (field 3)
+    row[0] &= ~np.uint8(1 << 3)                       # s1 not null
+    rel = 56                                          # start of the var section
+    size = total                                      # runs past the batch's row bytes
+    row[slot_at:slot_at + 8] = np.frombuffer(np.array([(rel << 32) | size], np.uint64).tobytes(),
+                                             np.uint8)
+    big[int(offs[r]):int(offs[r + 1])] = torch.from_numpy(row).to(dev)
+    bad = RowBatch(big[:total], b.row_offsets, n, enc.schema_hash)
+    got = enc.decode_batch(bad, sizing="bound")
+    ref = enc.decode_batch(bad, sizing="measure")
+    torch.cuda.synchronize()
+    need = int(got[3].offsets[n])
+    assert need > total and got[3].values.numel() >= need
+    assert torch.equal(got[3].offsets, ref[3].offsets)
+    assert torch.equal(got[3].values[:need], ref[3].values[:need])
+
+
+def test_c5_shard_size_property(oracle, dev):
+    """C5 per-GPU shard: 12.5M Struct-100 rows (the last of 8 shards of 100M, global rows
+    87.5M..100M, generated in HBM keyed by global row): decode(encode(cols)) == cols, every row
+    bitmap is zero, every row's slots == the interleaved columns (checked in 1M-row chunks), and
+    a sample of rows equals the oracle's encode of the same global rows."""
+    from fury_amd.encoder import Encoders
+    from fury_amd.shard import strong_shard
+    from fury_amd.workloads import gen_columns_torch
+    fields = SCHEMAS["struct100"]
+    start, n = strong_shard(100_000_000, 8, 7)
+    cols = gen_columns_torch("struct100", fields, n, seed=1234, start=start, device=dev)
+    enc = Encoders.bean(fields, device=dev)
+    b = enc.encode_batch(cols, n)
+    r = b.rows.view(n, 816)
+    step = 1_000_000
+    for c0 in range(0, n, step):
+        c1 = min(n, c0 + step)
+        assert int(r[c0:c1, :16].abs().sum()) == 0
+        slots = r[c0:c1, 16:].contiguous().view(torch.int64).view(c1 - c0, 100)
+        assert torch.equal(slots, torch.stack([c.values.view(torch.int64)[c0:c1] for c in cols], 1))
+    dec = enc.decode_batch(b, validity=False)
+    for c, d in zip(cols, dec):
+        assert torch.equal(c.values.view(torch.uint8), d.values)
+    del dec
+    for off in (0, n // 2, n - 300):
+        host = gen_columns("struct100", fields, 300, seed=1234, start=start + off)
+        want, _ = oracle.encode(fields, host, 300)
+        assert np.array_equal(b.rows[off * 816:(off + 300) * 816].cpu().numpy(), want)
