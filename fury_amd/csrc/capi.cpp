@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -20,6 +21,38 @@ int check_hip(int hip_status, const char* what) {
 }
 
 namespace {
+uint32_t* g_err_host = nullptr;     // host view of the device error word
+uint32_t* g_err_dev = nullptr;      // the same word as kernels address it
+std::once_flag g_err_once;
+}  // namespace
+
+uint32_t* device_error_word() {
+  std::call_once(g_err_once, [] {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+      (void)hipHostFree(p);
+      return;
+    }
+    *static_cast<volatile uint32_t*>(p) = 0;
+    g_err_host = static_cast<uint32_t*>(p);
+    g_err_dev = static_cast<uint32_t*>(d);
+  });
+  return g_err_dev;
+}
+
+int take_device_error() {
+  if (!g_err_host) return FURY_OK;
+  volatile uint32_t* w = g_err_host;
+  if (*w == 0) return FURY_OK;
+  *w = 0;
+  return set_error(FURY_ERR_DEVICE,
+                   "an earlier asynchronous launch failed on the device (a decoupled look-back "
+                   "gave up waiting): the outputs of that call are invalid");
+}
+
+namespace {
 
 bool misaligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; }
 
@@ -31,7 +64,7 @@ int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const c
   if (!s->device_ok)
     return set_error(FURY_ERR_UNSUPPORTED,
                      std::string(fn) + ": no device kernel for " + s->device_reason);
-  return FURY_OK;
+  return take_device_error();
 }
 
 int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
@@ -150,6 +183,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   }
   a->nvar = nvar;
   a->tile_rows = encode_tile_rows(*a);
+  a->err = device_error_word();
   // FURY_VAR_DBG selects kernel variants for A/B (bits 512 / 1024 / 2048: all correct).  Bits
   // 1-64 switch phases OFF for timing (scripts/diag_var.py) and leave wrong outputs, so they
   // are honoured only with FURY_DIAGNOSTIC=1.
@@ -458,6 +492,13 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
   if (p->cnt) (void)hipFree(p->cnt);
   delete p;
+}
+
+int fury_device_status(void* stream) {
+  const int st = check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream)),
+                           "hipStreamSynchronize");
+  if (st) return st;
+  return take_device_error();
 }
 
 int fury_set_tuning(const char* key, int32_t value) {

@@ -63,7 +63,15 @@ struct VarArgs {
   int64_t nrows;
   int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
   int32_t dbg;               // DIAGNOSTIC phase-skip bits (FURY_VAR_DBG), 0 in production
+  uint32_t* err;             // host-visible device error word (device_error_word()) or NULL
 };
+
+// Host-visible device error word: host-pinned, mapped memory a kernel sets (system-scope store)
+// when it cannot produce a valid result (a look-back that gave up).  Allocated once per process;
+// NULL if the runtime cannot map host memory.  take_device_error() reads and clears it and sets
+// the thread's last error (FURY_ERR_DEVICE) when it was raised.
+uint32_t* device_error_word();
+int take_device_error();
 
 // Device scratch for scans; grown on demand (hipMalloc outside graph capture only).
 struct Workspace {

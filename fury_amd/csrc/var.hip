@@ -1184,9 +1184,13 @@ constexpr int kDecImg = 24 * 1024;
 __device__ unsigned int g_lookback_timeouts = 0;     // spins abandoned (never expected)
 namespace {
 
-// look_back with a bounded spin: a predecessor that never publishes (only possible if workgroups
-// were not dispatched in launch order) is counted in g_lookback_timeouts instead of hanging.
-__device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q) {
+// look_back with a bounded spin.  Tiles are numbered by a ticket, so every predecessor is running
+// and publishes without waiting on anything: the wait always ends.  The bound is a safety net
+// against hardware faults; a look-back that gives up is counted in g_lookback_timeouts AND raised
+// in the host-visible device error word (`err`), which the next API call / fury_device_status()
+// reports as FURY_ERR_DEVICE -- its outputs are never passed off as valid.
+__device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q,
+                                     uint32_t* err) {
   const int lane = threadIdx.x & 63;
   int64_t excl = 0;
   uint32_t spins = 0;
@@ -1197,7 +1201,10 @@ __device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq
       v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
       if (__ballot((v >> 62) == 0) == 0) break;
       if (++spins > (1u << 24)) {
-        if (lane == 0) atomicAdd(&g_lookback_timeouts, 1u);
+        if (lane == 0) {
+          atomicAdd(&g_lookback_timeouts, 1u);
+          if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         return 0;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -1277,12 +1284,22 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 template <int K, int NT = kThreads>
 __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                            const int64_t* __restrict__ offs,
-                                                           uint64_t* __restrict__ status) {
+                                                           uint64_t* __restrict__ status,
+                                                           uint32_t* __restrict__ ticket) {
   __shared__ __attribute__((aligned(16))) uint64_t oimg[kDecImg / 8 * (NT / kThreads)];
   __shared__ int64_t tmp[NT / 64];
   __shared__ int64_t sbase[K];
+  __shared__ int64_t stile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = blockIdx.x, nb = gridDim.x;
+  // Tiles are numbered in the order workgroups START (a ticket), not by blockIdx: dispatch order
+  // is not guaranteed, and the look-back below only waits on tiles with smaller numbers, which
+  // therefore are already running -- every wait ends.  (FURY_VAR_DBG bit 4096: blockIdx order,
+  // for A/B only.)
+  if (!(a.dbg & 4096)) {
+    if (tid == 0) stile = atomicAdd(ticket, 1u);
+    __syncthreads();
+  }
+  const int64_t b = (a.dbg & 4096) ? static_cast<int64_t>(blockIdx.x) : stile, nb = gridDim.x;
   const int64_t r0 = b * NT;
   const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
@@ -1471,7 +1488,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     for (int k = 0; k < K; k++) {
       if (!is_seq(a.col[k])) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k);
+      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k, a.err);
       if (lane == 0) {
         sbase[k] = pre;
         if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
@@ -2057,21 +2074,23 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     // 0.274 ms) — scripts/ab_var.py.  Mode 0 picks by sequence count, 2 / 3 force 512 / 256.
     const bool wide = g_var_decode == 2 || (g_var_decode == 0 && nseq >= 2);
     const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
-    const size_t wsb = static_cast<size_t>(nbr) * a.ncols * 8;
+    // [ticket][status words: tiles x fields], zeroed per launch
+    const size_t wsb = (static_cast<size_t>(nbr) * a.ncols + 1) * 8;
     uint64_t* ws = nullptr;
     int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+    uint32_t* tk = reinterpret_cast<uint32_t*>(ws);
     if (!st) {
       switch (a.ncols) {
 #define FURY_DREG(KK)                                                                          \
   case KK:                                                                                     \
     if (wide)                                                                                  \
       hipLaunchKernelGGL((decode_var_reg<KK, 512>), dim3(nbr), dim3(512), 0, stream, a, rows,  \
-                         offs, ws);                                                            \
+                         offs, ws + 1, tk);                                                    \
     else                                                                                       \
       hipLaunchKernelGGL(decode_var_reg<KK>, dim3(nb), dim3(kThreads), 0, stream, a, rows,     \
-                         offs, ws);                                                            \
+                         offs, ws + 1, tk);                                                    \
     break;
         FURY_DREG(1) FURY_DREG(2) FURY_DREG(3) FURY_DREG(4) FURY_DREG(5) FURY_DREG(6) FURY_DREG(7)
         FURY_DREG(8) FURY_DREG(9) FURY_DREG(10) FURY_DREG(11) FURY_DREG(12) FURY_DREG(13)

@@ -484,6 +484,7 @@ class RowEncoder:
     def check_capacity(self, cols: List[Column], nrows: int) -> None:
         """Raises CapacityError when a decode into preallocated ``cols`` needed more payload
         (STRING/BINARY bytes, LIST child elements) than the buffers hold (synchronises)."""
+        self.device_status()
         if self._schema.is_fixed or self.nested or nrows == 0:
             return
         for f, c in zip(self._schema.fields, cols):
@@ -513,7 +514,14 @@ class RowEncoder:
             raise ClassNotCompatibleException(
                 f"Schema is not consistent, encoder schema is {self._schema}. self/peer schema "
                 f"hash are {self.schema_hash}/{batch.schema_hash}. Please check writer schema.")
-        return self._decode(batch, validity, False, stream, out, sizing)
+        cols = self._decode(batch, validity, False, stream, out, sizing)
+        self.device_status(stream)
+        return cols
+
+    def device_status(self, stream=None) -> None:
+        """Synchronises ``stream`` and raises FuryDeviceError if an earlier asynchronous call's
+        kernel could not produce a valid result (``fury_device_status``)."""
+        _check(N.lib().fury_device_status(_stream_handle(stream)))
 
     # -- host-memory batch path: the JNI boundary (off-heap buffers in, off-heap buffers out) --
     def encode_host(self, columns: Sequence[Column], nrows: int, rows=None, row_offsets=None,

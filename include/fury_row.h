@@ -210,6 +210,14 @@ int fury_decode_prepare(const fury_schema* schema, const void* rows, const int64
 int fury_decode_execute(fury_decode_plan* plan, fury_column* columns, int32_t arrow, void* stream);
 void fury_decode_plan_destroy(fury_decode_plan* plan);
 
+/* ---- asynchronous device errors (no reference equivalent) ------------------------------- */
+/* Synchronises `stream` and returns FURY_ERR_DEVICE if a kernel of an earlier asynchronous call
+ * (on any stream of this process) could not produce a valid result -- a decoupled look-back of
+ * the variable-length decode that gave up waiting -- and clears that state; FURY_OK otherwise.
+ * Every entry point also reports such a failure (without synchronising) the next time it is
+ * called.  By construction (ticket-ordered tiles) it is never raised on working hardware. */
+int fury_device_status(void* stream);
+
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
 /* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,
  * 8-byte, no-null schemas) is a bit set: bit 0 = pipelined persistent kernel (else one tile per

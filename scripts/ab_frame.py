@@ -37,7 +37,7 @@ def main():
     name = args.workload
     fields = SCHEMAS[name]
     n = args.rows or DEFAULT_ROWS[name]
-    cols = make_device_columns(name, fields, n, 0, 0, dev)
+    cols = make_device_columns(name, fields, n, 0, dev)
     enc = Encoders.bean(fields, device=dev)
     batch = enc.encode_batch(cols, n)
     stream, _ = enc.frame(batch)

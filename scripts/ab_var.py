@@ -33,7 +33,7 @@ def main():
     name = args.workload
     fields = SCHEMAS[name]
     n = args.rows or DEFAULT_ROWS[name]
-    cols = make_device_columns(name, fields, n, 0, 0, dev)
+    cols = make_device_columns(name, fields, n, 0, dev)
     enc = Encoders.bean(fields, device=dev)
     batch = enc.encode_batch(cols, n)
     offs = batch.row_offsets
@@ -59,6 +59,16 @@ def main():
                                enc.decode_into(batch, out), L.fury_set_tuning(b"var_decode", 3)),
         "decode_measure": lambda: L.fury_row_decode_measure(enc._schema.handle, _ptr(rows),
                                                             _ptr(offs), n, ccols, sh),
+        # round 2: tile order by ticket (default) vs blockIdx (4096); the LDS-DMA kernel (1024)
+        "decode_ticket": lambda: (L.fury_set_tuning(b"var_decode", 0), enc.decode_into(batch, out)),
+        "decode_order": lambda: (L.fury_set_tuning(b"var_decode", 0),
+                                 os.environ.__setitem__("FURY_VAR_DBG", "4096"),
+                                 enc.decode_into(batch, out),
+                                 os.environ.__setitem__("FURY_VAR_DBG", "0")),
+        "decode_lds": lambda: (L.fury_set_tuning(b"var_decode", 0),
+                               os.environ.__setitem__("FURY_VAR_DBG", "1024"),
+                               enc.decode_into(batch, out),
+                               os.environ.__setitem__("FURY_VAR_DBG", "0")),
     }
     times = {k: [] for k in legs}
     for _ in range(2):
@@ -84,7 +94,7 @@ def main():
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
                     for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass",
-                              "decode_512")}}
+                              "decode_512", "decode_ticket", "decode_order", "decode_lds")}}
     print(json.dumps(res), flush=True)
 
 

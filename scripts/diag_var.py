@@ -30,7 +30,7 @@ def main():
     dev = torch.device("cuda:0")
     fields = SCHEMAS[args.workload]
     n = args.rows or DEFAULT_ROWS[args.workload]
-    cols = make_device_columns(args.workload, fields, n, 0, 0, dev)
+    cols = make_device_columns(args.workload, fields, n, 0, dev)
     enc = Encoders.bean(fields, device=dev)
     batch = enc.encode_batch(cols, n)
     out = enc.decode_batch(batch)
