@@ -109,15 +109,56 @@ __global__ __launch_bounds__(kThreads) void frame_kernel(const uint8_t* __restri
   }
 }
 
+// ---- stream words at any base alignment ---------------------------------------------------------
+// The stream may start at any byte address (Java's encode(MemoryBuffer, T) frames at the buffer's
+// writerIndex).  Frames are 4-byte aligned RELATIVE to the stream start, so the parse works on
+// stream words (4 B).  A StreamView reads them from the 16-byte aligned buffer around the stream
+// (abase = base rounded down to 16): word j = bytes [off + 4j, off + 4j + 4) of abase, assembled
+// from the two aligned dwords it straddles (a funnel shift; one dword when off % 4 == 0).  Only
+// aligned dwords holding stream bytes are read (and, on the bulk path, whole 16-B chunks holding
+// them), so no access leaves the pages of the stream.
+struct StreamView {
+  const uint32_t* a;     // 16-byte aligned base (dwords)
+  int32_t o4;            // (base & 15) >> 2: dword shift
+  int32_t sh;            // (base & 3) * 8:   bit shift inside a dword
+  int64_t adw;           // aligned dwords readable from a: to the end of the last 16-B chunk
+};
+
+StreamView make_view(const uint8_t* in, int64_t len) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(in);
+  const uintptr_t off = p & 15;
+  StreamView v;
+  v.a = reinterpret_cast<const uint32_t*>(p - off);
+  v.o4 = static_cast<int32_t>(off >> 2);
+  v.sh = static_cast<int32_t>(off & 3) * 8;
+  v.adw = static_cast<int64_t>((off + len + 15) & ~uintptr_t(15)) >> 2;
+  return v;
+}
+
+// Stream word j (j < len / 4).
+__device__ __forceinline__ uint32_t sword(const StreamView& v, int64_t j) {
+  const int64_t q = j + v.o4;
+  const uint32_t lo = v.a[q];
+  return v.sh ? (lo >> v.sh) | (v.a[q + 1] << (32 - v.sh)) : lo;
+}
+
 // ---- sequential walk (reference semantics, fallback) -------------------------------------------
 // Encoders.decode(MemoryBuffer): readInt32 len, readInt64 hash (ClassNotCompatibleException on a
-// mismatch), row = next len - 8 bytes.  One lane.
+// mismatch), row = next len - 8 bytes.  One lane.  Starts at frame i0; for i0 > 0 frames
+// [0, i0) are already in frame_pos / row_offs (the path the parallel repair found) and the walk
+// resumes where frame i0 - 1 ends.
 __global__ void unframe_walk(const uint8_t* __restrict__ in, int64_t len, int64_t n, int64_t hash,
-                             int64_t* __restrict__ frame_pos, int64_t* __restrict__ row_offs,
-                             int32_t* __restrict__ err) {
+                             int64_t i0, int64_t* __restrict__ frame_pos,
+                             int64_t* __restrict__ row_offs, int32_t* __restrict__ err) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int64_t pos = 0, out = 0;
-  for (int64_t i = 0; i < n; i++) {
+  if (i0 > 0) {
+    int32_t l0;
+    memcpy(&l0, in + frame_pos[i0 - 1], 4);
+    pos = frame_pos[i0 - 1] + 4 + l0;
+    out = row_offs[i0 - 1] + (l0 - 8);
+  }
+  for (int64_t i = i0; i < n; i++) {
     if (pos + 12 > len) { *err = 2; return; }
     int32_t l;
     int64_t h;
@@ -131,19 +172,6 @@ __global__ void unframe_walk(const uint8_t* __restrict__ in, int64_t len, int64_
     pos += 4 + l;
   }
   row_offs[n] = out;
-}
-
-__global__ __launch_bounds__(kThreads) void unframe_copy_walked(const uint8_t* __restrict__ in,
-                                                                const int64_t* __restrict__ frame_pos,
-                                                                const int64_t* __restrict__ row_offs,
-                                                                int64_t n, uint8_t* __restrict__ out) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (i >= n) return;
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(in + frame_pos[i] + 12);
-  uint32_t* d = reinterpret_cast<uint32_t*>(out + row_offs[i]);
-  const int64_t words = (row_offs[i + 1] - row_offs[i]) >> 2;
-  for (int64_t w = lane; w < words; w += 64) d[w] = s[w];
 }
 
 // ---- speculative parallel parse -----------------------------------------------------------------
@@ -181,12 +209,11 @@ __device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave: exclusive prefix of workgroup b.  Workgroups are dispatched in blockIdx order, so
-// every predecessor is running or done; the spin is bounded all the same (a ticket atomic per
-// workgroup would serialise the whole launch on one address), and a workgroup that gives up
-// flags the parse as failed, which sends the stream to the sequential walk.
-// kWin predecessors per step; 64 measured faster than 256 (the polling traffic costs more than
-// the shorter chain saves).
+// One wave: exclusive prefix of piece b.  Pieces are numbered by a ticket in the order their
+// workgroups start, so every predecessor is running and the wait ends; the spin is bounded all the
+// same, and a workgroup that gives up flags the parse as failed (the stream is then re-parsed by
+// the walk, so results never depend on it).  kWin predecessors per step; 64 measured faster than
+// 256 (the polling traffic costs more than the shorter chain saves).
 template <int kWin>
 __device__ int64_t look_back(const uint64_t* status, int64_t b, int32_t* err) {
   constexpr int U = kWin / 64;            // predecessors per lane per step
@@ -232,44 +259,75 @@ __device__ int64_t look_back(const uint64_t* status, int64_t b, int32_t* err) {
 // consecutive 8-KB pieces (lane t of round r reads words r * kMarkSpan + 8 t .. + 8: coalesced),
 // so the look-back chain has one link per 64 KB of stream.  Candidates are staged in LDS in
 // stream order (at most kStage per workgroup: real frames are >= 20 B, so only a stream full of
-// false candidates overflows; it is flagged and goes to the walk).  The stream base is 16-byte
-// aligned (checked on the host); status (nb words) and err are zero at launch.
+// false candidates overflows; it is flagged and goes to the walk).  kAligned: the stream base
+// is 16-byte aligned (stream words are aligned dwords); otherwise each lane loads the 16 aligned
+// dwords around its 10 stream words and funnel-shifts them (StreamView).  ticket, status (nb
+// words) and err are zero at launch.
 constexpr int kRounds = 8;
 constexpr int kStage = 4096;
-template <int kWin>
-__global__ __launch_bounds__(kThreads) void unframe_scan(const uint32_t* __restrict__ in,
-                                                         int64_t len, int64_t hash, int64_t n,
+template <int kWin, bool kAligned>
+__global__ __launch_bounds__(kThreads) void unframe_scan(StreamView sv, int64_t len, int64_t hash,
+                                                         int64_t n, uint32_t* __restrict__ ticket,
                                                          uint64_t* __restrict__ status,
                                                          int64_t* __restrict__ cand,
                                                          int32_t* __restrict__ clen,
                                                          int64_t* __restrict__ total,
                                                          int32_t* __restrict__ err) {
   __shared__ int64_t spre;
+  __shared__ int64_t sb;
   __shared__ int32_t spos[kStage];        // candidate word index within the workgroup's span
   __shared__ int32_t slen[kStage];
-  const int64_t b = blockIdx.x;
+  if (threadIdx.x == 0) sb = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const int64_t b = sb;
   const int64_t W = len >> 2;
   const uint32_t hlo = static_cast<uint32_t>(hash);
   const uint32_t hhi = static_cast<uint32_t>(static_cast<uint64_t>(hash) >> 32);
   int tot = 0;                             // candidates staged so far (workgroup-uniform)
   bool overflow = false;
+  using v4u = __attribute__((ext_vector_type(4))) uint32_t;
   // every round's words are loaded before any is tested: 64 KB per workgroup in flight
   uint32_t xs[kRounds][kMarkWords + 2];
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
     const int64_t w0 = b * kRounds * kMarkSpan + r * kMarkSpan + threadIdx.x * kMarkWords;
     uint32_t* x = xs[r];
-    if (w0 + kMarkWords + 2 <= W) {
-      using v4u = __attribute__((ext_vector_type(4))) uint32_t;
-      const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0));
-      const v4u c = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0 + 4));
-      x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
-      x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
-      x[8] = in[w0 + 8];
-      x[9] = in[w0 + 9];
+    if (kAligned) {
+      const uint32_t* in = sv.a;
+      if (w0 + kMarkWords + 2 <= W) {
+        const v4u a = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0));
+        const v4u c = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(in + w0 + 4));
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        x[4] = c.x; x[5] = c.y; x[6] = c.z; x[7] = c.w;
+        x[8] = in[w0 + 8];
+        x[9] = in[w0 + 9];
+      } else {
+#pragma unroll
+        for (int j = 0; j < kMarkWords + 2; j++) x[j] = w0 + j < W ? in[w0 + j] : 0u;
+      }
+    } else if (w0 + 16 <= sv.adw && w0 + kMarkWords + 2 <= W) {
+      uint32_t d[16];                      // aligned dwords w0 .. w0 + 15 (w0 is 16-B aligned)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(sv.a + w0 + 4 * q));
+        d[4 * q] = t.x; d[4 * q + 1] = t.y; d[4 * q + 2] = t.z; d[4 * q + 3] = t.w;
+      }
+      // word w0 + j = dwords o4 + j, o4 + j + 1 (o4 <= 3, j <= 9: index <= 13)
+#pragma unroll
+      for (int j = 0; j < kMarkWords + 2; j++) {
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+          if (o == sv.o4) {
+            lo = d[o + j];
+            hi = d[o + j + 1];
+          }
+        }
+        x[j] = sv.sh ? (lo >> sv.sh) | (hi << (32 - sv.sh)) : lo;
+      }
     } else {
 #pragma unroll
-      for (int j = 0; j < kMarkWords + 2; j++) x[j] = w0 + j < W ? in[w0 + j] : 0u;
+      for (int j = 0; j < kMarkWords + 2; j++) x[j] = w0 + j < W ? sword(sv, w0 + j) : 0u;
     }
   }
   // candidate bits of every round, then ONE packed scan of the per-round counts (4 rounds of
@@ -370,15 +428,95 @@ __global__ __launch_bounds__(kThreads) void unframe_verify(const int64_t* __rest
   if (!ok) atomicOr(err, 4);
 }
 
-// Rows out of a verified stream: each workgroup owns kCopyFrames frames = one contiguous range of
+// ---- parallel repair: the frame chain through the candidates ------------------------------------
+// When the candidates do not verify (a payload that spells a plausible header), the frames are
+// still among them: frame 0 is the candidate at 0 and frame i + 1 the candidate where frame i
+// ends.  succ[k] = the candidate where candidate k ends (-1: none), a forest whose path from
+// candidate 0 is exactly the frame chain Encoders.decode walks (while its headers are valid).
+// Pointer doubling marks that path in log2(candidates) passes: before pass r every node at
+// distance < 2^r from candidate 0 is marked, and pass r marks jump_r(k) = succ^(2^r)(k) of every
+// marked k, so after it every node at distance < 2^(r+1) is (marks only ever spread along succ,
+// so nothing off the path is marked).  The marked candidates in stream order are frames 0, 1, ...
+__global__ __launch_bounds__(kThreads) void repair_succ(const int64_t* __restrict__ cand,
+                                                        const int32_t* __restrict__ clen, int64_t m,
+                                                        int32_t* __restrict__ succ,
+                                                        int64_t* __restrict__ mark) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (k >= m) return;
+  const int64_t e = cand[k] + 4 + clen[k];
+  int64_t found = -1;
+  // the next frame usually is one of the next few candidates; else binary search (cand sorted)
+  for (int64_t j = k + 1; j < m && j <= k + 3; j++) {
+    const int64_t c = cand[j];
+    if (c == e) { found = j; break; }
+    if (c > e) break;
+  }
+  if (found < 0 && k + 4 < m && cand[k + 3] < e) {
+    int64_t lo = k + 4, hi = m - 1;
+    while (lo <= hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      const int64_t c = cand[mid];
+      if (c == e) { found = mid; break; }
+      if (c < e) lo = mid + 1;
+      else hi = mid - 1;
+    }
+  }
+  succ[k] = static_cast<int32_t>(found);
+  mark[k] = (k == 0 && cand[0] == 0) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void repair_double(const int32_t* __restrict__ jump,
+                                                          int32_t* __restrict__ next, int64_t m,
+                                                          int64_t* __restrict__ mark) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (k >= m) return;
+  const int32_t j = jump[k];
+  if (j >= 0) {
+    if (mark[k]) mark[j] = 1;
+    next[k] = jump[j];
+  } else {
+    next[k] = -1;
+  }
+}
+
+// rank = exclusive scan of the marks (count = their total): frame rank of every marked candidate.
+__global__ __launch_bounds__(kThreads) void repair_gather(const int64_t* __restrict__ cand,
+                                                          const int64_t* __restrict__ rank,
+                                                          const int64_t* __restrict__ count,
+                                                          int64_t m, int64_t n,
+                                                          int64_t* __restrict__ frame_pos) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (k >= m) return;
+  const int64_t r = rank[k];
+  const int64_t nx = k + 1 < m ? rank[k + 1] : *count;
+  if (nx > r && r < n) frame_pos[r] = cand[k];
+}
+
+// Row offsets of frames [0, L) (L = min(path length, n)) and, when the path covers all n frames,
+// row_offs[n].
+__global__ __launch_bounds__(kThreads) void repair_offsets(const uint8_t* __restrict__ in,
+                                                           const int64_t* __restrict__ frame_pos,
+                                                           int64_t L, int64_t n,
+                                                           int64_t* __restrict__ row_offs) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= L) return;
+  row_offs[i] = frame_pos[i] - 12 * i;
+  if (i == n - 1) {
+    int32_t l;
+    memcpy(&l, in + frame_pos[i], 4);
+    row_offs[n] = frame_pos[i] + 4 + l - 12 * n;
+  }
+}
+
+// Rows out of a parsed stream: each workgroup owns kCopyFrames frames = one contiguous range of
 // the row buffer, written in 16-byte aligned chunks (a lane finds its chunk's frame by binary
-// search over the range's row offsets in LDS and reads the 4-byte aligned stream words).
-__global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restrict__ in,
+// search over the range's row offsets in LDS and reads the frame's stream words through the view).
+__global__ __launch_bounds__(kThreads) void unframe_copy(StreamView sv,
                                                          const int64_t* __restrict__ cand,
                                                          const int64_t* __restrict__ row_offs,
                                                          int64_t n, uint8_t* __restrict__ out,
                                                          const int32_t* __restrict__ err) {
-  if (*err) return;                  // speculation failed: the sequential walk takes over
+  if (err && *err) return;           // speculation failed: the repair / walk takes over
   __shared__ int64_t ro[kCopyFrames + 1];
   __shared__ int64_t src[kCopyFrames];
   const int64_t k0 = static_cast<int64_t>(blockIdx.x) * kCopyFrames;
@@ -400,7 +538,7 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
   // row-buffer dword at d (rows are whole 8-byte words, so a dword never straddles two rows)
   auto dword_at = [&](int64_t d, int& f) -> uint32_t {
     while (f + 1 < kn && ro[f + 1] <= d) f++;
-    return *reinterpret_cast<const uint32_t*>(in + src[f] + (d - ro[f]));
+    return sword(sv, (src[f] + (d - ro[f])) >> 2);
   };
   // 16-byte aligned chunks of the row buffer (non-temporal stores), dwords at the two ends
   const int64_t S = ro[0], E = ro[kn];
@@ -428,31 +566,24 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(const uint8_t* __restri
   }
 }
 
-std::atomic<int64_t> g_unframe_walks{0};   // streams parsed by the sequential walk
+std::atomic<int64_t> g_unframe_walks{0};     // streams parsed (partly) by the sequential walk
+std::atomic<int64_t> g_unframe_repairs{0};   // streams parsed by the parallel repair
 int g_unframe_mode = 0;   // tuning "unframe": 0 speculative, 1 always walk
 
-int unframe_walked(const uint8_t* in, int64_t len, int64_t n, int64_t hash, uint8_t* rows_out,
-                   int64_t* row_offs, hipStream_t stream) {
-  g_unframe_walks.fetch_add(1);
-  int64_t* fp = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&fp), n * 8 + 8, stream),
-                     "hipMallocAsync");
-  if (st) return st;
-  int32_t* err = reinterpret_cast<int32_t*>(fp + n);
-  (void)hipMemsetAsync(err, 0, 4, stream);
-  hipLaunchKernelGGL(unframe_walk, dim3(1), dim3(64), 0, stream, in, len, n, hash, fp, row_offs,
-                     err);
-  int32_t herr = 0;
-  (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
-  st = check_hip(hipStreamSynchronize(stream), "unframe sync");
-  if (!st && herr == 0 && n > 0) {
-    const int64_t blocks = (n + (kThreads / 64) - 1) / (kThreads / 64);
-    hipLaunchKernelGGL(unframe_copy_walked, dim3(blocks), dim3(kThreads), 0, stream, in, fp,
-                       row_offs, n, rows_out);
-    st = check_hip(hipGetLastError(), "unframe copy launch");
+struct DevBuf {                               // stream-ordered scratch freed on every exit
+  void* p = nullptr;
+  hipStream_t s;
+  explicit DevBuf(hipStream_t st) : s(st) {}
+  ~DevBuf() {
+    if (p) (void)hipFreeAsync(p, s);
   }
-  (void)hipFreeAsync(fp, stream);
-  if (st) return st;
+  int alloc(int64_t bytes) {
+    return check_hip(hipMallocAsync(&p, static_cast<size_t>(bytes < 16 ? 16 : bytes), s),
+                     "hipMallocAsync");
+  }
+};
+
+int walk_status(int32_t herr, int64_t hash) {
   if (herr == 1)
     return set_error(FURY_ERR_CLASS_NOT_COMPATIBLE,
                      "Schema is not consistent: peer schema hash differs from " +
@@ -461,11 +592,111 @@ int unframe_walked(const uint8_t* in, int64_t len, int64_t n, int64_t hash, uint
   return FURY_OK;
 }
 
+// Frames [i0, n) by the sequential walk (frames [0, i0) already in fp / row_offs), then the copy.
+int unframe_walked(const uint8_t* in, int64_t len, int64_t n, int64_t hash, int64_t i0,
+                   int64_t* fp, uint8_t* rows_out, int64_t* row_offs, hipStream_t stream) {
+  g_unframe_walks.fetch_add(1);
+  DevBuf eb(stream);
+  int st = eb.alloc(8);
+  if (st) return st;
+  int32_t* err = static_cast<int32_t*>(eb.p);
+  (void)hipMemsetAsync(err, 0, 4, stream);
+  hipLaunchKernelGGL(unframe_walk, dim3(1), dim3(64), 0, stream, in, len, n, hash, i0, fp,
+                     row_offs, err);
+  int32_t herr = 0;
+  (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
+  st = check_hip(hipStreamSynchronize(stream), "unframe sync");
+  if (st) return st;
+  if (herr) return walk_status(herr, hash);
+  const int64_t cb = (n + kCopyFrames - 1) / kCopyFrames;
+  hipLaunchKernelGGL(unframe_copy, dim3(cb), dim3(kThreads), 0, stream, make_view(in, len), fp,
+                     row_offs, n, rows_out, nullptr);
+  return check_hip(hipGetLastError(), "unframe copy launch");
+}
+
+int64_t scan_blocks(int64_t len) {
+  return ((len >> 2) + kRounds * kMarkSpan - 1) / (kRounds * kMarkSpan);
+}
+
+// Launches the candidate scan over the whole stream: the first `want` candidates to cand / clen,
+// the count of all of them to *total.  ws: ticket + status (scan_blocks + 1 words), zeroed here.
+void launch_scan(const uint8_t* in, int64_t len, int64_t hash, int64_t want, uint64_t* ws,
+                 int64_t* cand, int32_t* clen, int64_t* total, int32_t* err, hipStream_t stream) {
+  const int64_t nb = scan_blocks(len);
+  (void)hipMemsetAsync(ws, 0, (nb + 1) * 8, stream);
+  const StreamView sv = make_view(in, len);
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(ws);
+  if ((reinterpret_cast<uintptr_t>(in) & 15) == 0)
+    hipLaunchKernelGGL((unframe_scan<64, true>), dim3(nb), dim3(kThreads), 0, stream, sv, len,
+                       hash, want, ticket, ws + 1, cand, clen, total, err);
+  else
+    hipLaunchKernelGGL((unframe_scan<64, false>), dim3(nb), dim3(kThreads), 0, stream, sv, len,
+                       hash, want, ticket, ws + 1, cand, clen, total, err);
+}
+
+// The candidates did not verify: find the frame chain among ALL candidates in parallel
+// (pointer doubling), fall back to the walk only for what the chain does not cover (a frame the
+// candidate test rejects: the error Encoders.decode reports, or a length that is not a multiple
+// of 8, which Java never writes).
+int unframe_repair(const uint8_t* in, int64_t len, int64_t n, int64_t hash, int64_t m,
+                   int64_t* fp, uint8_t* rows_out, int64_t* row_offs, hipStream_t stream) {
+  if (m <= 0 || m > 0x7fffffffLL)
+    return unframe_walked(in, len, n, hash, 0, fp, rows_out, row_offs, stream);
+  g_unframe_repairs.fetch_add(1);
+  const int64_t nb = scan_blocks(len);
+  // [cand m][mark m][scan ws][ticket+status nb+1][total][err][clen m][jump m][next m]
+  const int64_t sw = scan_workspace(m);
+  const int64_t w64 = m + m + sw + (nb + 1) + 2;
+  DevBuf buf(stream);
+  int st = buf.alloc(w64 * 8 + 3 * m * 4 + 64);
+  if (st) return st;
+  int64_t* cand = static_cast<int64_t*>(buf.p);
+  int64_t* mark = cand + m;
+  int64_t* sws = mark + m;
+  uint64_t* ws = reinterpret_cast<uint64_t*>(sws + sw);
+  int64_t* total = reinterpret_cast<int64_t*>(ws + nb + 1);
+  int32_t* err = reinterpret_cast<int32_t*>(total + 1);
+  int32_t* clen = reinterpret_cast<int32_t*>(cand + w64);
+  int32_t* jump = clen + m;
+  int32_t* next = jump + m;
+  (void)hipMemsetAsync(err, 0, 8, stream);
+  launch_scan(in, len, hash, m, ws, cand, clen, total, err, stream);
+  const int64_t g = (m + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(repair_succ, dim3(g), dim3(kThreads), 0, stream, cand, clen, m, jump, mark);
+  for (int64_t span = 1; span < m; span <<= 1) {
+    hipLaunchKernelGGL(repair_double, dim3(g), dim3(kThreads), 0, stream, jump, next, m, mark);
+    int32_t* t = jump;
+    jump = next;
+    next = t;
+  }
+  int64_t path = 0;                               // marked candidates = frames on the chain
+  device_scan(mark, m, total, sws, stream);
+  int32_t herr = 0;
+  (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
+  (void)hipMemcpyAsync(&path, total, 8, hipMemcpyDeviceToHost, stream);
+  if ((st = check_hip(hipGetLastError(), "unframe repair launch"))) return st;
+  if ((st = check_hip(hipStreamSynchronize(stream), "unframe repair sync"))) return st;
+  if (herr) return unframe_walked(in, len, n, hash, 0, fp, rows_out, row_offs, stream);
+  hipLaunchKernelGGL(repair_gather, dim3(g), dim3(kThreads), 0, stream, cand, mark, total, m, n,
+                     fp);
+  const int64_t L = path < n ? path : n;
+  if (L > 0)
+    hipLaunchKernelGGL(repair_offsets, dim3((L + kThreads - 1) / kThreads), dim3(kThreads), 0,
+                       stream, in, fp, L, n, row_offs);
+  if ((st = check_hip(hipGetLastError(), "unframe repair launch"))) return st;
+  if (L < n) return unframe_walked(in, len, n, hash, L, fp, rows_out, row_offs, stream);
+  const int64_t cb = (n + kCopyFrames - 1) / kCopyFrames;
+  hipLaunchKernelGGL(unframe_copy, dim3(cb), dim3(kThreads), 0, stream, make_view(in, len), fp,
+                     row_offs, n, rows_out, nullptr);
+  return check_hip(hipGetLastError(), "unframe copy launch");
+}
+
 }  // namespace
 
 int unframe_mode() { return g_unframe_mode; }
 void set_unframe_mode(int v) { g_unframe_mode = v; }
 int64_t unframe_walk_count() { return g_unframe_walks.load(); }
+int64_t unframe_repair_count() { return g_unframe_repairs.load(); }
 
 int launch_frame_rows(const uint8_t* rows, const int64_t* offs, int64_t n, int64_t fixed,
                       int64_t hash, uint8_t* out, int64_t* fo, hipStream_t stream) {
@@ -476,45 +707,50 @@ int launch_frame_rows(const uint8_t* rows, const int64_t* offs, int64_t n, int64
   return check_hip(hipGetLastError(), "frame launch");
 }
 
+// Any base alignment: the scan reads stream words through a StreamView.  A stream that does not
+// verify is repaired in parallel (unframe_repair); the sequential walk only parses what the
+// repair cannot (error reporting).
 int launch_unframe_rows(const uint8_t* in, int64_t len, int64_t n, int64_t hash, uint8_t* rows_out,
                         int64_t* row_offs, hipStream_t stream) {
-  const bool aligned = (reinterpret_cast<uintptr_t>(in) & 15) == 0;
-  if (n == 0 || len < 12 || !aligned || g_unframe_mode == 1)
-    return unframe_walked(in, len, n, hash, rows_out, row_offs, stream);
-  const int64_t W = len >> 2;
-  const int64_t nb = (W + kRounds * kMarkSpan - 1) / (kRounds * kMarkSpan);
-  if (nb > 0x7fffffff) return set_error(FURY_ERR_INVALID_ARGUMENT, "stream too large");
-  // workspace: [cand n][status nb][total][err (8 B)][clen n x 4 B]
-  const int64_t words = n + nb + 2;
-  uint8_t* buf = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&buf), words * 8 + n * 4, stream),
-                     "hipMallocAsync");
+  if (n == 0) return check_hip(hipMemsetAsync(row_offs, 0, 8, stream), "memset");
+  DevBuf fpb(stream);
+  int st = fpb.alloc(n * 8);
   if (st) return st;
-  int64_t* cand = reinterpret_cast<int64_t*>(buf);
-  uint64_t* status = reinterpret_cast<uint64_t*>(cand + n);
-  int64_t* total = reinterpret_cast<int64_t*>(status + nb);
+  int64_t* fp = static_cast<int64_t*>(fpb.p);       // frame positions
+  if (len < 12 || g_unframe_mode == 1)
+    return unframe_walked(in, len, n, hash, 0, fp, rows_out, row_offs, stream);
+  const int64_t nb = scan_blocks(len);
+  if (nb > 0x7fffffff) return set_error(FURY_ERR_INVALID_ARGUMENT, "stream too large");
+  // workspace: [ticket + status (nb + 1)][total][err (8 B)][clen n x 4 B]
+  const int64_t words = nb + 1 + 2;
+  DevBuf buf(stream);
+  if ((st = buf.alloc(words * 8 + n * 4))) return st;
+  uint64_t* ws = static_cast<uint64_t*>(buf.p);
+  int64_t* total = reinterpret_cast<int64_t*>(ws + nb + 1);
   int32_t* err = reinterpret_cast<int32_t*>(total + 1);
-  int32_t* clen = reinterpret_cast<int32_t*>(buf + words * 8);
-  (void)hipMemsetAsync(status, 0, (nb + 2) * 8, stream);
-  hipLaunchKernelGGL(unframe_scan<64>, dim3(nb),
-                     dim3(kThreads), 0, stream,
-                     reinterpret_cast<const uint32_t*>(in), len, hash, n, status, cand, clen,
-                     total, err);
+  int32_t* clen = reinterpret_cast<int32_t*>(ws + words);
+  (void)hipMemsetAsync(total, 0, 16, stream);
+  launch_scan(in, len, hash, n, ws, fp, clen, total, err, stream);
   const int64_t vb = (n + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(unframe_verify, dim3(vb), dim3(kThreads), 0, stream, cand, clen, total, n,
+  hipLaunchKernelGGL(unframe_verify, dim3(vb), dim3(kThreads), 0, stream, fp, clen, total, n,
                      row_offs, err);
   const int64_t cb = (n + kCopyFrames - 1) / kCopyFrames;
-  hipLaunchKernelGGL(unframe_copy, dim3(cb), dim3(kThreads), 0, stream, in, cand, row_offs, n,
-                     rows_out, err);
+  hipLaunchKernelGGL(unframe_copy, dim3(cb), dim3(kThreads), 0, stream, make_view(in, len), fp,
+                     row_offs, n, rows_out, err);
   st = check_hip(hipGetLastError(), "unframe launch");
   int32_t herr = 0;
-  if (!st) (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
-  (void)hipFreeAsync(buf, stream);
+  int64_t m = 0;
+  if (!st) {
+    (void)hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, stream);
+    (void)hipMemcpyAsync(&m, total, 8, hipMemcpyDeviceToHost, stream);
+  }
   const int st2 = check_hip(hipStreamSynchronize(stream), "unframe sync");
   if (st) return st;
   if (st2) return st2;
   if (herr == 0) return FURY_OK;
-  return unframe_walked(in, len, n, hash, rows_out, row_offs, stream);
+  if (herr & (8 | 16))            // a look-back gave up / too many candidates in a piece
+    return unframe_walked(in, len, n, hash, 0, fp, rows_out, row_offs, stream);
+  return unframe_repair(in, len, n, hash, m, fp, rows_out, row_offs, stream);
 }
 
 }  // namespace fury

@@ -228,8 +228,11 @@ int fury_device_status(void* stream);
  * (tile + nt loads/stores + pair-mode deep decode).
  * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
  * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles.
- * Key "unframe": 0 speculative parallel stream parse (sequential walk when it does not verify),
- * 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk parsed.
+ * Key "unframe": 0 speculative parallel stream parse (a stream that does not verify -- a payload
+ * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
+ * errors), 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk
+ * parsed (wholly or from the first frame the repair could not place), "unframe_repairs" =
+ * streams the parallel repair parsed.
  * fury_get_tuning("lookback_timeouts") = decoupled look-backs of the variable-length decode that
  * gave up waiting (must stay 0; synchronous device read). */
 int fury_set_tuning(const char* key, int32_t value);
@@ -241,9 +244,11 @@ int32_t fury_get_tuning(const char* key);
  * receives where each frame starts; frame i starts at row_offsets[i] + 12 * i. */
 int fury_frame_rows(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, void* out, int64_t* frame_offsets, void* stream);
-/* Parses such a stream back (sequential frame walk on device): writes row_offsets[0..nrows]
- * into a packed copy `rows_out` and checks every schemaHash; a mismatch returns
- * FURY_ERR_CLASS_NOT_COMPATIBLE.  Synchronises `stream`. */
+/* Parses such a stream back (RowEncoder.decode(MemoryBuffer) nrows times): writes
+ * row_offsets[0..nrows] and the rows packed into `rows_out`, checking every schemaHash; a
+ * mismatch returns FURY_ERR_CLASS_NOT_COMPATIBLE, a frame past the end FURY_ERR_OUT_OF_BOUNDS.
+ * `stream_bytes` may start at any byte address.  Parallel on the device (speculative header scan
+ * + verify, parallel repair when a payload spells a header).  Synchronises `stream`. */
 int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64_t stream_len,
                       int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream);
 

@@ -53,10 +53,34 @@ def main():
     aw.write(batch)
     dcols = aw.finish()
     ipc_len = ipc_record_batch_message(enc, dcols, n).numel()
+    # round 2: the same stream at a 1-byte offset (Java frames at any writerIndex), and a stream
+    # whose payloads spell a plausible header every ~100 frames (parallel repair, no walk)
+    shifted_buf = torch.empty(stream.numel() + 64, dtype=torch.uint8, device=dev)
+    shifted_buf[1:1 + stream.numel()] = stream
+    shifted = shifted_buf[1:1 + stream.numel()]
+    assert torch.equal(enc.unframe(shifted, n).rows, batch.rows), "unframe at offset 1"
+    fake = stream.clone()
+    if batch.row_offsets is not None:
+        fo = (batch.row_offsets[:-1] + 12 * torch.arange(n, device=dev))
+    else:
+        fo = torch.arange(n, device=dev, dtype=torch.int64) * (batch.rows.numel() // n + 12)
+    pick = fo[3::97] + 12 + 16                      # 8-byte slot 1 of every 97th row
+    hdr = torch.tensor(list((24).to_bytes(4, "little")) +
+                       list((enc.schema_hash & (2**64 - 1)).to_bytes(8, "little")),
+                       dtype=torch.uint8, device=dev)
+    for j in range(12):
+        fake[pick + j] = hdr[j]
+    rep0 = N.lib().fury_get_tuning(b"unframe_repairs")
+    fr = enc.unframe(fake, n)
+    assert N.lib().fury_get_tuning(b"unframe_repairs") == rep0 + 1, "fake headers not repaired"
+    fake_rows = fr.rows.clone()
     legs = {
         "ipc": (lambda: ipc_record_batch_message(enc, dcols, n), 2 * ipc_len),
         "frame": (lambda: enc.frame(batch), row_bytes + offs_bytes + stream.numel() + 8 * (n + 1)),
         "unframe": (lambda: enc.unframe(stream, n), stream.numel() + row_bytes + 8 * (n + 1)),
+        "unframe_offset1": (lambda: enc.unframe(shifted, n),
+                            stream.numel() + row_bytes + 8 * (n + 1)),
+        "unframe_repair": (lambda: enc.unframe(fake, n), stream.numel() + row_bytes + 8 * (n + 1)),
     }
     res = {k: [] for k in legs}
     res["unframe_walk"] = []
@@ -78,6 +102,7 @@ def main():
         torch.cuda.synchronize()
         N.lib().fury_set_tuning(b"unframe", 0)
         res["unframe_walk"].append(e0.elapsed_time(e1))
+    assert torch.equal(enc.unframe(fake, n).rows, fake_rows)
     walks = N.lib().fury_get_tuning(b"unframe_walks") - walks0
     assert walks == args.rounds, f"speculative parse fell back {walks - args.rounds} times"
     ms = {k: round(statistics.median(v), 4) for k, v in res.items()}

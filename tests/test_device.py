@@ -269,9 +269,15 @@ def test_stream_encode_decode(oracle, dev, name, n):
     assert_columns_equal(fields, dec, oracle.decode(fields, rows, offs, n), n)
 
 
+def _repairs():
+    from fury_amd import _native as N
+    return N.lib().fury_get_tuning(b"unframe_repairs")
+
+
 def test_unframe_fake_header_in_payload(oracle, dev):
     """A row whose slots spell a plausible frame header ([len 16][schema hash]) is a false
-    candidate: verification fails, the walk re-parses, results are still the oracle's."""
+    candidate: verification fails and the parallel repair (pointer doubling over the candidates)
+    finds the real frame chain -- no sequential walk; results are still the oracle's."""
     from fury_amd.encoder import Encoders
     fields = SCHEMAS["struct100"]
     n = 600
@@ -284,29 +290,95 @@ def test_unframe_fake_header_in_payload(oracle, dev):
         f0[r] = np.uint64(16 | ((h & 0xFFFFFFFF) << 32))
         f1[r] = np.uint64(h >> 32)
     stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
-    w0 = _walks()
+    w0, r0 = _walks(), _repairs()
     got = enc.unframe(stream, n)
-    assert _walks() == w0 + 1, "fake headers must send the stream to the sequential walk"
+    assert _walks() == w0, "fake headers are repaired in parallel, not walked"
+    assert _repairs() == r0 + 1
     rows, _ = oracle.encode(fields, host, n)
     assert np.array_equal(got.rows.cpu().numpy(), rows)
 
 
-def test_unframe_unaligned_and_truncated(oracle, dev):
-    from fury_amd.encoder import Encoders, FuryError
-    fields = SCHEMAS["mixed"]
-    n = 777
-    host = gen_columns("mixed", fields, n, seed=6)
+def _stream_at(stream, shift, dev, tail=0):
+    """The stream copied to byte offset `shift` of a fresh buffer (Java frames at any
+    writerIndex), optionally followed by `tail` junk bytes."""
+    buf = torch.full((stream.numel() + shift + tail + 64,), 0xA5, dtype=torch.uint8, device=dev)
+    buf[shift:shift + stream.numel()] = stream
+    return buf[shift:shift + stream.numel() + tail]
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3, 4, 5, 8, 9, 13])
+@pytest.mark.parametrize("name,n", [("mixed", 2777), ("struct100", 300), ("nested", 1500)])
+def test_unframe_any_byte_offset(oracle, dev, name, n, shift):
+    """CodecBuilderTest.java:51-67 decodes a stream written after a 1-byte offset: streams at
+    1..13-byte offsets parse in parallel (no walk, no repair) to the oracle's rows, and a
+    two-row decode_stream at offset 1 round-trips like the Java test."""
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=shift + n)
     enc = Encoders.bean(fields, device=dev)
     stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    s = _stream_at(stream, shift, dev, tail=7)
+    w0, r0 = _walks(), _repairs()
+    got = enc.unframe(s, n)
+    assert (_walks(), _repairs()) == (w0, r0)
     rows, offs = oracle.encode(fields, host, n)
-    buf = torch.zeros(stream.numel() + 4, dtype=torch.uint8, device=dev)
-    buf[4:] = stream
-    got = enc.unframe(buf[4:], n)          # 4-byte aligned base: the walk parses it
     assert np.array_equal(got.rows.cpu().numpy(), rows)
+    if got.row_offsets is not None:
+        assert np.array_equal(got.row_offsets.cpu().numpy(), offs)
+    dec = [column_to_host(c) for c in enc.decode_stream(s, 2)]
+    assert_columns_equal(fields, dec, oracle.decode(fields, rows[:offs[2]], offs[:3], 2), 2)
+
+
+@pytest.mark.parametrize("shift", [0, 1, 6])
+def test_unframe_fake_header_unaligned(oracle, dev, shift):
+    """Fake headers in payloads at an unaligned base: repaired in parallel, oracle-exact."""
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS["mixed"]
+    n = 5000
+    host = gen_columns("mixed", fields, n, seed=9)
+    enc = Encoders.bean(fields, device=dev)
+    h = enc.schema_hash & (2**64 - 1)
+    b = host[1].values.view(np.uint64)        # b: Long (slot 1) + c: Double (slot 2)
+    c = host[2].values.view(np.uint64)
+    va, vb = host[1].validity, host[2].validity
+    for r in range(3, n, 97):                  # slots of b, c spell [len 24][hash] at word 4k
+        b[r] = np.uint64(24 | ((h & 0xFFFFFFFF) << 32))
+        c[r] = np.uint64(h >> 32)
+        va[r >> 3] |= np.uint8(1 << (r & 7))
+        vb[r >> 3] |= np.uint8(1 << (r & 7))
+    stream, _ = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    s = _stream_at(stream, shift, dev)
+    w0, r0 = _walks(), _repairs()
+    got = enc.unframe(s, n)
+    assert _walks() == w0 and _repairs() == r0 + 1
+    rows, offs = oracle.encode(fields, host, n)
+    assert np.array_equal(got.rows.cpu().numpy(), rows)
+    assert np.array_equal(got.row_offsets.cpu().numpy(), offs)
+
+
+@pytest.mark.parametrize("shift", [0, 3])
+def test_unframe_errors_match_decode(oracle, dev, shift):
+    """Errors are Encoders.decode's: a frame with another schema's hash in the middle of the
+    stream -> ClassNotCompatibleException; a stream cut inside a frame -> IndexOutOfBounds;
+    asking for fewer frames than the stream holds -> that prefix."""
+    from fury_amd.encoder import ClassNotCompatibleException, Encoders, FuryError
+    fields = SCHEMAS["mixed"]
+    n = 4000
+    host = gen_columns("mixed", fields, n, seed=6)
+    enc = Encoders.bean(fields, device=dev)
+    stream, fo = enc.frame(enc.encode_batch(_dev_cols(host, dev), n))
+    rows, offs = oracle.encode(fields, host, n)
+    bad = stream.clone()
+    p = int(fo[2500])
+    bad[p + 4] ^= 1                            # frame 2500's schema hash
+    with pytest.raises(ClassNotCompatibleException):
+        enc.unframe(_stream_at(bad, shift, dev), n)
+    short = enc.unframe(_stream_at(bad, shift, dev), 2500)     # the frames before it are fine
+    assert np.array_equal(short.rows.cpu().numpy(), rows[:offs[2500]])
     with pytest.raises(FuryError):
-        enc.unframe(stream[:-8], n)        # last frame runs past the end
-    short = enc.unframe(stream, n - 1)     # fewer frames than the stream holds: a prefix
-    assert np.array_equal(short.rows.cpu().numpy(), rows[:offs[n - 1]])
+        enc.unframe(_stream_at(stream[:-8], shift, dev), n)    # last frame runs past the end
+    prefix = enc.unframe(_stream_at(stream, shift, dev), n - 1)
+    assert np.array_equal(prefix.rows.cpu().numpy(), rows[:offs[n - 1]])
 
 
 def test_unframe_large_fast_path(dev):
