@@ -56,6 +56,7 @@ SIGNATURES = {
     "fury_lower_camel_to_lower_underscore": (_I32, [ctypes.c_char_p, ctypes.c_char_p,
                                                     ctypes.c_size_t]),
     "fury_schema_create": (ctypes.c_int, [ctypes.POINTER(FuryField), _I32, ctypes.POINTER(_P)]),
+    "fury_collection_schema_create": (ctypes.c_int, [ctypes.POINTER(FuryField), ctypes.POINTER(_P)]),
     "fury_schema_destroy": (None, [_P]),
     "fury_schema_get_info": (ctypes.c_int, [_P, ctypes.POINTER(FurySchemaInfo)]),
     "fury_row_measure": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _P]),

@@ -208,6 +208,11 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   g->ntop = s->num_fields;
   g->nrows = nrows;
   g->err = nullptr;
+  g->root = s->root;
+  if (s->root && !decode && cols && cols[0].validity)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "collection batch: the top-level column has no validity (toArray / toMap of a "
+                     "null collection is not defined)");
   std::vector<const fury_column*> col(nn, nullptr);
   for (int k = 0; k < s->num_fields; k++) col[k] = &cols[k];
   for (size_t i = 0; i < nn; i++) {
@@ -450,6 +455,7 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
     g.nnodes = nn;
     g.ntop = s->num_fields;
     g.nrows = nrows;
+    g.root = s->root;
     for (int i = 0; i < nn; i++) {
       g.node[i].type = s->nodes[i].type_id;
       g.node[i].first_child = s->nodes[i].first_child;
@@ -538,6 +544,7 @@ int32_t fury_get_tuning(const char* key) {
 int fury_frame_rows(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, void* out, int64_t* frame_offsets, void* stream) {
   if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
+  if (s->root) return set_error(FURY_ERR_UNSUPPORTED, "row framing of a collection schema");
   if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
   if (nrows == 0) return FURY_OK;
   if (!rows || !out) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/out is null");
@@ -551,6 +558,7 @@ int fury_frame_rows(const fury_schema* s, const void* rows, const int64_t* row_o
 int fury_unframe_rows(const fury_schema* s, const void* stream_bytes, int64_t stream_len,
                       int64_t nrows, void* rows_out, int64_t* row_offsets, void* stream) {
   if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, "schema is null");
+  if (s->root) return set_error(FURY_ERR_UNSUPPORTED, "row framing of a collection schema");
   if (nrows < 0 || stream_len < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "negative size");
   if (nrows == 0) return FURY_OK;
   if (!stream_bytes || !rows_out || !row_offsets)

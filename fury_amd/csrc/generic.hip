@@ -224,8 +224,25 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
   }
 }
 
+// Entry r of the batch: a row of the ntop top-level fields (root 0), or -- ArrayEncoder.toArray /
+// MapEncoder.toMap (ArrayEncoderBuilder.java:118-140, MapEncoderBuilder.java:152-208) -- the
+// top-level BinaryArray (root 1) / BinaryMap [int64 keyBytes][keys][values] (root 2) of node 0's
+// entry r, written at the buffer start exactly as inside a row (element offsets are relative to
+// the array itself).
 template <bool W>
-__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf) {
+__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf, int root = 0) {
+  if (root) {
+    const GenNode& n = nodes[0];
+    const int64_t b = n.offsets[r];
+    const int64_t m = n.offsets[r + 1] - b;
+    int64_t cursor = root == 2 ? 8 : 0;
+    put_array<1, W>(nodes, n.first_child, b, m, buf, cursor);
+    if (root == 2) {
+      if (W) st8(buf, static_cast<uint64_t>(cursor - 8));      // key array bytes
+      put_array<1, W>(nodes, n.first_child + 1, b, m, buf, cursor);
+    }
+    return cursor;
+  }
   const int64_t bmb = gbm(ntop);
   const int64_t fixed = bmb + 8 * ntop;
   if (W) zero_bytes(buf, fixed);                       // fresh buffer: bitmap + slots zero
@@ -248,7 +265,7 @@ __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int
   __shared__ GenNode sn[kGenMaxNodes];
   const GenNode* nodes = stage_nodes(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows) sizes[r] = put_row<false>(nodes, g.ntop, r, nullptr);
+  if (r < g.nrows) sizes[r] = put_row<false>(nodes, g.ntop, r, nullptr, g.root);
 }
 
 __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
@@ -258,7 +275,7 @@ __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
   __shared__ GenNode sn[kGenMaxNodes];
   const GenNode* nodes = stage_nodes(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows && offs[r + 1] <= cap) put_row<true>(nodes, g.ntop, r, rows + offs[r]);
+  if (r < g.nrows && offs[r + 1] <= cap) put_row<true>(nodes, g.ntop, r, rows + offs[r], g.root);
 }
 
 // ---- decode ----------------------------------------------------------------------------------
@@ -440,8 +457,19 @@ __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const u
     const uint8_t* row = rows + offs[r];
     const int64_t bmb = gbm(g.ntop);
     Cursors cur{e, b, &vmask, &bmask};
-    for (int k = 0; k < g.ntop; k++)
-      get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
+    if (g.root) {        // a top-level BinaryArray / BinaryMap: node 0's entry r
+      const GenNode& n = nodes[0];
+      const int64_t en = e[0]++;
+      if (W && n.validity) vmask |= 1ull;
+      const uint8_t* ka = g.root == 2 ? row + 8 : row;
+      const int64_t m = static_cast<int32_t>(ld8(ka));
+      get_array<1, W>(nodes, n.first_child, ka, m, cur);
+      if (g.root == 2) get_array<1, W>(nodes, n.first_child + 1, row + 8 + static_cast<int64_t>(ld8(row)), m, cur);
+      if (W) n.offsets[en + 1] = static_cast<int32_t>(e[n.first_child]);
+    } else {
+      for (int k = 0; k < g.ntop; k++)
+        get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
+    }
     if (!W) {
       for (int i = 0; i < g.nnodes; i++) {
         cnt[(2 * i) * g.nrows + r] = e[i];

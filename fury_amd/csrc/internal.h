@@ -59,6 +59,8 @@ struct fury_schema {
   std::string device_reason;      // why not, when device_ok == 0
   int32_t num_var = 0;            // fields of kind kBytes / kDecimal / kListFixed
   int32_t generic = 0;            // nested schema: encode/decode run the generic engine
+  int32_t root = 0;               // 0: rows of the fields; 1 / 2: batches of top-level
+                                  // BinaryArrays / BinaryMaps (ArrayEncoder / MapEncoder)
   int32_t depth = 0;              // deepest nesting level (top-level fields = 1)
   std::vector<fury::GenTpl> nodes;
 };

@@ -115,6 +115,8 @@ struct GenArgs {
   int32_t ntop;            // top-level fields = nodes [0, ntop)
   int64_t nrows;
   int32_t* err;            // optional device flag (never NULL when set by the host)
+  int32_t root;            // fury_schema.root: 0 rows, 1 top-level arrays, 2 top-level maps
+  int32_t pad_;
 };
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);

@@ -287,6 +287,36 @@ int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema
   return FURY_OK;
 }
 
+int fury_collection_schema_create(const fury_field* field, fury_schema** out) {
+  if (!out) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_collection_schema_create: out is null");
+  *out = nullptr;
+  if (!field) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_collection_schema_create: field is null");
+  if (field->type_id != FURY_TYPE_LIST && field->type_id != FURY_TYPE_MAP)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "a collection schema's field must be a LIST (ArrayEncoder) or MAP (MapEncoder)");
+  fury_schema* s = nullptr;
+  int st = fury_schema_create(field, 1, &s);
+  if (st) return st;
+  // Every entry is one top-level BinaryArray / BinaryMap: always the generic engine, no row
+  // header, no schema hash (these encoders frame [int32 size][bytes], Encoders.java:372-386).
+  s->root = field->type_id == FURY_TYPE_LIST ? 1 : 2;
+  s->is_fixed = 0;
+  s->bitmap_bytes = 0;
+  s->fixed_size = 0;
+  s->schema_hash = 0;
+  if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost) {
+    s->device_ok = 1;
+    s->generic = 1;
+    s->device_reason.clear();
+  } else {
+    s->device_ok = 0;
+    s->device_reason = "collection type beyond " + std::to_string(kGenMaxNodesHost) + " nodes / " +
+                       std::to_string(kGenMaxDepthHost - 1) + " levels";
+  }
+  *out = s;
+  return FURY_OK;
+}
+
 int32_t fury_schema_num_nodes(const fury_schema* s) {
   return s ? static_cast<int32_t>(s->nodes.size()) : -1;
 }

@@ -96,14 +96,23 @@ def _c_fields(fields: Sequence[Field], keep: list):
 
 
 class Schema:
-    """A schema handle (``fury_schema``): layout + ``DataTypes.computeSchemaHash``."""
+    """A schema handle (``fury_schema``): layout + ``DataTypes.computeSchemaHash``.
+    ``collection=True``: the schema of an ArrayEncoder / MapEncoder (one LIST or MAP field whose
+    batch entries are top-level BinaryArrays / BinaryMaps, ``fury_collection_schema_create``)."""
 
-    def __init__(self, fields: Sequence[Field]):
+    def __init__(self, fields: Sequence[Field], collection: bool = False):
         self.fields: List[Field] = list(fields)
+        self.collection = collection
         keep: list = []
         h = ctypes.c_void_p()
-        _check(N.lib().fury_schema_create(_c_fields(self.fields, keep), len(self.fields),
-                                          ctypes.byref(h)))
+        if collection:
+            if len(self.fields) != 1:
+                raise IllegalArgumentException("a collection schema has exactly one field")
+            _check(N.lib().fury_collection_schema_create(_c_fields(self.fields, keep),
+                                                         ctypes.byref(h)))
+        else:
+            _check(N.lib().fury_schema_create(_c_fields(self.fields, keep), len(self.fields),
+                                              ctypes.byref(h)))
         self._h = h
         info = N.FurySchemaInfo()
         _check(N.lib().fury_schema_get_info(h, ctypes.byref(info)))
@@ -342,7 +351,9 @@ class RowEncoder:
     @property
     def nested(self) -> bool:
         """True when the schema has STRUCT / MAP / LIST-of-variable-length fields (decoded by the
-        two-step plan API)."""
+        two-step plan API); always for collection schemas."""
+        if getattr(self._schema, "collection", False):
+            return True
         def deep(f: Field) -> bool:
             if f.type_id in (STRUCT, MAP):
                 return True
@@ -695,12 +706,114 @@ def _alloc_node(f: Field, m: int, nbytes: int, validity: bool, device) -> Column
     raise UnsupportedOperationException(f"no device decode for {f}")
 
 
+class _CollectionEncoder(RowEncoder):
+    """Batch codec of top-level collections over the device engine: batch entry i is one
+    BinaryArray (ArrayEncoder) / BinaryMap (MapEncoder).  The batch methods of RowEncoder apply
+    unchanged with ONE column, the collection column (no validity: toArray / toMap of a null
+    collection is not defined)."""
+
+    def __init__(self, field: Field, device=None):
+        self._schema = Schema([field], collection=True)
+        self.device = torch.device(device if device is not None else "cuda")
+        self._field = field
+
+    def _column(self, values: list) -> Column:
+        from .beans import values_to_column
+        c = values_to_column(self._field, list(values))
+        c.validity = None
+        return column_to_device(c, self.device)
+
+    def _values(self, data: bytes) -> list:
+        from .beans import value_at
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.device)
+        offs = torch.tensor([0, len(data)], dtype=torch.int64, device=self.device)
+        cols = self.decode_batch(RowBatch(t, offs, 1, 0))
+        return value_at(self._field, column_to_host(cols[0]), 0)
+
+    def _bytes(self, values: list) -> bytes:
+        b = self.encode_batch([self._column([values])], 1)
+        return bytes(b.rows.cpu().numpy())
+
+    def encode_stream(self, values: list) -> bytes:
+        """``encode(MemoryBuffer, T)``: [int32 size][bytes] (Encoders.java:372-386 / 575-590)."""
+        body = self._bytes(values)
+        return struct.pack("<i", len(body)) + body
+
+    def decode_stream(self, data: bytes, offset: int = 0):
+        """``decode(MemoryBuffer)`` at ``offset``: returns (value, next offset)."""
+        size = struct.unpack_from("<i", data, offset)[0]
+        return self._values(data[offset + 4:offset + 4 + size]), offset + 4 + size
+
+
+class ArrayEncoder(_CollectionEncoder):
+    """``Encoders.arrayEncoder`` (Encoders.java:230-386): List -> BinaryArray.  ``field`` is the
+    LIST field TypeInference infers for the collection type (its element: a bean STRUCT, a LIST,
+    a MAP, or a scalar)."""
+
+    def field(self) -> Field:
+        return self._field
+
+    def to_array(self, values: list) -> bytes:
+        """``toArray(obj)`` bytes: [int64 n][null bitmap][n slots][variable section]."""
+        return self._bytes(values)
+
+    def from_array(self, data: bytes) -> list:
+        return self._values(data)
+
+    def encode(self, values: list) -> bytes:
+        """``encode(T)`` of a fresh encoder: ``writer.getBuffer().getBytes(0, 8 + size)``
+        (Encoders.java:365-369) = the array followed by 8 bytes of the zeroed buffer -- the length
+        ArrayEncoderTest pins (224 / 1576 / 10824).  The reference never rewinds its writer, so a
+        second encode() on the same Java encoder returns the FIRST array's bytes (SURVEY §7 trap 5);
+        that bug is not reproduced: every call here returns this fresh-encoder result."""
+        return self._bytes(values) + bytes(8)
+
+    def decode(self, data: bytes) -> list:
+        """``decode(byte[])``: the array at offset 0 (trailing bytes ignored, as pointTo does)."""
+        return self._values(data)
+
+
+class MapEncoder(_CollectionEncoder):
+    """``Encoders.mapEncoder`` (Encoders.java:420-600, MapEncoderBuilder.java:152-208): Map ->
+    BinaryMap [int64 keyArrayBytes][key BinaryArray][value BinaryArray].  A map value is a list
+    of (key, value) pairs in iteration order."""
+
+    def key_field(self) -> Field:
+        return self._field.children[0]
+
+    def value_field(self) -> Field:
+        return self._field.children[1]
+
+    def to_map(self, pairs: list) -> bytes:
+        return self._bytes(pairs)
+
+    def from_map(self, data: bytes) -> list:
+        return self._values(data)
+
+    def encode(self, pairs: list) -> bytes:
+        """``encode(T)``: ``map.getBuf().getBytes(baseOffset, sizeInBytes)`` = the BinaryMap."""
+        return self._bytes(pairs)
+
+    def decode(self, data: bytes) -> list:
+        return self._values(data)
+
+
 class Encoders:
-    """``Encoders`` factory (Encoders.java:60-73)."""
+    """``Encoders`` factory (Encoders.java:60-73, 230-420)."""
 
     @staticmethod
     def bean(fields: Sequence[Field], device=None) -> RowEncoder:
         return RowEncoder(fields, device)
+
+    @staticmethod
+    def array_encoder(elem: Field, device=None, name: str = "value") -> ArrayEncoder:
+        """``arrayEncoder(List<elem>)``: the LIST field of element field ``elem``."""
+        return ArrayEncoder(Field(name, LIST, True, (elem,)), device)
+
+    @staticmethod
+    def map_encoder(key: Field, value: Field, device=None, name: str = "value") -> MapEncoder:
+        """``mapEncoder(Map<key, value>)``: the MAP field of the key / value fields."""
+        return MapEncoder(Field(name, MAP, True, (key, value)), device)
 
 
 class ArrowWriter:

@@ -192,6 +192,21 @@ int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* 
 int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* columns, void* stream);
 
+/* ---- ArrayEncoder / MapEncoder batches (Encoders.arrayEncoder / mapEncoder,
+ *      FMT/encoder/Encoders.java:230-600, ArrayEncoderBuilder.java:118-140,
+ *      MapEncoderBuilder.java:152-208) ----------------------------------------------------- */
+/* A collection schema: its batch entries are top-level BinaryArrays (`field` of type LIST:
+ * ArrayEncoder.toArray(obj)) or BinaryMaps (`field` of type MAP: [int64 keyArrayBytes][key
+ * BinaryArray][value BinaryArray], MapEncoder.toMap(obj)) instead of rows.  The batch entry points
+ * take it unchanged: fury_row_measure / fury_row_encode / fury_row_encode_measured write entry i
+ * at row_offsets[i] (every entry a multiple of 8 bytes), fury_decode_prepare /
+ * fury_decode_execute decode.  `columns` is ONE column, the collection column itself (LIST:
+ * offsets + element child; MAP: offsets + child [keys, values]) with validity NULL: a collection
+ * handed to toArray / toMap is never null.  schema_hash is 0 (these encoders carry no hash; their
+ * encode(MemoryBuffer, T) frames [int32 size][bytes]), and the row framing entry points return
+ * FURY_ERR_UNSUPPORTED for them. */
+int fury_collection_schema_create(const fury_field* field, fury_schema** out);
+
 /* ---- nested schemas: two-step decode --------------------------------------------------- */
 /* Schemas with STRUCT / MAP / LIST-of-variable-length fields produce a TREE of Arrow columns whose
  * sizes depend on the data.  Nodes are the schema's fields at every level, numbered breadth-first:

@@ -199,6 +199,37 @@ def encode_array(elem: F, values: list) -> bytes:
     return bytes(buf.data[aw.start:buf.writer_index])
 
 
+def encode_map(key: F, value: F, pairs: list) -> bytes:
+    """MapEncoder.toMap(map) bytes (FMT/encoder/MapEncoderBuilder.java:152-208): the key writer
+    writes writeDirectly(-1) at its writer index, the key array, then patches that word with the
+    key array's size; the value writer (same buffer) appends the value array.  Result =
+    [int64 keyArrayBytes][key BinaryArray][value BinaryArray] (BinaryMap.java:30-37)."""
+    buf = Buffer()
+    start = buf.writer_index
+    kw = Writer(buf, True, elem=key)
+    kw.write_directly(-1)
+    _serialize_array(kw, key, [k for k, _ in pairs])
+    buf.put(start, struct.pack("<q", buf.writer_index - kw.start))
+    vw = Writer(buf, True, elem=value)
+    _serialize_array(vw, value, [v for _, v in pairs])
+    return bytes(buf.data[start:buf.writer_index])
+
+
+def decode_array(elem: F, data: bytes) -> list:
+    """ArrayEncoder.fromArray of a top-level BinaryArray at offset 0."""
+    return read_array(data, 0, elem)
+
+
+def decode_map(key: F, value: F, data: bytes) -> list:
+    """MapEncoder.fromMap of a top-level BinaryMap at offset 0 (BinaryMap.pointTo :62-77)."""
+    kb = struct.unpack_from("<q", data, 0)[0]
+    keys = read_array(data, 8, key)
+    vals = read_array(data, 8 + kb, value)
+    if len(keys) != len(vals):
+        raise ValueError("key / value count mismatch (UnsupportedOperationException)")
+    return list(zip(keys, vals))
+
+
 # ---------------------------------------------------------------------------------------------
 # Reader + C++ Row::ToString formatting (cpp/fury/row/row.cc), used for the row_test.cc known
 # answer.

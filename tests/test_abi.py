@@ -187,3 +187,24 @@ def test_host_decode_empty_batch_writes_arrow_offsets():
     assert L.fury_row_decode_host(m.handle, None, None, 0, cols, 0) == 0
     for k in range(3, 6):
         assert offs[k][0] == 0 and offs[k][1] == 77
+
+
+def test_collection_schema_create():
+    """fury_collection_schema_create: LIST -> ArrayEncoder, MAP -> MapEncoder schemas (no hash,
+    no row header); anything else is an IllegalArgumentException; row framing is refused."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import IllegalArgumentException, Schema
+    s = Schema([T.Field("v", T.LIST, True, (T.struct_field("item", SCHEMAS["bar"]),))],
+               collection=True)
+    assert (s.schema_hash, s.fixed_size, s.is_fixed, s.num_fields) == (0, 0, False, 1)
+    m = Schema([T.map_field("v", T.field("key", T.STRING), T.field("value", T.INT32))],
+               collection=True)
+    assert m.schema_hash == 0
+    with pytest.raises(IllegalArgumentException):
+        Schema([T.field("x", T.INT32)], collection=True)
+    with pytest.raises(IllegalArgumentException):
+        Schema([T.field("x", T.INT32), T.field("y", T.INT32)], collection=True)
+    L = N.lib()
+    buf = ctypes.create_string_buffer(64)
+    assert L.fury_frame_rows(s.handle, buf, buf, 1, buf, buf, None) == 2
+    assert L.fury_unframe_rows(m.handle, buf, 64, 1, buf, buf, None) == 2

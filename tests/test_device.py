@@ -911,3 +911,176 @@ def test_c5_shard_size_property(oracle, dev):
         host = gen_columns("struct100", fields, 300, seed=1234, start=start + off)
         want, _ = oracle.encode(fields, host, 300)
         assert np.array_equal(b.rows[off * 816:(off + 300) * 816].cpu().numpy(), want)
+
+
+# ---- round 2: ArrayEncoder / MapEncoder batches on the device ---------------------------------
+def _bar_item(name="item"):
+    return T.struct_field(name, SCHEMAS["bar"])
+
+
+def test_array_encoder_known_answer_224(dev):
+    """ArrayEncoderTest.testListEncoder: 5 Bars -> encode() is 224 bytes; device bytes equal the
+    bean restatement; decode(encode(x)) == x; toArray/fromArray round trip."""
+    from fury_amd.encoder import Encoders
+    from oracle import bean_oracle as B
+    elem = _bar_item()
+    enc = Encoders.array_encoder(elem, device=dev)
+    bars = [{"f1": k, "f2": f"i{k}"} for k in range(5)]
+    bs = enc.encode(bars)
+    assert len(bs) == 224
+    assert bs[:-8] == B.encode_array(elem, bars) and bs[-8:] == bytes(8)
+    assert enc.decode(bs) == bars
+    assert enc.from_array(enc.to_array(bars)) == bars
+
+
+def test_array_encoder_known_answer_1576(dev):
+    """ArrayEncoderTest.testNestListEncoder: List<List<List<Bar>>> -> 1576 bytes."""
+    from fury_amd.encoder import Encoders
+    from oracle import bean_oracle as B
+    l1 = T.Field("item", T.LIST, True, (_bar_item(),))
+    l2 = T.Field("item", T.LIST, True, (l1,))
+    vals = [[[{"f1": k, "f2": f"s{k}"} for k in range(3)] for _ in range(i)] for i in range(5)]
+    enc = Encoders.array_encoder(l2, device=dev)
+    bs = enc.encode(vals)
+    assert len(bs) == 1576
+    assert bs[:-8] == B.encode_array(l2, vals)
+    assert enc.decode(bs) == vals
+
+
+def test_array_encoder_known_answer_10824(dev):
+    """ArrayEncoderTest.testNestArrayWithMapEncoder: List<List<Map<Foo, List<Bar>>>> -> 10824."""
+    from fury_amd.encoder import Encoders
+    from oracle import bean_oracle as B
+    key = T.Field("key", T.STRUCT, False, tuple(SCHEMAS["foo"]))
+    value = T.Field("value", T.LIST, True, (_bar_item(),))
+    m = T.Field("item", T.MAP, True, (key, value))
+    l1 = T.Field("item", T.LIST, True, (m,))
+    foo = {"f1": 2, "f2": "str", "f3": ["a", "b", "c"], "f4": [("k1", 1), ("k2", 2)],
+           "f5": {"f1": 1, "f2": "str"}}
+    vals = [[[(foo, [{"f1": j, "f2": f"x{j}"}])] for j in range(3)] for _ in range(10)]
+    enc = Encoders.array_encoder(l1, device=dev)
+    bs = enc.encode(vals)
+    assert len(bs) == 10824
+    assert bs[:-8] == B.encode_array(l1, vals)
+    assert enc.decode(bs) == vals
+
+
+def _collection_batch_case(kind, n, rng):
+    bar = _bar_item()
+    if kind == "list_bar":
+        elem = bar
+        vals = [[None if rng.random() < 0.1 else {"f1": int(rng.integers(-99, 99)),
+                                                  "f2": None if rng.random() < 0.2 else "s" * int(rng.integers(0, 12))}
+                 for _ in range(int(rng.integers(0, 6)))] for _ in range(n)]
+    elif kind == "list_long":
+        elem = T.field("item", T.INT64)
+        vals = [[None if rng.random() < 0.1 else int(x) for x in rng.integers(-2**62, 2**62, int(rng.integers(0, 70)))]
+                for _ in range(n)]
+    elif kind == "list_str":
+        elem = T.field("item", T.STRING)
+        vals = [[None if rng.random() < 0.1 else "é" * int(rng.integers(0, 9)) for _ in range(int(rng.integers(0, 5)))]
+                for _ in range(n)]
+    else:   # list of list<int32>
+        elem = T.Field("item", T.LIST, True, (T.field("item", T.INT32),))
+        vals = [[None if rng.random() < 0.1 else [int(x) for x in rng.integers(0, 9, int(rng.integers(0, 4)))]
+                 for _ in range(int(rng.integers(0, 4)))] for _ in range(n)]
+    return elem, vals
+
+
+@pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list"])
+def test_array_encoder_batch_vs_oracle(oracle, dev, kind):
+    """A batch of top-level arrays (entry i = toArray(values[i])) encoded on the device: bytes and
+    offsets == the columnar C restatement's LIST field bytes (row[16:], same layout), decode ==
+    the oracle's decoded column, encode_measured == encode."""
+    from fury_amd.beans import beans_to_columns, value_at
+    from fury_amd.encoder import Encoders, column_to_host
+    n = 1500
+    elem, vals = _collection_batch_case(kind, n, np.random.default_rng(len(kind)))
+    enc = Encoders.array_encoder(elem, device=dev)
+    col = beans_to_columns([enc.field()], [{"value": v} for v in vals])[0]
+    col.validity = None
+    batch = enc.encode_batch([column_to_device_host(col, dev)], n)
+    lf = enc.field()
+    rows, offs = oracle.encode([lf], [col], n)
+    sizes = np.diff(offs) - 16
+    want = np.concatenate([rows[offs[i] + 16:offs[i + 1]] for i in range(n)])
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    assert np.array_equal(np.diff(batch.row_offsets.cpu().numpy()), sizes)
+    dec = column_to_host(enc.decode_batch(batch)[0])
+    assert [value_at(lf, dec, i) for i in range(n)] == vals
+    rows2 = torch.full((want.size + 64,), 0xEE, dtype=torch.uint8, device=dev)
+    offs2 = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    enc.encode_measured_into([column_to_device_host(col, dev)], n, rows2[:want.size], offs2)
+    assert torch.equal(rows2[:want.size], batch.rows) and torch.equal(offs2, batch.row_offsets)
+
+
+def column_to_device_host(col, dev):
+    from fury_amd.encoder import column_to_device
+    return column_to_device(col, dev)
+
+
+@pytest.mark.parametrize("kind", ["str_bar", "str_listlist_bar", "str_list_int", "bar_bar",
+                                  "str_list_map"])
+def test_map_encoder_shapes(oracle, dev, kind):
+    """MapEncoderTest shapes (testMapEncoder, testNestListEncoder, testSimpleNestArrayWith-
+    MapEncoder1, testKVStructMap, testNestArrayWithMapEncoder): toMap bytes == the bean
+    restatement of MapEncoderBuilder, decode(encode(m)) == m, and the streaming form
+    [int32 size][map] twice after a 1-byte offset decodes twice (CodecBuilderTest
+    testStreamingEncode)."""
+    from fury_amd.encoder import Encoders
+    from oracle import bean_oracle as B
+    bar = T.struct_field("value", SCHEMAS["bar"])
+    skey = T.field("key", T.STRING)
+    if kind == "str_bar":
+        key, value = skey, bar
+        m = [(f"i{k}", {"f1": k, "f2": f"i{k}"}) for k in range(5)]
+    elif kind == "str_listlist_bar":
+        key = skey
+        value = T.Field("value", T.LIST, True, (T.Field("item", T.LIST, True, (_bar_item(),)),))
+        m = [(str(i), [[{"f1": k, "f2": f"s{k}"} for k in range(3)] for _ in range(i)])
+             for i in range(5)]
+    elif kind == "str_list_int":
+        key, value = skey, T.Field("value", T.LIST, True, (T.field("item", T.INT32),))
+        m = [("k1", [1, 2])]
+    elif kind == "bar_bar":
+        key = T.Field("key", T.STRUCT, True, tuple(SCHEMAS["bar"]))
+        value = bar
+        m = [({"f1": 1, "f2": "a"}, {"f1": 2, "f2": None})]
+    else:
+        key = T.Field("key", T.STRUCT, True, tuple(SCHEMAS["foo"]))
+        value = T.Field("value", T.LIST, True, (_bar_item(),))
+        foo = {"f1": 2, "f2": "str", "f3": ["a", "b", "c"], "f4": [("k1", 1), ("k2", 2)],
+               "f5": {"f1": 1, "f2": "str"}}
+        inner = [[(foo, [{"f1": j, "f2": f"x{j}"}])] for j in range(3)]   # 3 one-entry maps
+        value = T.Field("value", T.LIST, True, (T.map_field("item", key, value),))
+        key = skey
+        m = [(str(i), inner) for i in range(10)]
+    enc = Encoders.map_encoder(key, value, device=dev)
+    data = enc.encode(m)
+    assert data == B.encode_map(key, value, m)
+    assert enc.decode(data) == m and enc.from_map(enc.to_map(m)) == m
+    buf = b"\xff" + enc.encode_stream(m) + enc.encode_stream(m)
+    v1, p = enc.decode_stream(buf, 1)
+    v2, p = enc.decode_stream(buf, p)
+    assert v1 == m and v2 == m and p == len(buf)
+
+
+def test_map_encoder_batch_vs_oracle(oracle, dev):
+    """A batch of 3,000 top-level maps<String, Long> with null values: device bytes == the MAP
+    field's bytes in the C restatement's rows, decode == values."""
+    from fury_amd.beans import beans_to_columns, value_at
+    from fury_amd.encoder import Encoders, column_to_host
+    rng = np.random.default_rng(4)
+    n = 3000
+    vals = [[("k" * int(rng.integers(1, 9)), None if rng.random() < 0.2 else int(rng.integers(-9, 9)))
+             for _ in range(int(rng.integers(0, 7)))] for _ in range(n)]
+    enc = Encoders.map_encoder(T.field("key", T.STRING), T.field("value", T.INT64), device=dev)
+    mf = enc._field
+    col = beans_to_columns([mf], [{"value": v} for v in vals])[0]
+    col.validity = None
+    batch = enc.encode_batch([column_to_device_host(col, dev)], n)
+    rows, offs = oracle.encode([mf], [col], n)
+    want = np.concatenate([rows[offs[i] + 16:offs[i + 1]] for i in range(n)])
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    dec = column_to_host(enc.decode_batch(batch)[0])
+    assert [value_at(mf, dec, i) for i in range(n)] == vals

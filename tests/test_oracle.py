@@ -186,3 +186,44 @@ def test_golden_fixture_regression(oracle, name):
     rows, offs = oracle.encode(fields, cols, n)
     assert np.array_equal(offs, d["row_offsets"])
     assert np.array_equal(rows, d["rows"])
+
+
+def test_map_encoder_restatement_round_trips(oracle):
+    """MapEncoderTest-shaped maps through the bean restatement of MapEncoderBuilder: toMap bytes
+    decode back (BinaryMap.pointTo), and equal the MAP field's bytes inside a row written by the
+    columnar C restatement (a top-level BinaryMap is laid out exactly as a map in a row's variable
+    section: row = [bitmap 8][slot 8][map])."""
+    from fury_amd.beans import beans_to_columns
+    bar = T.struct_field("value", SCHEMAS["bar"])
+    key = T.field("key", T.STRING)
+    pairs = [(f"i{k}", {"f1": k, "f2": f"i{k}"}) for k in range(5)]
+    data = B.encode_map(key, bar, pairs)
+    assert B.decode_map(key, bar, data) == pairs
+    lbar = T.Field("value", T.LIST, True, (T.Field("item", T.LIST, True,
+                                                   (T.struct_field("item", SCHEMAS["bar"]),)),))
+    nested = [(str(i), [[{"f1": k, "f2": f"s{k}"} for k in range(3)] for _ in range(i)])
+              for i in range(5)]
+    for kf, vf, v in ((key, bar, pairs), (key, lbar, nested)):
+        m = T.Field("m", T.MAP, True, (kf, vf))
+        rows, offs = oracle.encode([m], beans_to_columns([m], [{"m": v}]), 1)
+        assert rows[16:offs[1]].tobytes() == B.encode_map(kf, vf, v)
+
+
+def test_array_encoder_restatement_matches_row_restatement(oracle):
+    """Top-level BinaryArray bytes (bean restatement of ArrayEncoderBuilder) == the LIST field's
+    bytes inside a row (columnar C restatement), for lists of beans, strings, lists and maps."""
+    from fury_amd.beans import beans_to_columns
+    bar = T.struct_field("item", SCHEMAS["bar"])
+    cases = [
+        (bar, [{"f1": k, "f2": f"i{k}"} for k in range(5)]),
+        (T.field("item", T.STRING), ["a", None, "bcdefghij", ""]),
+        (T.Field("item", T.LIST, True, (T.field("item", T.INT32),)), [[1, 2], None, [], [3]]),
+        (T.map_field("item", T.field("key", T.STRING), T.field("value", T.INT64)),
+         [[("x", 1), ("yy", None)], []]),
+    ]
+    for elem, vals in cases:
+        lf = T.Field("l", T.LIST, True, (elem,))
+        rows, offs = oracle.encode([lf], beans_to_columns([lf], [{"l": vals}]), 1)
+        got = B.encode_array(elem, vals)
+        assert rows[16:offs[1]].tobytes() == got
+        assert B.decode_array(elem, got) == vals
