@@ -82,6 +82,9 @@ SIGNATURES = {
     "fury_row_encode_host": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _I64, _P,
                                             ctypes.POINTER(_I64), _I32]),
     "fury_row_decode_host": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(FuryColumn), _I32]),
+    "fury_decode_host_prepare": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(_I64),
+                                                ctypes.POINTER(_I64), ctypes.POINTER(_P), _I32]),
+    "fury_decode_host_execute": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn)]),
     "fury_arrow_ipc_schema": (ctypes.c_int, [_P, _P, _I64, ctypes.POINTER(_I64)]),
     "fury_arrow_ipc_record_batch": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _I64,
                                                    ctypes.POINTER(_I64), _P]),

@@ -270,15 +270,6 @@ int gen_measure(const fury_schema* s, const fury_column* cols, int64_t nrows, in
 }  // namespace
 }  // namespace fury
 
-struct fury_decode_plan {
-  const fury_schema* schema = nullptr;
-  const uint8_t* rows = nullptr;
-  const int64_t* offs = nullptr;
-  int64_t nrows = 0;
-  int64_t* cnt = nullptr;      // [2 * nodes][nrows] scanned start positions
-  bool arrow = false;
-};
-
 using namespace fury;
 
 extern "C" {
@@ -481,6 +472,7 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
     if (node_entries) node_entries[i] = totals[2 * i];
     if (node_bytes) node_bytes[i] = totals[2 * i + 1];
   }
+  p->totals = totals;
   *plan = p;
   return FURY_OK;
 }
@@ -497,6 +489,8 @@ int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, v
 void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
   if (p->cnt) (void)hipFree(p->cnt);
+  if (p->owned) (void)hipFree(p->owned);
+  if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
   delete p;
 }
 

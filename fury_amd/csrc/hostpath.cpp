@@ -283,7 +283,8 @@ int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* ro
                     int64_t n, fury_column* host, int32_t device) {
   if (s->generic)
     return set_error(FURY_ERR_UNSUPPORTED,
-                     "host-memory decode of nested schemas: use the device API (fury_decode_prepare)");
+                     "host-memory decode of a nested schema: its output sizes depend on the data; "
+                     "use fury_decode_host_prepare / fury_decode_host_execute");
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
   Streams ss;
@@ -383,12 +384,149 @@ int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* ro
   return ss.sync();
 }
 
+// Bytes of node buffers with m entries / b payload bytes (fury_row.h two-step decode contract).
+int64_t node_values_bytes(int32_t t, int64_t m, int64_t b) {
+  if (t == FURY_TYPE_BOOL) return (m + 7) / 8;
+  if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY) return b;
+  if (t == FURY_TYPE_DECIMAL) return 16 * m;
+  const int w = type_width_of(t);
+  return w > 0 ? m * w : 0;
+}
+bool node_has_offsets(int32_t t) {
+  return t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST ||
+         t == FURY_TYPE_MAP;
+}
+
 }  // namespace
 }  // namespace fury
 
 using namespace fury;
 
 extern "C" {
+
+int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64_t* row_offsets,
+                             int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
+                             fury_decode_plan** plan, int32_t device) {
+  if (!s || !plan) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_decode_host_prepare: null argument");
+  *plan = nullptr;
+  if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "nrows < 0");
+  if (nrows > 0 && (!rows || (!row_offsets && !s->is_fixed)))
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "rows / row_offsets is null");
+  if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  hipStream_t hs = nullptr;
+  if ((st = check_hip(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking), "hipStreamCreate")))
+    return st;
+  // stage the rows and their offsets (fixed-width rows: offsets i * fixed_size) in HBM
+  const int64_t total = nrows == 0 ? 0 : s->is_fixed && !row_offsets ? nrows * s->fixed_size
+                                                                      : row_offsets[nrows];
+  uint8_t* d = nullptr;
+  const int64_t rb = (total + 255) & ~int64_t(255);
+  st = check_hip(hipMalloc(reinterpret_cast<void**>(&d), rb + (nrows + 1) * 8 + 16), "hipMalloc");
+  if (st) {
+    (void)hipStreamDestroy(hs);
+    return st;
+  }
+  int64_t* doffs = reinterpret_cast<int64_t*>(d + rb);
+  if (total > 0) (void)hipMemcpyAsync(d, rows, total, hipMemcpyHostToDevice, hs);
+  if (nrows > 0) {
+    if (row_offsets) {
+      (void)hipMemcpyAsync(doffs, row_offsets, (nrows + 1) * 8, hipMemcpyHostToDevice, hs);
+    } else {
+      std::vector<int64_t> o(nrows + 1);
+      for (int64_t i = 0; i <= nrows; i++) o[i] = i * s->fixed_size;
+      (void)hipMemcpyAsync(doffs, o.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, hs);
+      if ((st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) {
+        (void)hipFree(d);
+        (void)hipStreamDestroy(hs);
+        return st;
+      }
+    }
+  }
+  fury_decode_plan* p = nullptr;
+  st = fury_decode_prepare(s, d, doffs, nrows, node_entries, node_bytes, &p, hs);
+  if (st) {
+    (void)hipFree(d);
+    (void)hipStreamDestroy(hs);
+    return st;
+  }
+  p->owned = d;
+  p->owned_stream = hs;
+  p->device = device;
+  *plan = p;
+  return FURY_OK;
+}
+
+int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
+  if (!p || !p->owned_stream)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "fury_decode_host_execute: needs a plan from fury_decode_host_prepare");
+  const fury_schema* s = p->schema;
+  if (s->num_fields > 0 && !host) return set_error(FURY_ERR_INVALID_ARGUMENT, "columns is null");
+  int st = check_hip(hipSetDevice(p->device), "hipSetDevice");
+  if (st) return st;
+  hipStream_t hs = static_cast<hipStream_t>(p->owned_stream);
+  const int nn = static_cast<int>(s->nodes.size());
+  // the host column tree in node (breadth-first) order
+  std::vector<const fury_column*> hc(nn, nullptr);
+  for (int k = 0; k < s->num_fields; k++) hc[k] = &host[k];
+  for (int i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    if (!hc[i]) return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": missing column");
+    if (t.num_children > 0) {
+      if (!hc[i]->child) return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": child columns missing");
+      for (int j = 0; j < t.num_children; j++) hc[t.first_child + j] = &hc[i]->child[j];
+    }
+  }
+  DeviceArena arena;
+  std::vector<fury_column> dc(nn);
+  for (int i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    const fury_column& h = *hc[i];
+    const int64_t m = p->totals[2 * i], b = p->totals[2 * i + 1];
+    fury_column& d = dc[i];
+    d = fury_column{};
+    void* v = nullptr;
+    if (h.validity) {
+      if ((st = arena.alloc(bitmap_alloc(m), &v))) return st;
+      (void)hipMemsetAsync(v, 0, bitmap_alloc(m), hs);
+      d.validity = static_cast<uint8_t*>(v);
+    }
+    if (node_has_offsets(t.type_id)) {
+      if (!h.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": output offsets is null");
+      if ((st = arena.alloc((m + 1) * 4, &v))) return st;
+      d.offsets = static_cast<int32_t*>(v);
+    }
+    const int64_t vb = node_values_bytes(t.type_id, m, b);
+    if (t.type_id != FURY_TYPE_LIST && t.type_id != FURY_TYPE_MAP && t.type_id != FURY_TYPE_STRUCT) {
+      if (!h.values && vb > 0)
+        return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": output values is null");
+      if ((t.type_id == FURY_TYPE_STRING || t.type_id == FURY_TYPE_BINARY) && h.capacity < vb)
+        return set_error(FURY_ERR_CAPACITY, "node " + std::to_string(i) + " needs " +
+                                                std::to_string(vb) + " payload bytes");
+      const int64_t alloc = t.type_id == FURY_TYPE_BOOL ? bitmap_alloc(m) : vb + 16;
+      if ((st = arena.alloc(alloc, &v))) return st;
+      if (t.type_id == FURY_TYPE_BOOL) (void)hipMemsetAsync(v, 0, alloc, hs);
+      d.values = v;
+      d.capacity = vb;
+    }
+    if (t.num_children > 0) d.child = &dc[t.first_child];
+  }
+  if ((st = fury_decode_execute(p, dc.data(), 0, hs))) return st;
+  for (int i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    const fury_column& h = *hc[i];
+    const fury_column& d = dc[i];
+    const int64_t m = p->totals[2 * i], b = p->totals[2 * i + 1];
+    if (h.validity && m > 0)
+      (void)hipMemcpyAsync(h.validity, d.validity, (m + 7) / 8, hipMemcpyDeviceToHost, hs);
+    if (d.offsets) (void)hipMemcpyAsync(h.offsets, d.offsets, (m + 1) * 4, hipMemcpyDeviceToHost, hs);
+    const int64_t vb = node_values_bytes(t.type_id, m, b);
+    if (d.values && vb > 0) (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
+  }
+  return check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+}
 
 int fury_host_register(void* p, int64_t bytes) {
   if (!p || bytes <= 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_host_register: empty range");

@@ -65,6 +65,20 @@ struct fury_schema {
   std::vector<fury::GenTpl> nodes;
 };
 
+// Decode plan of the two-step (nested) decode, device and host-memory flavours.
+struct fury_decode_plan {
+  const fury_schema* schema = nullptr;
+  const uint8_t* rows = nullptr;
+  const int64_t* offs = nullptr;
+  int64_t nrows = 0;
+  int64_t* cnt = nullptr;          // [2 * nodes][nrows] scanned start positions
+  bool arrow = false;
+  std::vector<int64_t> totals;     // per node: Arrow entries, payload bytes
+  void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)
+  void* owned_stream = nullptr;    // host flavour: its stream
+  int32_t device = 0;
+};
+
 namespace fury {
 
 // Per-thread last error (fury_last_error).

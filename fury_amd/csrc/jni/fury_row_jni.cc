@@ -164,4 +164,51 @@ JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeD
   if (st) throw_status(env, st);
 }
 
+JNIEXPORT jint JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeSchemaNumNodes(
+    JNIEnv*, jclass, jlong schema) {
+  return fury_schema_num_nodes(reinterpret_cast<const fury_schema*>(schema));
+}
+
+// Nested schemas, step 1: rows staged in HBM, per node (breadth-first) Arrow entries and payload
+// bytes into counts[2 * i], counts[2 * i + 1]; returns the plan.
+JNIEXPORT jlong JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeDecodeHostPrepare(
+    JNIEnv* env, jclass, jlong schema, jlong rows, jlong row_offsets, jlong nrows,
+    jlongArray counts, jint device) {
+  const fury_schema* s = reinterpret_cast<const fury_schema*>(schema);
+  const int nn = fury_schema_num_nodes(s);
+  std::vector<int64_t> e(nn > 0 ? nn : 1), b(nn > 0 ? nn : 1);
+  fury_decode_plan* plan = nullptr;
+  const int st = fury_decode_host_prepare(s, reinterpret_cast<const void*>(rows),
+                                          reinterpret_cast<const int64_t*>(row_offsets), nrows,
+                                          e.data(), b.data(), &plan, device);
+  if (st) {
+    throw_status(env, st);
+    return 0;
+  }
+  std::vector<jlong> c(2 * static_cast<size_t>(nn));
+  for (int i = 0; i < nn; i++) {
+    c[2 * i] = e[i];
+    c[2 * i + 1] = b[i];
+  }
+  env->SetLongArrayRegion(counts, 0, static_cast<jsize>(c.size()), c.data());
+  return reinterpret_cast<jlong>(plan);
+}
+
+// Step 2: decode into the host buffers the caller sized from the counts (descriptor tree as
+// nativeDecodeHost), copy back.
+JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeDecodeHostExecute(
+    JNIEnv* env, jclass, jlong schema, jlong plan, jlongArray desc) {
+  const fury_schema* s = reinterpret_cast<const fury_schema*>(schema);
+  ColumnTree tree;
+  std::vector<fury_column> cols;
+  int st = columns_from(env, s, desc, &tree, &cols);
+  if (!st) st = fury_decode_host_execute(reinterpret_cast<fury_decode_plan*>(plan), cols.data());
+  if (st) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeDecodePlanDestroy(
+    JNIEnv*, jclass, jlong plan) {
+  fury_decode_plan_destroy(reinterpret_cast<fury_decode_plan*>(plan));
+}
+
 }  // extern "C"

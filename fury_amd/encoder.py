@@ -568,6 +568,8 @@ class RowEncoder:
         numpy columns are allocated: validity for nullable fields, and payload / element
         buffers bounded by the row bytes (a row holds every byte it decodes to)."""
         from .workloads import Column as C
+        if self.nested and out is None:
+            return self._decode_host_nested(rows, row_offsets, nrows, device_index)
         if out is None:
             out = []
             rb = max(_nbytes(rows), 16)
@@ -593,6 +595,31 @@ class RowEncoder:
         _check(N.lib().fury_row_decode_host(self._schema.handle, _hptr(rows), _hptr(row_offsets),
                                             nrows, _c_host_columns(out, keep), device_index))
         return out
+
+    def _decode_host_nested(self, rows, row_offsets, nrows: int, device_index: int = 0):
+        """Nested schemas through fury_decode_host_prepare / fury_decode_host_execute: node
+        sizes first, then numpy buffers of exactly those sizes, filled in one call."""
+        L = N.lib()
+        h = self._schema.handle
+        nn = L.fury_schema_num_nodes(h)
+        entries = (ctypes.c_int64 * max(nn, 1))()
+        nbytes = (ctypes.c_int64 * max(nn, 1))()
+        plan = ctypes.c_void_p()
+        _check(L.fury_decode_host_prepare(h, _hptr(rows), _hptr(row_offsets), nrows, entries,
+                                          nbytes, ctypes.byref(plan), device_index))
+        try:
+            order = _bfs(self._schema.fields)
+            cols = [_alloc_host_node(f, int(entries[i]), int(nbytes[i]))
+                    for i, (f, _) in enumerate(order)]
+            for i, (f, first) in enumerate(order):
+                if f.children:
+                    cols[i].child = [cols[first + j] for j in range(len(f.children))]
+            top = cols[:len(self._schema.fields)]
+            keep: list = []
+            _check(L.fury_decode_host_execute(plan, _c_host_columns(top, keep)))
+        finally:
+            L.fury_decode_plan_destroy(plan)
+        return top
 
     # -- framing (Encoders.java:165-182, 201-213) ------------------------------------------
     def frame(self, batch: RowBatch, stream=None):
@@ -679,6 +706,27 @@ def _bfs(fields: Sequence[Field]):
         q.extend(f.children)
         i += 1
     return out
+
+
+def _alloc_host_node(f: Field, m: int, nbytes: int) -> Column:
+    """Host (numpy) buffers for one schema node with m Arrow entries (fury_decode_host_execute
+    contract: exact sizes)."""
+    vb = np.zeros((m + 7) // 8 + 8, np.uint8)
+    t = f.type_id
+    if t == BOOL:
+        return Column(values=np.zeros((m + 7) // 8 + 8, np.uint8), validity=vb)
+    if type_width(t) > 0:
+        return Column(values=np.zeros(m * type_width(t) + 8, np.uint8), validity=vb)
+    if t in (STRING, BINARY):
+        return Column(values=np.zeros(max(nbytes, 1), np.uint8), validity=vb,
+                      offsets=np.zeros(m + 1, np.int32))
+    if t == DECIMAL:
+        return Column(values=np.zeros(16 * m + 16, np.uint8), validity=vb)
+    if t in (LIST, MAP):
+        return Column(validity=vb, offsets=np.zeros(m + 1, np.int32))
+    if t == STRUCT:
+        return Column(validity=vb)
+    raise UnsupportedOperationException(f"no device decode for {f}")
 
 
 def _alloc_node(f: Field, m: int, nbytes: int, validity: bool, device) -> Column:

@@ -285,10 +285,25 @@ int fury_row_encode_host(const fury_schema* schema, const fury_column* columns, 
                          int64_t* row_bytes, int32_t device);
 /* Host rows -> host columns (fromRow semantics, like fury_row_decode).  Variable-length flat
  * schemas: STRING/BINARY payload capacity in fury_column.capacity, LIST element bytes in the
- * child's capacity (FURY_ERR_CAPACITY when short); nested schemas: FURY_ERR_UNSUPPORTED (use
- * the device API). */
+ * child's capacity (FURY_ERR_CAPACITY when short); nested schemas: FURY_ERR_UNSUPPORTED (their
+ * output sizes depend on the data: fury_decode_host_prepare / fury_decode_host_execute below). */
 int fury_row_decode_host(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                          int64_t nrows, fury_column* columns, int32_t device);
+
+/* Host-memory decode of ANY schema (nested beans, maps, lists of structs / strings, collection
+ * schemas), in the two steps of the device API (the output sizes depend on the data):
+ * fury_decode_host_prepare stages the rows in HBM and returns every schema node's Arrow entries
+ * and payload bytes (breadth-first node order, see fury_decode_prepare); the caller allocates the
+ * host buffers from them (validity (entries + 7) / 8 bytes, offsets entries + 1 int32, values
+ * entries * width / (entries + 7) / 8 for BOOL / node_bytes for STRING-BINARY (checked against
+ * fury_column.capacity) / 16 * entries for DECIMAL) and calls fury_decode_host_execute, which
+ * decodes in HBM and copies every buffer back (synchronous).  The plan is freed by
+ * fury_decode_plan_destroy.  Replaces generated fromRow + ArrowWriter for nested beans
+ * (FMT/encoder/BaseBinaryEncoderBuilder.java:459-706, FMT/vectorized/ArrowWriter.java:519-640). */
+int fury_decode_host_prepare(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                             int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
+                             fury_decode_plan** plan, int32_t device);
+int fury_decode_host_execute(fury_decode_plan* plan, fury_column* columns);
 
 /* ---- Arrow IPC (ArrowUtils.serializeRecordBatch, FMT/vectorized/ArrowUtils.java:63-72;
  *      ArrowSerializers stream writers, FMT/vectorized/ArrowSerializers.java:128-167) --------- */

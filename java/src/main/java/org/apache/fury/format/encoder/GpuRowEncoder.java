@@ -9,8 +9,9 @@
  * exact bytes and exceptions.
  * Batch API: Arrow columns (a VectorSchemaRoot, as ArrowWriter produces them, ArrowWriter.java:
  * 55-99) <-> packed rows in off-heap MemoryBuffers, through fury_row_encode_host /
- * fury_row_decode_host (include/fury_row.h): the buffers' addresses cross JNI, the bytes cross
- * PCIe inside the native call, the rows are bit-identical to toRow(obj) for every object.
+ * fury_row_decode_host, and fury_decode_host_prepare / _execute for nested beans
+ * (include/fury_row.h): the buffers' addresses cross JNI, the bytes cross PCIe inside the native
+ * call, the rows are bit-identical to toRow(obj) for every object.
  */
 package org.apache.fury.format.encoder;
 
@@ -38,6 +39,8 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
   private final RowEncoder<T> cpu;
   private final long schemaHandle;      // fury_schema*, freed by close()
   private final int device;
+  private final boolean nested;         // nested beans / maps / lists of var elements
+  private final int numNodes;
 
   public GpuRowEncoder(Class<T> beanClass, int device) {
     this.cpu = Encoders.bean(beanClass);
@@ -53,6 +56,25 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
     }
     this.schemaHandle =
         nativeSchemaCreate(names.toArray(new String[0]), m, cpu.schema().getFields().size());
+    this.numNodes = nativeSchemaNumNodes(schemaHandle);
+    boolean deep = false;
+    for (Field f : cpu.schema().getFields()) {
+      deep |= isNested(f);
+    }
+    this.nested = deep;
+  }
+
+  private static boolean isNested(Field f) {
+    org.apache.arrow.vector.types.pojo.ArrowType t = f.getType();
+    if (t instanceof org.apache.arrow.vector.types.pojo.ArrowType.Struct
+        || t instanceof org.apache.arrow.vector.types.pojo.ArrowType.Map) {
+      return true;
+    }
+    if (t instanceof org.apache.arrow.vector.types.pojo.ArrowType.List) {
+      Field e = f.getChildren().get(0);
+      return DataTypes.getTypeWidth(e.getType()) < 0 || isNested(e);
+    }
+    return false;
   }
 
   // ---- RowEncoder<T>: the reference implementation, unchanged ----------------------------
@@ -78,20 +100,80 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
         rows.size(), rowOffsets == null ? 0 : addressOf(rowOffsets), device);
   }
 
-  /** Decodes nrows rows into `out` (vectors allocated by the caller for nrows values and, for
-   * strings / lists, enough payload capacity); sets the value counts. */
+  /** Decodes nrows rows into `out`.  Flat schemas: vectors allocated by the caller for nrows
+   * values and, for strings / lists, enough payload capacity.  Schemas with nested beans, maps or
+   * lists of structs / strings: the vectors are (re)allocated here from the per-node sizes the
+   * device counts (fury_decode_host_prepare), then filled (fury_decode_host_execute).  Sets the
+   * value counts. */
   public void decodeBatch(MemoryBuffer rows, MemoryBuffer rowOffsets, int nrows,
                           VectorSchemaRoot out) {
     checkOffHeap(rows);
+    long offs = rowOffsets == null ? 0 : addressOf(rowOffsets);
+    if (nested) {
+      decodeNested(rows.getUnsafeAddress(), offs, nrows, out);
+      return;
+    }
     long[] desc = describe(out, true);
-    nativeDecodeHost(schemaHandle, rows.getUnsafeAddress(),
-        rowOffsets == null ? 0 : addressOf(rowOffsets), nrows, desc, device);
-    out.setRowCount(nrows);
-    for (FieldVector v : out.getFieldVectors()) {
+    nativeDecodeHost(schemaHandle, rows.getUnsafeAddress(), offs, nrows, desc, device);
+    for (FieldVector v : out.getFieldVectors()) {       // offsets are written: no hole filling
       if (v instanceof BaseVariableWidthVector) {
         ((BaseVariableWidthVector) v).setLastSet(nrows - 1);
+      } else if (v instanceof ListVector) {
+        ((ListVector) v).setLastSet(nrows - 1);
       }
     }
+    out.setRowCount(nrows);
+  }
+
+  private void decodeNested(long rows, long rowOffsets, int nrows, VectorSchemaRoot out) {
+    long[] counts = new long[2 * numNodes];             // per node: entries, payload bytes
+    long plan = nativeDecodeHostPrepare(schemaHandle, rows, rowOffsets, nrows, counts, device);
+    try {
+      List<FieldVector> nodes = breadthFirst(out);      // the C ABI's node order
+      for (int i = 0; i < nodes.size(); i++) {          // parents before children
+        FieldVector v = nodes.get(i);
+        int entries = (int) counts[2 * i];
+        if (v instanceof BaseVariableWidthVector) {
+          ((BaseVariableWidthVector) v).allocateNew(Math.max(counts[2 * i + 1], 1), entries);
+        } else {
+          v.setInitialCapacity(entries);
+          v.allocateNew();
+        }
+      }
+      nativeDecodeHostExecute(schemaHandle, plan, describe(out, true));
+      for (int i = nodes.size() - 1; i >= 0; i--) {     // children first
+        FieldVector v = nodes.get(i);
+        int entries = (int) counts[2 * i];
+        if (v instanceof BaseVariableWidthVector) {
+          ((BaseVariableWidthVector) v).setLastSet(entries - 1);
+        } else if (v instanceof ListVector) {
+          ((ListVector) v).setLastSet(entries - 1);
+        }
+        v.setValueCount(entries);
+      }
+      out.setRowCount(nrows);
+    } finally {
+      nativeDecodePlanDestroy(plan);
+    }
+  }
+
+  /** Vectors in the schema-node order of fury_row.h: top-level fields, then every node's
+   * children (LIST: data vector; STRUCT: fields; MAP: key, value -- the entries struct skipped). */
+  private static List<FieldVector> breadthFirst(VectorSchemaRoot root) {
+    List<FieldVector> q = new ArrayList<>(root.getFieldVectors());
+    for (int i = 0; i < q.size(); i++) {
+      FieldVector v = q.get(i);
+      if (v instanceof MapVector) {
+        StructVector entries = (StructVector) ((MapVector) v).getDataVector();
+        q.add((FieldVector) entries.getChildByOrdinal(0));
+        q.add((FieldVector) entries.getChildByOrdinal(1));
+      } else if (v instanceof ListVector) {
+        q.add(((ListVector) v).getDataVector());
+      } else if (v instanceof StructVector) {
+        q.addAll(((StructVector) v).getChildrenFromFields());
+      }
+    }
+    return q;
   }
 
   public void close() {
@@ -177,4 +259,9 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
                                               long rowsCapacity, long rowOffsets, int device);
   private static native void nativeDecodeHost(long schema, long rows, long rowOffsets, long nrows,
                                               long[] columns, int device);
+  private static native int nativeSchemaNumNodes(long schema);
+  private static native long nativeDecodeHostPrepare(long schema, long rows, long rowOffsets,
+                                                     long nrows, long[] counts, int device);
+  private static native void nativeDecodeHostExecute(long schema, long plan, long[] columns);
+  private static native void nativeDecodePlanDestroy(long plan);
 }
