@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -42,11 +43,19 @@ uint32_t* device_error_word() {
   return g_err_dev;
 }
 
+std::atomic<int64_t> g_err_taken{0};
+
+int64_t device_error_count() {
+  const volatile uint32_t* w = g_err_host;
+  return g_err_taken.load() + (w && *w ? 1 : 0);
+}
+
 int take_device_error() {
   if (!g_err_host) return FURY_OK;
   volatile uint32_t* w = g_err_host;
   if (*w == 0) return FURY_OK;
   *w = 0;
+  g_err_taken.fetch_add(1);
   return set_error(FURY_ERR_DEVICE,
                    "an earlier asynchronous launch failed on the device (a decoupled look-back "
                    "gave up waiting): the outputs of that call are invalid");
@@ -190,7 +199,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   if (const char* e = getenv("FURY_VAR_DBG")) {
     a->dbg = atoi(e);
     const char* d = getenv("FURY_DIAGNOSTIC");
-    if (!d || std::string(d) != "1") a->dbg &= ~127;
+    if (!d || std::string(d) != "1") a->dbg &= ~255;
   }
   return FURY_OK;
 }

@@ -72,6 +72,7 @@ struct VarArgs {
 // the thread's last error (FURY_ERR_DEVICE) when it was raised.
 uint32_t* device_error_word();
 int take_device_error();
+int64_t device_error_count();        // failures raised so far (taken or pending), no sync
 
 // Device scratch for scans; grown on demand (hipMalloc outside graph capture only).
 struct Workspace {

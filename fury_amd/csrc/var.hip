@@ -1,1850 +1,13 @@
-// var.hip — gfx950 kernels for schemas with variable-length fields (STRING/BINARY, DECIMAL,
-// LIST of fixed-width elements): row-size measure + device scan, encode, decode-measure,
-// decode / row->Arrow, and the [int32 len][int64 hash][row] stream framing.
-//
-// Reference semantics (FMT = java/fury-format/src/main/java/org/apache/fury/format):
-//   var bytes  BinaryWriter.writeUnaligned: append at the writer index, pad to 8 with zeros
-//              (pad word zeroed first), slot = (relativeOffset << 32) | unpaddedSize
-//              (FMT/row/binary/writer/BinaryWriter.java:106-121,187-194)
-//   decimal    BinaryWriter.writeDecimal: 16 bytes appended (BinaryWriter.java:204-219)
-//   list       serializeFor(List) -> BinaryArrayWriter.reset(n) + per-element write, slot =
-//              offset/size of [int64 n][bitmap][values, tail zeroed]
-//              (FMT/encoder/BaseBinaryEncoderBuilder.java:198-278,
-//               FMT/row/binary/writer/BinaryArrayWriter.java:91-163)
-//   decode     UnsafeTrait.getBinary / getArray + BinaryArray.toXxxArray
-//              (FMT/row/binary/UnsafeTrait.java:115-178, BinaryArray.java:69-78,157-197);
-//   to Arrow   ArrowWriter StringWriter / ListWriter (FMT/vectorized/ArrowWriter.java:421-540)
-//
-// MI355X design: one workgroup of 256 threads owns 256 consecutive rows, i.e. one contiguous
-// byte range of the row buffer (rows are packed by the exclusive scan of their sizes).  The
-// group builds (encode) or reads (decode) its rows through an LDS image of that range so that
-// global traffic is 16-byte-per-lane contiguous even though each row is built by one thread;
-// ranges larger than the LDS budget fall back to direct 8-byte global accesses.
-#include <hip/hip_runtime.h>
-
-#include <cstdint>
-#include <cstring>
-#include <string>
-
-#include "internal.h"
-#include "kernels.h"
+// var.hip — host launchers of the variable-length kernels (schemas with STRING/BINARY, DECIMAL,
+// LIST of fixed-width elements) and the kernels other than the register-staged ones; the device
+// code is in var_dev.h, the register-staged template instances in var_reg_enc.hip and
+// var_reg_dec_{lo,hi}.hip (separate translation units so they compile in parallel).
+#define FURY_VAR_MAIN
+#include "var_dev.h"
 
 namespace fury {
 
 namespace {
-
-constexpr int kThreads = 256;                 // = rows per workgroup
-constexpr int kDecodeStage = 32 * 1024;       // LDS image of the group's row range (decode)
-constexpr int kStrStage = 8 * 1024;           // LDS image of one column's Arrow payload range
-
-__device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
-  return (bits[i >> 3] >> (i & 7)) & 1;
-}
-__device__ __forceinline__ int64_t rnd8(int64_t n) { return (n + 7) & ~int64_t(7); }
-__host__ __device__ __forceinline__ int64_t r16(int64_t x) { return (x + 15) & ~int64_t(15); }
-__device__ __forceinline__ int64_t bm_bytes(int64_t n) { return ((n + 63) >> 6) << 3; }
-
-__device__ __forceinline__ uint64_t load_fixed(const uint8_t* p, int64_t i, int w) {
-  switch (w) {
-    case 8: return *reinterpret_cast<const uint64_t*>(p + i * 8);
-    case 4: return *reinterpret_cast<const uint32_t*>(p + i * 4);
-    case 2: return *reinterpret_cast<const uint16_t*>(p + i * 2);
-    case 1: return p[i];
-    default: return bit_at(p, i);
-  }
-}
-
-// 64-lane block scan helpers -------------------------------------------------------------------
-__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int64_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
-}
-
-// Exclusive scan over the NT threads of the block; *total gets the block sum.
-template <int NT = kThreads>
-__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* total, int64_t* tmp) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t x = wave_incl_scan(v);
-  if (lane == 63) tmp[wid] = x;
-  __syncthreads();
-  int64_t pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < NT / 64; w++) {
-    const int64_t s = tmp[w];
-    pre += (w < wid) ? s : 0;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return pre + x - v;
-}
-
-// --- encode side -------------------------------------------------------------------------------
-
-// Copies len bytes from an unaligned source to an 8-byte aligned destination as whole 8-byte
-// words, zero-filling the pad (writeUnaligned + zeroOutPaddingBytes).  Source words are read
-// aligned; no word past the one holding the last source byte is touched.
-__device__ __forceinline__ void copy_to_aligned(uint64_t* dst, const uint8_t* src, int64_t len) {
-  if (len <= 0) return;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src) & 7;
-  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s);
-  if (len <= 32) {
-    // short string: every source word is requested before any is used (one memory latency
-    // instead of one per word); words past the last source byte are not read
-    const int nsrc = static_cast<int>((s + len + 7) >> 3);       // <= 5
-    uint64_t w[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) w[j] = j < nsrc ? ap[j] : 0;
-    const int nw = static_cast<int>((len + 7) >> 3);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      if (k < nw) {
-        uint64_t x = s ? (w[k] >> (8 * s)) | (w[k + 1] << (64 - 8 * s)) : w[k];
-        const int64_t rem = len - 8 * k;
-        if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
-        dst[k] = x;
-      }
-    }
-    return;
-  }
-  const int64_t nw = (len + 7) >> 3;
-  const int64_t last_src_word = (static_cast<int64_t>(s) + len - 1) >> 3;
-  uint64_t lo = ap[0];
-  for (int64_t k = 0; k < nw; k++) {
-    uint64_t w;
-    if (s == 0) {
-      w = (k == 0) ? lo : ap[k];
-    } else {
-      const uint64_t hi = (k + 1 <= last_src_word) ? ap[k + 1] : 0;
-      w = (lo >> (8 * s)) | (hi << (64 - 8 * s));
-      lo = hi;
-    }
-    const int64_t rem = len - 8 * k;
-    if (rem < 8) w &= (~0ull) >> (8 * (8 - rem));
-    dst[k] = w;
-  }
-}
-
-// BinaryArrayWriter image of n elements of a fixed-width list column; returns its size.
-// `vals` points at the first element's value bytes, `vbits`/`vbit0` at its Arrow validity bit
-// (vbits == nullptr: no element nulls).  Sources may be global or an LDS staging copy.
-__device__ int64_t write_array(uint8_t* dst, int width, const uint8_t* vals, const uint8_t* vbits,
-                               int64_t vbit0, int64_t n) {
-  const int ew = width == 0 ? 1 : width;
-  const int64_t hb = 8 + bm_bytes(n);
-  const int64_t data = n * ew;
-  const int64_t fp = rnd8(data);
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  d64[0] = static_cast<uint64_t>(n);                     // numElements as an 8-byte word
-  for (int64_t w = 0; w < (hb - 8) >> 3; w++) {          // element null bits (bit = 1 null)
-    uint64_t word = 0;
-    if (vbits) {
-      const int64_t lim = min<int64_t>(64, n - 64 * w);
-      for (int64_t t = 0; t < lim; t++)
-        if (!bit_at(vbits, vbit0 + 64 * w + t)) word |= 1ull << t;
-    }
-    d64[1 + w] = word;
-  }
-  uint64_t* out = reinterpret_cast<uint64_t*>(dst + hb);
-  if (width == 8 && !vbits) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(vals);
-    for (int64_t j = 0; j < n; j++) out[j] = src[j];
-    return hb + fp;
-  }
-  const int per = 8 / ew;
-  for (int64_t q = 0; q < (fp >> 3); q++) {
-    uint64_t word = 0;
-    for (int t = 0; t < per; t++) {
-      const int64_t j = q * per + t;
-      if (j >= n) break;
-      if (vbits && !bit_at(vbits, vbit0 + j)) continue;   // null element stays 0
-      uint64_t v;
-      switch (width) {
-        case 8: v = reinterpret_cast<const uint64_t*>(vals)[j]; break;
-        case 4: v = reinterpret_cast<const uint32_t*>(vals)[j]; break;
-        case 2: v = reinterpret_cast<const uint16_t*>(vals)[j]; break;
-        case 1: v = vals[j]; break;
-        default: v = bit_at(vals, vbit0 + j); break;       // bool: bit-packed, same bit origin
-      }
-      word |= (ew == 8) ? v : (v << (8 * ew * t));
-    }
-    out[q] = word;
-  }
-  return hb + fp;
-}
-
-// Cooperative 8-byte-aligned copy of [0, bytes) between LDS and global (16 B per lane when the
-// global side is 16-byte aligned).
-template <bool kToGlobal, int NT = kThreads>
-__device__ __forceinline__ void copy_range(uint8_t* g, uint8_t* l, int64_t bytes) {
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  int64_t head = 0;
-  if ((reinterpret_cast<uintptr_t>(g) & 15) && bytes >= 8) head = 8;
-  if (head && threadIdx.x == 0) {
-    if (kToGlobal) *reinterpret_cast<uint64_t*>(g) = *reinterpret_cast<uint64_t*>(l);
-    else *reinterpret_cast<uint64_t*>(l) = *reinterpret_cast<uint64_t*>(g);
-  }
-  const int64_t body = (bytes - head) >> 4;
-  // LDS side may be only 8-aligned at g+head: move 2 x 8 bytes per lane on the LDS side.
-  for (int64_t i = threadIdx.x; i < body; i += NT) {
-    uint8_t* gp = g + head + 16 * i;
-    uint8_t* lp = l + head + 16 * i;
-    if (kToGlobal) {
-      const uint64_t x = reinterpret_cast<uint64_t*>(lp)[0], y = reinterpret_cast<uint64_t*>(lp)[1];
-      v4 v;
-      v.x = static_cast<uint32_t>(x); v.y = static_cast<uint32_t>(x >> 32);
-      v.z = static_cast<uint32_t>(y); v.w = static_cast<uint32_t>(y >> 32);
-      __builtin_nontemporal_store(v, reinterpret_cast<v4*>(gp));
-    } else {
-      const v4 v = __builtin_nontemporal_load(reinterpret_cast<const v4*>(gp));
-      reinterpret_cast<uint64_t*>(lp)[0] = (static_cast<uint64_t>(v.y) << 32) | v.x;
-      reinterpret_cast<uint64_t*>(lp)[1] = (static_cast<uint64_t>(v.w) << 32) | v.z;
-    }
-  }
-  const int64_t done = head + 16 * body;
-  if (done < bytes && threadIdx.x == NT - 1) {    // one trailing 8-byte word
-    if (kToGlobal) *reinterpret_cast<uint64_t*>(g + done) = *reinterpret_cast<uint64_t*>(l + done);
-    else *reinterpret_cast<uint64_t*>(l + done) = *reinterpret_cast<uint64_t*>(g + done);
-  }
-}
-
-// Exclusive scan of small arrays (<= kSmallScan entries): one workgroup, a few block scans.
-constexpr int64_t kSmallScan = 16 * kThreads;
-__global__ __launch_bounds__(kThreads) void scan_small(int64_t* __restrict__ s, int64_t n,
-                                                       int64_t* __restrict__ total) {
-  __shared__ int64_t tmp[kThreads / 64];
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n; base += kThreads) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < n ? s[i] : 0;
-    int64_t tot;
-    const int64_t ex = block_excl_scan(v, &tot, tmp);
-    if (i < n) s[i] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
-// One level of the hierarchical scan: each workgroup scans 256 entries in place (exclusive) and
-// emits their total.
-__global__ __launch_bounds__(kThreads) void scan_groups(int64_t* __restrict__ s, int64_t n,
-                                                        int64_t* __restrict__ gsum) {
-  __shared__ int64_t tmp[kThreads / 64];
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  const int64_t v = i < n ? s[i] : 0;
-  int64_t tot;
-  const int64_t ex = block_excl_scan(v, &tot, tmp);
-  if (i < n) s[i] = ex;
-  if (threadIdx.x == 0) gsum[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kThreads) void add_groups(int64_t* __restrict__ s, int64_t n,
-                                                       const int64_t* __restrict__ gpre) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (i < n) s[i] += gpre[blockIdx.x];
-}
-
-// --- cross-workgroup scan (decoupled look-back) ---------------------------------------------
-constexpr int kSeqChunk = 8;                          // var outputs resolved per look-back round
-constexpr uint64_t kAgg = 1ull << 62, kInc = 2ull << 62, kValMask = (1ull << 62) - 1;
-
-__device__ __forceinline__ uint64_t ld_status(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int64_t wave_sum(int64_t x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
-}
-
-// One wave: exclusive prefix of logical group b in sequence q.  Status words pack a 2-bit flag
-// (0 = not yet published, kAgg = group total, kInc = inclusive prefix) over a 62-bit value.
-__device__ int64_t look_back(const uint64_t* status, int64_t b, int nseq, int q) {
-  const int lane = threadIdx.x & 63;
-  int64_t excl = 0;
-  for (int64_t j = b - 1;; j -= 64) {
-    const int64_t idx = j - lane;
-    uint64_t v;
-    for (;;) {
-      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
-      if (__ballot((v >> 62) == 0) == 0) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint64_t inc = __ballot((v >> 62) == 2);
-    const int stop = inc ? __builtin_ctzll(inc) : 63;
-    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
-    if (inc) return excl;
-  }
-}
-
-// ---- tile-staged encode ------------------------------------------------------------------------
-// One workgroup of kEncRows threads owns kEncRows consecutive rows.  Every input the tile reads
-// is a contiguous global range (a column's values / validity bytes / offsets for the tile, then
-// each string column's payload bytes and each list column's element values + validity between
-// the tile's first and last offsets), so the tile is staged in LDS by LDS-DMA
-// (global_load_lds_dwordx4: 16-B pieces, no register round trip, all pieces of a phase in flight
-// together): two dependent round trips to HBM per tile (meta, then payloads).  Each thread then
-// builds its row from LDS into an LDS image of the tile's contiguous output range, which leaves
-// with 16-B stores.
-constexpr int kEncRows = 256;                 // threads per encode workgroup = max rows per tile
-constexpr int kEncPool = 50 * 1024;           // LDS: staged inputs + row image (3 groups per CU)
-constexpr int kMetaPool = 16 * 1024;          // bound on a tile's staged per-row inputs
-constexpr uint32_t kNone = 0xffffffffu;
-
-struct PipeLayout {
-  int rows;                   // rows per tile
-  uint32_t msz, psz, isz;     // LDS bytes: meta slot, payload slot, row image
-};
-
-// LDS byte offsets of one tile's staged inputs, per column (kNone = not present / not staged).
-struct MetaMap {
-  uint32_t fix[kMaxVarCols];   // fixed values (row r0) / bool bits (byte r0/8) / decimal values
-  uint32_t val[kMaxVarCols];   // validity bits, byte r0/8
-  uint32_t off[kMaxVarCols];   // int32 offsets, entry r0
-  uint32_t pay[kMaxVarCols];   // payload bytes at offsets[r0] (bool elements: byte offsets[r0]/8)
-  uint32_t pvb[kMaxVarCols];   // list element validity, byte offsets[r0]/8
-};
-
-// Issues LDS-DMA copies of the 16-B-aligned pieces covering [gb, ge) into pool[at...]; returns
-// the LDS offset of byte gb and advances `at` (kept 16-aligned).  Reading whole aligned pieces
-// never leaves the pages holding the range.
-template <int NT>
-__device__ __forceinline__ uint32_t stage_range(uint8_t* pool, uint32_t& at, const uint8_t* gb,
-                                                const uint8_t* ge, bool issue = true) {
-  const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
-  const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
-  const uint32_t nch = static_cast<uint32_t>((hi - lo) >> 4);
-  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t i0 = wave * 64; issue && i0 < nch; i0 += NT) {
-    if (i0 + lane < nch)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * (i0 + lane)),
-                                       pool + at + 16 * i0, 16, 0, 0);
-  }
-  const uint32_t r = at + static_cast<uint32_t>(reinterpret_cast<uint64_t>(gb) - lo);
-  at += nch * 16;
-  return r;
-}
-
-__device__ __forceinline__ int32_t lds_i32(const uint8_t* pool, uint32_t off) {
-  return *reinterpret_cast<const int32_t*>(pool + off);
-}
-__device__ __forceinline__ bool lds_bit(const uint8_t* pool, uint32_t off, int64_t i) {
-  return (pool[off + (i >> 3)] >> (i & 7)) & 1;
-}
-
-// Phase A: stage every column's per-row inputs of rows [r0, r0 + nr).
-template <int NT>
-__device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int64_t nr,
-                                               uint8_t* pool, MetaMap& mm, uint32_t at = 0) {
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    uint32_t fix = kNone, val = kNone, off = kNone;
-    if (c.validity) val = stage_range<NT>(pool, at, c.validity + (r0 >> 3), c.validity + ((r0 + nr + 7) >> 3));
-    switch (c.kind) {
-      case kFixed:
-        fix = stage_range<NT>(pool, at, c.values + r0 * c.width, c.values + (r0 + nr) * c.width);
-        break;
-      case kBool:
-        fix = stage_range<NT>(pool, at, c.values + (r0 >> 3), c.values + ((r0 + nr + 7) >> 3));
-        break;
-      case kDecimal:
-        fix = stage_range<NT>(pool, at, c.values + 16 * r0, c.values + 16 * (r0 + nr));
-        break;
-      default:      // kBytes, kListFixed
-        off = stage_range<NT>(pool, at, reinterpret_cast<const uint8_t*>(c.offsets + r0),
-                              reinterpret_cast<const uint8_t*>(c.offsets + r0 + nr + 1));
-        break;
-    }
-    if (threadIdx.x == 0) {
-      mm.fix[k] = fix;
-      mm.val[k] = val;
-      mm.off[k] = off;
-      mm.pay[k] = kNone;
-      mm.pvb[k] = kNone;
-    }
-  }
-  return at;
-}
-
-// Row size of tile row t from the staged inputs (writerIndex growth of toRow).
-__device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MetaMap& mm,
-                                                 const uint8_t* pool, int t) {
-  int64_t sz = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind < kBytes) continue;
-    if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) continue;
-    if (c.kind == kDecimal) {
-      sz += 16;
-      continue;
-    }
-    const int64_t n = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - lds_i32(pool, mm.off[k] + 4 * t);
-    if (c.kind == kBytes) sz += rnd8(n);
-    else sz += 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
-  }
-  return sz;
-}
-
-// Bytes the payload staging of the tile needs (uniform; from the staged offsets).
-__device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MetaMap& mm,
-                                                 const uint8_t* pool, int nr) {
-  uint64_t need = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
-    if (e <= b) continue;
-    int64_t bytes;
-    if (c.kind == kBytes) bytes = e - b;
-    else if (c.width == 0) bytes = ((e + 7) >> 3) - (b >> 3);
-    else bytes = (e - b) * c.width;
-    need += static_cast<uint64_t>(bytes) + 32;
-    if (c.kind == kListFixed && c.elem_validity) need += static_cast<uint64_t>(((e + 7) >> 3) - (b >> 3)) + 32;
-  }
-  return need;
-}
-
-// Phase C: stage the payload ranges.
-template <int NT>
-__device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, uint8_t* pool,
-                                               uint32_t at, int nr) {
-  const bool iss = !(a.dbg & 1);
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
-    uint32_t pay = kNone, pvb = kNone;
-    if (e > b) {
-      if (c.kind == kBytes) pay = stage_range<NT>(pool, at, c.values + b, c.values + e, iss);
-      else if (c.width == 0) pay = stage_range<NT>(pool, at, c.values + (b >> 3), c.values + ((e + 7) >> 3), iss);
-      else pay = stage_range<NT>(pool, at, c.values + b * c.width, c.values + e * c.width, iss);
-      if (c.kind == kListFixed && c.elem_validity)
-        pvb = stage_range<NT>(pool, at, c.elem_validity + (b >> 3), c.elem_validity + ((e + 7) >> 3), iss);
-    }
-    if (threadIdx.x == 0) {
-      mm.pay[k] = pay;
-      mm.pvb[k] = pvb;
-    }
-  }
-}
-
-// Builds tile row t at dst (8-byte aligned) exactly as toRow does.  Per-row inputs come from the
-// staged meta in `pool`; a column's payload from `pay` when it was staged (mm.pay[k] != kNone),
-// else straight from global memory.
-__device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& mm,
-                                               const uint8_t* pool, const uint8_t* pay, int t,
-                                               uint8_t* dst) {
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    uint64_t slot = 0;
-    if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) {
-      nullbits |= 1ull << k;
-    } else {
-      switch (c.kind) {
-        case kFixed: {
-          const uint8_t* p = pool + mm.fix[k] + t * c.width;
-          switch (c.width) {
-            case 8: slot = *reinterpret_cast<const uint64_t*>(p); break;
-            case 4: slot = *reinterpret_cast<const uint32_t*>(p); break;
-            case 2: slot = *reinterpret_cast<const uint16_t*>(p); break;
-            default: slot = *p; break;
-          }
-          break;
-        }
-        case kBool:
-          slot = lds_bit(pool, mm.fix[k], t);
-          break;
-        case kBytes: {
-          const int64_t ob = lds_i32(pool, mm.off[k]);
-          const int64_t o0 = lds_i32(pool, mm.off[k] + 4 * t);
-          const int64_t len = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - o0;
-          const uint8_t* src = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0 - ob) : c.values + o0;
-          copy_to_aligned(d64 + (cursor >> 3), src, len);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-          cursor += rnd8(len);
-          break;
-        }
-        case kDecimal: {
-          const uint64_t* s = reinterpret_cast<const uint64_t*>(pool + mm.fix[k] + 16 * t);
-          d64[cursor >> 3] = s[0];
-          d64[(cursor >> 3) + 1] = s[1];
-          slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
-          cursor += 16;
-          break;
-        }
-        default: {   // kListFixed
-          const int64_t ob = lds_i32(pool, mm.off[k]);
-          const int64_t o0 = lds_i32(pool, mm.off[k] + 4 * t);
-          const int64_t n = lds_i32(pool, mm.off[k] + 4 * (t + 1)) - o0;
-          const uint8_t* vals;
-          const uint8_t* vb = nullptr;
-          if (c.width == 0)
-            vals = mm.pay[k] != kNone ? pay + mm.pay[k] + ((o0 >> 3) - (ob >> 3)) : c.values + (o0 >> 3);
-          else
-            vals = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0 - ob) * c.width : c.values + o0 * c.width;
-          if (c.elem_validity)
-            vb = mm.pvb[k] != kNone ? pay + mm.pvb[k] + ((o0 >> 3) - (ob >> 3)) : c.elem_validity + (o0 >> 3);
-          const int64_t sz = write_array(dst + cursor, c.width, vals, vb, o0 & 7, n);
-          slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
-          cursor += sz;
-          break;
-        }
-      }
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
-}
-
-// DIAGNOSTIC: build_tile_row with the column kinds known at compile time (experiment on the
-// cost of interpreting the schema at run time).
-struct SpecMixed {
-  static constexpr int n = 6;
-  static constexpr int kind[6] = {kFixed, kFixed, kFixed, kBytes, kBytes, kBytes};
-  static constexpr int width[6] = {4, 8, 8, 1, 1, 1};
-};
-template <class S>
-__device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MetaMap& mm,
-                                                    const uint8_t* pool, const uint8_t* pay, int t,
-                                                    uint8_t* dst) {
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-  bool ok[S::n];
-  uint64_t fixv[S::n];
-  int32_t o0[S::n], o1[S::n], ob[S::n];
-#pragma unroll
-  for (int k = 0; k < S::n; k++) {
-    ok[k] = mm.val[k] == kNone || lds_bit(pool, mm.val[k], t);
-    if (S::kind[k] == kFixed) {
-      const uint8_t* p = pool + mm.fix[k] + t * S::width[k];
-      fixv[k] = S::width[k] == 8 ? *reinterpret_cast<const uint64_t*>(p)
-                                 : *reinterpret_cast<const uint32_t*>(p);
-    } else {
-      ob[k] = lds_i32(pool, mm.off[k]);
-      o0[k] = lds_i32(pool, mm.off[k] + 4 * t);
-      o1[k] = lds_i32(pool, mm.off[k] + 4 * (t + 1));
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < S::n; k++) {
-    const VarCol& c = a.col[k];
-    uint64_t slot = 0;
-    if (!ok[k]) {
-      nullbits |= 1ull << k;
-    } else if (S::kind[k] == kFixed) {
-      slot = fixv[k];
-    } else {
-      const int64_t len = o1[k] - o0[k];
-      const uint8_t* src = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0[k] - ob[k]) : c.values + o0[k];
-      copy_to_aligned(d64 + (cursor >> 3), src, len);
-      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-      cursor += rnd8(len);
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;
-}
-
-// Encode workgroup: rows [r0, r0 + R) at the offsets fury_row_measure produced.  Bytes at or
-// past `cap` are never written.
-template <int POOL, bool kStagePay>
-__device__ __forceinline__ void encode_tile(const VarArgs& a, const int64_t* __restrict__ offs,
-                                            uint8_t* __restrict__ rows, int64_t cap, int64_t tile,
-                                            uint8_t* pool, MetaMap& mm) {
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;                 // rows per tile (host-chosen so the meta fits)
-  const int64_t r0 = tile * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  // the offset loads go out together with the meta DMA
-  const int64_t base = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - base;
-  const int64_t ex = live ? offs[r0 + tid] - base : 0;
-  const uint32_t img_at = stage_meta<kEncRows>(a, r0, nr, pool, mm);
-  __syncthreads();
-  const uint64_t img = static_cast<uint64_t>((bytes + 15) & ~int64_t(15));
-  const bool img_fits = img_at + img <= POOL;
-  const bool pay_fits =
-      kStagePay && img_fits && img_at + img + payload_need(a, mm, pool, nr) <= POOL;
-  if (pay_fits) {
-    stage_payloads<kEncRows>(a, mm, pool, static_cast<uint32_t>(img_at + img), nr);
-    __syncthreads();
-  }
-  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (img_fits) {
-    uint8_t* image = pool + img_at;
-    if (live && (a.dbg & 256)) {
-      build_tile_row_spec<SpecMixed>(a, mm, pool, pool, tid, image + ex);
-    } else if (live && !(a.dbg & 2)) {
-      build_tile_row(a, mm, pool, pool, tid, image + ex);
-    }
-    __syncthreads();
-    if (!(a.dbg & 4)) copy_range<true, kEncRows>(rows + base, image, room);
-  } else if (live && ex + tile_row_size(a, mm, pool, tid) <= room) {
-    build_tile_row(a, mm, pool, pool, tid, rows + base + ex);    // oversized tile: straight to HBM
-  }
-}
-
-__global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
-                                                              const int64_t* __restrict__ offs,
-                                                              uint8_t* __restrict__ rows,
-                                                              int64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
-  __shared__ MetaMap mm;
-  encode_tile<kEncPool, true>(a, offs, rows, cap, blockIdx.x, pool, mm);
-}
-
-// Payloads read straight from global memory (no payload staging): a smaller LDS pool, so more
-// workgroups share a CU.
-constexpr int kEncPoolDirect = 38 * 1024;
-__global__ __launch_bounds__(kEncRows) void encode_var_kernel_d(VarArgs a,
-                                                                const int64_t* __restrict__ offs,
-                                                                uint8_t* __restrict__ rows,
-                                                                int64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPoolDirect];
-  __shared__ MetaMap mm;
-  encode_tile<kEncPoolDirect, false>(a, offs, rows, cap, blockIdx.x, pool, mm);
-}
-
-__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Waits until at most n of this wave's vector-memory operations are outstanding (n uniform).
-// The n youngest are the image stores just issued, so every older operation — the next tile's
-// LDS-DMA — has landed, while the stores keep draining.
-__device__ __forceinline__ void wait_vm_le(int n) {
-  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
-#define FURY_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    FURY_VMW(0) FURY_VMW(1) FURY_VMW(2) FURY_VMW(3) FURY_VMW(4) FURY_VMW(5) FURY_VMW(6)
-    FURY_VMW(7) FURY_VMW(8) FURY_VMW(9) FURY_VMW(10) FURY_VMW(11) FURY_VMW(12) FURY_VMW(13)
-    FURY_VMW(14) FURY_VMW(15)
-#undef FURY_VMW
-  }
-}
-
-// Stores img[0, bytes) to g (any alignment): each wave writes a contiguous quarter of the 16-byte
-// aligned body with 16-B non-temporal stores, wave 0 the unaligned head and wave 3 the tail by
-// single-byte lanes.  Returns the number of store instructions this wave issued (uniform).
-__device__ __forceinline__ int store_image(uint8_t* g, const uint8_t* img, int64_t bytes) {
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (bytes <= 0) return 0;
-  const int64_t head = min<int64_t>(bytes, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
-  const int64_t body = (bytes - head) >> 4;
-  const int64_t tail = bytes - head - 16 * body;
-  int cnt = 0;
-  if (head > 0 && wave == 0) {
-    if (lane < head) g[lane] = img[lane];
-    cnt++;
-  }
-  const int64_t q = (body + 3) >> 2;
-  const int64_t j0 = wave * q, j1 = min<int64_t>(body, j0 + q);
-  for (int64_t j = j0; j < j1; j += 64) {
-    const int64_t i = j + lane;
-    if (i < j1) {
-      const uint8_t* lp = img + head + 16 * i;
-      const uint64_t x = reinterpret_cast<const uint64_t*>(lp)[0];
-      const uint64_t y = reinterpret_cast<const uint64_t*>(lp)[1];
-      v4 v;
-      v.x = static_cast<uint32_t>(x); v.y = static_cast<uint32_t>(x >> 32);
-      v.z = static_cast<uint32_t>(y); v.w = static_cast<uint32_t>(y >> 32);
-      __builtin_nontemporal_store(v, reinterpret_cast<v4*>(g + head + 16 * i));
-    }
-    cnt++;
-  }
-  if (tail > 0 && wave == 3) {
-    const int64_t t0 = head + 16 * body;
-    if (lane < tail) g[t0 + lane] = img[t0 + lane];
-    cnt++;
-  }
-  return cnt;
-}
-
-// ---- register-staged encode (schemas of <= kRegCols fields) -----------------------------------
-// One workgroup builds one tile of R rows (thread = row) into an LDS image of the tile's
-// contiguous output range, then stores it with 16-B stores.  The per-row inputs of every column
-// are loaded straight into registers (the column count is a template parameter, so the per-column
-// values live in VGPRs and all the loads are issued together: one HBM round trip), and the
-// string / decimal / list bytes are then read from global memory by their row's thread (a second
-// round trip, issued for all columns at once).  LDS holds only the image, so five workgroups
-// share a CU.
-constexpr int kRegCols = 16;
-constexpr int kRegImg = 30 * 1024;
-
-// Copies len bytes at global src to 8-byte aligned dst (LDS or global) as whole words, zero pad.
-template <typename D>
-__device__ __forceinline__ void put_string(D* dst, const uint8_t* src, int64_t len) {
-  if (len <= 0) return;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src) & 7;
-  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s);
-  const int64_t nw = (len + 7) >> 3;
-  const int64_t nsrc = (static_cast<int64_t>(s) + len + 7) >> 3;
-  for (int64_t k0 = 0; k0 < nw; k0 += 4) {
-    uint64_t w[5];
-#pragma unroll
-    for (int j = 0; j < 5; j++) w[j] = k0 + j < nsrc ? ap[k0 + j] : 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int64_t k = k0 + j;
-      if (k < nw) {
-        uint64_t x = s ? (w[j] >> (8 * s)) | (w[j + 1] << (64 - 8 * s)) : w[j];
-        const int64_t rem = len - 8 * k;
-        if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
-        dst[k] = x;
-      }
-    }
-  }
-}
-
-// 64 bits of a bitmap starting at bit i, reading only the aligned words that hold wanted bits
-// (bits past `lim` are garbage).
-__device__ __forceinline__ uint64_t load_bits64(const uint8_t* bits, int64_t i, int lim) {
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(bits) + (i >> 3);
-  const uint64_t* a = reinterpret_cast<const uint64_t*>(addr & ~uintptr_t(7));
-  const int sh = static_cast<int>((addr & 7) * 8 + (i & 7));
-  const uint64_t lo = a[0];
-  if (sh == 0) return lo;
-  const uint64_t hi = sh + lim > 64 ? a[1] : 0;
-  return (lo >> sh) | (hi << (64 - sh));
-}
-
-// BinaryArrayWriter image of n elements read from global memory (register-staged encode):
-// element values and validity words are fetched in batches so their loads overlap.
-template <typename D>
-__device__ __forceinline__ int64_t put_array(D* d64, int width, const uint8_t* vals,
-                                             const uint8_t* vbits, int64_t vbit0, int64_t n) {
-  const int ew = width == 0 ? 1 : width;
-  const int64_t nbw = (n + 63) >> 6;
-  d64[0] = static_cast<uint64_t>(n);
-  for (int64_t w = 0; w < nbw; w++) {
-    const int lim = static_cast<int>(min<int64_t>(64, n - 64 * w));
-    const uint64_t valid = vbits ? load_bits64(vbits, vbit0 + 64 * w, lim) : ~0ull;
-    const uint64_t m = lim == 64 ? ~0ull : ((1ull << lim) - 1);
-    d64[1 + w] = ~valid & m;                            // bit = 1 null
-  }
-  D* out = d64 + 1 + nbw;
-  if (ew == 8) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(vals);
-    for (int64_t j0 = 0; j0 < n; j0 += 8) {
-      const int lim = static_cast<int>(min<int64_t>(8, n - j0));
-      const uint64_t vm = vbits ? load_bits64(vbits, vbit0 + j0, lim) : ~0ull;
-      uint64_t x[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) x[u] = u < lim ? src[j0 + u] : 0;
-#pragma unroll
-      for (int u = 0; u < 8; u++)
-        if (u < lim) out[j0 + u] = ((vm >> u) & 1) ? x[u] : 0;
-    }
-    return 8 * (1 + nbw + n);
-  }
-  const int per = 8 / ew;
-  const int64_t nw = (n * ew + 7) >> 3;
-  for (int64_t q = 0; q < nw; q++) {
-    const int lim = static_cast<int>(min<int64_t>(per, n - q * per));
-    const uint64_t vm = vbits ? load_bits64(vbits, vbit0 + q * per, lim) : ~0ull;
-    uint64_t word = 0;
-    for (int t = 0; t < lim; t++) {
-      const int64_t j = q * per + t;
-      if (!((vm >> t) & 1)) continue;                  // null element stays 0
-      uint64_t x;
-      switch (width) {
-        case 4: x = reinterpret_cast<const uint32_t*>(vals)[j]; break;
-        case 2: x = reinterpret_cast<const uint16_t*>(vals)[j]; break;
-        case 1: x = vals[j]; break;
-        default: x = bit_at(vals, vbit0 + j); break;   // bool: bit-packed, same bit origin
-      }
-      word |= x << (8 * ew * t);
-    }
-    out[q] = word;
-  }
-  return 8 * (1 + nbw + nw);
-}
-
-// Builds row r (tile thread t) at d64 from the register-staged inputs.
-template <int K, typename D>
-__device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const uint64_t* v,
-                                              uint64_t valid, D* d64) {
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    uint64_t slot = 0;
-    if (!((valid >> k) & 1)) {
-      nullbits |= 1ull << k;
-    } else if (c.kind == kFixed || c.kind == kBool) {
-      slot = v[k];
-    } else if (c.kind == kBytes) {
-      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
-      const int64_t len = o1 - o0;
-      put_string(d64 + (cursor >> 3), c.values + o0, len);
-      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-      cursor += rnd8(len);
-    } else if (c.kind == kDecimal) {
-      const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values) + 2 * r;
-      d64[cursor >> 3] = s[0];
-      d64[(cursor >> 3) + 1] = s[1];
-      slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
-      cursor += 16;
-    } else {   // kListFixed
-      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
-      const int64_t n = o1 - o0;
-      const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + int64_t(o0) * c.width;
-      const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
-      const int64_t sz = put_array(d64 + (cursor >> 3), c.width, vals, vb, o0 & 7, n);
-      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(sz);
-      cursor += sz;
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;
-}
-
-template <int K>
-__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
-                                                           const int64_t* __restrict__ offs,
-                                                           uint8_t* __restrict__ rows, int64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint64_t img[kRegImg / 8];
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t r = live ? r0 + tid : r0;
-  const int64_t base = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - base;
-  const int64_t ex = offs[r] - base;
-  // per-row inputs of every column: one batch of independent loads
-  uint64_t v[K];
-  uint64_t valid = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    const bool ok = !c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1);
-    valid |= static_cast<uint64_t>(ok) << k;
-    uint64_t x = 0;
-    switch (c.kind) {
-      case kFixed: x = load_fixed(c.values, r, c.width); break;
-      case kBool: x = bit_at(c.values, r); break;
-      case kBytes:
-      case kListFixed:
-        x = static_cast<uint32_t>(c.offsets[r]) |
-            (static_cast<uint64_t>(static_cast<uint32_t>(c.offsets[r + 1])) << 32);
-        break;
-      default: break;
-    }
-    v[k] = x;
-  }
-  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (bytes <= kRegImg) {
-    if (live) reg_build_row<K>(a, r, v, valid, img + (ex >> 3));
-    __syncthreads();
-    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
-  } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
-    const int64_t sz = offs[r + 1] - offs[r];
-    if (ex + sz <= room) reg_build_row<K>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
-  }
-}
-
-// ---- pipelined encode ------------------------------------------------------------------------
-// A fixed grid of resident workgroups (2 per CU) walks the tiles t = blockIdx.x + i * gridDim.x.
-// Each workgroup double-buffers its inputs: while tile t is built from slot s and stored, the
-// LDS-DMA of tile t + gridDim.x (its row offsets, per-row inputs and payload ranges) is already in
-// flight into slot s ^ 1, so one HBM round trip per tile is overlapped with the build instead of
-// two being waited for.  The payload ranges of the next tile come from scalar loads of the two
-// bounding string/list offsets, so they do not wait for that tile's meta to land.
-struct PipeSlot {
-  MetaMap mm;
-  uint32_t offs_at;          // LDS offset (in the meta slot) of the staged offs[r0]
-  uint32_t pad_;
-};
-
-template <int NT>
-__device__ __forceinline__ void pipe_issue(const VarArgs& a, const int64_t* __restrict__ offs,
-                                           int64_t t, uint8_t* meta, uint8_t* pay, uint32_t psz,
-                                           PipeSlot& ps) {
-  const int R = a.tile_rows;
-  const int64_t r0 = t * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  uint32_t at = 0;
-  const uint32_t oa = stage_range<NT>(meta, at, reinterpret_cast<const uint8_t*>(offs + r0),
-                                      reinterpret_cast<const uint8_t*>(offs + r0 + nr + 1));
-  stage_meta<NT>(a, r0, nr, meta, ps.mm, at);        // sets every mm.pay / mm.pvb to kNone
-  uint32_t pat = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
-    if (e <= b) continue;
-    const uint8_t *gb, *ge;
-    if (c.kind == kBytes) { gb = c.values + b; ge = c.values + e; }
-    else if (c.width == 0) { gb = c.values + (b >> 3); ge = c.values + ((e + 7) >> 3); }
-    else { gb = c.values + b * c.width; ge = c.values + e * c.width; }
-    const bool vb = c.kind == kListFixed && c.elem_validity;
-    const uint8_t* vgb = vb ? c.elem_validity + (b >> 3) : nullptr;
-    const uint8_t* vge = vb ? c.elem_validity + ((e + 7) >> 3) : nullptr;
-    auto span = [](const uint8_t* x, const uint8_t* y) -> uint64_t {
-      return ((reinterpret_cast<uint64_t>(y) + 15) & ~uint64_t(15)) -
-             (reinterpret_cast<uint64_t>(x) & ~uint64_t(15));
-    };
-    const uint64_t need = span(gb, ge) + (vb ? span(vgb, vge) : 0);
-    if (pat + need > psz) continue;                   // this column reads global memory
-    const uint32_t pa = stage_range<NT>(pay, pat, gb, ge);
-    const uint32_t pv = vb ? stage_range<NT>(pay, pat, vgb, vge) : kNone;
-    if (threadIdx.x == 0) {
-      ps.mm.pay[k] = pa;
-      ps.mm.pvb[k] = pv;
-    }
-  }
-  if (threadIdx.x == 0) ps.offs_at = oa;
-}
-
-__device__ __forceinline__ int pipe_build_store(const VarArgs& a, uint8_t* __restrict__ rows,
-                                                 int64_t cap, int64_t t, const uint8_t* meta,
-                                                 const uint8_t* pay, uint8_t* img, uint32_t isz,
-                                                 const PipeSlot& ps) {
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;
-  const int64_t r0 = t * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t* so = reinterpret_cast<const int64_t*>(meta + ps.offs_at);
-  const int64_t base = so[0];
-  const int64_t bytes = so[nr] - base;
-  const int64_t ex = live ? so[tid] - base : 0;
-  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (bytes + 16 <= isz) {
-    if (live) build_tile_row(a, ps.mm, meta, pay, tid, img + ex);
-    __syncthreads();
-    return store_image(rows + base, img, room);
-  }
-  if (live && ex + tile_row_size(a, ps.mm, meta, tid) <= room)
-    build_tile_row(a, ps.mm, meta, pay, tid, rows + base + ex);   // oversized tile: straight to HBM
-  return 0;                                                       // wait for everything
-}
-
-__global__ __launch_bounds__(kEncRows) void encode_var_pipe(VarArgs a,
-                                                            const int64_t* __restrict__ offs,
-                                                            uint8_t* __restrict__ rows,
-                                                            int64_t cap, int64_t ntiles,
-                                                            uint32_t msz, uint32_t psz,
-                                                            uint32_t isz) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ PipeSlot ps[2];
-  uint8_t* img = lds + 2 * msz + 2 * psz;
-  int64_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  int s = 0;
-  pipe_issue<kEncRows>(a, offs, t, lds, lds + 2 * msz, psz, ps[0]);
-  wait_dma();
-  __syncthreads();
-  for (;;) {
-    const int64_t tn = t + gridDim.x;
-    if (tn < ntiles)
-      pipe_issue<kEncRows>(a, offs, tn, lds + (s ^ 1) * msz, lds + 2 * msz + (s ^ 1) * psz, psz,
-                           ps[s ^ 1]);
-    const int nst =
-        pipe_build_store(a, rows, cap, t, lds + s * msz, lds + 2 * msz + s * psz, img, isz, ps[s]);
-    wait_vm_le(nst);
-    __syncthreads();
-    if (tn >= ntiles) break;
-    t = tn;
-    s ^= 1;
-  }
-}
-
-// ---- measure: row sizes (writerIndex growth of toRow) and their exclusive scan.  Each thread
-// sizes 4 consecutive rows (one validity nibble and 5 consecutive offsets per column), so a
-// 256-thread workgroup covers 1,024 rows and writes their group-relative exclusive offsets and its
-// total; a device scan of the (few) group totals and one add pass finish the scan.  (A single
-// pass with a decoupled look-back was measured slower: the ticket atomic that orders the
-// workgroups serialises at this workgroup count.)
-constexpr int kMeasRows = 4;                                   // rows per thread
-constexpr int kMeasTile = kThreads * kMeasRows;                // rows per workgroup
-
-__device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
-  int64_t sz = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind < kBytes) continue;
-    if (c.validity && !bit_at(c.validity, r)) continue;          // null: setNullAt only
-    if (c.kind == kDecimal) {
-      sz += 16;
-      continue;
-    }
-    const int64_t n = c.offsets[r + 1] - c.offsets[r];
-    if (c.kind == kBytes) sz += rnd8(n);
-    else sz += 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
-  }
-  return sz;
-}
-
-__global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
-                                                           int64_t* __restrict__ gsum) {
-  __shared__ int64_t tmp[kThreads / 64];
-  const int64_t b = blockIdx.x;
-  const int64_t r = b * kMeasTile + kMeasRows * threadIdx.x;   // first of this thread's rows
-  int64_t sz[kMeasRows];
-  if (r + kMeasRows <= a.nrows) {                 // whole quad: vector-friendly straight line
-#pragma unroll
-    for (int j = 0; j < kMeasRows; j++) sz[j] = a.fixed_size;
-    for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
-      if (c.kind < kBytes) continue;
-      const uint32_t vb = c.validity ? (c.validity[r >> 3] >> (r & 7)) : 0xffu;
-      if (c.kind == kDecimal) {
-#pragma unroll
-        for (int j = 0; j < kMeasRows; j++) sz[j] += ((vb >> j) & 1) ? 16 : 0;
-        continue;
-      }
-      int32_t o[kMeasRows + 1];
-#pragma unroll
-      for (int j = 0; j <= kMeasRows; j++) o[j] = c.offsets[r + j];
-#pragma unroll
-      for (int j = 0; j < kMeasRows; j++) {
-        const int64_t n = o[j + 1] - o[j];
-        const int64_t add = c.kind == kBytes ? rnd8(n)
-                                             : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
-        sz[j] += ((vb >> j) & 1) ? add : 0;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < kMeasRows; j++) sz[j] = r + j < a.nrows ? row_size_of(a, r + j) : 0;
-  }
-  int64_t loc[kMeasRows], run = 0;
-#pragma unroll
-  for (int j = 0; j < kMeasRows; j++) {
-    loc[j] = run;
-    run += sz[j];
-  }
-  int64_t total;
-  const int64_t ex = block_excl_scan(run, &total, tmp);
-#pragma unroll
-  for (int j = 0; j < kMeasRows; j++)
-    if (r + j < a.nrows) offs[r + j] = ex + loc[j];
-  if (threadIdx.x == 0) gsum[b] = total;
-}
-
-// offs[r] += prefix of r's measure group; offs[n] = total.
-__global__ __launch_bounds__(kThreads) void add_group_prefix(int64_t* __restrict__ offs, int64_t n,
-                                                             const int64_t* __restrict__ prefix,
-                                                             const int64_t* __restrict__ total) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  if (r < n) offs[r] += prefix[r / kMeasTile];
-  if (r == n - 1) offs[n] = *total;
-}
-
-// --- decode side -------------------------------------------------------------------------------
-
-// Per row and var field: STRING/BINARY -> unpadded size; LIST -> numElements; else 0.
-__device__ __forceinline__ int64_t var_count(const VarArgs& a, const VarCol& c, int k,
-                                             const uint8_t* row) {
-  if ((row[k >> 3] >> (k & 7)) & 1) return 0;                  // null
-  const uint64_t slot = *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k);
-  if (c.kind == kBytes) return static_cast<int64_t>(static_cast<uint32_t>(slot));
-  if (c.kind == kListFixed) {
-    const int32_t rel = static_cast<int32_t>(slot >> 32);
-    return static_cast<int32_t>(*reinterpret_cast<const int64_t*>(row + rel));
-  }
-  return 0;
-}
-
-__global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
-                                                                  const uint8_t* __restrict__ rows,
-                                                                  const int64_t* __restrict__ offs,
-                                                                  int64_t* __restrict__ sums,
-                                                                  int64_t nb) {
-  __shared__ int64_t tmp[kThreads / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
-  const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
-  const int64_t rbeg = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - rbeg;
-  const int64_t r = r0 + threadIdx.x;
-  // stage the group's contiguous row range (LDS-DMA, 16-B pieces) so the per-row slot reads
-  // below hit LDS instead of scattered HBM lines
-  const bool staged = bytes + 32 <= kDecodeStage;
-  uint32_t d0 = 0;
-  if (staged) {
-    uint32_t at = 0;
-    d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
-    __syncthreads();
-  }
-  const uint8_t* row =
-      r < a.nrows ? (staged ? stage + d0 + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
-  int seq = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t cnt = row ? var_count(a, c, k, row) : 0;
-    int64_t total;
-    const int64_t ex = block_excl_scan(cnt, &total, tmp);
-    if (row) c.offsets[r] = static_cast<int32_t>(ex);
-    if (threadIdx.x == 0) sums[seq * nb + blockIdx.x] = total;
-    seq++;
-  }
-}
-
-__global__ __launch_bounds__(kThreads) void decode_measure_fix(VarArgs a,
-                                                               const int64_t* __restrict__ sums,
-                                                               const int64_t* __restrict__ totals,
-                                                               int64_t nb) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  int seq = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    if (r < a.nrows) c.offsets[r] += static_cast<int32_t>(sums[seq * nb + blockIdx.x]);
-    if (r == a.nrows - 1) c.offsets[a.nrows] = static_cast<int32_t>(totals[seq]);
-    seq++;
-  }
-}
-
-// Byte i (0 <= i < len) of an 8-byte-aligned source, read as whole aligned words.
-__device__ __forceinline__ uint32_t src_byte(const uint8_t* src, int64_t i) {
-  const uint64_t w = reinterpret_cast<const uint64_t*>(src)[i >> 3];
-  return static_cast<uint32_t>((w >> (8 * (i & 7))) & 0xff);
-}
-
-// Writes src[0, len) (8-byte-aligned source: a row's var section) to dst + q (any alignment).
-// 32-bit words wholly inside the destination range are written whole; the partial words at the
-// two ends are written byte by byte, so neighbouring strings (other threads) are never touched
-// and no atomics or pre-zeroing are needed (byte stores are masked in LDS and in HBM).
-__device__ __forceinline__ void put_bytes(uint8_t* dst, int64_t q, const uint8_t* src, int64_t len) {
-  if (len <= 0) return;
-  const int64_t end = q + len;
-  const int64_t w0 = (q + 3) >> 2;                 // first whole word
-  const int64_t w1 = end >> 2;                     // one past the last whole word
-  if (w0 >= w1) {
-    for (int64_t i = 0; i < len; i++) dst[q + i] = static_cast<uint8_t>(src_byte(src, i));
-    return;
-  }
-  for (int64_t i = q; i < 4 * w0; i++) dst[i] = static_cast<uint8_t>(src_byte(src, i - q));
-  const int64_t d = 4 * w0 - q;                    // source index of the first whole word
-  const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
-  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-  for (int64_t w = w0; w < w1; w++) {
-    const int64_t si = d + 4 * (w - w0);           // 4 source bytes [si, si + 4)
-    const int64_t j = si >> 3;
-    const int o = static_cast<int>(si & 7);
-    uint64_t x = s64[j] >> (8 * o);
-    if (o > 4) x |= s64[j + 1] << (64 - 8 * o);
-    d32[w] = static_cast<uint32_t>(x);
-  }
-  for (int64_t i = 4 * w1; i < end; i++) dst[i] = static_cast<uint8_t>(src_byte(src, i - q));
-}
-
-template <bool kToGlobal>
-__device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, int64_t p0, int64_t p1,
-                                                 int64_t a0) {
-  // [p0, p1) of g <- l[p - a0]: unaligned ends byte by byte, aligned middle 16 B per lane.
-  const int64_t m0 = min<int64_t>((p0 + 15) & ~int64_t(15), p1);
-  const int64_t m1 = max<int64_t>(p1 & ~int64_t(15), m0);
-  for (int64_t i = p0 + threadIdx.x; i < m0; i += kThreads) g[i] = l[i - a0];
-  for (int64_t i = m1 + threadIdx.x; i < p1; i += kThreads) g[i] = l[i - a0];
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  for (int64_t i = m0 + 16 * threadIdx.x; i < m1; i += 16 * kThreads)
-    __builtin_nontemporal_store(*reinterpret_cast<const v4*>(l + (i - a0)),
-                                reinterpret_cast<v4*>(g + i));
-}
-
-__device__ __forceinline__ bool is_seq(const VarCol& c) {
-  return c.kind == kBytes || c.kind == kListFixed;
-}
-
-// ---- register-staged decode (schemas of <= kRegCols fields) -----------------------------------
-// One workgroup decodes 256 rows (thread = row).  Each thread loads its row's null word and slots
-// straight into registers (one batch of loads; the L2 serves the neighbouring lanes' lines), so
-// LDS holds only the output assembly images.  STRING/BINARY/LIST counts are scanned in the
-// workgroup and chained across workgroups by a decoupled look-back in launch order; fixed-width
-// fields leave as coalesced column stores while predecessors publish.  Each variable-length
-// column's Arrow range for the tile is assembled in LDS (string bytes OR-ed at byte offsets into a
-// zeroed image — rows keep strings 8-byte aligned, so every source word is one aligned load; list
-// elements at their element slots; validity / bool bits OR-ed into a bit image) and leaves with
-// 16-B stores, byte-exact at the two ends and with atomic and/or on bitmap words shared with the
-// neighbouring tiles.
-constexpr int kDecImg = 24 * 1024;
-
-}  // namespace
-__device__ unsigned int g_lookback_timeouts = 0;     // spins abandoned (never expected)
-namespace {
-
-// look_back with a bounded spin.  Tiles are numbered by a ticket, so every predecessor is running
-// and publishes without waiting on anything: the wait always ends.  The bound is a safety net
-// against hardware faults; a look-back that gives up is counted in g_lookback_timeouts AND raised
-// in the host-visible device error word (`err`), which the next API call / fury_device_status()
-// reports as FURY_ERR_DEVICE -- its outputs are never passed off as valid.
-__device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q,
-                                     uint32_t* err) {
-  const int lane = threadIdx.x & 63;
-  int64_t excl = 0;
-  uint32_t spins = 0;
-  for (int64_t j = b - 1;; j -= 64) {
-    const int64_t idx = j - lane;
-    uint64_t v;
-    for (;;) {
-      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
-      if (__ballot((v >> 62) == 0) == 0) break;
-      if (++spins > (1u << 24)) {
-        if (lane == 0) {
-          atomicAdd(&g_lookback_timeouts, 1u);
-          if (err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        return 0;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint64_t inc = __ballot((v >> 62) == 2);
-    const int stop = inc ? __builtin_ctzll(inc) : 63;
-    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
-    if (inc) return excl;
-  }
-}
-
-// Stores image bytes img[0, n) to g[0, n) (g any alignment, img 16-aligned LDS with >= 16 bytes
-// of readable padding past n): byte stores up to g's 16-byte boundary, then 16-B non-temporal
-// stores whose data is funnel-shifted out of aligned image words, then the byte tail.
-template <int NT = kThreads>
-__device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, int64_t n) {
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  if (n <= 0) return;
-  const int64_t head = min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
-  const int64_t body = (n - head) >> 4;
-  const int64_t t0 = head + 16 * body;
-  if (threadIdx.x < head) g[threadIdx.x] = img[threadIdx.x];
-  if (threadIdx.x < n - t0) g[t0 + threadIdx.x] = img[t0 + threadIdx.x];
-  const uint64_t* i64 = reinterpret_cast<const uint64_t*>(img);
-  const int sh = static_cast<int>(head & 7) * 8;
-  for (int64_t m = threadIdx.x; m < body; m += NT) {
-    const int64_t off = head + 16 * m;
-    const int64_t q = off >> 3;
-    uint64_t x, y;
-    if (sh == 0) {
-      x = i64[q];
-      y = i64[q + 1];
-    } else {
-      const uint64_t w0 = i64[q], w1 = i64[q + 1], w2 = i64[q + 2];
-      x = (w0 >> sh) | (w1 << (64 - sh));
-      y = (w1 >> sh) | (w2 << (64 - sh));
-    }
-    v4 vv;
-    vv.x = static_cast<uint32_t>(x); vv.y = static_cast<uint32_t>(x >> 32);
-    vv.z = static_cast<uint32_t>(y); vv.w = static_cast<uint32_t>(y >> 32);
-    __builtin_nontemporal_store(vv, reinterpret_cast<v4*>(g + head + 16 * m));
-  }
-}
-
-// Stores a bit image (image bit i = global bit gbit0 + i, >= 1 word of padding) to the global
-// bitmap bits [gbit0, gbit0 + n): whole words plainly, the words shared with neighbouring tiles
-// with atomic and/or of exactly these bits.
-template <int NT = kThreads>
-__device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t* img, int64_t gbit0,
-                                                   int64_t n) {
-  if (n <= 0) return;
-  const int64_t end = gbit0 + n;
-  const int64_t w0 = gbit0 >> 5, w1 = (end + 31) >> 5;
-  uint32_t* g = reinterpret_cast<uint32_t*>(bits);
-  for (int64_t w = w0 + threadIdx.x; w < w1; w += NT) {
-    const int64_t i0 = 32 * w - gbit0;
-    uint32_t x;
-    if (i0 < 0) {
-      x = img[0] << (-i0);
-    } else {
-      const int64_t q = i0 >> 5;
-      const int s = static_cast<int>(i0 & 31);
-      x = s ? (img[q] >> s) | (img[q + 1] << (32 - s)) : img[q];
-    }
-    uint32_t m = ~0u;
-    if (w == w0) m &= ~0u << (gbit0 & 31);
-    if (w == w1 - 1 && (end & 31)) m &= (1u << (end & 31)) - 1;
-    if (m == ~0u) {
-      g[w] = x;
-    } else {
-      atomicAnd(g + w, ~m);
-      atomicOr(g + w, x & m);
-    }
-  }
-}
-
-template <int K, int NT = kThreads>
-__global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
-                                                           const int64_t* __restrict__ offs,
-                                                           uint64_t* __restrict__ status,
-                                                           uint32_t* __restrict__ ticket) {
-  __shared__ __attribute__((aligned(16))) uint64_t oimg[kDecImg / 8 * (NT / kThreads)];
-  __shared__ int64_t tmp[NT / 64];
-  __shared__ int64_t sbase[K];
-  __shared__ int64_t stile;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // Tiles are numbered in the order workgroups START (a ticket), not by blockIdx: dispatch order
-  // is not guaranteed, and the look-back below only waits on tiles with smaller numbers, which
-  // therefore are already running -- every wait ends.  (FURY_VAR_DBG bit 4096: blockIdx order,
-  // for A/B only.)
-  if (!(a.dbg & 4096)) {
-    if (tid == 0) stile = atomicAdd(ticket, 1u);
-    __syncthreads();
-  }
-  const int64_t b = (a.dbg & 4096) ? static_cast<int64_t>(blockIdx.x) : stile, nb = gridDim.x;
-  const int64_t r0 = b * NT;
-  const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t r = live ? r0 + tid : r0;
-  const uint8_t* row = rows + offs[r];
-  const uint64_t* row64 = reinterpret_cast<const uint64_t*>(row);
-  // null word + slots: one batch of loads
-  const uint64_t nullw = live ? row64[0] : ~0ull;
-  uint64_t slot[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) slot[k] = row64[1 + k];
-  // element counts of LIST fields (dependent load of the array header)
-  uint32_t cnt[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    const bool isnull = (nullw >> k) & 1;
-    cnt[k] = 0;
-    if (!isnull && c.kind == kBytes) cnt[k] = static_cast<uint32_t>(slot[k]);
-    if (!isnull && c.kind == kListFixed)
-      cnt[k] = static_cast<uint32_t>(*reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot[k] >> 32)));
-  }
-  // in-tile exclusive scans, two columns per 64-bit scan (tile totals < 2^32)
-  uint32_t ex[K], tot[K];
-#pragma unroll
-  for (int k = 0; k < K; k += 2) {
-    const bool s0 = is_seq(a.col[k]);
-    const bool s1 = k + 1 < K && is_seq(a.col[k + 1]);
-    ex[k] = tot[k] = 0;
-    if (k + 1 < K) ex[k + 1] = tot[k + 1] = 0;
-    if (!s0 && !s1) continue;
-    const uint64_t pk = cnt[k] | (k + 1 < K ? static_cast<uint64_t>(cnt[k + 1]) << 32 : 0);
-    int64_t t64;
-    const uint64_t e64 = static_cast<uint64_t>(block_excl_scan<NT>(static_cast<int64_t>(pk), &t64, tmp));
-    ex[k] = static_cast<uint32_t>(e64);
-    tot[k] = static_cast<uint32_t>(t64);
-    if (k + 1 < K) {
-      ex[k + 1] = static_cast<uint32_t>(e64 >> 32);
-      tot[k + 1] = static_cast<uint32_t>(static_cast<uint64_t>(t64) >> 32);
-    }
-  }
-  if (tid == 0) {
-#pragma unroll
-    for (int k = 0; k < K; k++)
-      if (is_seq(a.col[k]))
-        st_status(status + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
-  }
-  // tile-relative LDS images of every variable-length column (image byte / bit i = the tile's
-  // i-th output byte / element); laid out from the tile totals alone, so the rows are scattered
-  // into them while the predecessors' prefixes are still being resolved
-  uint32_t img_at[K];
-  uint32_t used = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    img_at[k] = kNone;
-    if (!is_seq(c) || !c.values || tot[k] == 0) continue;
-    int64_t need;
-    if (c.kind == kBytes) need = r16(tot[k] + 16);
-    else if (c.width == 0) need = r16((((tot[k] + 31) >> 5) + 1) * 4);
-    else need = r16(int64_t(tot[k]) * c.width + 16);
-    if (c.kind == kListFixed && c.elem_validity) need += r16((((tot[k] + 31) >> 5) + 1) * 4);
-    if (used + need <= kDecImg * (NT / kThreads)) {
-      img_at[k] = used;
-      used += static_cast<uint32_t>(need);
-    }
-  }
-  for (uint32_t i = 16 * tid; i < used; i += 16 * NT)
-    *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    if (img_at[k] == kNone || !live || cnt[k] == 0 || (a.dbg & 16)) continue;
-    const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
-    uint8_t* im = reinterpret_cast<uint8_t*>(oimg) + img_at[k];
-    if (c.kind == kBytes) {
-      const int64_t len = cnt[k];
-      const int64_t d = ex[k];
-      uint64_t* iw = reinterpret_cast<uint64_t*>(im) + (d >> 3);
-      const int sh = static_cast<int>(d & 7) * 8;
-      const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
-      const int64_t nw = (len + 7) >> 3;
-      for (int64_t j0 = 0; j0 < nw; j0 += 4) {
-        uint64_t w[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) w[u] = j0 + u < nw ? s64[j0 + u] : 0;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int64_t j = j0 + u;
-          if (j >= nw) break;
-          uint64_t x = w[u];
-          const int64_t rem = len - 8 * j;
-          if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
-          atomicOr(reinterpret_cast<unsigned long long*>(iw + j), x << sh);
-          if (sh && (x >> (64 - sh))) atomicOr(reinterpret_cast<unsigned long long*>(iw + j + 1), x >> (64 - sh));
-        }
-      }
-      continue;
-    }
-    // LIST of fixed-width elements: values at element slots, bits by OR
-    const int64_t n = cnt[k];
-    const int ew = c.width == 0 ? 1 : c.width;
-    const uint8_t* ev = src + 8 + bm_bytes(n);
-    const int64_t vb = c.width == 0 ? r16((((tot[k] + 31) >> 5) + 1) * 4) : r16(int64_t(tot[k]) * c.width + 16);
-    uint32_t* bimg = reinterpret_cast<uint32_t*>(im + vb);
-    for (int64_t j0 = 0; j0 < n; j0 += 8) {
-      const int lim = static_cast<int>(min<int64_t>(8, n - j0));
-      const uint64_t nulls = load_bits64(src + 8, j0, lim);
-      uint64_t x[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        x[u] = 0;
-        if (u < lim) {
-          switch (ew) {
-            case 8: x[u] = reinterpret_cast<const uint64_t*>(ev)[j0 + u]; break;
-            case 4: x[u] = reinterpret_cast<const uint32_t*>(ev)[j0 + u]; break;
-            case 2: x[u] = reinterpret_cast<const uint16_t*>(ev)[j0 + u]; break;
-            default: x[u] = ev[j0 + u]; break;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        if (u >= lim) break;
-        const bool valid = !((nulls >> u) & 1);
-        const int64_t e = ex[k] + j0 + u;                     // tile-relative element
-        const uint64_t val = valid ? x[u] : 0;
-        if (c.width == 8) {
-          reinterpret_cast<uint64_t*>(im)[e] = val;
-        } else if (c.width == 0) {
-          if (val & 0xff) atomicOr(reinterpret_cast<uint32_t*>(im) + (e >> 5), 1u << (e & 31));
-        } else if (val) {
-          const int64_t bo = e * ew;
-          atomicOr(reinterpret_cast<uint32_t*>(im) + (bo >> 2), static_cast<uint32_t>(val << (8 * (bo & 3))));
-        }
-        if (c.elem_validity && valid) atomicOr(bimg + (e >> 5), 1u << (e & 31));
-      }
-    }
-  }
-  // fixed-width fields, decimals and every field's validity (no dependency on other tiles)
-  const int64_t rbase = r0 + 64 * wave;
-  const int64_t nvalid = a.nrows - rbase;
-  const int nwords = nvalid >= 64 ? 2 : nvalid <= 0 ? 0 : static_cast<int>((nvalid + 31) >> 5);
-#pragma unroll
-  for (int k = 0; k < ((a.dbg & 8) ? 0 : K); k++) {
-    const VarCol& c = a.col[k];
-    const bool isnull = (nullw >> k) & 1;
-    if (c.validity) {
-      const uint64_t ok = __ballot(live && !isnull);
-      if (lane < nwords)
-        reinterpret_cast<uint32_t*>(c.validity)[(rbase >> 5) + lane] = static_cast<uint32_t>(ok >> (32 * lane));
-    }
-    uint8_t* dst = const_cast<uint8_t*>(c.values);
-    if (!dst) continue;
-    const uint64_t x = isnull ? 0 : slot[k];
-    if (c.kind == kFixed) {
-      if (live) {
-        switch (c.width) {
-          case 8: __builtin_nontemporal_store(x, reinterpret_cast<uint64_t*>(dst) + r); break;
-          case 4: __builtin_nontemporal_store(static_cast<uint32_t>(x), reinterpret_cast<uint32_t*>(dst) + r); break;
-          case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(x); break;
-          default: dst[r] = static_cast<uint8_t>(x); break;
-        }
-      }
-    } else if (c.kind == kBool) {
-      const uint64_t bits = __ballot(live && (x & 0xff) != 0);
-      if (lane < nwords)
-        reinterpret_cast<uint32_t*>(dst)[(rbase >> 5) + lane] = static_cast<uint32_t>(bits >> (32 * lane));
-    } else if (c.kind == kDecimal && live) {
-      uint64_t lo = 0, hi = 0;
-      if (!isnull) {
-        const uint64_t* s = reinterpret_cast<const uint64_t*>(row + static_cast<int32_t>(x >> 32));
-        lo = s[0];
-        hi = s[1];
-      }
-      uint64_t* d = reinterpret_cast<uint64_t*>(dst + 16 * r);
-      d[0] = lo;
-      d[1] = hi;
-    }
-  }
-  // prefixes of the variable-length columns: one wave per column (round robin)
-  {
-    int q = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      if (!is_seq(a.col[k])) continue;
-      if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k, a.err);
-      if (lane == 0) {
-        sbase[k] = pre;
-        if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
-      }
-    }
-  }
-  __syncthreads();
-  // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    if (!is_seq(c)) continue;
-    const int64_t gb = sbase[k];
-    if (live) c.offsets[r] = static_cast<int32_t>(gb + ex[k]);
-    if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot[k]);
-    if (img_at[k] != kNone || !c.values || !live || cnt[k] == 0) continue;
-    uint8_t* dst = const_cast<uint8_t*>(c.values);
-    const int64_t cap = c.capacity;
-    const int64_t pos = gb + ex[k];
-    const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
-    if (c.kind == kBytes) {
-      put_bytes(dst, pos, src, max<int64_t>(0, min<int64_t>(cnt[k], cap - pos)));
-      continue;
-    }
-    const int64_t n = cnt[k];
-    const int ew = c.width == 0 ? 1 : c.width;
-    const uint8_t* ev = src + 8 + bm_bytes(n);
-    for (int64_t j = 0; j < n; j++) {
-      const int64_t e = pos + j;
-      if (e >= cap) break;
-      const bool valid = !((src[8 + (j >> 3)] >> (j & 7)) & 1);
-      uint64_t x = 0;
-      if (valid) {
-        switch (ew) {
-          case 8: x = reinterpret_cast<const uint64_t*>(ev)[j]; break;
-          case 4: x = reinterpret_cast<const uint32_t*>(ev)[j]; break;
-          case 2: x = reinterpret_cast<const uint16_t*>(ev)[j]; break;
-          default: x = ev[j]; break;
-        }
-      }
-      switch (c.width) {
-        case 8: reinterpret_cast<uint64_t*>(dst)[e] = x; break;
-        case 4: reinterpret_cast<uint32_t*>(dst)[e] = static_cast<uint32_t>(x); break;
-        case 2: reinterpret_cast<uint16_t*>(dst)[e] = static_cast<uint16_t>(x); break;
-        case 1: dst[e] = static_cast<uint8_t>(x); break;
-        default: {
-          uint32_t* wd = reinterpret_cast<uint32_t*>(dst) + (e >> 5);
-          const uint32_t m = 1u << (e & 31);
-          if (valid && x) atomicOr(wd, m); else atomicAnd(wd, ~m);
-        }
-      }
-      if (c.elem_validity) {
-        uint32_t* wd = reinterpret_cast<uint32_t*>(c.elem_validity) + (e >> 5);
-        const uint32_t m = 1u << (e & 31);
-        if (valid) atomicOr(wd, m); else atomicAnd(wd, ~m);
-      }
-    }
-  }
-  // images -> HBM at the resolved positions
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
-    if (img_at[k] == kNone) continue;
-    const int64_t gb = sbase[k];
-    uint8_t* dst = const_cast<uint8_t*>(c.values);
-    const uint8_t* im = reinterpret_cast<const uint8_t*>(oimg) + img_at[k];
-    const int64_t n = max<int64_t>(0, min<int64_t>(tot[k], c.capacity - gb));
-    if (c.kind == kBytes) {
-      store_shifted<NT>(dst + gb, im, n);
-      continue;
-    }
-    int64_t vb;
-    if (c.width == 0) {
-      vb = r16((((tot[k] + 31) >> 5) + 1) * 4);
-      store_bits_shifted<NT>(dst, reinterpret_cast<const uint32_t*>(im), gb, n);
-    } else {
-      vb = r16(int64_t(tot[k]) * c.width + 16);
-      store_shifted<NT>(dst + gb * c.width, im, n * c.width);
-    }
-    if (c.elem_validity)
-      store_bits_shifted<NT>(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
-  }
-}
-
-// Decode / row->Arrow, single pass: 256 rows per workgroup.  Arrow offsets of STRING/BINARY and
-// LIST fields are a scan over ALL rows, so groups chain their totals with a decoupled look-back
-// (each group publishes its aggregate, then resolves its prefix from its predecessors' published
-// words; groups take logical numbers from a ticket so every group they wait on is already
-// running).  The group's row range is staged in LDS with 16-B loads; fixed fields leave as
-// coalesced per-column stores with ballot-built validity while the look-back is in flight;
-// string payloads are assembled in an LDS image of the group's output range; list elements are
-// spread one per lane over the group's flat element range (row found by binary search over the
-// group's element starts) so child values and validity bits leave coalesced.
-// Last t in [0, nr) with pos[t] <= idx: the row holding element idx (empty rows share their
-// successor's start and are skipped).
-__device__ __forceinline__ int find_row(const int32_t* pos, int nr, int32_t idx) {
-  int lo = 0, hi = nr;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (pos[mid] <= idx) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// 64 bits of an Arrow bitmap starting at 64-aligned bit gbit0: bits in `mask` get `val`.
-// Words wholly owned by this group are stored; words shared with a neighbouring group are
-// updated with atomic and/or of exactly these bits.
-__device__ __forceinline__ void put_bits64(uint8_t* bits, int64_t gbit0, uint64_t val,
-                                           uint64_t mask, int64_t cap) {
-  if (gbit0 + 64 > cap) mask &= cap <= gbit0 ? 0 : (~0ull >> (64 - (cap - gbit0)));
-  const int lane = threadIdx.x & 63;
-  if (lane < 2) {
-    const uint32_t m = static_cast<uint32_t>(mask >> (32 * lane));
-    const uint32_t v = static_cast<uint32_t>(val >> (32 * lane)) & m;
-    uint32_t* w = reinterpret_cast<uint32_t*>(bits) + (gbit0 >> 5) + lane;
-    if (m == ~0u) {
-      *w = v;
-    } else if (m) {
-      atomicAnd(w, ~m);
-      atomicOr(w, v);
-    }
-  }
-}
-
-struct DecodeShared {
-  int32_t pos[kSeqChunk][kThreads + 1];   // group-relative exclusive starts; [nr] = group total
-  int64_t rowoff[kThreads];                // row start relative to the group's first row
-  int64_t base[kSeqChunk];                 // global start of the group's range, per sequence
-  int64_t tmp[kThreads / 64];
-  int64_t blk;
-};
-
-
-// Counts + in-group scans of the sequences [cbase, cbase + nchunk); publishes the aggregates.
-__device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row, DecodeShared& sh,
-                                            int cbase, int nchunk, int64_t b, uint64_t* status,
-                                            int nseq) {
-  int seq = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
-    if (!is_seq(c)) continue;
-    const int q = seq++ - cbase;
-    if (q < 0) continue;
-    if (q >= nchunk) break;
-    const int64_t cnt = row ? var_count(a, c, k, row) : 0;
-    int64_t tot;
-    const int64_t ex = block_excl_scan(cnt, &tot, sh.tmp);
-    sh.pos[q][threadIdx.x] = static_cast<int32_t>(ex);
-    if (threadIdx.x == 0) {
-      sh.pos[q][kThreads] = static_cast<int32_t>(tot);
-      if (status)
-        st_status(status + b * nseq + cbase + q, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot));
-    }
-  }
-  __syncthreads();
-}
-
-template <bool kLookBack>
-__device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh, int cbase,
-                                              int nchunk, int64_t b, uint64_t* status, int nseq) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (!kLookBack) {     // offsets precomputed by the sizing pass (fury_row_decode_measure)
-    if (threadIdx.x < nchunk) {
-      int seq = 0;
-      for (int k = 0; k < a.ncols; k++) {
-        if (!is_seq(a.col[k])) continue;
-        if (seq++ == cbase + static_cast<int>(threadIdx.x)) {
-          sh.base[threadIdx.x] = a.col[k].offsets[b * kThreads];
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    return;
-  }
-  for (int q = w; q < nchunk; q += kThreads / 64) {
-    const int64_t ex = (b == 0 || (a.dbg & 32)) ? 0 : look_back(status, b, nseq, cbase + q);
-    if (lane == 0) {
-      sh.base[q] = ex;
-      if (b > 0)
-        st_status(status + b * nseq + cbase + q,
-                  kInc | static_cast<uint64_t>(ex + sh.pos[q][kThreads]));
-    }
-  }
-  __syncthreads();
-}
-
-template <bool kStaged, bool kLookBack>
-__device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* src, uint8_t* oimg,
-                                             DecodeShared& sh, int64_t b, int64_t nb, int nr,
-                                             uint64_t* status, int nseq) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int64_t r0 = b * kThreads;
-  const int64_t r = r0 + tid;
-  const bool live = tid < nr;
-  const uint8_t* row = live ? src + sh.rowoff[tid] : nullptr;
-  const int64_t rbase = r - lane;                               // this wave's first row
-  const int64_t nvalid = a.nrows - rbase;
-  const int nbytes = nvalid >= 64 ? 8 : static_cast<int>((nvalid + 7) >> 3);
-
-  if (kLookBack && nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
-
-  // fixed-width fields and every field's validity: no dependency on other groups
-  for (int k = 0; k < ((a.dbg & 8) ? 0 : a.ncols); k++) {
-    const VarCol& c = a.col[k];
-    const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
-    const uint64_t slot =
-        (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
-    if (c.validity) {
-      const uint64_t ok = __ballot(live && !isnull);
-      if (lane < nbytes) c.validity[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));
-    }
-    uint8_t* dst = const_cast<uint8_t*>(c.values);
-    if (c.kind == kFixed) {
-      if (live && dst) {
-        switch (c.width) {
-          case 8: __builtin_nontemporal_store(slot, reinterpret_cast<uint64_t*>(dst) + r); break;
-          case 4: reinterpret_cast<uint32_t*>(dst)[r] = static_cast<uint32_t>(slot); break;
-          case 2: reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(slot); break;
-          default: dst[r] = static_cast<uint8_t>(slot); break;
-        }
-      }
-    } else if (c.kind == kBool) {
-      const uint64_t bits = __ballot(live && (slot & 0xff) != 0);
-      if (lane < nbytes && dst) dst[(rbase >> 3) + lane] = static_cast<uint8_t>(bits >> (8 * lane));
-    } else if (c.kind == kDecimal) {
-      if (live && dst) {
-        uint64_t* d = reinterpret_cast<uint64_t*>(dst + 16 * r);
-        uint64_t lo = 0, hi = 0;
-        if (!isnull) {
-          const uint8_t* s = row + static_cast<int32_t>(slot >> 32);
-          lo = reinterpret_cast<const uint64_t*>(s)[0];
-          hi = reinterpret_cast<const uint64_t*>(s)[1];
-        }
-        d[0] = lo;
-        d[1] = hi;
-      }
-    }
-  }
-
-  for (int cbase = 0; cbase < nseq; cbase += kSeqChunk) {
-    const int nchunk = min(kSeqChunk, nseq - cbase);
-    if (cbase > 0 || !kLookBack) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
-    chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq);
-    int seq = 0;
-    for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
-      if (!is_seq(c)) continue;
-      const int q = seq++ - cbase;
-      if (q < 0) continue;
-      if (q >= nchunk) break;
-      const int64_t gb = sh.base[q];
-      const int32_t tot = sh.pos[q][kThreads];
-      if (live) c.offsets[r] = static_cast<int32_t>(gb + sh.pos[q][tid]);
-      if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot);
-      uint8_t* dst = const_cast<uint8_t*>(c.values);
-      if (tot == 0 || !dst || (a.dbg & 16)) continue;
-      const int64_t cap = c.capacity;
-      if (c.kind == kBytes) {
-        const int64_t p0 = gb, p1 = gb + tot;
-        const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
-        const uint64_t slot =
-            (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
-        const int64_t len = (live && !isnull) ? static_cast<uint32_t>(slot) : 0;
-        const uint8_t* s = live ? row + static_cast<int32_t>(slot >> 32) : nullptr;
-        const int64_t pos = p0 + sh.pos[q][tid];
-        // LDS byte i <-> global byte a0 + i, a0 = 16-aligned address of payload byte p0
-        const int64_t a0 = p0 - static_cast<int64_t>(reinterpret_cast<uintptr_t>(dst + p0) & 15);
-        if (p1 - a0 <= kStrStage) {
-          put_bytes(oimg, pos - a0, s, len);
-          __syncthreads();
-          if (cap > p0) copy_bytes_range<true>(dst, oimg, p0, min<int64_t>(p1, cap), a0);
-          __syncthreads();
-        } else {
-          put_bytes(dst, pos, s, max<int64_t>(0, min<int64_t>(len, cap - pos)));
-        }
-        continue;
-      }
-      // LIST of fixed-width elements -> Arrow child values + element validity
-      const int ew = c.width == 0 ? 1 : c.width;
-      const int sh0 = static_cast<int>(gb & 63);
-      const int64_t span = sh0 + tot;
-      for (int64_t u0 = 0; u0 < span; u0 += kThreads) {
-        const int64_t i = u0 + tid - sh0;                       // element index in the group
-        const bool act = i >= 0 && i < tot;
-        bool valid = false;
-        uint64_t v = 0;
-        if (act) {
-          const int t = find_row(sh.pos[q], nr, static_cast<int32_t>(i));
-          const uint8_t* rw = src + sh.rowoff[t];
-          const uint64_t sl = *reinterpret_cast<const uint64_t*>(rw + a.bitmap_bytes + 8 * k);
-          const uint8_t* arr = rw + static_cast<int32_t>(sl >> 32);
-          const int64_t n = *reinterpret_cast<const int64_t*>(arr);
-          const int64_t j = i - sh.pos[q][t];
-          valid = !((arr[8 + (j >> 3)] >> (j & 7)) & 1);
-          if (valid) {
-            const uint8_t* p = arr + 8 + bm_bytes(n) + j * ew;
-            switch (ew) {
-              case 8: v = *reinterpret_cast<const uint64_t*>(p); break;
-              case 4: v = *reinterpret_cast<const uint32_t*>(p); break;
-              case 2: v = *reinterpret_cast<const uint16_t*>(p); break;
-              default: v = *p; break;
-            }
-          }
-          const int64_t e = gb + i;
-          if (e < cap) {
-            switch (c.width) {
-              case 8: __builtin_nontemporal_store(v, reinterpret_cast<uint64_t*>(dst) + e); break;
-              case 4: reinterpret_cast<uint32_t*>(dst)[e] = static_cast<uint32_t>(v); break;
-              case 2: reinterpret_cast<uint16_t*>(dst)[e] = static_cast<uint16_t>(v); break;
-              case 1: dst[e] = static_cast<uint8_t>(v); break;
-              default: break;                                 // bool elements: bits below
-            }
-          }
-        }
-        const uint64_t am = __ballot(act);
-        const int64_t gbit0 = gb - sh0 + (u0 + tid - lane);     // 64-aligned
-        if (c.elem_validity) put_bits64(c.elem_validity, gbit0, __ballot(act && valid), am, cap);
-        if (c.width == 0) put_bits64(dst, gbit0, __ballot(act && valid && v != 0), am, cap);
-      }
-    }
-  }
-}
-
-template <bool kLookBack>
-__global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
-                                                              const uint8_t* __restrict__ rows,
-                                                              const int64_t* __restrict__ offs,
-                                                              uint64_t* __restrict__ status,
-                                                              uint32_t* __restrict__ ticket,
-                                                              int nseq) {
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
-  __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
-  __shared__ DecodeShared sh;
-  if (kLookBack && !(a.dbg & 64)) {
-    if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
-    __syncthreads();
-  }
-  const int64_t b = (kLookBack && !(a.dbg & 64)) ? sh.blk : blockIdx.x;
-  const int64_t r0 = b * kThreads;
-  const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
-  const int64_t rbeg = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - rbeg;
-  if (threadIdx.x < nr) sh.rowoff[threadIdx.x] = offs[r0 + threadIdx.x] - rbeg;
-  if (bytes + 32 <= kDecodeStage) {          // LDS-DMA: every piece in flight at once
-    uint32_t at = 0;
-    const uint32_t d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
-    __syncthreads();
-    decode_group<true, kLookBack>(a, stage + d0, oimg, sh, b, gridDim.x, nr, status, nseq);
-  } else {
-    __syncthreads();
-    decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
-  }
-}
-
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back (tile rows by sequence
@@ -1897,13 +60,7 @@ int var_decode_mode() { return g_var_decode; }
 
 // Look-back spins abandoned so far (each one would have left wrong Arrow offsets behind; never
 // observed: workgroups are dispatched in launch order).  Synchronous device read.
-int64_t lookback_timeouts() {
-  unsigned int v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_lookback_timeouts), sizeof(v), 0,
-                          hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
-  return v;
-}
+int64_t lookback_timeouts() { return device_error_count(); }
 void set_var_decode_mode(int v) { g_var_decode = v; }
 // LDS plan of the pipelined encode: per workgroup 2 meta slots + 2 payload slots + 1 row image
 // within kPipeLds, so kPipeGroupsPerCU workgroups share a CU.  Payload and row sizes are
@@ -1997,14 +154,7 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     VarArgs b = a;
     b.tile_rows = reg_tile_rows(a);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
-    switch (a.ncols) {
-#define FURY_REG(KK) case KK: hipLaunchKernelGGL(encode_var_reg<KK>, dim3(nt), dim3(kEncRows), 0, stream, b, offs, rows, cap); break;
-      FURY_REG(1) FURY_REG(2) FURY_REG(3) FURY_REG(4) FURY_REG(5) FURY_REG(6) FURY_REG(7)
-      FURY_REG(8) FURY_REG(9) FURY_REG(10) FURY_REG(11) FURY_REG(12) FURY_REG(13) FURY_REG(14)
-      FURY_REG(15) FURY_REG(16)
-#undef FURY_REG
-      default: break;
-    }
+    return launch_encode_var_reg(b, offs, rows, cap, nt, stream);
   } else if (a.dbg & 512) {
     hipLaunchKernelGGL(encode_var_kernel_d, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
   } else {
@@ -2053,6 +203,30 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   return st ? st : st2;
 }
 
+// LDS bytes of decode_var_reg's output images for tiles of `tile` rows: every variable-length
+// column's expected tile payload (its output capacity / nrows: the exact size after
+// fury_row_decode_measure, an over-estimate under bound sizing) with 30 % headroom, the bitmap
+// images of lists, and alignment slack -- capped at the static maximum.  A tile whose payload
+// does not fit its image stores that column straight to HBM (correct, slower), so the estimate
+// only moves speed.  FURY_VAR_DBG bit 8192: always the maximum (A/B).
+uint32_t dec_img_bytes(const VarArgs& a, int tile) {
+  const int64_t cap = static_cast<int64_t>(kDecImg) * (tile / kThreads);
+  if ((a.dbg & 8192) || a.nrows <= 0) return static_cast<uint32_t>(cap);
+  int64_t need = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.col[k];
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    if (!c.values) continue;
+    const double per = static_cast<double>(c.capacity) / static_cast<double>(a.nrows);
+    const double bytes = c.kind == kBytes ? per : per * (c.width == 0 ? 0.125 : c.width);
+    need += r16(static_cast<int64_t>(bytes * tile * 1.3) + 64);
+    if (c.kind == kListFixed && c.elem_validity) need += r16(static_cast<int64_t>(per * tile * 1.3 / 8) + 64);
+  }
+  need = (need + 1023) & ~int64_t(1023);
+  if (need < 4096) need = 4096;
+  return static_cast<uint32_t>(need < cap ? need : cap);
+}
+
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                       hipStream_t stream, bool arrow) {
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
@@ -2081,25 +255,8 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     uint32_t* tk = reinterpret_cast<uint32_t*>(ws);
-    if (!st) {
-      switch (a.ncols) {
-#define FURY_DREG(KK)                                                                          \
-  case KK:                                                                                     \
-    if (wide)                                                                                  \
-      hipLaunchKernelGGL((decode_var_reg<KK, 512>), dim3(nbr), dim3(512), 0, stream, a, rows,  \
-                         offs, ws + 1, tk);                                                    \
-    else                                                                                       \
-      hipLaunchKernelGGL(decode_var_reg<KK>, dim3(nb), dim3(kThreads), 0, stream, a, rows,     \
-                         offs, ws + 1, tk);                                                    \
-    break;
-        FURY_DREG(1) FURY_DREG(2) FURY_DREG(3) FURY_DREG(4) FURY_DREG(5) FURY_DREG(6) FURY_DREG(7)
-        FURY_DREG(8) FURY_DREG(9) FURY_DREG(10) FURY_DREG(11) FURY_DREG(12) FURY_DREG(13)
-        FURY_DREG(14) FURY_DREG(15) FURY_DREG(16)
-#undef FURY_DREG
-        default: break;
-      }
-      st = check_hip(hipGetLastError(), "decode_var_reg launch");
-    }
+    const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
+    if (!st) st = launch_decode_var_reg(a, rows, offs, ws + 1, tk, img, wide, nb, nbr, stream);
     const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
     return st ? st : st2;
   }

@@ -65,6 +65,10 @@ def main():
                                  os.environ.__setitem__("FURY_VAR_DBG", "4096"),
                                  enc.decode_into(batch, out),
                                  os.environ.__setitem__("FURY_VAR_DBG", "0")),
+        "decode_maximg": lambda: (L.fury_set_tuning(b"var_decode", 0),
+                                  os.environ.__setitem__("FURY_VAR_DBG", "8192"),
+                                  enc.decode_into(batch, out),
+                                  os.environ.__setitem__("FURY_VAR_DBG", "0")),
         "decode_lds": lambda: (L.fury_set_tuning(b"var_decode", 0),
                                os.environ.__setitem__("FURY_VAR_DBG", "1024"),
                                enc.decode_into(batch, out),
@@ -94,7 +98,8 @@ def main():
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
                     for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass",
-                              "decode_512", "decode_ticket", "decode_order", "decode_lds")}}
+                              "decode_512", "decode_ticket", "decode_order", "decode_lds",
+                              "decode_maximg")}}
     print(json.dumps(res), flush=True)
 
 

@@ -3,8 +3,10 @@ outputs are wrong when a bit is set — timing only).
 
     python scripts/diag_var.py [--workload mixed|nested] [--rows N]
 
-encode bits: 1 skip payload staging, 2 skip row build, 4 skip the image store.
-decode bits: 8 skip fixed fields, 16 skip string/list payload, 32 skip look-back (base 0).
+encode bits: 1 skip payload staging, 2 skip row build, 4 skip the image store, 64 input loads
+only (register-staged kernel).
+decode bits: 8 skip fixed fields, 16 skip string/list payload, 32 skip look-back (base 0), 128
+row loads only.
 """
 import argparse
 import json
@@ -51,13 +53,13 @@ def main():
         return round(statistics.median(xs) * 1e3, 1)
 
     res = {"workload": args.workload, "rows": n, "encode_us": {}, "decode_us": {}}
-    for d in (0,):
+    for d in (0, 2, 4, 6, 64):
         os.environ["FURY_VAR_DBG"] = str(d)
         res["encode_us"][d] = t(lambda: enc.encode_into(cols, n, batch.rows, batch.row_offsets))
     os.environ["FURY_VAR_DBG"] = "0"          # restore valid rows before the decode legs
     enc.encode_into(cols, n, batch.rows, batch.row_offsets)
     torch.cuda.synchronize()
-    for d in (0, 8, 16, 32, 56, 1024):
+    for d in (0, 8, 16, 32, 56, 128, 4096, 4096 + 32):
         os.environ["FURY_VAR_DBG"] = str(d)
         res["decode_us"][d] = t(lambda: enc.decode_into(batch, out))
     os.environ["FURY_VAR_DBG"] = "0"

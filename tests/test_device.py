@@ -214,6 +214,8 @@ def test_var_decode_modes_bit_exact(oracle, dev, mode):
         for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
                         ("nested", 4097), ("beanb", 700)):
             _roundtrip(oracle, name, n, dev, seed=n + mode)
+        _roundtrip(oracle, "mixed", 3000, dev, seed=mode, str_max=600)   # tiles beyond the stage
+        _roundtrip(oracle, "nested", 2000, dev, seed=mode, list_max=200)
     finally:
         N.lib().fury_set_tuning(b"var_decode", old)
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
