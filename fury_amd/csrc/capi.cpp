@@ -61,6 +61,66 @@ int take_device_error() {
                    "gave up waiting): the outputs of that call are invalid");
 }
 
+// Pinned staging ring for per-call column tables: the host table is copied into the ring, then
+// DMA-ed to a stream-ordered device allocation on the caller's stream (no host synchronisation);
+// a ring region is reused only after the event of the copy that read it has completed.
+namespace {
+std::mutex g_ring_mu;
+uint8_t* g_ring = nullptr;
+size_t g_ring_head = 0;
+constexpr size_t kRingBytes = 4u << 20;
+struct RingUse {
+  size_t off, bytes;
+  hipEvent_t ev;
+};
+std::vector<RingUse> g_ring_pending;
+}  // namespace
+
+DeviceTable::~DeviceTable() {
+  if (dev) (void)hipFreeAsync(dev, stream);
+}
+
+int upload_table(const void* host, size_t bytes, hipStream_t stream, DeviceTable* out) {
+  if (bytes == 0 || bytes > kRingBytes)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "column table size");
+  std::lock_guard<std::mutex> lock(g_ring_mu);
+  if (!g_ring) {
+    void* p = nullptr;
+    int st = check_hip(hipHostMalloc(&p, kRingBytes, hipHostMallocDefault), "hipHostMalloc");
+    if (st) return st;
+    g_ring = static_cast<uint8_t*>(p);
+  }
+  size_t off = (g_ring_head + 255) & ~size_t(255);
+  if (off + bytes > kRingBytes) off = 0;
+  for (size_t i = 0; i < g_ring_pending.size();) {   // wait for copies still reading the region
+    RingUse& u = g_ring_pending[i];
+    const bool overlap = u.off < off + bytes && off < u.off + u.bytes;
+    if (overlap || hipEventQuery(u.ev) == hipSuccess) {
+      if (overlap) (void)hipEventSynchronize(u.ev);
+      (void)hipEventDestroy(u.ev);
+      g_ring_pending[i] = g_ring_pending.back();
+      g_ring_pending.pop_back();
+    } else {
+      i++;
+    }
+  }
+  std::memcpy(g_ring + off, host, bytes);
+  out->host.assign(static_cast<const uint8_t*>(host), static_cast<const uint8_t*>(host) + bytes);
+  g_ring_head = off + bytes;
+  int st = check_hip(hipMallocAsync(&out->dev, bytes, stream), "hipMallocAsync");
+  if (st) return st;
+  out->stream = stream;
+  st = check_hip(hipMemcpyAsync(out->dev, g_ring + off, bytes, hipMemcpyHostToDevice, stream),
+                 "hipMemcpyAsync column table");
+  if (st) return st;
+  hipEvent_t ev;
+  if ((st = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate")))
+    return st;
+  (void)hipEventRecord(ev, stream);
+  g_ring_pending.push_back(RingUse{off, bytes, ev});
+  return FURY_OK;
+}
+
 namespace {
 
 bool misaligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; }
@@ -77,15 +137,18 @@ int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const c
 }
 
 int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
-               bool need_validity, FixedArgs* a, bool* fast) {
-  if (s->num_fields > kMaxFixedCols)
+               bool need_validity, FixedArgs* a, bool* fast, DeviceTable* dt, hipStream_t hs) {
+  if (s->num_fields > kMaxWideFixedCols)
     return set_error(FURY_ERR_UNSUPPORTED, "fixed-width device path handles at most " +
-                                               std::to_string(kMaxFixedCols) + " fields");
+                                               std::to_string(kMaxWideFixedCols) +
+                                               " fields (a 64-row tile must fit the LDS)");
   *a = FixedArgs{};
   a->ncols = s->num_fields;
   a->bitmap_bytes = s->bitmap_bytes;
   a->row_size = s->fixed_size;
   a->nrows = nrows;
+  const bool wide = s->num_fields > kMaxFixedCols;
+  std::vector<FixedCol> tab(wide ? s->num_fields : 0);
   bool all8 = true, anyv = false;
   for (int k = 0; k < s->num_fields; k++) {
     const FieldPlan& p = s->plan[k];
@@ -101,32 +164,40 @@ int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, boo
     if (need_validity && !c.validity)
       return set_error(FURY_ERR_INVALID_ARGUMENT,
                        "column " + std::to_string(k) + ": Arrow output needs a validity buffer");
-    a->col[k].values = static_cast<const uint8_t*>(c.values);
-    a->col[k].validity = c.validity;
-    a->col[k].width = w;
+    FixedCol& fc = wide ? tab[k] : a->col[k];
+    fc.values = static_cast<const uint8_t*>(c.values);
+    fc.validity = c.validity;
+    fc.width = w;
     if (w != 8) all8 = false;
     if (c.validity) anyv = true;
   }
   (void)decode;
-  *fast = all8 && !anyv;
+  *fast = all8 && !anyv && !wide;         // wide tables run the general tile kernel only
+  if (wide) {
+    const int st = upload_table(tab.data(), tab.size() * sizeof(FixedCol), hs, dt);
+    if (st) return st;
+    a->tab = static_cast<const FixedCol*>(dt->dev);
+  }
   return FURY_OK;
 }
 
 int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
-             bool need_validity, VarArgs* a) {
-  if (s->num_fields > kMaxVarCols)
+             bool need_validity, VarArgs* a, DeviceTable* dt, hipStream_t hs) {
+  if (s->num_fields > kMaxWideVarCols)
     return set_error(FURY_ERR_UNSUPPORTED, "variable-length device path handles at most " +
-                                               std::to_string(kMaxVarCols) + " fields");
+                                               std::to_string(kMaxWideVarCols) + " fields");
   *a = VarArgs{};
   a->ncols = s->num_fields;
   a->bitmap_bytes = s->bitmap_bytes;
   a->fixed_size = s->fixed_size;
   a->nrows = nrows;
+  const bool wide = s->num_fields > kMaxVarCols;
+  std::vector<VarCol> tab(wide ? s->num_fields : 0);
   int nvar = 0;
   for (int k = 0; k < s->num_fields; k++) {
     const FieldPlan& p = s->plan[k];
     const fury_column& c = cols[k];
-    VarCol& v = a->col[k];
+    VarCol& v = wide ? tab[k] : a->col[k];
     const std::string who = "column " + std::to_string(k) + " (" + s->fields[k].name + ")";
     v.kind = p.kind;
     v.nullable = p.nullable;
@@ -191,7 +262,15 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     }
   }
   a->nvar = nvar;
-  a->tile_rows = encode_tile_rows(*a);
+  if (wide) {                      // wider than the argument block: the table goes to the device
+    const int st = upload_table(tab.data(), tab.size() * sizeof(VarCol), hs, dt);
+    if (st) return st;
+    a->tab = static_cast<const VarCol*>(dt->dev);
+    a->htab = reinterpret_cast<const VarCol*>(dt->host.data());
+    a->tile_rows = encode_tile_rows(*a);
+  } else {
+    a->tile_rows = encode_tile_rows(*a);
+  }
   a->err = device_error_word();
   // FURY_VAR_DBG selects kernel variants for A/B (bits 512 / 1024 / 2048: all correct).  Bits
   // 1-64 switch phases OFF for timing (scripts/diag_var.py) and leave wrong outputs, so they
@@ -291,7 +370,8 @@ int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrow
   if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
   if (s->generic) return gen_measure(s, cols, nrows, row_offsets, static_cast<hipStream_t>(stream));
   VarArgs a;
-  st = var_args(s, cols, nrows, false, false, &a);
+  DeviceTable dt;
+  st = var_args(s, cols, nrows, false, false, &a, &dt, static_cast<hipStream_t>(stream));
   if (st) return st;
   return launch_measure_rows(a, row_offsets, static_cast<hipStream_t>(stream));
 }
@@ -308,7 +388,8 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
     // Fixed schemas: rows are contiguous at i * fixed_size (row_offsets, when given, are those).
     FixedArgs a;
     bool fast = false;
-    st = fixed_args(s, cols, nrows, false, false, &a, &fast);
+    DeviceTable dt;
+    st = fixed_args(s, cols, nrows, false, false, &a, &fast, &dt, hs);
     if (st) return st;
     return launch_encode_fixed(a, static_cast<uint8_t*>(rows), hs, fast);
   }
@@ -322,7 +403,8 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
     return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), INT64_MAX, hs);
   }
   VarArgs a;
-  st = var_args(s, cols, nrows, false, false, &a);
+  DeviceTable dt;
+  st = var_args(s, cols, nrows, false, false, &a, &dt, hs);
   if (st) return st;
   return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), INT64_MAX, hs);
 }
@@ -356,7 +438,8 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
     return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
   }
   VarArgs a;
-  st = var_args(s, cols, nrows, false, false, &a);
+  DeviceTable dt;
+  st = var_args(s, cols, nrows, false, false, &a, &dt, hs);
   if (st) return st;
   st = launch_measure_rows(a, row_offsets, hs);
   if (st || nrows == 0) return st;
@@ -386,7 +469,8 @@ int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_
                      "nested schema: size outputs with fury_decode_prepare / fury_decode_execute");
   if (!rows || !row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/row_offsets null");
   VarArgs a;
-  st = var_args(s, cols, nrows, true, false, &a);
+  DeviceTable dt;
+  st = var_args(s, cols, nrows, true, false, &a, &dt, static_cast<hipStream_t>(stream));
   if (st) return st;
   return launch_decode_measure(a, static_cast<const uint8_t*>(rows), row_offsets,
                                static_cast<hipStream_t>(stream));
@@ -404,7 +488,8 @@ static int decode_impl(const fury_schema* s, const void* rows, const int64_t* ro
     if (misaligned(rows, 16)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 16-byte aligned");
     FixedArgs a;
     bool fast = false;
-    st = fixed_args(s, cols, nrows, true, arrow, &a, &fast);
+    DeviceTable dt;
+    st = fixed_args(s, cols, nrows, true, arrow, &a, &fast, &dt, hs);
     if (st) return st;
     return launch_decode_fixed(a, static_cast<const uint8_t*>(rows), hs, fast);
   }
@@ -415,7 +500,8 @@ static int decode_impl(const fury_schema* s, const void* rows, const int64_t* ro
     return set_error(FURY_ERR_INVALID_ARGUMENT,
                      "nested schema: decode with fury_decode_prepare / fury_decode_execute");
   VarArgs a;
-  st = var_args(s, cols, nrows, true, arrow, &a);
+  DeviceTable dt;
+  st = var_args(s, cols, nrows, true, arrow, &a, &dt, hs);
   if (st) return st;
   return launch_decode_var(a, static_cast<const uint8_t*>(rows), row_offsets, hs, arrow);
 }

@@ -76,6 +76,11 @@ __device__ __forceinline__ uint8_t* values_of(const FixedArgs& a, int c, int lan
   }
 }
 
+// Column record c of the general path: argument block, or the device table of a wide schema.
+__device__ __forceinline__ const FixedCol& fcol(const FixedArgs& a, int c) {
+  return a.tab ? a.tab[c] : a.col[c];
+}
+
 // Tile of workgroup b.  Workgroups are dealt round-robin to the 8 XCDs (b % 8); tile_order 1
 // gives each XCD one contiguous eighth of the tiles (b -> (b % 8) * (nb / 8) + b / 8 on the
 // largest multiple of 8, identity on the tail), so an XCD's L2 and TLB see one address range.
@@ -279,11 +284,12 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
         if (kFast) {
           v[u] = ld8<NT>(values_of<R>(a, c, lane) + row * 8);
         } else {
-          const uint8_t* vb = a.col[c].validity;
+          const FixedCol& fc = fcol(a, c);
+          const uint8_t* vb = fc.validity;
           if (vb && !((vb[row >> 3] >> (row & 7)) & 1)) {
             isnull[u] = true;
           } else {
-            v[u] = load_value(a.col[c].values, row, a.col[c].width);
+            v[u] = load_value(fc.values, row, fc.width);
           }
         }
       }
@@ -369,8 +375,9 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       bool isnull = live && ((rowp[c >> 3] >> (c & 7)) & 1);
       uint64_t v = 0;
       if (live && !isnull) v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-      const int w = a.col[c].width;
-      uint8_t* dst = const_cast<uint8_t*>(a.col[c].values);
+      const FixedCol& fc = fcol(a, c);
+      const int w = fc.width;
+      uint8_t* dst = const_cast<uint8_t*>(fc.values);
       // rows [rbase, rbase + 64) of this wave; rbase % 64 == 0 and R % 64 == 0
       const int64_t rbase = row - lane;
       const int64_t nvalid = a.nrows - rbase;                    // >= 1 for live waves
@@ -381,7 +388,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       } else if (live) {
         store_value(dst, row, w, v);
       }
-      uint8_t* vb = a.col[c].validity;
+      uint8_t* vb = fc.validity;
       if (vb) {
         uint64_t ok = __ballot(live && !isnull);
         if (lane < nbytes) vb[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 #include "internal.h"
 
@@ -24,8 +25,14 @@ struct FixedCol {
   int32_t pad_;
 };
 
+// Schemas wider than kMaxFixedCols take their column table from device memory (uploaded per
+// call, FixedArgs.tab) and run the general tile kernel with 64-row tiles; kMaxWideFixedCols keeps
+// a 64-row tile (bitmap + 8 B per field per row) within the 160 KB of LDS.
+constexpr int kMaxWideFixedCols = 315;
+
 struct FixedArgs {
   FixedCol col[kMaxFixedCols];
+  const FixedCol* tab;                // device table for > kMaxFixedCols fields, else NULL
   int32_t ncols;
   int32_t bitmap_bytes;
   int32_t row_size;
@@ -40,6 +47,8 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
 
 // ---- variable-length schemas ----------------------------------------------------------------
 constexpr int kMaxVarCols = 64;
+// Wider schemas: column table in device memory (VarArgs.tab), LDS-DMA / ticketed kernels.
+constexpr int kMaxWideVarCols = 256;
 
 // One top-level field as seen by the var kernels.
 struct VarCol {
@@ -56,6 +65,8 @@ struct VarCol {
 
 struct VarArgs {
   VarCol col[kMaxVarCols];
+  const VarCol* tab;         // device table for > kMaxVarCols fields, else NULL
+  const VarCol* htab;        // its host copy (launchers only; never read on the device)
   int32_t ncols;
   int32_t bitmap_bytes;
   int32_t fixed_size;
@@ -73,6 +84,19 @@ struct VarArgs {
 uint32_t* device_error_word();
 int take_device_error();
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
+
+// Copies a host column table to device memory on `stream` (stream-ordered: through a pinned
+// staging ring, no host synchronisation); the table is freed stream-ordered when the holder goes.
+struct DeviceTable {
+  void* dev = nullptr;
+  hipStream_t stream = nullptr;
+  std::vector<uint8_t> host;          // host copy of the table (for the launchers)
+  DeviceTable() = default;
+  DeviceTable(const DeviceTable&) = delete;
+  DeviceTable& operator=(const DeviceTable&) = delete;
+  ~DeviceTable();
+};
+int upload_table(const void* host, size_t bytes, hipStream_t stream, DeviceTable* out);
 
 // Device scratch for scans; grown on demand (hipMalloc outside graph capture only).
 struct Workspace {

@@ -8,6 +8,9 @@
 namespace fury {
 
 namespace {
+// Column k on the host side of a launch: the argument block, or the host copy of a wide table.
+const VarCol& hcol(const VarArgs& a, int k) { return a.htab ? a.htab[k] : a.col[k]; }
+
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back (tile rows by sequence
@@ -76,7 +79,7 @@ bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
   double pay_row = 0, img_row = a.fixed_size;
   int nvarc = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = hcol(a, k);
     if (c.kind == kDecimal) img_row += 16;
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     nvarc++;
@@ -93,7 +96,7 @@ bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
   for (int R = kEncRows; R >= 32; R -= 32) {
     int64_t meta = 8 * int64_t(R + 1) + 32;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
+      const VarCol& c = hcol(a, k);
       if (c.validity) meta += R / 8 + 32;
       if (c.kind == kFixed) meta += int64_t(R) * c.width + 32;
       else if (c.kind == kBool) meta += R / 8 + 32;
@@ -119,7 +122,7 @@ bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
 int reg_tile_rows(const VarArgs& a) {
   double img_row = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = hcol(a, k);
     if (c.kind == kDecimal) img_row += 16;
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const double per = c.capacity > 0 && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
@@ -135,7 +138,7 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
   if (a.nrows == 0) return FURY_OK;
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
   PipeLayout L;
-  if ((a.dbg & 2048) && plan_encode_pipe(a, &L)) {
+  if ((a.dbg & 2048) && !a.tab && plan_encode_pipe(a, &L)) {
     VarArgs b = a;
     b.tile_rows = L.rows;
     const int64_t nt = (a.nrows + L.rows - 1) / L.rows;
@@ -155,21 +158,26 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     b.tile_rows = reg_tile_rows(a);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     return launch_encode_var_reg(b, offs, rows, cap, nt, stream);
+  } else if (a.tab) {          // wider than the argument block: column table in device memory
+    hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
+                       offs, rows, cap);
   } else if (a.dbg & 512) {
     hipLaunchKernelGGL(encode_var_kernel_d, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
   } else {
-    hipLaunchKernelGGL(encode_var_kernel, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
+    hipLaunchKernelGGL(encode_var_kernel<MetaMap>, dim3(nb), dim3(kEncRows), 0, stream, a, offs,
+                       rows, cap);
   }
   return check_hip(hipGetLastError(), "encode_var launch");
 }
 
-// Rows per encode tile so that the staged per-row inputs of a tile fit kMetaPool (always true at
-// 8 rows: <= 64 columns x (validity + 16-B decimal) pieces).
+// Rows per encode tile so that the staged per-row inputs of a tile fit kMetaPool; at 8 rows even
+// kMaxWideVarCols columns of nullable decimals (~176 B of staged pieces each) stay within the
+// kEncPool the LDS-DMA kernel stages them in.
 int encode_tile_rows(const VarArgs& a) {
   for (int R = kEncRows; R >= 8; R >>= 1) {
     int64_t meta = 0;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
+      const VarCol& c = hcol(a, k);
       if (c.validity) meta += R / 8 + 32;
       if (c.kind == kFixed) meta += int64_t(R) * c.width + 32;
       else if (c.kind == kBool) meta += R / 8 + 32;
@@ -185,7 +193,7 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
                           hipStream_t stream) {
   int nseq = 0;
   for (int k = 0; k < a.ncols; k++)
-    if (a.col[k].kind == kBytes || a.col[k].kind == kListFixed) nseq++;
+    if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
   if (nseq == 0 || a.nrows == 0) return FURY_OK;
   const int64_t nb = nblocks(a.nrows);
   int64_t* ws = nullptr;
@@ -214,7 +222,7 @@ uint32_t dec_img_bytes(const VarArgs& a, int tile) {
   if ((a.dbg & 8192) || a.nrows <= 0) return static_cast<uint32_t>(cap);
   int64_t need = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = hcol(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     if (!c.values) continue;
     const double per = static_cast<double>(c.capacity) / static_cast<double>(a.nrows);
@@ -233,7 +241,7 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   if (a.nrows == 0) return FURY_OK;
   int nseq = 0;
   for (int k = 0; k < a.ncols; k++)
-    if (a.col[k].kind == kBytes || a.col[k].kind == kListFixed) nseq++;
+    if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
   const int64_t nb = nblocks(a.nrows);
   if (g_var_decode == 1) {       // sizing pass, then the decode kernel reads those offsets
     int st = launch_decode_measure(a, rows, offs, stream);

@@ -42,6 +42,12 @@ constexpr int kThreads = 256;                 // = rows per workgroup
 constexpr int kDecodeStage = 32 * 1024;       // LDS image of the group's row range (decode)
 constexpr int kStrStage = 8 * 1024;           // LDS image of one column's Arrow payload range
 
+// Column record k: from the kernel argument block, or -- schemas wider than kMaxVarCols -- from
+// the device table the host uploaded for the call (VarArgs.tab).  Uniform branch, scalar loads.
+__device__ __forceinline__ const VarCol& vc(const VarArgs& a, int k) {
+  return a.tab ? a.tab[k] : a.col[k];
+}
+
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
 }
@@ -316,13 +322,16 @@ struct PipeLayout {
 };
 
 // LDS byte offsets of one tile's staged inputs, per column (kNone = not present / not staged).
-struct MetaMap {
-  uint32_t fix[kMaxVarCols];   // fixed values (row r0) / bool bits (byte r0/8) / decimal values
-  uint32_t val[kMaxVarCols];   // validity bits, byte r0/8
-  uint32_t off[kMaxVarCols];   // int32 offsets, entry r0
-  uint32_t pay[kMaxVarCols];   // payload bytes at offsets[r0] (bool elements: byte offsets[r0]/8)
-  uint32_t pvb[kMaxVarCols];   // list element validity, byte offsets[r0]/8
+template <int N>
+struct MetaMapN {
+  uint32_t fix[N];   // fixed values (row r0) / bool bits (byte r0/8) / decimal values
+  uint32_t val[N];   // validity bits, byte r0/8
+  uint32_t off[N];   // int32 offsets, entry r0
+  uint32_t pay[N];   // payload bytes at offsets[r0] (bool elements: byte offsets[r0]/8)
+  uint32_t pvb[N];   // list element validity, byte offsets[r0]/8
 };
+using MetaMap = MetaMapN<kMaxVarCols>;
+using MetaMapWide = MetaMapN<kMaxWideVarCols>;
 
 // Issues LDS-DMA copies of the 16-B-aligned pieces covering [gb, ge) into pool[at...]; returns
 // the LDS offset of byte gb and advances `at` (kept 16-aligned).  Reading whole aligned pieces
@@ -352,11 +361,11 @@ __device__ __forceinline__ bool lds_bit(const uint8_t* pool, uint32_t off, int64
 }
 
 // Phase A: stage every column's per-row inputs of rows [r0, r0 + nr).
-template <int NT>
+template <int NT, class MM>
 __device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int64_t nr,
-                                               uint8_t* pool, MetaMap& mm, uint32_t at = 0) {
+                                               uint8_t* pool, MM& mm, uint32_t at = 0) {
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     uint32_t fix = kNone, val = kNone, off = kNone;
     if (c.validity) val = stage_range<NT>(pool, at, c.validity + (r0 >> 3), c.validity + ((r0 + nr + 7) >> 3));
     switch (c.kind) {
@@ -386,11 +395,12 @@ __device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int
 }
 
 // Row size of tile row t from the staged inputs (writerIndex growth of toRow).
-__device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MetaMap& mm,
+template <class MM>
+__device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MM& mm,
                                                  const uint8_t* pool, int t) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind < kBytes) continue;
     if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) continue;
     if (c.kind == kDecimal) {
@@ -405,11 +415,12 @@ __device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MetaMap
 }
 
 // Bytes the payload staging of the tile needs (uniform; from the staged offsets).
-__device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MetaMap& mm,
+template <class MM>
+__device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MM& mm,
                                                  const uint8_t* pool, int nr) {
   uint64_t need = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
     if (e <= b) continue;
@@ -424,12 +435,12 @@ __device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MetaMap
 }
 
 // Phase C: stage the payload ranges.
-template <int NT>
-__device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, uint8_t* pool,
+template <int NT, class MM>
+__device__ __forceinline__ void stage_payloads(const VarArgs& a, MM& mm, uint8_t* pool,
                                                uint32_t at, int nr) {
   const bool iss = !(a.dbg & 1);
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
     uint32_t pay = kNone, pvb = kNone;
@@ -450,7 +461,8 @@ __device__ __forceinline__ void stage_payloads(const VarArgs& a, MetaMap& mm, ui
 // Builds tile row t at dst (8-byte aligned) exactly as toRow does.  Per-row inputs come from the
 // staged meta in `pool`; a column's payload from `pay` when it was staged (mm.pay[k] != kNone),
 // else straight from global memory.
-__device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& mm,
+template <class MM>
+__device__ __forceinline__ void build_tile_row(const VarArgs& a, const MM& mm,
                                                const uint8_t* pool, const uint8_t* pay, int t,
                                                uint8_t* dst) {
   uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
@@ -458,10 +470,10 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
   int64_t cursor = a.fixed_size;
   uint64_t nullbits = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     uint64_t slot = 0;
     if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) {
-      nullbits |= 1ull << k;
+      nullbits |= 1ull << (k & 63);
     } else {
       switch (c.kind) {
         case kFixed: {
@@ -515,8 +527,12 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MetaMap& 
       }
     }
     d64[nslot0 + k] = slot;
+    if ((k & 63) == 63) {                    // > 64 fields: one bitmap word per 64 fields
+      d64[k >> 6] = nullbits;
+      nullbits = 0;
+    }
   }
-  d64[0] = nullbits;                         // var path: <= 64 fields -> one bitmap word
+  if (a.ncols & 63) d64[(a.ncols - 1) >> 6] = nullbits;
 }
 
 // DIAGNOSTIC: build_tile_row with the column kinds known at compile time (experiment on the
@@ -526,8 +542,8 @@ struct SpecMixed {
   static constexpr int kind[6] = {kFixed, kFixed, kFixed, kBytes, kBytes, kBytes};
   static constexpr int width[6] = {4, 8, 8, 1, 1, 1};
 };
-template <class S>
-__device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MetaMap& mm,
+template <class S, class MM>
+__device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MM& mm,
                                                     const uint8_t* pool, const uint8_t* pay, int t,
                                                     uint8_t* dst) {
   uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
@@ -552,7 +568,7 @@ __device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const Meta
   }
 #pragma unroll
   for (int k = 0; k < S::n; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     uint64_t slot = 0;
     if (!ok[k]) {
       nullbits |= 1ull << k;
@@ -572,10 +588,10 @@ __device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const Meta
 
 // Encode workgroup: rows [r0, r0 + R) at the offsets fury_row_measure produced.  Bytes at or
 // past `cap` are never written.
-template <int POOL, bool kStagePay>
+template <int POOL, bool kStagePay, class MM>
 __device__ __forceinline__ void encode_tile(const VarArgs& a, const int64_t* __restrict__ offs,
                                             uint8_t* __restrict__ rows, int64_t cap, int64_t tile,
-                                            uint8_t* pool, MetaMap& mm) {
+                                            uint8_t* pool, MM& mm) {
   const int tid = threadIdx.x;
   const int R = a.tile_rows;                 // rows per tile (host-chosen so the meta fits)
   const int64_t r0 = tile * R;
@@ -611,12 +627,13 @@ __device__ __forceinline__ void encode_tile(const VarArgs& a, const int64_t* __r
 }
 
 #ifdef FURY_VAR_MAIN
+template <class MM = MetaMap>
 __global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
                                                               const int64_t* __restrict__ offs,
                                                               uint8_t* __restrict__ rows,
                                                               int64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPool];
-  __shared__ MetaMap mm;
+  __shared__ MM mm;
   encode_tile<kEncPool, true>(a, offs, rows, cap, blockIdx.x, pool, mm);
 }
 #endif  // FURY_VAR_MAIN
@@ -910,7 +927,7 @@ __device__ __forceinline__ void pipe_issue(const VarArgs& a, const int64_t* __re
   stage_meta<NT>(a, r0, nr, meta, ps.mm, at);        // sets every mm.pay / mm.pvb to kNone
   uint32_t pat = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
     if (e <= b) continue;
@@ -1005,7 +1022,7 @@ constexpr int kMeasTile = kThreads * kMeasRows;                // rows per workg
 __device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind < kBytes) continue;
     if (c.validity && !bit_at(c.validity, r)) continue;          // null: setNullAt only
     if (c.kind == kDecimal) {
@@ -1030,7 +1047,7 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* _
 #pragma unroll
     for (int j = 0; j < kMeasRows; j++) sz[j] = a.fixed_size;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
+      const VarCol& c = vc(a, k);
       if (c.kind < kBytes) continue;
       const uint32_t vb = c.validity ? (c.validity[r >> 3] >> (r & 7)) : 0xffu;
       if (c.kind == kDecimal) {
@@ -1120,7 +1137,7 @@ __global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
       r < a.nrows ? (staged ? stage + d0 + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t cnt = row ? var_count(a, c, k, row) : 0;
     int64_t total;
@@ -1140,7 +1157,7 @@ __global__ __launch_bounds__(kThreads) void decode_measure_fix(VarArgs a,
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     if (r < a.nrows) c.offsets[r] += static_cast<int32_t>(sums[seq * nb + blockIdx.x]);
     if (r == a.nrows - 1) c.offsets[a.nrows] = static_cast<int32_t>(totals[seq]);
@@ -1670,7 +1687,7 @@ __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row
                                             int nseq) {
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     if (!is_seq(c)) continue;
     const int q = seq++ - cbase;
     if (q < 0) continue;
@@ -1696,9 +1713,9 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
     if (threadIdx.x < nchunk) {
       int seq = 0;
       for (int k = 0; k < a.ncols; k++) {
-        if (!is_seq(a.col[k])) continue;
+        if (!is_seq(vc(a, k))) continue;
         if (seq++ == cbase + static_cast<int>(threadIdx.x)) {
-          sh.base[threadIdx.x] = a.col[k].offsets[b * kThreads];
+          sh.base[threadIdx.x] = vc(a, k).offsets[b * kThreads];
           break;
         }
       }
@@ -1735,7 +1752,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
 
   // fixed-width fields and every field's validity: no dependency on other groups
   for (int k = 0; k < ((a.dbg & 8) ? 0 : a.ncols); k++) {
-    const VarCol& c = a.col[k];
+    const VarCol& c = vc(a, k);
     const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
     const uint64_t slot =
         (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
@@ -1777,7 +1794,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
     chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq);
     int seq = 0;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = a.col[k];
+      const VarCol& c = vc(a, k);
       if (!is_seq(c)) continue;
       const int q = seq++ - cbase;
       if (q < 0) continue;

@@ -208,3 +208,24 @@ def test_collection_schema_create():
     buf = ctypes.create_string_buffer(64)
     assert L.fury_frame_rows(s.handle, buf, buf, 1, buf, buf, None) == 2
     assert L.fury_unframe_rows(m.handle, buf, 64, 1, buf, buf, None) == 2
+
+
+def test_wide_schema_limits_reported_on_host():
+    """Beyond the widest tiles (315 fixed-width / 256 variable-length fields) the device calls
+    report UnsupportedOperationException before touching the GPU."""
+    import numpy as np
+    from fury_amd import _native as N
+    from fury_amd.encoder import Schema
+    L = N.lib()
+    buf = np.zeros(64, np.uint64)
+    for n, kind in ((316, T.INT64), (257, T.STRING)):
+        s = Schema([T.field(f"f{i:03d}", kind) for i in range(n)])
+        cols = (N.FuryColumn * n)()
+        for k in range(n):
+            cols[k].values = buf.ctypes.data
+            cols[k].offsets = buf.ctypes.data
+        if kind == T.INT64:
+            assert L.fury_row_encode(s.handle, cols, 1, None, buf.ctypes.data, None) == 2
+        else:
+            assert L.fury_row_encode(s.handle, cols, 1, buf.ctypes.data, buf.ctypes.data, None) == 2
+        assert "at most" in N.last_error()

@@ -1086,3 +1086,42 @@ def test_map_encoder_batch_vs_oracle(oracle, dev):
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     dec = column_to_host(enc.decode_batch(batch)[0])
     assert [value_at(mf, dec, i) for i in range(n)] == vals
+
+
+# ---- round 2: schemas wider than the kernel argument block (column table in device memory) ----
+def test_wide_fixed_300_fields(oracle, dev):
+    """300 fixed-width fields (int8..int64, float, double, bool, date, timestamp; every third one
+    nullable): beyond the argument block's 128 columns the general tile kernel reads the column
+    table the host uploaded for the call.  Encode / decode / rows_to_arrow oracle-exact."""
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    kinds = [T.INT64, T.FLOAT64, T.INT32, T.BOOL, T.INT16, T.FLOAT32, T.INT8, T.DATE32, T.TIMESTAMP]
+    fields = [(T.field if i % 3 == 0 else T.not_null_field)(f"f{i:03d}", kinds[i % len(kinds)])
+              for i in range(300)]
+    n = 1500
+    host = gen_columns("wide", fields, n, seed=30, null_pct=15)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    assert enc.schema().is_fixed and enc.schema().fixed_size == 40 + 8 * 300
+    want, offs = oracle.encode(fields, host, n)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()],
+                         oracle.decode(fields, want, offs, n), n)
+
+
+@pytest.mark.parametrize("ncols,n", [(100, 2000), (200, 700), (256, 300)])
+def test_wide_var_schemas_beyond_arg_block(oracle, dev, ncols, n):
+    """100 / 200 / 256-field schemas with strings, lists, bools and nulls (multi-word row null
+    bitmaps): encode (measure + encode), encode_measured, decode and rows_to_arrow oracle-exact."""
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    fields = _wide_fields(ncols)
+    host = gen_columns("wide", fields, n, seed=ncols, null_pct=20, str_max=48, list_max=9,
+                       list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    rows, offs, total = _encode_measured(enc, _dev_cols(host, dev), n, dev)
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()],
+                         oracle.decode(fields, want, want_offs, n), n)
