@@ -286,12 +286,16 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
 // Generic engine arguments: schema nodes (breadth-first) + the column tree walked in the same
 // order (LIST: child[0] = elements; STRUCT: child[0..n); MAP: child[0] keys, child[1] values).
 int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
-             bool need_validity, GenArgs* g) {
+             bool need_validity, GenArgs* g, DeviceTable* dt, hipStream_t hs) {
   const size_t nn = s->nodes.size();
-  if (nn > static_cast<size_t>(kGenMaxNodes))
+  if (nn > static_cast<size_t>(kGenMaxWideNodes))
     return set_error(FURY_ERR_UNSUPPORTED, "nested schema has more than " +
-                                               std::to_string(kGenMaxNodes) + " nodes");
+                                               std::to_string(kGenMaxWideNodes) + " nodes");
+  const bool wide = nn > static_cast<size_t>(kGenMaxNodes);
+  std::vector<GenNode> tab(wide ? nn : 0);
+  GenNode* nodes = nullptr;
   *g = GenArgs{};
+  nodes = wide ? tab.data() : g->node;
   g->nnodes = static_cast<int32_t>(nn);
   g->ntop = s->num_fields;
   g->nrows = nrows;
@@ -308,7 +312,7 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     const fury_column* c = col[i];
     const std::string who = "schema node " + std::to_string(i);
     if (!c) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": missing column");
-    GenNode& n = g->node[i];
+    GenNode& n = nodes[i];
     n.values = static_cast<const uint8_t*>(c->values);
     n.validity = c->validity;
     n.offsets = c->offsets;
@@ -318,7 +322,7 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     // breadth-first order: a node's parent is set before it
     if (i < static_cast<size_t>(s->num_fields)) n.row_aligned = 1;
     if (n.row_aligned && t.type_id == FURY_TYPE_STRUCT)
-      for (int j = 0; j < t.num_children; j++) g->node[t.first_child + j].row_aligned = 1;
+      for (int j = 0; j < t.num_children; j++) nodes[t.first_child + j].row_aligned = 1;
     if (t.num_children > 0) {
       if (!c->child) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": child columns missing");
       for (int j = 0; j < t.num_children; j++) col[t.first_child + j] = &c->child[j];
@@ -334,13 +338,19 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     if (decode && t.type_id == FURY_TYPE_BOOL && c->values && misaligned(c->values, 4))
       return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": bool bitmap must be 4-byte aligned");
   }
+  if (wide) {                      // more nodes than the argument block: table to the device
+    const int st = upload_table(tab.data(), tab.size() * sizeof(GenNode), hs, dt);
+    if (st) return st;
+    g->tab = static_cast<const GenNode*>(dt->dev);
+  }
   return FURY_OK;
 }
 
 int gen_measure(const fury_schema* s, const fury_column* cols, int64_t nrows, int64_t* offs,
                 hipStream_t stream) {
   GenArgs g;
-  int st = gen_args(s, cols, nrows, false, false, &g);
+  DeviceTable dt;
+  int st = gen_args(s, cols, nrows, false, false, &g, &dt, stream);
   if (st) return st;
   if (nrows == 0) return check_hip(hipMemsetAsync(offs, 0, 8, stream), "memset");
   st = launch_gen_measure(g, offs, stream);
@@ -398,7 +408,8 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
                      "variable-length schema needs row_offsets from fury_row_measure");
   if (s->generic) {
     GenArgs g;
-    st = gen_args(s, cols, nrows, false, false, &g);
+    DeviceTable dt;
+    st = gen_args(s, cols, nrows, false, false, &g, &dt, hs);
     if (st) return st;
     return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), INT64_MAX, hs);
   }
@@ -433,7 +444,8 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
     st = gen_measure(s, cols, nrows, row_offsets, hs);
     if (st || nrows == 0) return st;
     GenArgs g;
-    st = gen_args(s, cols, nrows, false, false, &g);
+    DeviceTable dt;
+    st = gen_args(s, cols, nrows, false, false, &g, &dt, hs);
     if (st) return st;
     return launch_gen_encode(g, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
   }
@@ -542,18 +554,28 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
     g.ntop = s->num_fields;
     g.nrows = nrows;
     g.root = s->root;
+    const bool wide = nn > kGenMaxNodes;
+    std::vector<GenNode> tab(wide ? nn : 0);
+    GenNode* nodes = wide ? tab.data() : g.node;
     for (int i = 0; i < nn; i++) {
-      g.node[i].type = s->nodes[i].type_id;
-      g.node[i].first_child = s->nodes[i].first_child;
-      g.node[i].num_children = s->nodes[i].num_children;
+      nodes[i].type = s->nodes[i].type_id;
+      nodes[i].first_child = s->nodes[i].first_child;
+      nodes[i].num_children = s->nodes[i].num_children;
+    }
+    DeviceTable dt;
+    if (wide) {
+      const int st0 = upload_table(tab.data(), tab.size() * sizeof(GenNode), hs, &dt);
+      if (st0) { delete p; return st0; }
+      g.tab = static_cast<const GenNode*>(dt.dev);
     }
     const int64_t cells = 2 * static_cast<int64_t>(nn) * nrows;
     int64_t* dev = nullptr;
-    int st = check_hip(hipMalloc(reinterpret_cast<void**>(&dev),
-                                 (cells + 2 * nn + scan_workspace(cells) + 2 * nn + 1) * 8),
-                       "hipMalloc");
+    // [counts cells][totals 2 nn][scan workspace][wide schemas: cursor scratch cells]
+    const int64_t words = cells + 2 * nn + scan_workspace(cells) + 2 * nn + 1 + (wide ? cells : 0);
+    int st = check_hip(hipMalloc(reinterpret_cast<void**>(&dev), words * 8), "hipMalloc");
     if (st) { delete p; return st; }
     p->cnt = dev;
+    p->scratch = wide ? dev + (words - cells) : nullptr;
     st = launch_gen_count(g, p->rows, row_offsets, dev, hs);
     int64_t* tot = dev + cells;
     int64_t* ws = tot + 2 * nn;
@@ -576,9 +598,11 @@ int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, v
   if (!p) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_decode_execute: plan is null");
   if (p->nrows == 0) return FURY_OK;
   GenArgs g;
-  int st = gen_args(p->schema, cols, p->nrows, true, arrow != 0, &g);
+  DeviceTable dt;
+  hipStream_t hs = static_cast<hipStream_t>(stream);
+  int st = gen_args(p->schema, cols, p->nrows, true, arrow != 0, &g, &dt, hs);
   if (st) return st;
-  return launch_gen_decode(g, p->rows, p->offs, p->cnt, static_cast<hipStream_t>(stream));
+  return launch_gen_decode(g, p->rows, p->offs, p->cnt, p->scratch, hs);
 }
 
 void fury_decode_plan_destroy(fury_decode_plan* p) {

@@ -254,37 +254,48 @@ __device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* b
 
 // The node table is copied from the argument block into LDS once per workgroup and passed to
 // the (non-inlined, recursive-by-depth) helpers as a pointer: taking the address of the kernel
-// argument itself would make the compiler copy the whole block into per-lane scratch.
+// argument itself would make the compiler copy the whole block into per-lane scratch.  Schemas
+// with more nodes than the argument block holds (kWide) read the table the host uploaded for the
+// call straight from device memory (uniform indices: scalar loads).
+template <bool kWide>
 __device__ __forceinline__ const GenNode* stage_nodes(const GenArgs& g, GenNode* lds) {
+  if (kWide) return g.tab;
   for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) lds[i] = g.node[i];
   __syncthreads();
   return lds;
 }
 
+template <bool kWide>
 __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int64_t* __restrict__ sizes) {
-  __shared__ GenNode sn[kGenMaxNodes];
-  const GenNode* nodes = stage_nodes(g, sn);
+  __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
+  const GenNode* nodes = stage_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
   if (r < g.nrows) sizes[r] = put_row<false>(nodes, g.ntop, r, nullptr, g.root);
 }
 
+template <bool kWide>
 __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
                                                                  uint8_t* __restrict__ rows,
                                                                  int64_t cap) {
-  __shared__ GenNode sn[kGenMaxNodes];
-  const GenNode* nodes = stage_nodes(g, sn);
+  __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
+  const GenNode* nodes = stage_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
   if (r < g.nrows && offs[r + 1] <= cap) put_row<true>(nodes, g.ntop, r, rows + offs[r], g.root);
 }
 
 // ---- decode ----------------------------------------------------------------------------------
-// Per thread, per node: running Arrow entry index and payload byte position, in LDS.
+// Per thread, per node: running Arrow entry index and payload byte position -- in LDS (stride 1,
+// bytes after the nnodes entries), or, for schemas wider than the LDS budget, in the plan's
+// per-(node, row) count array itself (stride 2 * nrows: the row's own slots).
 struct Cursors {
-  int64_t* e;   // [node]
-  int64_t* b;   // [node]
+  int64_t* base;
+  int64_t sn;        // stride between nodes
+  int64_t ob;        // offset of the byte cursors
   uint64_t* vmask;   // row-aligned nodes: validity bit of this row's entry, by node index
   uint64_t* bmask;   // row-aligned BOOL nodes: value bit of this row's entry
+  __device__ __forceinline__ int64_t& e(int ni) const { return base[ni * sn]; }
+  __device__ __forceinline__ int64_t& b(int ni) const { return base[ni * sn + ob]; }
 };
 
 template <int D, bool W>
@@ -310,7 +321,7 @@ __device__ void null_entry(const GenNode* nodes, int ni, Cursors cur) {
     return;
   } else {
     const GenNode& n = nodes[ni];
-    const int64_t e = cur.e[ni]++;
+    const int64_t e = cur.e(ni)++;
     if (W) {
       const int w = gwidth(n.type);
       if (w > 0 && n.type != FURY_TYPE_BOOL && n.values) {
@@ -321,7 +332,7 @@ __device__ void null_entry(const GenNode* nodes, int ni, Cursors cur) {
         st8(const_cast<uint8_t*>(n.values) + 16 * e + 8, 0);
       } else if (n.offsets) {                          // zero-length string / list / map
         const int64_t pos = (n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY)
-                                ? cur.b[ni] : cur.e[n.first_child];
+                                ? cur.b(ni) : cur.e(n.first_child);
         n.offsets[e + 1] = static_cast<int32_t>(pos);
       }
     }
@@ -349,9 +360,9 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
       null_entry<D, W>(nodes, ni, cur);
       return;
     }
-    const int64_t e = cur.e[ni]++;
+    const int64_t e = cur.e(ni)++;
     if (W && n.validity) {
-      if (n.row_aligned) *cur.vmask |= 1ull << ni;   // written by a wave ballot (entry = row)
+      if (n.row_aligned && ni < 64) *cur.vmask |= 1ull << ni;   // a wave ballot (entry = row)
       else set_valid_bit(n.validity, e);
     }
     const uint8_t* sp = base + slot_addr;
@@ -367,7 +378,7 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
       if (!dst) return;
       if (n.type == FURY_TYPE_BOOL) {
         if (v & 0xff) {
-          if (n.row_aligned) *cur.bmask |= 1ull << ni;
+          if (n.row_aligned && ni < 64) *cur.bmask |= 1ull << ni;
           else set_valid_bit(dst, e);
         }
       } else if (w == 8) {
@@ -387,8 +398,8 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
     switch (n.type) {
       case FURY_TYPE_STRING:
       case FURY_TYPE_BINARY: {
-        const int64_t pos = cur.b[ni];
-        cur.b[ni] = pos + size;
+        const int64_t pos = cur.b(ni);
+        cur.b(ni) = pos + size;
         if (W) {
           uint8_t* dst = const_cast<uint8_t*>(n.values);
           if (dst) copy_to_unaligned(dst + pos, vp, size);
@@ -405,7 +416,7 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
       case FURY_TYPE_LIST: {
         const int64_t m = static_cast<int32_t>(ld8(vp));
         get_array<D, W>(nodes, n.first_child, vp, m, cur);
-        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e[n.first_child]);
+        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e(n.first_child));
         return;
       }
       case FURY_TYPE_STRUCT: {
@@ -422,7 +433,7 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
         const int64_t m = static_cast<int32_t>(ld8(ka));
         get_array<D, W>(nodes, n.first_child, ka, m, cur);
         get_array<D, W>(nodes, n.first_child + 1, va, m, cur);
-        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e[n.first_child]);
+        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e(n.first_child));
         return;
       }
       default:
@@ -436,44 +447,51 @@ __device__ void get_value(const GenNode* nodes, int ni, bool present, const uint
 // The per-thread cursors live in dynamic LDS sized for the schema's node count (2 x 8 B x
 // nnodes per thread), so small schemas keep many workgroups per CU (a fixed kGenMaxNodes-sized
 // array held this latency-bound interpreter to 3 waves per CU).
-template <bool W>
+template <bool W, bool kWide>
 __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               int64_t* __restrict__ cnt) {
   static_assert(kThreads == 64, "one wave = 64 consecutive rows (ballot bitmap words)");
   extern __shared__ int64_t cur_lds[];
-  __shared__ GenNode sn[kGenMaxNodes];
-  const GenNode* nodes = stage_nodes(g, sn);
+  __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
+  const GenNode* nodes = stage_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   const bool live = r < g.nrows;
   uint64_t vmask = 0, bmask = 0;
   if (live) {
-    int64_t* e = cur_lds + threadIdx.x * (2 * g.nnodes);
-    int64_t* b = e + g.nnodes;
-    for (int i = 0; i < g.nnodes; i++) {
-      e[i] = W ? cnt[(2 * i) * g.nrows + r] : 0;
-      b[i] = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
+    Cursors cur;
+    if (kWide) {             // cursors = the row's slots of the count array (see Cursors)
+      cur = Cursors{cnt + r, 2 * g.nrows, g.nrows, &vmask, &bmask};
+      if (!W)
+        for (int i = 0; i < g.nnodes; i++) cur.e(i) = cur.b(i) = 0;
+    } else {
+      cur = Cursors{cur_lds + threadIdx.x * (2 * g.nnodes), 1, g.nnodes, &vmask, &bmask};
+      for (int i = 0; i < g.nnodes; i++) {
+        cur.e(i) = W ? cnt[(2 * i) * g.nrows + r] : 0;
+        cur.b(i) = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
+      }
     }
+    int64_t* e = &cur.e(0);
     const uint8_t* row = rows + offs[r];
     const int64_t bmb = gbm(g.ntop);
-    Cursors cur{e, b, &vmask, &bmask};
     if (g.root) {        // a top-level BinaryArray / BinaryMap: node 0's entry r
       const GenNode& n = nodes[0];
-      const int64_t en = e[0]++;
+      const int64_t en = cur.e(0)++;
       if (W && n.validity) vmask |= 1ull;
       const uint8_t* ka = g.root == 2 ? row + 8 : row;
       const int64_t m = static_cast<int32_t>(ld8(ka));
       get_array<1, W>(nodes, n.first_child, ka, m, cur);
       if (g.root == 2) get_array<1, W>(nodes, n.first_child + 1, row + 8 + static_cast<int64_t>(ld8(row)), m, cur);
-      if (W) n.offsets[en + 1] = static_cast<int32_t>(e[n.first_child]);
+      if (W) n.offsets[en + 1] = static_cast<int32_t>(cur.e(n.first_child));
     } else {
       for (int k = 0; k < g.ntop; k++)
         get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
     }
-    if (!W) {
+    (void)e;
+    if (!W && !kWide) {
       for (int i = 0; i < g.nnodes; i++) {
-        cnt[(2 * i) * g.nrows + r] = e[i];
-        cnt[(2 * i + 1) * g.nrows + r] = b[i];
+        cnt[(2 * i) * g.nrows + r] = cur.e(i);
+        cnt[(2 * i + 1) * g.nrows + r] = cur.b(i);
       }
     }
   }
@@ -486,7 +504,7 @@ __global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const u
   const int nwords = left >= 64 ? 2 : static_cast<int>((left + 31) >> 5);
   for (int i = 0; i < g.nnodes; i++) {
     const GenNode& n = nodes[i];
-    if (!n.row_aligned) continue;
+    if (!n.row_aligned || i >= 64) continue;   // nodes >= 64: per-entry atomics (get_value)
     if (n.validity) {
       const uint64_t bits = __ballot(live && ((vmask >> i) & 1));
       if (lane < nwords)
@@ -524,40 +542,63 @@ size_t cursor_lds(const GenArgs& g) {
 
 // Arrow offsets start at 0 for every node that has them.
 __global__ void gen_offsets_zero(GenArgs g) {
-  const int i = threadIdx.x;
-  if (i < g.nnodes && g.node[i].offsets) g.node[i].offsets[0] = 0;
+  for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) {
+    const GenNode& n = g.tab ? g.tab[i] : g.node[i];
+    if (n.offsets) n.offsets[0] = 0;
+  }
 }
 
 }  // namespace
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
   const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  hipLaunchKernelGGL(gen_measure_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
+  if (g.tab)
+    hipLaunchKernelGGL(gen_measure_kernel<true>, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
+  else
+    hipLaunchKernelGGL(gen_measure_kernel<false>, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
   return check_hip(hipGetLastError(), "gen_measure launch");
 }
 
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  hipLaunchKernelGGL(gen_encode_kernel, dim3(blocks), dim3(kEncThreads), 0, stream, g, offs, rows,
-                     cap);
+  if (g.tab)
+    hipLaunchKernelGGL(gen_encode_kernel<true>, dim3(blocks), dim3(kEncThreads), 0, stream, g,
+                       offs, rows, cap);
+  else
+    hipLaunchKernelGGL(gen_encode_kernel<false>, dim3(blocks), dim3(kEncThreads), 0, stream, g,
+                       offs, rows, cap);
   return check_hip(hipGetLastError(), "gen_encode launch");
 }
 
 int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
                      hipStream_t stream) {
   const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(gen_decode_kernel<false>, dim3(blocks), dim3(kThreads), cursor_lds(g), stream, g, rows,
-                     offs, cnt);
+  if (g.tab)
+    hipLaunchKernelGGL((gen_decode_kernel<false, true>), dim3(blocks), dim3(kThreads), 0, stream,
+                       g, rows, offs, cnt);
+  else
+    hipLaunchKernelGGL((gen_decode_kernel<false, false>), dim3(blocks), dim3(kThreads),
+                       cursor_lds(g), stream, g, rows, offs, cnt);
   return check_hip(hipGetLastError(), "gen_count launch");
 }
 
+// `cnt` holds the scanned start positions; a wide schema's write pass advances its cursors in
+// place, so it runs on a copy (`scratch`, same size) and the plan stays reusable.
 int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                      hipStream_t stream) {
-  hipLaunchKernelGGL(gen_offsets_zero, dim3(1), dim3(kGenMaxNodes), 0, stream, g);
+                      int64_t* scratch, hipStream_t stream) {
+  hipLaunchKernelGGL(gen_offsets_zero, dim3(1), dim3(256), 0, stream, g);
   const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  hipLaunchKernelGGL(gen_decode_kernel<true>, dim3(blocks), dim3(kThreads), cursor_lds(g), stream, g, rows,
-                     offs, cnt);
+  if (g.tab) {
+    const int st = check_hip(hipMemcpyAsync(scratch, cnt, 2 * g.nnodes * g.nrows * 8,
+                                            hipMemcpyDeviceToDevice, stream), "cursor copy");
+    if (st) return st;
+    hipLaunchKernelGGL((gen_decode_kernel<true, true>), dim3(blocks), dim3(kThreads), 0, stream,
+                       g, rows, offs, scratch);
+  } else {
+    hipLaunchKernelGGL((gen_decode_kernel<true, false>), dim3(blocks), dim3(kThreads),
+                       cursor_lds(g), stream, g, rows, offs, cnt);
+  }
   return check_hip(hipGetLastError(), "gen_decode launch");
 }
 

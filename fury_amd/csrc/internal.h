@@ -72,6 +72,7 @@ struct fury_decode_plan {
   const int64_t* offs = nullptr;
   int64_t nrows = 0;
   int64_t* cnt = nullptr;          // [2 * nodes][nrows] scanned start positions
+  int64_t* scratch = nullptr;      // wide schemas: cursor copy of cnt for the write pass
   bool arrow = false;
   std::vector<int64_t> totals;     // per node: Arrow entries, payload bytes
   void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)

@@ -121,7 +121,8 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                       hipStream_t stream, bool arrow);
 // ---- generic (nested) schema engine: generic.hip --------------------------------------------
-constexpr int kGenMaxNodes = 48;      // schema tree nodes (fields at every level)
+constexpr int kGenMaxNodes = 48;      // schema tree nodes in the argument block
+constexpr int kGenMaxWideNodes = 4096;  // beyond 48: node table uploaded per call (GenArgs.tab)
 constexpr int kGenMaxDepth = 8;       // nesting levels (checked at schema creation)
 
 struct GenNode {
@@ -142,6 +143,7 @@ struct GenArgs {
   int32_t* err;            // optional device flag (never NULL when set by the host)
   int32_t root;            // fury_schema.root: 0 rows, 1 top-level arrays, 2 top-level maps
   int32_t pad_;
+  const GenNode* tab;      // device node table for > kGenMaxNodes nodes, else NULL
 };
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
@@ -150,7 +152,7 @@ int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int6
 int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
                      hipStream_t stream);
 int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                      hipStream_t stream);
+                      int64_t* scratch, hipStream_t stream);
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);

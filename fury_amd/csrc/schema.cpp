@@ -16,7 +16,7 @@
 namespace fury {
 
 // keep in sync with kGenMaxNodes / kGenMaxDepth (kernels.h; this TU is host-only C++)
-constexpr int kGenMaxNodesHost = 48;
+constexpr int kGenMaxNodesHost = 4096;   // = kGenMaxWideNodes (kernels.h)
 constexpr int kGenMaxDepthHost = 8;
 
 static thread_local std::string g_last_error;

@@ -1125,3 +1125,68 @@ def test_wide_var_schemas_beyond_arg_block(oracle, dev, ncols, n):
     w.write(batch)
     assert_columns_equal(fields, [column_to_host(c) for c in w.finish()],
                          oracle.decode(fields, want, want_offs, n), n)
+
+
+def _wide_nested_fields():
+    """A bean with 60 scalar / string fields plus a nested bean, a map and a list of beans: 90
+    schema nodes, beyond the argument block's 48."""
+    fs = []
+    for i in range(60):
+        t = [T.INT64, T.STRING, T.INT32, T.FLOAT64, T.BOOL][i % 5]
+        fs.append(T.field(f"a{i:02d}", t))
+    inner = [T.field(f"i{j}", [T.INT32, T.STRING][j % 2]) for j in range(10)]
+    fs.append(T.struct_field("b_inner", inner))
+    fs.append(T.map_field("c_map", T.field("key", T.STRING), T.field("value", T.INT64)))
+    fs.append(T.Field("d_list", T.LIST, True, (T.struct_field("item", SCHEMAS["bar"]),)))
+    return fs
+
+
+def _wide_nested_beans(fields, n, seed):
+    rng = np.random.default_rng(seed)
+
+    def val(f):
+        if rng.random() < 0.15:
+            return None
+        t = f.type_id
+        if t == T.INT64:
+            return int(rng.integers(-2**62, 2**62))
+        if t == T.INT32:
+            return int(rng.integers(-2**31, 2**31))
+        if t == T.FLOAT64:
+            return float(rng.random())
+        if t == T.BOOL:
+            return bool(rng.integers(0, 2))
+        if t == T.STRING:
+            return "x" * int(rng.integers(0, 20))
+        if t == T.STRUCT:
+            return {c.name: val(c) for c in f.children}
+        if t == T.MAP:
+            return [("k" * int(rng.integers(1, 5)), int(rng.integers(0, 9)))
+                    for _ in range(int(rng.integers(0, 4)))]
+        if t == T.LIST:
+            return [{"f1": int(rng.integers(0, 9)), "f2": "s" * int(rng.integers(0, 5))}
+                    for _ in range(int(rng.integers(0, 4)))]
+        raise ValueError(t)
+    return [{f.name: val(f) for f in fields} for _ in range(n)]
+
+
+@pytest.mark.parametrize("n", [1, 700, 5000])
+def test_nested_schema_beyond_48_nodes(oracle, dev, n):
+    """90-node nested schema: node table uploaded per call, decode cursors in the plan's count
+    array.  Rows oracle-exact, decode == beans, the plan re-executes identically, Arrow ok."""
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = _wide_nested_fields()
+    beans = _wide_nested_beans(fields, n, seed=n)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    assert enc.nested
+    batch = enc.encode_batch(_dev_cols(host, dev), n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.row_offsets.cpu().numpy(), want_offs)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    assert columns_to_beans(fields, dec, n) == beans
+    assert_columns_equal(fields, dec, oracle.decode(fields, want, want_offs, n), n)
+    rows, offs, total = _encode_measured(enc, _dev_cols(host, dev), n, dev)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
