@@ -337,39 +337,61 @@ def run(args):
 
 def end_to_end(enc, cols, n, dev, stream):
     """Host columns -> rows in host memory -> columns in host memory through the host-memory
-    batch path a JVM caller uses: the host buffers are ordinary allocations (as a
-    DirectByteBuffer's memory is) pinned once with fury_host_register (hipHostRegister), then
-    fury_row_encode_host / fury_row_decode_host.  The PCIe-inclusive rate reported in DESIGN.md,
-    never `value`."""
+    batch path a JVM caller uses (fury_row_encode_host / fury_row_decode_host).  Two kinds of
+    host buffers: pinned allocations (fury_host_alloc = hipHostMalloc; GpuRowEncoder.allocatePinned
+    on the JVM) — the headline `GBps_algorithmic` — and ordinary 4 KB-page allocations pinned in
+    place with fury_host_register (hipHostRegister; a DirectByteBuffer registered as is).  Both
+    take the direct path (the kernels read and write host memory over PCIe).  The
+    PCIe-inclusive rate reported in DESIGN.md, never `value`."""
     import numpy as np
     import torch
     from fury_amd import _native as N
+    from fury_amd.encoder import host_empty
     from fury_amd.workloads import Column
     fixed = enc.schema().fixed_size
-    host_cols = [Column(values=c.values.view(torch.uint8).cpu().numpy().copy()) for c in cols]
-    host_rows = np.empty(n * fixed, dtype=np.uint8)
-    out = [Column(values=np.empty(n * 8, dtype=np.uint8)) for _ in cols]
-    bufs = [c.values for c in host_cols] + [host_rows] + [c.values for c in out]
     L = N.lib()
-    for a in bufs:
-        assert L.fury_host_register(a.ctypes.data, a.nbytes) == 0, N.last_error()
-    try:
-        enc.encode_host(host_cols, n, rows=host_rows)      # warm-up (workspace, streams)
+    src = [c.values.view(torch.uint8).cpu().numpy() for c in cols]
+
+    def run(alloc):
+        host_cols = [Column(values=alloc(n * 8)) for _ in cols]
+        for h, v in zip(host_cols, src):
+            h.values[:] = v
+        host_rows = alloc(n * fixed)
+        out = [Column(values=alloc(n * 8)) for _ in cols]
+        d0 = L.fury_get_tuning(b"host_direct")
+        enc.encode_host(host_cols, n, rows=host_rows)      # warm-up (streams, pool)
         reps = 3
         t0 = time.perf_counter()
         for _ in range(reps):
             enc.encode_host(host_cols, n, rows=host_rows)
             enc.decode_host(host_rows, None, n, out=out)
         dt = (time.perf_counter() - t0) / reps
-    finally:
-        for a in bufs:
-            L.fury_host_unregister(a.ctypes.data)
-    for k in (0, len(cols) // 2, len(cols) - 1):
-        assert np.array_equal(out[k].values, host_cols[k].values), "host-path round trip"
+        assert L.fury_get_tuning(b"host_direct") == d0 + 1 + 2 * reps, "staged, not direct"
+        for k in (0, len(cols) // 2, len(cols) - 1):
+            assert np.array_equal(out[k].values, host_cols[k].values), "host-path round trip"
+        return dt
+
+    registered = []
+
+    def reg_alloc(nbytes):
+        a = np.empty(nbytes, dtype=np.uint8)
+        assert L.fury_host_register(a.ctypes.data, a.nbytes) == 0, N.last_error()
+        registered.append(a)
+        return a
+
     alg = 2 * (n * 800 + n * fixed)
+    dt = run(host_empty)
+    try:
+        dt_reg = run(reg_alloc)
+    finally:
+        for a in registered:
+            L.fury_host_unregister(a.ctypes.data)
     return {"GBps_algorithmic": round(alg / dt / 1e9, 2), "ms_per_step": round(dt * 1e3, 2),
-            "what": "host columns pinned by fury_host_register (hipHostRegister) -> "
-                    "fury_row_encode_host -> host rows -> fury_row_decode_host -> host columns"}
+            "registered_GBps_algorithmic": round(alg / dt_reg / 1e9, 2),
+            "what": "host columns in fury_host_alloc (hipHostMalloc) buffers -> "
+                    "fury_row_encode_host -> host rows -> fury_row_decode_host -> host columns, "
+                    "direct (kernels on host memory over PCIe); registered_*: the same with "
+                    "malloc'd buffers pinned by fury_host_register (4 KB pages)"}
 
 
 if __name__ == "__main__":

@@ -77,6 +77,8 @@ SIGNATURES = {
     "fury_get_tuning": (_I32, [ctypes.c_char_p]),
     "fury_frame_rows": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P]),
     "fury_unframe_rows": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P]),
+    "fury_host_alloc": (ctypes.c_int, [_I64, ctypes.POINTER(ctypes.c_void_p)]),
+    "fury_host_free": (ctypes.c_int, [_P]),
     "fury_host_register": (ctypes.c_int, [_P, _I64]),
     "fury_host_unregister": (ctypes.c_int, [_P]),
     "fury_row_encode_host": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _I64, _P,

@@ -649,6 +649,8 @@ int32_t fury_get_tuning(const char* key) {
     return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")
     return static_cast<int32_t>(unframe_walk_count());
+  if (key && std::string(key) == "host_direct")
+    return static_cast<int32_t>(host_direct_count());
   if (key && std::string(key) == "unframe_repairs")
     return static_cast<int32_t>(unframe_repair_count());
   return -1;

@@ -3,18 +3,22 @@
 // through HBM and back inside one call.  This is what the JNI glue calls with
 // GetDirectBufferAddress pointers; the device entry points of capi.cpp do the work.
 //
-// Fixed-width schemas (Struct-100) are streamed in 64-row-aligned chunks on three HIP streams:
-// chunk k's H2D copies, chunk k-1's kernel and chunk k-2's D2H copies overlap, so the call runs
-// at the PCIe rate (both directions of the link busy) rather than at the sum of the three
-// phases.  Variable-length schemas are staged whole: their row offsets are a scan over the
-// whole batch.  Pinning (hipHostRegister) is the caller's choice (fury_host_register): pinned
-// buffers DMA at the link rate, pageable ones are bounced through the runtime's staging buffers.
+// Fixed-width schemas (Struct-100) whose buffers are all pinned run the kernel directly on the
+// host memory (fixed_direct: both PCIe directions busy at once, no HBM staging).  Otherwise
+// they are streamed in 64-row-aligned chunks on three HIP streams (chunk k's H2D copies, chunk
+// k-1's kernel, chunk k-2's D2H copies).  Variable-length schemas are staged whole: their row
+// offsets are a scan over the whole batch.  Pinning (hipHostRegister) is the caller's choice
+// (fury_host_register): pinned buffers DMA at the link rate, pageable ones are bounced through
+// the runtime's staging buffers.
 #include <hip/hip_runtime.h>
 
+#include <array>
+#include <atomic>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <set>
 #include <string>
@@ -42,17 +46,29 @@ struct DeviceArena {                            // frees everything it handed ou
   }
 };
 
+// The calling thread's HIP streams on `device`: created on its first host call and kept for the
+// thread's lifetime (never destroyed: a thread_local destructor may run after the HIP runtime is
+// gone at process exit).  Creating and destroying them per call was most of a small call's
+// ~1.4 ms cost (scripts/ab_host_zc.py "api_tiny").  Every call ends with sync(), so a call
+// finds its streams idle.
 struct Streams {
   hipStream_t s[kStages] = {};
-  ~Streams() {
-    for (auto& x : s)
-      if (x) (void)hipStreamDestroy(x);
-  }
-  int create() {
-    for (auto& x : s) {
-      const int st = check_hip(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate");
-      if (st) return st;
+  int create(int device) {
+    thread_local std::map<int, std::array<hipStream_t, kStages>> pool;
+    auto it = pool.find(device);
+    if (it == pool.end()) {
+      std::array<hipStream_t, kStages> a{};
+      for (auto& x : a) {
+        const int st = check_hip(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "hipStreamCreate");
+        if (st) {
+          for (auto& y : a)
+            if (y) (void)hipStreamDestroy(y);
+          return st;
+        }
+      }
+      it = pool.emplace(device, a).first;
     }
+    for (int g = 0; g < kStages; g++) s[g] = it->second[g];
     return FURY_OK;
   }
   int sync() {
@@ -112,15 +128,113 @@ int64_t rows_per_chunk(const fury_schema* s, int64_t n) {
   return c < 64 ? 64 : c;
 }
 
+std::atomic<int64_t> g_host_direct{0};       // host calls run by fixed_direct
+
+// Device address through which a kernel reaches host bytes [p, p + bytes): memory pinned by
+// hipHostMalloc or hipHostRegister (fury_host_register) only — nullptr for pageable memory,
+// which the GPU cannot address without XNACK.
+uint8_t* device_view(const void* p, int64_t bytes) {
+  if (!p || bytes <= 0) return nullptr;
+  auto view = [](const uint8_t* q) -> uint8_t* {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, q) != hipSuccess) {
+      (void)hipGetLastError();                  // pageable: not an error of the call
+      return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return static_cast<uint8_t*>(a.devicePointer) + (q - static_cast<const uint8_t*>(a.hostPointer));
+  };
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  uint8_t* d0 = view(b);
+  uint8_t* d1 = d0 ? view(b + bytes - 1) : nullptr;   // the whole range is in one mapping
+  return d1 == d0 + (bytes - 1) ? d0 : nullptr;
+}
+
+// Fixed-width schemas whose host buffers are all pinned: the encode / decode kernel reads and
+// writes them directly over PCIe, with no HBM staging.  Loads of one direction and stores of
+// the other are in flight together, so both directions of the link carry data at once — the
+// staged copies did not overlap on the MI355X box (rows_per_chunk).  Measured Struct-100 1M rows
+// (scripts/ab_host_zc.py, profiles/r02_host_direct.json): staged 58 GB/s, direct 92 GB/s
+// encode / 88 GB/s decode (algorithmic column + row bytes).  The fixed kernels read their inputs
+// and write value columns with exact-width accesses; decode output bitmaps (validity, BOOL
+// values) are written as whole words and a host bitmap is only (n + 7) / 8 bytes, so those go to
+// HBM and are copied back.  *used = false (and nothing ran) when any buffer is pageable.
+int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
+                 bool decode, int32_t device, bool* used) {
+  *used = false;
+  if (getenv("FURY_HOST_STAGED")) return FURY_OK;      // A/B switch: force the staged path
+  const int nf = s->num_fields;
+  // the device entry points' alignment rules (16-B rows, width-aligned values) hold for the
+  // staged buffers; host buffers that miss them are staged too
+  auto aligned = [](const void* q, int64_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; };
+  uint8_t* drows = device_view(rows, n * s->fixed_size);
+  if (!drows || !aligned(drows, 16)) return FURY_OK;
+  std::vector<fury_column> dc(nf);
+  std::vector<int64_t> bits(2 * nf, -1);               // decode: workspace offsets of bitmaps
+  int64_t ws_bytes = 0;
+  auto bitmap = [&](int64_t* off) {
+    *off = ws_bytes;
+    ws_bytes += ((bitmap_alloc(n) + 255) / 256) * 256;
+  };
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    dc[k] = fury_column{};
+    if (decode && p.kind == kBool) {
+      bitmap(&bits[2 * k]);
+    } else {
+      dc[k].values = device_view(host[k].values, fixed_bytes(p, n));
+      if (!dc[k].values || (p.width > 1 && !aligned(dc[k].values, p.width))) return FURY_OK;
+    }
+    if (host[k].validity) {
+      if (decode) {
+        bitmap(&bits[2 * k + 1]);
+      } else if (!(dc[k].validity = device_view(host[k].validity, (n + 7) / 8))) {
+        return FURY_OK;
+      }
+    }
+  }
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  Streams ss;
+  if ((st = ss.create(device))) return st;
+  hipStream_t hs = ss.s[0];
+  uint8_t* ws = nullptr;
+  if (ws_bytes > 0) {
+    keep_pool(device);
+    if ((st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), ws_bytes, hs), "hipMallocAsync")))
+      return st;
+    for (int k = 0; k < nf; k++) {
+      if (bits[2 * k] >= 0) dc[k].values = ws + bits[2 * k];
+      if (bits[2 * k + 1] >= 0) dc[k].validity = ws + bits[2 * k + 1];
+    }
+  }
+  *used = true;
+  g_host_direct.fetch_add(1);
+  st = decode ? fury_row_decode(s, drows, nullptr, n, dc.data(), hs)
+              : fury_row_encode(s, dc.data(), n, nullptr, drows, hs);
+  for (int k = 0; k < nf && !st; k++) {
+    if (bits[2 * k] >= 0)
+      (void)hipMemcpyAsync(host[k].values, dc[k].values, (n + 7) / 8, hipMemcpyDeviceToHost, hs);
+    if (bits[2 * k + 1] >= 0)
+      (void)hipMemcpyAsync(host[k].validity, dc[k].validity, (n + 7) / 8, hipMemcpyDeviceToHost, hs);
+  }
+  if (!st) st = check_hip(hipGetLastError(), "hipMemcpyAsync D2H bitmaps");
+  if (ws) (void)hipFreeAsync(ws, hs);
+  const int st2 = ss.sync();
+  return st ? st : st2;
+}
+
 int fixed_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows, bool decode,
                int32_t device) {
   if (n == 0) return FURY_OK;
-  int st = check_hip(hipSetDevice(device), "hipSetDevice");
-  if (st) return st;
+  bool used = false;
+  int st = fixed_direct(s, host, n, rows, decode, device, &used);
+  if (st || used) return st;
+  if ((st = check_hip(hipSetDevice(device), "hipSetDevice"))) return st;
   const int64_t C = rows_per_chunk(s, n);
   const int nf = s->num_fields;
   Streams ss;
-  if ((st = ss.create())) return st;
+  if ((st = ss.create(device))) return st;
   // one stream-ordered workspace for all stages (pooled by the runtime across calls)
   std::vector<int64_t> col_off(nf), val_off(nf);
   int64_t stage = ((C * s->fixed_size + 255) / 256) * 256;
@@ -250,7 +364,7 @@ int var_encode_host(const fury_schema* s, const fury_column* host, int64_t n, ui
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
   Streams ss;
-  if ((st = ss.create())) return st;
+  if ((st = ss.create(device))) return st;
   hipStream_t hs = ss.s[0];
   DeviceArena arena;
   std::deque<std::vector<fury_column>> kids;     // stable addresses: children point into it
@@ -288,7 +402,7 @@ int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* ro
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
   Streams ss;
-  if ((st = ss.create())) return st;
+  if ((st = ss.create(device))) return st;
   hipStream_t hs = ss.s[0];
   DeviceArena arena;
   const int64_t total = row_offsets[n];
@@ -398,6 +512,9 @@ bool node_has_offsets(int32_t t) {
 }
 
 }  // namespace
+
+int64_t host_direct_count() { return g_host_direct.load(); }
+
 }  // namespace fury
 
 using namespace fury;
@@ -526,6 +643,18 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     if (d.values && vb > 0) (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
   }
   return check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+}
+
+int fury_host_alloc(int64_t bytes, void** out) {
+  if (!out || bytes <= 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_host_alloc: empty range");
+  *out = nullptr;
+  return check_hip(hipHostMalloc(out, static_cast<size_t>(bytes), hipHostMallocDefault),
+                   "hipHostMalloc");
+}
+
+int fury_host_free(void* p) {
+  if (!p) return FURY_OK;
+  return check_hip(hipHostFree(p), "hipHostFree");
 }
 
 int fury_host_register(void* p, int64_t bytes) {

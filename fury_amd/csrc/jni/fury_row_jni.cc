@@ -211,4 +211,32 @@ JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeD
   fury_decode_plan_destroy(reinterpret_cast<fury_decode_plan*>(plan));
 }
 
+// Pinned host memory: GpuRowEncoder.allocatePinned / freePinned / pin / unpin and
+// PinnedAllocationManager (Arrow buffers the GPU reaches directly).
+JNIEXPORT jlong JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeHostAlloc(
+    JNIEnv* env, jclass, jlong bytes) {
+  void* p = nullptr;
+  const int st = fury_host_alloc(bytes, &p);
+  if (st) throw_status(env, st);
+  return reinterpret_cast<jlong>(p);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeHostFree(
+    JNIEnv* env, jclass, jlong address) {
+  const int st = fury_host_free(reinterpret_cast<void*>(address));
+  if (st) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeHostRegister(
+    JNIEnv* env, jclass, jlong address, jlong bytes) {
+  const int st = fury_host_register(reinterpret_cast<void*>(address), bytes);
+  if (st) throw_status(env, st);
+}
+
+JNIEXPORT void JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_nativeHostUnregister(
+    JNIEnv* env, jclass, jlong address) {
+  const int st = fury_host_unregister(reinterpret_cast<void*>(address));
+  if (st) throw_status(env, st);
+}
+
 }  // extern "C"

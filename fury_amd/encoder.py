@@ -203,6 +203,28 @@ def _c_host_columns(cols: Sequence[Column], keep: list):
     return arr
 
 
+class _PinnedBlock:
+    """hipHostMalloc'd host memory (fury_host_alloc), freed when the last array over it goes."""
+
+    def __init__(self, nbytes: int):
+        self._ptr = ctypes.c_void_p()
+        _check(N.lib().fury_host_alloc(max(nbytes, 1), ctypes.byref(self._ptr)))
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "version": 3,
+                                    "data": (self._ptr.value, False)}
+
+    def __del__(self):
+        if self._ptr.value:
+            N.lib().fury_host_free(self._ptr)
+            self._ptr = ctypes.c_void_p()
+
+
+def host_empty(nbytes: int, dtype=np.uint8) -> np.ndarray:
+    """A pinned host buffer for the host-memory batch path (include/fury_row.h fury_host_alloc):
+    the GPU reaches it directly, so fixed-width encode_host / decode_host run without staging
+    (GpuRowEncoder.allocatePinned is the JVM's equivalent)."""
+    return np.asarray(_PinnedBlock(nbytes)).view(dtype)
+
+
 def _tree_bytes(cols: Sequence[Column]) -> int:
     return sum(_nbytes(c.values) + _nbytes(c.validity) + _nbytes(c.offsets) +
                (_tree_bytes(c.child) if c.child else 0) for c in cols)

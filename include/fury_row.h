@@ -247,7 +247,8 @@ int fury_device_status(void* stream);
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk
  * parsed (wholly or from the first frame the repair could not place), "unframe_repairs" =
- * streams the parallel repair parsed.
+ * streams the parallel repair parsed.  "host_direct" = fury_row_encode_host / _decode_host calls
+ * on a fixed-width schema that ran the kernel directly on pinned host buffers (no staging).
  * fury_get_tuning("lookback_timeouts") = decoupled look-backs of the variable-length decode that
  * gave up waiting (must stay 0; synchronous device read). */
 int fury_set_tuning(const char* key, int32_t value);
@@ -271,9 +272,15 @@ int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64
 /* The functions below take HOST pointers (a JVM's off-heap buffers) and run the device path
  * inside the call (synchronous): Encoders.bean(...).encode over a batch
  * (FMT/encoder/Encoders.java:185-213) and decode (:165-182), with the bytes crossing PCIe.
- * Fixed-width schemas are streamed in chunks over three HIP streams (H2D, kernels and D2H of
- * consecutive chunks overlap); variable-length schemas are staged whole.  `device` is the HIP
- * device ordinal.  Pin long-lived buffers once with fury_host_register (hipHostRegister). */
+ * Fixed-width schemas whose buffers are ALL pinned (fury_host_alloc or fury_host_register) run
+ * the kernel directly on host memory — loads and stores cross PCIe in both directions at once,
+ * no HBM staging ("host_direct" counts these calls); otherwise they are staged through HBM
+ * (chunked over three HIP streams).  Variable-length schemas are staged whole.  `device` is the
+ * HIP device ordinal.  Buffers from fury_host_alloc (hipHostMalloc) run fastest; registering
+ * ordinary 4 KB-page memory (fury_host_register, hipHostRegister) pins it in place but the GPU
+ * then walks 4 KB translations (host path). */
+int fury_host_alloc(int64_t bytes, void** out);  /* pinned host memory, freed by fury_host_free */
+int fury_host_free(void* ptr);
 int fury_host_register(void* ptr, int64_t bytes);
 int fury_host_unregister(void* ptr);
 /* Host columns (fury_column layout, host pointers) -> host rows.  Fixed-width: rows are

@@ -180,6 +180,36 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
     nativeSchemaDestroy(schemaHandle);
   }
 
+  // ---- pinned host memory (fury_host_alloc / fury_host_register) ---------------------------
+  // encodeBatch / decodeBatch of fixed-width beans run the kernels directly on host memory when
+  // every buffer of the call is pinned (no staging through HBM; both PCIe directions busy).
+
+  /** Off-heap memory the GPU reaches directly (hipHostMalloc); release with freePinned. */
+  public static MemoryBuffer allocatePinned(int bytes) {
+    return MemoryBuffer.fromNativeAddress(nativeHostAlloc(bytes), bytes);
+  }
+
+  public static void freePinned(MemoryBuffer buffer) {
+    nativeHostFree(buffer.getUnsafeAddress());
+  }
+
+  /** Pins existing off-heap memory in place (hipHostRegister), e.g. a long-lived ArrowBuf. */
+  public static void pin(long address, long bytes) {
+    nativeHostRegister(address, bytes);
+  }
+
+  public static void unpin(long address) {
+    nativeHostUnregister(address);
+  }
+
+  static long hostAlloc(long bytes) {
+    return nativeHostAlloc(bytes);
+  }
+
+  static void hostFree(long address) {
+    nativeHostFree(address);
+  }
+
   // ---- column descriptors: 5 longs per node in pre-order ----------------------------------
   // {values address, validity address, offsets address, values capacity, number of children};
   // a MAP's children are its keys and values vectors (the "entries" struct is skipped, as in
@@ -264,4 +294,8 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
                                                      long nrows, long[] counts, int device);
   private static native void nativeDecodeHostExecute(long schema, long plan, long[] columns);
   private static native void nativeDecodePlanDestroy(long plan);
+  private static native long nativeHostAlloc(long bytes);
+  private static native void nativeHostFree(long address);
+  private static native void nativeHostRegister(long address, long bytes);
+  private static native void nativeHostUnregister(long address);
 }

@@ -109,3 +109,114 @@ def test_host_pinned_buffers():
     finally:
         N.lib().fury_host_unregister(buf.ctypes.data)
     assert np.array_equal(rows, rows_ref)
+
+
+def _fixed_nullable():
+    from fury_amd.types import (BOOL, DATE32, FLOAT32, FLOAT64, INT8, INT16, INT32, INT64,
+                                TIMESTAMP, field, not_null_field)
+    return [field("a_bool", BOOL), field("b_byte", INT8), field("c_short", INT16),
+            not_null_field("d_int", INT32), field("e_float", FLOAT32), field("f_date", DATE32),
+            field("g_ts", TIMESTAMP), not_null_field("i_flag", BOOL),
+            field("j_double", FLOAT64), not_null_field("k_long", INT64)]
+
+
+def enc_is_fixed(fields):
+    from fury_amd.encoder import Schema
+    return Schema(fields).is_fixed
+
+
+def _pinned(a):
+    import torch
+    return None if a is None else torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).pin_memory()
+
+
+@pytest.mark.parametrize("name,n", [("struct100", 70_001), ("fixed_nullable", 33_333),
+                                    ("fixed_nullable", 1), ("fixed_nullable", 64)])
+def test_host_direct_pinned_fixed(oracle, name, n):
+    """Fixed-width schemas with every host buffer pinned run the kernel directly on host memory
+    (fury_get_tuning("host_direct") counts it): rows bit-exact vs the oracle, decode into pinned
+    outputs whose bitmaps are exactly (n + 7) / 8 bytes (the guard bytes after them untouched)."""
+    import torch
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders
+    from fury_amd.workloads import Column
+    fields = SCHEMAS["struct100"] if name == "struct100" else _fixed_nullable()
+    assert enc_is_fixed(fields)
+    host = gen_columns(name, fields, n, seed=5)
+    pinned = [Column(values=_pinned(c.values), validity=_pinned(c.validity)) for c in host]
+    enc = Encoders.bean(fields, device="cuda:0")
+    want, _ = oracle.encode(fields, host, n)
+    L = N.lib()
+    d0 = L.fury_get_tuning(b"host_direct")
+    rows = torch.empty(want.size, dtype=torch.uint8).pin_memory()
+    got, _ = enc.encode_host(pinned, n, rows=rows)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 1, "encode did not take the direct path"
+    assert np.array_equal(got.numpy(), want)
+    ref = oracle.decode(fields, want, None, n)
+    nb = (n + 7) // 8
+    out = []
+    for f, c in zip(fields, host):
+        from fury_amd.types import BOOL, type_width
+        vb = nb if f.type_id == BOOL else n * (16 if type_width(f.type_id) <= 0 else type_width(f.type_id))
+        v = torch.full((vb + 8,), 0xAB, dtype=torch.uint8).pin_memory()
+        m = torch.full((nb + 8,), 0xAB, dtype=torch.uint8).pin_memory() if f.nullable else None
+        out.append((v, m))
+    cols = [Column(values=v[:-8], validity=None if m is None else m[:-8]) for v, m in out]
+    enc.decode_host(rows, None, n, out=cols)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 2, "decode did not take the direct path"
+    assert_columns_equal(fields, cols, ref, n)
+    for v, m in out:
+        assert bool((v[-8:] == 0xAB).all()), "decode wrote past a values buffer"
+        if m is not None:
+            assert bool((m[-8:] == 0xAB).all()), "decode wrote past a validity bitmap"
+
+
+def test_host_direct_falls_back_for_pageable_and_misaligned(oracle):
+    """One pageable column, or a pinned row buffer that is not 16-byte aligned, sends the call
+    down the staged path (same bytes)."""
+    import torch
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders
+    from fury_amd.workloads import Column
+    fields = SCHEMAS["struct100"]
+    n = 3000
+    host = gen_columns("struct100", fields, n, seed=9)
+    want, _ = oracle.encode(fields, host, n)
+    pinned = [Column(values=_pinned(c.values)) for c in host]
+    mixed = pinned[:-1] + [host[-1]]
+    enc = Encoders.bean(fields, device="cuda:0")
+    L = N.lib()
+    d0 = L.fury_get_tuning(b"host_direct")
+    rows = torch.empty(want.size, dtype=torch.uint8).pin_memory()
+    assert np.array_equal(enc.encode_host(mixed, n, rows=rows)[0].numpy(), want)
+    shifted = torch.empty(want.size + 8, dtype=torch.uint8).pin_memory()[8:]
+    assert np.array_equal(enc.encode_host(pinned, n, rows=shifted)[0].numpy(), want)
+    assert L.fury_get_tuning(b"host_direct") == d0
+    assert np.array_equal(enc.encode_host(pinned, n, rows=rows)[0].numpy(), want)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 1
+
+
+def test_host_empty_buffers_take_direct_path(oracle):
+    """fury_host_alloc buffers (encoder.host_empty) are device-visible: encode_host / decode_host
+    on them run direct, bit-exact."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders, host_empty
+    from fury_amd.workloads import Column
+    fields = SCHEMAS["struct100"]
+    n = 4099
+    host = gen_columns("struct100", fields, n, seed=21)
+    cols = []
+    for c in host:
+        b = host_empty(c.values.nbytes)
+        b[:] = c.values.view(np.uint8)
+        cols.append(Column(values=b))
+    enc = Encoders.bean(fields, device="cuda:0")
+    want, _ = oracle.encode(fields, host, n)
+    d0 = N.lib().fury_get_tuning(b"host_direct")
+    rows = host_empty(want.size)
+    got, _ = enc.encode_host(cols, n, rows=rows)
+    out = [Column(values=host_empty(n * 8)) for _ in fields]
+    enc.decode_host(rows, None, n, out=out)
+    assert N.lib().fury_get_tuning(b"host_direct") == d0 + 2
+    assert np.array_equal(got, want)
+    assert all(np.array_equal(o.values, c.values.view(np.uint8)) for o, c in zip(out, host))
