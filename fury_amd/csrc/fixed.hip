@@ -530,8 +530,10 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
 // Kernel variant for fixed-width fast-path schemas (fury_set_tuning("fixed_variant", v) or env
 // FURY_FIXED_VARIANT), a bit set: 1 = pipelined persistent kernel, 2 = nt stores, 4 = nt loads.
 static int g_variant = -1;
+static thread_local int t_variant = -1;      // the calling thread's override (host direct path)
 
 int fixed_variant() {
+  if (t_variant >= 0) return t_variant;
   if (g_variant < 0) {
     const char* e = getenv("FURY_FIXED_VARIANT");
     // tile kernel + nt loads + nt stores + pair-mode deep decode (A/B: profiles/r01_ab_fixed*.json)
@@ -541,6 +543,7 @@ int fixed_variant() {
 }
 
 void set_fixed_variant(int v) { g_variant = v; }
+void set_thread_fixed_variant(int v) { t_variant = v; }
 
 namespace {
 

@@ -210,6 +210,12 @@ int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8
   }
   *used = true;
   g_host_direct.fetch_add(1);
+  // Plain (not non-temporal) loads and stores, one tile per workgroup: over PCIe the HBM-tuned
+  // default (variant 54) measured 92 / 88 GB/s, variant 0 95 / 89 (r02_host_direct.json sweep).
+  struct VariantScope {
+    VariantScope() { set_thread_fixed_variant(getenv("FURY_FIXED_VARIANT") ? -1 : 0); }
+    ~VariantScope() { set_thread_fixed_variant(-1); }
+  } scope;
   st = decode ? fury_row_decode(s, drows, nullptr, n, dc.data(), hs)
               : fury_row_encode(s, dc.data(), n, nullptr, drows, hs);
   for (int k = 0; k < nf && !st; k++) {

@@ -168,6 +168,7 @@ int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t n
 int unframe_mode();
 void set_unframe_mode(int v);
 int64_t unframe_walk_count();
+void set_thread_fixed_variant(int v);  // fixed.hip: per-thread variant override, -1 = none
 int64_t host_direct_count();     // hostpath.cpp: host calls run directly on pinned memory
 int64_t unframe_repair_count();      // streams parsed by the parallel repair (pointer doubling)
 int launch_unframe_rows(const uint8_t* in, int64_t in_len, int64_t nrows, int64_t schema_hash,
