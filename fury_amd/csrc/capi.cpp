@@ -7,6 +7,7 @@
 #include <cstring>
 #include <atomic>
 #include <mutex>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -76,8 +77,78 @@ struct RingUse {
 std::vector<RingUse> g_ring_pending;
 }  // namespace
 
+// ---- device workspace cache -------------------------------------------------------------------
+// Per-call workspaces (scan scratch, column tables, decode plans) come from power-of-two size
+// classes cached per device instead of hipMallocAsync / hipFreeAsync: on the box hipFreeAsync
+// took ~110 us of host time per call (HIP API trace of scripts/ab_generic.py), more than most of
+// the kernels it serves.  A freed block records an event on its stream; reuse on the same stream
+// is ordered by the stream, on another stream it waits for that event (hipStreamWaitEvent, no host
+// sync).  Cached free bytes are capped (kCacheCap); beyond that blocks go back to the pool.
+namespace {
+struct CacheBlock {
+  void* p;
+  size_t cls;
+  int device;
+  hipStream_t stream;
+  hipEvent_t ev;
+};
+std::mutex g_cache_mu;
+std::vector<CacheBlock> g_cache_free;
+std::unordered_map<void*, std::pair<size_t, int>> g_cache_live;
+size_t g_cache_bytes = 0;                     // bytes in g_cache_free
+constexpr size_t kCacheCap = size_t(16) << 30;
+}  // namespace
+
+int dev_alloc(int64_t bytes, hipStream_t stream, void** out) {
+  *out = nullptr;
+  size_t cls = 4096;
+  while (cls < static_cast<size_t>(bytes > 0 ? bytes : 1)) cls <<= 1;
+  int device = 0;
+  (void)hipGetDevice(&device);
+  {
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    for (size_t i = 0; i < g_cache_free.size(); i++) {
+      CacheBlock b = g_cache_free[i];
+      if (b.cls != cls || b.device != device) continue;
+      g_cache_free[i] = g_cache_free.back();
+      g_cache_free.pop_back();
+      g_cache_bytes -= cls;
+      if (b.stream != stream) (void)hipStreamWaitEvent(stream, b.ev, 0);
+      (void)hipEventDestroy(b.ev);
+      g_cache_live[b.p] = {cls, device};
+      *out = b.p;
+      return FURY_OK;
+    }
+  }
+  keep_pool(device);
+  const int st = check_hip(hipMallocAsync(out, cls, stream), "hipMallocAsync");
+  if (st) return st;
+  std::lock_guard<std::mutex> lock(g_cache_mu);
+  g_cache_live[*out] = {cls, device};
+  return FURY_OK;
+}
+
+void dev_free(void* p, hipStream_t stream) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lock(g_cache_mu);
+  auto it = g_cache_live.find(p);
+  if (it == g_cache_live.end()) return;
+  const size_t cls = it->second.first;
+  const int device = it->second.second;
+  g_cache_live.erase(it);
+  hipEvent_t ev = nullptr;
+  if (g_cache_bytes + cls > kCacheCap ||
+      hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFreeAsync(p, stream);
+    return;
+  }
+  (void)hipEventRecord(ev, stream);
+  g_cache_free.push_back(CacheBlock{p, cls, device, stream, ev});
+  g_cache_bytes += cls;
+}
+
 DeviceTable::~DeviceTable() {
-  if (dev) (void)hipFreeAsync(dev, stream);
+  if (dev) dev_free(dev, stream);
 }
 
 int upload_table(const void* host, size_t bytes, hipStream_t stream, DeviceTable* out) {
@@ -107,7 +178,7 @@ int upload_table(const void* host, size_t bytes, hipStream_t stream, DeviceTable
   std::memcpy(g_ring + off, host, bytes);
   out->host.assign(static_cast<const uint8_t*>(host), static_cast<const uint8_t*>(host) + bytes);
   g_ring_head = off + bytes;
-  int st = check_hip(hipMallocAsync(&out->dev, bytes, stream), "hipMallocAsync");
+  int st = dev_alloc(static_cast<int64_t>(bytes), stream, &out->dev);
   if (st) return st;
   out->stream = stream;
   st = check_hip(hipMemcpyAsync(out->dev, g_ring + off, bytes, hipMemcpyHostToDevice, stream),
@@ -356,13 +427,12 @@ int gen_measure(const fury_schema* s, const fury_column* cols, int64_t nrows, in
   st = launch_gen_measure(g, offs, stream);
   if (st) return st;
   int64_t* ws = nullptr;
-  st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), scan_workspace(nrows) * 8, stream),
-                 "hipMallocAsync");
+  st = dev_alloc(scan_workspace(nrows) * 8, stream, reinterpret_cast<void**>(&ws));
   if (st) return st;
   device_scan(offs, nrows, offs + nrows, ws, stream);
   st = check_hip(hipGetLastError(), "scan launch");
-  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-  return st ? st : st2;
+  dev_free(ws, stream);
+  return st;
 }
 
 }  // namespace
@@ -545,7 +615,13 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   p->offs = row_offsets;
   p->nrows = nrows;
   std::vector<int64_t> totals(2 * nn, 0);
-  if (nrows > 0) {
+  if (nrows > 0 && gen_decode_mode() == 0) {
+    const int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
+    if (st) {
+      delete p;
+      return st;
+    }
+  } else if (nrows > 0) {
     // Count pass: the column tree is not needed (null columns everywhere).
     std::vector<fury_column> dummy(nn);
     std::vector<fury_column> top(s->num_fields);
@@ -572,9 +648,15 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
     int64_t* dev = nullptr;
     // [counts cells][totals 2 nn][scan workspace][wide schemas: cursor scratch cells]
     const int64_t words = cells + 2 * nn + scan_workspace(cells) + 2 * nn + 1 + (wide ? cells : 0);
-    int st = check_hip(hipMalloc(reinterpret_cast<void**>(&dev), words * 8), "hipMalloc");
+    // stream-ordered pool memory: a hipMalloc / hipFree pair of this size per call cost
+    // milliseconds (hipFree synchronises the device), more than the count pass itself
+    int device = 0;
+    (void)hipGetDevice(&device);
+    keep_pool(device);
+    int st = dev_alloc(words * 8, hs, reinterpret_cast<void**>(&dev));
     if (st) { delete p; return st; }
     p->cnt = dev;
+    p->cnt_stream = hs;
     p->scratch = wide ? dev + (words - cells) : nullptr;
     st = launch_gen_count(g, p->rows, row_offsets, dev, hs);
     int64_t* tot = dev + cells;
@@ -596,19 +678,30 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
 
 int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, void* stream) {
   if (!p) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_decode_execute: plan is null");
-  if (p->nrows == 0) return FURY_OK;
   GenArgs g;
   DeviceTable dt;
   hipStream_t hs = static_cast<hipStream_t>(stream);
   int st = gen_args(p->schema, cols, p->nrows, true, arrow != 0, &g, &dt, hs);
   if (st) return st;
+  if (p->nrows == 0) {              // an empty batch still yields valid Arrow offsets ([0])
+    const GenNode* nodes = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
+    for (int i = 0; i < g.nnodes && !st; i++)
+      if (nodes[i].offsets)
+        st = check_hip(hipMemsetAsync(nodes[i].offsets, 0, 4, hs), "hipMemsetAsync offsets");
+    return st;
+  }
+  if (p->lv) {
+    const GenNode* outs = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
+    return lv_execute(p->lv, outs, p->rows, p->offs, hs);
+  }
   return launch_gen_decode(g, p->rows, p->offs, p->cnt, p->scratch, hs);
 }
 
 void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
-  if (p->cnt) (void)hipFree(p->cnt);
-  if (p->owned) (void)hipFree(p->owned);
+  if (p->cnt) dev_free(p->cnt, static_cast<hipStream_t>(p->cnt_stream));
+  if (p->lv) lv_free(p->lv);
+  if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
   if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
   delete p;
 }
@@ -633,6 +726,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_decode_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "gen_decode") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "gen_decode: 0..1");
+    set_gen_decode_mode(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "unframe") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "unframe: 0..1");
     set_unframe_mode(value);
@@ -649,6 +747,7 @@ int32_t fury_get_tuning(const char* key) {
     return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")
     return static_cast<int32_t>(unframe_walk_count());
+  if (key && std::string(key) == "gen_decode") return gen_decode_mode();
   if (key && std::string(key) == "host_direct")
     return static_cast<int32_t>(host_direct_count());
   if (key && std::string(key) == "unframe_repairs")

@@ -575,11 +575,10 @@ struct DevBuf {                               // stream-ordered scratch freed on
   hipStream_t s;
   explicit DevBuf(hipStream_t st) : s(st) {}
   ~DevBuf() {
-    if (p) (void)hipFreeAsync(p, s);
+    if (p) dev_free(p, s);
   }
   int alloc(int64_t bytes) {
-    return check_hip(hipMallocAsync(&p, static_cast<size_t>(bytes < 16 ? 16 : bytes), s),
-                     "hipMallocAsync");
+    return dev_alloc(bytes < 16 ? 16 : bytes, s, &p);
   }
 };
 

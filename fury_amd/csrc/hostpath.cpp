@@ -32,15 +32,23 @@ namespace {
 
 constexpr int kStages = 3;
 
-struct DeviceArena {                            // frees everything it handed out
+// Stream-ordered device allocations on `stream` (pooled: keep_pool), freed on it when the arena
+// goes — after the call's last use of them in stream order.
+struct DeviceArena {
+  hipStream_t stream;
   std::vector<void*> ptrs;
+  explicit DeviceArena(hipStream_t s) : stream(s) {
+    int device = 0;
+    (void)hipGetDevice(&device);
+    keep_pool(device);
+  }
   ~DeviceArena() {
-    for (void* p : ptrs) (void)hipFree(p);
+    for (void* p : ptrs) dev_free(p, stream);
   }
   int alloc(int64_t bytes, void** out) {
     *out = nullptr;
     if (bytes <= 0) bytes = 16;
-    const int st = check_hip(hipMalloc(out, static_cast<size_t>(bytes)), "hipMalloc");
+    const int st = dev_alloc(bytes, stream, out);
     if (!st) ptrs.push_back(*out);
     return st;
   }
@@ -87,21 +95,6 @@ int64_t fixed_bytes(const FieldPlan& p, int64_t n) {
 }
 // Device bitmap buffers are written as 32-bit words (fury_row.h): pad to 4 bytes.
 int64_t bitmap_alloc(int64_t n) { return ((n + 31) / 32) * 4 + 4; }
-
-// The stream-ordered pool of `device` keeps freed workspace memory instead of returning it at
-// every synchronisation (the default release threshold 0 re-mapped ~1.7 GB per call).  Once per
-// device, thread-safe.
-void keep_pool(int device) {
-  static std::mutex mu;
-  static std::set<int> done;
-  std::lock_guard<std::mutex> lock(mu);
-  if (!done.insert(device).second) return;
-  hipMemPool_t pool;
-  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
-    uint64_t keep = UINT64_MAX;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-  }
-}
 
 // Bytes one row occupies in a stage (row image + its column values + validity bits, rounded up).
 int64_t stage_bytes_per_row(const fury_schema* s) {
@@ -201,7 +194,7 @@ int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8
   uint8_t* ws = nullptr;
   if (ws_bytes > 0) {
     keep_pool(device);
-    if ((st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), ws_bytes, hs), "hipMallocAsync")))
+    if ((st = dev_alloc(ws_bytes, hs, reinterpret_cast<void**>(&ws))))
       return st;
     for (int k = 0; k < nf; k++) {
       if (bits[2 * k] >= 0) dc[k].values = ws + bits[2 * k];
@@ -225,7 +218,7 @@ int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8
       (void)hipMemcpyAsync(host[k].validity, dc[k].validity, (n + 7) / 8, hipMemcpyDeviceToHost, hs);
   }
   if (!st) st = check_hip(hipGetLastError(), "hipMemcpyAsync D2H bitmaps");
-  if (ws) (void)hipFreeAsync(ws, hs);
+  if (ws) dev_free(ws, hs);
   const int st2 = ss.sync();
   return st ? st : st2;
 }
@@ -255,8 +248,7 @@ int fixed_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t
   }
   keep_pool(device);                          // keep the workspace pooled between calls
   uint8_t* ws = nullptr;
-  if ((st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), stage * kStages, ss.s[0]),
-                      "hipMallocAsync")))
+  if ((st = dev_alloc(stage * kStages, ss.s[0], reinterpret_cast<void**>(&ws))))
     return st;
   hipEvent_t ready;
   (void)hipEventCreateWithFlags(&ready, hipEventDisableTiming);
@@ -308,7 +300,7 @@ int fixed_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t
     }
   }
   const int st2 = ss.sync();                  // every stage done before the workspace goes
-  (void)hipFreeAsync(ws, ss.s[0]);
+  dev_free(ws, ss.s[0]);
   const int st3 = check_hip(hipStreamSynchronize(ss.s[0]), "hipStreamSynchronize");
   (void)hipEventDestroy(ready);
   return st ? st : st2 ? st2 : st3;
@@ -372,7 +364,7 @@ int var_encode_host(const fury_schema* s, const fury_column* host, int64_t n, ui
   Streams ss;
   if ((st = ss.create(device))) return st;
   hipStream_t hs = ss.s[0];
-  DeviceArena arena;
+  DeviceArena arena(hs);
   std::deque<std::vector<fury_column>> kids;     // stable addresses: children point into it
   std::vector<fury_column> dcols(s->num_fields);
   for (int k = 0; k < s->num_fields; k++)
@@ -410,7 +402,7 @@ int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* ro
   Streams ss;
   if ((st = ss.create(device))) return st;
   hipStream_t hs = ss.s[0];
-  DeviceArena arena;
+  DeviceArena arena(hs);
   const int64_t total = row_offsets[n];
   void *drows = nullptr, *doffs = nullptr;
   if ((st = arena.alloc(total, &drows)) || (st = arena.alloc((n + 1) * 8, &doffs))) return st;
@@ -521,6 +513,21 @@ bool node_has_offsets(int32_t t) {
 
 int64_t host_direct_count() { return g_host_direct.load(); }
 
+// The stream-ordered pool of `device` keeps freed workspace memory instead of returning it at
+// every synchronisation (the default release threshold 0 re-mapped ~1.7 GB per call).  Once per
+// device, thread-safe.
+void keep_pool(int device) {
+  static std::mutex mu;
+  static std::set<int> done;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!done.insert(device).second) return;
+  hipMemPool_t pool;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+  }
+}
+
 }  // namespace fury
 
 using namespace fury;
@@ -546,7 +553,8 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
                                                                       : row_offsets[nrows];
   uint8_t* d = nullptr;
   const int64_t rb = (total + 255) & ~int64_t(255);
-  st = check_hip(hipMalloc(reinterpret_cast<void**>(&d), rb + (nrows + 1) * 8 + 16), "hipMalloc");
+  keep_pool(device);
+  st = dev_alloc(rb + (nrows + 1) * 8 + 16, hs, reinterpret_cast<void**>(&d));
   if (st) {
     (void)hipStreamDestroy(hs);
     return st;
@@ -561,7 +569,7 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
       for (int64_t i = 0; i <= nrows; i++) o[i] = i * s->fixed_size;
       (void)hipMemcpyAsync(doffs, o.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, hs);
       if ((st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) {
-        (void)hipFree(d);
+        dev_free(d, hs);
         (void)hipStreamDestroy(hs);
         return st;
       }
@@ -570,7 +578,7 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
   fury_decode_plan* p = nullptr;
   st = fury_decode_prepare(s, d, doffs, nrows, node_entries, node_bytes, &p, hs);
   if (st) {
-    (void)hipFree(d);
+    dev_free(d, hs);
     (void)hipStreamDestroy(hs);
     return st;
   }
@@ -602,7 +610,7 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
       for (int j = 0; j < t.num_children; j++) hc[t.first_child + j] = &hc[i]->child[j];
     }
   }
-  DeviceArena arena;
+  DeviceArena arena(hs);
   std::vector<fury_column> dc(nn);
   for (int i = 0; i < nn; i++) {
     const GenTpl& t = s->nodes[i];

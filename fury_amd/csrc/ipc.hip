@@ -524,7 +524,7 @@ int ipc_record_batch(const fury_schema* s, const fury_column* cols, int64_t n, u
   uint8_t* tab = nullptr;
   int st = FURY_OK;
   if (!chunks.empty()) {
-    st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&tab), tb + cb, stream), "hipMallocAsync");
+    st = dev_alloc(tb + cb, stream, reinterpret_cast<void**>(&tab));
     if (st) return st;
     (void)hipMemcpyAsync(tab, copies.data(), tb, hipMemcpyHostToDevice, stream);
     (void)hipMemcpyAsync(tab + tb, chunks.data(), cb, hipMemcpyHostToDevice, stream);
@@ -537,7 +537,7 @@ int ipc_record_batch(const fury_schema* s, const fury_column* cols, int64_t n, u
                        reinterpret_cast<const IpcChunk*>(tab + tb), out);
     st = check_hip(hipGetLastError(), "ipc gather launch");
   }
-  if (tab) (void)hipFreeAsync(tab, stream);
+  if (tab) dev_free(tab, stream);
   const int st2 = check_hip(hipStreamSynchronize(stream), "ipc sync");
   return st ? st : st2;
 }

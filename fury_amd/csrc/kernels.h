@@ -85,6 +85,11 @@ uint32_t* device_error_word();
 int take_device_error();
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
 
+// Cached device workspace (capi.cpp): stream-ordered like hipMallocAsync / hipFreeAsync, without
+// their per-call host cost.
+int dev_alloc(int64_t bytes, hipStream_t stream, void** out);
+void dev_free(void* p, hipStream_t stream);
+
 // Copies a host column table to device memory on `stream` (stream-ordered: through a pinned
 // staging ring, no host synchronisation); the table is freed stream-ordered when the holder goes.
 struct DeviceTable {
@@ -153,6 +158,18 @@ int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs,
                      hipStream_t stream);
 int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
                       int64_t* scratch, hipStream_t stream);
+// Level-by-level nested decode (levels.hip): prepare = per-level count / scan / expand passes
+// (totals[2 i] entries, totals[2 i + 1] payload bytes of node i), execute = one write pass into
+// the outputs of gen_args' node table.  Tuning "gen_decode": 0 this engine (default), 1 the
+// thread-per-row interpreter of generic.hip.
+struct LvPlan;
+int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, int64_t nrows,
+               hipStream_t hs, LvPlan** out, std::vector<int64_t>* totals);
+int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
+               hipStream_t hs);
+void lv_free(LvPlan* p);
+int gen_decode_mode();
+void set_gen_decode_mode(int v);
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);
@@ -169,6 +186,7 @@ int unframe_mode();
 void set_unframe_mode(int v);
 int64_t unframe_walk_count();
 void set_thread_fixed_variant(int v);  // fixed.hip: per-thread variant override, -1 = none
+void keep_pool(int device);      // hostpath.cpp: keep freed stream-pool memory pooled
 int64_t host_direct_count();     // hostpath.cpp: host calls run directly on pinned memory
 int64_t unframe_repair_count();      // streams parsed by the parallel repair (pointer doubling)
 int launch_unframe_rows(const uint8_t* in, int64_t in_len, int64_t nrows, int64_t schema_hash,

@@ -1,0 +1,581 @@
+// levels.hip — decode of nested schemas level by level (the plan API: fury_decode_prepare /
+// fury_decode_execute).  Reference semantics are those of generic.hip's row interpreter
+// (FMT/encoder/BaseBinaryEncoderBuilder.java:459-706 getters, FMT/vectorized/ArrowWriter.java:
+// 205-640): entries of a node in (parent entry, element) order, a null struct gives a null entry
+// in every child, a null list / map a zero-length entry, null values zeroed.
+//
+// MI355X design.  One thread per Arrow ENTRY of one schema node (blockIdx.y = node), not per
+// row: consecutive lanes own consecutive entries, so every output buffer is written by
+// coalesced stores and every validity / bool bitmap by wave ballots (two whole 32-bit words per
+// 64 entries, no atomics).  Each entry is described by its source: the container it lives in
+// (row / nested struct row / BinaryArray) and its slot there.  Top-level fields read theirs
+// straight from the row (entry = row); every other node that is not a fixed-width scalar gets a
+// materialised source array (16 B per entry), written by its parent's level:
+//   prepare, per nesting level L:  count   (elements of each LIST / MAP entry, payload bytes
+//                                           of each STRING / BINARY entry)
+//                                  scan    (exclusive starts = Arrow offsets)
+//                                  expand  (sources of level L+1's entries)
+//   execute, one launch:           write   (values, offsets, payloads, validity of every node)
+// Fixed-width scalars below a STRUCT / LIST / MAP are written by their parent's thread (a
+// struct child's entry index is the struct's; array elements are copied by the array's owner),
+// so they need neither a source array nor a pass of their own.  The host synchronises once per
+// level that holds lists or maps (their totals size the next level), and once at the end.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+#include "kernels.h"
+
+namespace fury {
+
+struct LvSrc {             // where an entry's slot is: rows + base + off; base < 0: null entry
+  int64_t base;            // container start (byte offset into the rows buffer)
+  int64_t off;             // slot offset inside the container; < 0: the value is AT base
+};
+
+enum : int32_t { kLvTop = 0, kLvInline = 1, kLvMat = 2 };
+
+struct LvNode {
+  const uint8_t* values;   // outputs (execute): values / payload / bool bitmap
+  uint8_t* validity;
+  int32_t* offsets;
+  LvSrc* src;              // kLvMat: one source per entry
+  int64_t* start;          // STRING / BINARY / LIST / MAP: exclusive starts [m + 1]
+  int64_t m;               // Arrow entries
+  int32_t type;
+  int32_t first_child;
+  int32_t num_children;
+  int32_t kind;            // kLvTop / kLvInline / kLvMat
+  int32_t slot;            // top-level field index (kLvTop)
+  int32_t es;              // element bytes in its container (8: a slot; w: array element)
+};
+
+struct LvPlan {
+  std::vector<LvNode> nodes;        // device pointers (src, start) and entry counts
+  std::vector<void*> bufs;          // stream-pool allocations owned by the plan
+  hipStream_t stream = nullptr;     // the stream they were allocated on (freed on it)
+  int32_t ntop = 0;
+  int32_t root = 0;
+};
+
+namespace {
+
+constexpr int kLv = 256;                      // threads per workgroup (4 waves)
+
+struct LvArgs {
+  const LvNode* nodes;                        // device table
+  const int32_t* list;                        // blockIdx.y -> node index
+  const uint8_t* rows;
+  const int64_t* offs;
+  int64_t* out;                               // lv_gather output
+  int32_t ntop;
+  int32_t root;
+};
+
+__device__ __forceinline__ bool lbit(const uint8_t* b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
+__device__ __forceinline__ int64_t lbm(int64_t n) { return ((n + 63) >> 6) << 3; }
+__device__ __forceinline__ uint64_t lld8(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+
+__device__ __forceinline__ int lwidth(int t) {
+  switch (t) {
+    case FURY_TYPE_BOOL: case FURY_TYPE_INT8: return 1;
+    case FURY_TYPE_INT16: return 2;
+    case FURY_TYPE_INT32: case FURY_TYPE_FLOAT32: case FURY_TYPE_DATE32: return 4;
+    case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
+    default: return -1;
+  }
+}
+
+__device__ __forceinline__ uint64_t load_w(const uint8_t* p, int w) {
+  switch (w) {
+    case 8: return lld8(p);
+    case 4: return *reinterpret_cast<const uint32_t*>(p);
+    case 2: return *reinterpret_cast<const uint16_t*>(p);
+    default: return *p;
+  }
+}
+
+__device__ __forceinline__ void store_w(uint8_t* p, int w, uint64_t v) {
+  switch (w) {
+    case 8: *reinterpret_cast<uint64_t*>(p) = v; break;
+    case 4: *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(v); break;
+    case 2: *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v); break;
+    default: *p = static_cast<uint8_t>(v); break;
+  }
+}
+
+// Bits of 64 consecutive entries (the wave's, starting at a multiple of 64) as two whole 32-bit
+// words; words at or past m are not written.  Every lane of the wave calls it.
+__device__ __forceinline__ void ballot_bits(uint8_t* bits, int64_t e, bool pred, int64_t m) {
+  const uint64_t b = __ballot(pred);
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (e - lane) >> 5;
+  if (lane < 2 && (w0 + lane) * 32 < m)
+    reinterpret_cast<uint32_t*>(bits)[w0 + lane] = static_cast<uint32_t>(b >> (32 * lane));
+}
+
+// One bit of a bitmap shared with other threads (array elements of different owners).
+__device__ __forceinline__ void atomic_bit(uint8_t* bits, int64_t i) {
+  uint32_t* wp = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits + (i >> 3)) & ~uintptr_t(3));
+  const int sh = static_cast<int>((reinterpret_cast<uintptr_t>(bits + (i >> 3)) & 3) * 8 + (i & 7));
+  atomicOr(wp, 1u << sh);
+}
+
+// len bytes from an 8-aligned source to any destination (only [dst, dst + len) written).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len) {
+  if (len <= 0) return;
+  const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
+  for (int64_t t = 0; t < head; t++) dst[t] = src[t];
+  const int64_t body = (len - head) >> 3;
+  const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
+  const int sh = static_cast<int>(head) * 8;
+  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst + head);
+  for (int64_t w = 0; w < body; w++) {
+    const uint64_t lo = s64[w];
+    d64[w] = sh ? (lo >> sh) | (s64[w + 1] << (64 - sh)) : lo;
+  }
+  for (int64_t t = head + 8 * body; t < len; t++) dst[t] = src[t];
+}
+
+// The value of entry e of node n: null flag, its container base, and for variable-length types
+// the value's start (vp) and size (from the slot's (relOffset << 32) | size).
+struct LvVal {
+  bool null;
+  int64_t base;            // container start
+  int64_t slot;            // absolute slot offset (< 0: the value is at base)
+};
+
+__device__ __forceinline__ LvVal lv_source(const LvArgs& a, const LvNode& n, int64_t e) {
+  if (n.kind == kLvTop) {
+    const int64_t base = a.offs[e];
+    if (a.root) return {false, base, -1};                       // a top-level array / map
+    return {lbit(a.rows + base, n.slot), base, base + lbm(a.ntop) + 8 * n.slot};
+  }
+  const LvSrc s = n.src[e];
+  return {s.base < 0, s.base, s.off < 0 ? -1 : s.base + s.off};
+}
+
+__device__ __forceinline__ const uint8_t* lv_var(const LvArgs& a, const LvVal& v, uint32_t* size) {
+  if (v.slot < 0) {
+    *size = 0;
+    return a.rows + v.base;
+  }
+  const uint64_t oas = lld8(a.rows + v.slot);
+  *size = static_cast<uint32_t>(oas);
+  return a.rows + v.base + static_cast<int32_t>(oas >> 32);
+}
+
+// Pass 1 of a level: per entry, elements (LIST / MAP) or payload bytes (STRING / BINARY).
+__global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
+  const LvNode& n = a.nodes[a.list[blockIdx.y]];
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
+  if (e >= n.m) return;
+  const LvVal v = lv_source(a, n, e);
+  int64_t c = 0;
+  if (!v.null) {
+    uint32_t size;
+    const uint8_t* vp = lv_var(a, v, &size);
+    if (n.type == FURY_TYPE_LIST) c = static_cast<int32_t>(lld8(vp));
+    else if (n.type == FURY_TYPE_MAP) c = static_cast<int32_t>(lld8(vp + 8));
+    else c = size;
+  }
+  n.start[e] = c;
+}
+
+// Sources of the entries of an array's elements [p0, p0 + m) (non-scalar element node c).
+__device__ __forceinline__ void expand_array(const LvArgs& a, const LvNode& c, const uint8_t* arr,
+                                             int64_t m, int64_t p0) {
+  const int64_t ab = arr - a.rows;
+  const int64_t hb = 8 + lbm(m);
+  for (int64_t j = 0; j < m; j++)
+    c.src[p0 + j] = lbit(arr + 8, j) ? LvSrc{-1, 0} : LvSrc{ab, hb + 8 * j};
+}
+
+// Pass 3 of a level: the sources of the next level's materialised entries.
+__global__ __launch_bounds__(kLv) void lv_expand(LvArgs a) {
+  const LvNode& n = a.nodes[a.list[blockIdx.y]];
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
+  if (e >= n.m) return;
+  const LvVal v = lv_source(a, n, e);
+  if (n.type == FURY_TYPE_STRUCT) {
+    uint32_t size;
+    const uint8_t* vp = v.null ? nullptr : lv_var(a, v, &size);
+    const int64_t vb = v.null ? -1 : vp - a.rows;
+    const int nc = n.num_children;
+    for (int k = 0; k < nc; k++) {
+      const LvNode& c = a.nodes[n.first_child + k];
+      if (c.kind != kLvMat) continue;
+      c.src[e] = (v.null || lbit(vp, k)) ? LvSrc{-1, 0} : LvSrc{vb, lbm(nc) + 8 * k};
+    }
+    return;
+  }
+  if (v.null) return;                                    // a null list / map has no elements
+  uint32_t size;
+  const uint8_t* vp = lv_var(a, v, &size);
+  const int64_t p0 = n.start[e];
+  const int64_t m = n.start[e + 1] - p0;
+  if (n.type == FURY_TYPE_LIST) {
+    const LvNode& c = a.nodes[n.first_child];
+    if (c.kind == kLvMat) expand_array(a, c, vp, m, p0);
+  } else {                                               // MAP: [keyBytes][keys][values]
+    const LvNode& k = a.nodes[n.first_child];
+    const LvNode& w = a.nodes[n.first_child + 1];
+    if (k.kind == kLvMat) expand_array(a, k, vp + 8, m, p0);
+    if (w.kind == kLvMat) expand_array(a, w, vp + 8 + static_cast<int64_t>(lld8(vp)), m, p0);
+  }
+}
+
+// start[m] of every listed node -> out[j] (the level's totals in one small copy).
+__global__ void lv_gather(LvArgs a, int32_t count) {
+  const int j = threadIdx.x + blockIdx.x * blockDim.x;
+  if (j >= count) return;
+  const LvNode& n = a.nodes[a.list[j]];
+  a.out[j] = n.start[n.m];
+}
+
+// Array elements of a scalar element node c: entries [p0, p0 + m) from arr (elements es = w
+// bytes after [int64 n][bitmap]); bits through atomics (words shared with other owners).
+__device__ __forceinline__ void write_elements(const LvNode& c, const uint8_t* arr, int64_t m,
+                                               int64_t p0) {
+  const int w = lwidth(c.type);
+  const uint8_t* el = arr + 8 + lbm(m);
+  uint8_t* dst = const_cast<uint8_t*>(c.values);
+  for (int64_t j = 0; j < m; j++) {
+    const bool valid = !lbit(arr + 8, j);
+    const int64_t idx = p0 + j;
+    if (c.validity && valid) atomic_bit(c.validity, idx);
+    if (!dst) continue;
+    const uint64_t x = valid ? load_w(el + j * w, w) : 0;
+    if (c.type == FURY_TYPE_BOOL) {
+      if (x & 0xff) atomic_bit(dst, idx);
+    } else {
+      store_w(dst + idx * w, w, x);
+    }
+  }
+}
+
+// The write pass: every entry of every listed node (kLvTop / kLvMat), plus the scalar children
+// its thread owns.  Types are uniform per workgroup (blockIdx.y = node), so the ballots below
+// are reached by whole waves.
+__global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
+  const LvNode& n = a.nodes[a.list[blockIdx.y]];
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
+  if (e0 >= n.m) return;
+  const int64_t e = e0 + threadIdx.x;
+  const bool live = e < n.m;
+  LvVal v{true, 0, -1};
+  if (live) v = lv_source(a, n, e);
+  const bool valid = live && !v.null;
+  if (n.validity) ballot_bits(n.validity, e, valid, n.m);
+  const int t = n.type;
+  const int w = lwidth(t);
+  if (w > 0) {                                           // a top-level scalar (slot of 8 B)
+    const uint64_t x = valid ? load_w(a.rows + v.slot, w) : 0;
+    uint8_t* dst = const_cast<uint8_t*>(n.values);
+    if (t == FURY_TYPE_BOOL) {
+      if (dst) ballot_bits(dst, e, valid && (x & 0xff), n.m);
+    } else if (live && dst) {
+      store_w(dst + e * w, w, x);
+    }
+    return;
+  }
+  uint32_t size = 0;
+  const uint8_t* vp = valid ? lv_var(a, v, &size) : nullptr;
+  switch (t) {
+    case FURY_TYPE_STRING:
+    case FURY_TYPE_BINARY: {
+      if (!live) return;
+      const int64_t pos = n.start[e];
+      if (valid && n.values) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
+      n.offsets[e + 1] = static_cast<int32_t>(pos + (valid ? size : 0));
+      if (e == 0) n.offsets[0] = 0;
+      return;
+    }
+    case FURY_TYPE_DECIMAL: {
+      if (!live || !n.values) return;
+      uint64_t* d = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(n.values) + 16 * e);
+      d[0] = valid ? lld8(vp) : 0;
+      d[1] = valid ? lld8(vp + 8) : 0;
+      return;
+    }
+    case FURY_TYPE_LIST:
+    case FURY_TYPE_MAP: {
+      if (!live) return;
+      const int64_t p0 = n.start[e];
+      const int64_t p1 = n.start[e + 1];
+      n.offsets[e + 1] = static_cast<int32_t>(p1);
+      if (e == 0) n.offsets[0] = 0;
+      if (!valid) return;
+      if (t == FURY_TYPE_LIST) {
+        const LvNode& c = a.nodes[n.first_child];
+        if (c.kind == kLvInline) write_elements(c, vp, p1 - p0, p0);
+      } else {
+        const LvNode& k = a.nodes[n.first_child];
+        const LvNode& x = a.nodes[n.first_child + 1];
+        if (k.kind == kLvInline) write_elements(k, vp + 8, p1 - p0, p0);
+        if (x.kind == kLvInline)
+          write_elements(x, vp + 8 + static_cast<int64_t>(lld8(vp)), p1 - p0, p0);
+      }
+      return;
+    }
+    case FURY_TYPE_STRUCT: {                             // scalar fields: entry index = e
+      const int nc = n.num_children;
+      for (int k = 0; k < nc; k++) {
+        const LvNode& c = a.nodes[n.first_child + k];
+        if (c.kind != kLvInline) continue;
+        const int cw = lwidth(c.type);
+        const bool cv = valid && !lbit(vp, k);
+        const uint64_t x = cv ? load_w(vp + lbm(nc) + 8 * k, cw) : 0;
+        if (c.validity) ballot_bits(c.validity, e, cv, n.m);
+        uint8_t* dst = const_cast<uint8_t*>(c.values);
+        if (!dst) continue;
+        if (c.type == FURY_TYPE_BOOL) ballot_bits(dst, e, cv && (x & 0xff), n.m);
+        else if (live) store_w(dst + e * cw, cw, x);
+      }
+      return;
+    }
+    default:
+      return;
+  }
+}
+
+bool counted(int32_t t) {
+  return t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST || t == FURY_TYPE_MAP;
+}
+
+int host_width(int32_t t) {
+  switch (t) {
+    case FURY_TYPE_BOOL: case FURY_TYPE_INT8: return 1;
+    case FURY_TYPE_INT16: return 2;
+    case FURY_TYPE_INT32: case FURY_TYPE_FLOAT32: case FURY_TYPE_DATE32: return 4;
+    case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
+    default: return -1;
+  }
+}
+
+// The node table + launch list for one kernel, uploaded stream-ordered (kept alive by dt until
+// the launches before its release have run).
+int upload_args(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t* rows,
+                const int64_t* offs, hipStream_t hs, DeviceTable* dt, LvArgs* a) {
+  const size_t nb = p.nodes.size() * sizeof(LvNode);
+  std::vector<uint8_t> buf(nb + list.size() * sizeof(int32_t));
+  memcpy(buf.data(), p.nodes.data(), nb);
+  if (!list.empty()) memcpy(buf.data() + nb, list.data(), list.size() * sizeof(int32_t));
+  const int st = upload_table(buf.data(), buf.size(), hs, dt);
+  if (st) return st;
+  a->nodes = static_cast<const LvNode*>(dt->dev);
+  a->list = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(dt->dev) + nb);
+  a->rows = rows;
+  a->offs = offs;
+  a->out = nullptr;
+  a->ntop = p.ntop;
+  a->root = p.root;
+  return FURY_OK;
+}
+
+int64_t max_m(const LvPlan& p, const std::vector<int32_t>& list) {
+  int64_t m = 0;
+  for (int i : list) m = std::max(m, p.nodes[i].m);
+  return m;
+}
+
+dim3 grid_of(const LvPlan& p, const std::vector<int32_t>& list) {
+  return dim3(static_cast<unsigned>((max_m(p, list) + kLv - 1) / kLv),
+              static_cast<unsigned>(list.size()));
+}
+
+int pool_alloc(LvPlan* p, int64_t bytes, void** out) {
+  *out = nullptr;
+  const int st = dev_alloc(bytes > 0 ? bytes : 16, p->stream, out);
+  if (!st) p->bufs.push_back(*out);
+  return st;
+}
+
+// start[m] of the listed nodes -> host (one gather kernel, one copy, one sync).
+int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t* rows,
+                 const int64_t* offs, hipStream_t hs, int64_t* dev_out, std::vector<int64_t>* out) {
+  out->assign(list.size(), 0);
+  if (list.empty()) return FURY_OK;
+  DeviceTable dt;
+  LvArgs a;
+  int st = upload_args(p, list, rows, offs, hs, &dt, &a);
+  if (st) return st;
+  a.out = dev_out;
+  hipLaunchKernelGGL(lv_gather, dim3(static_cast<unsigned>((list.size() + 255) / 256)), dim3(256), 0,
+                     hs, a, static_cast<int32_t>(list.size()));
+  if ((st = check_hip(hipGetLastError(), "lv_gather launch"))) return st;
+  if ((st = check_hip(hipMemcpyAsync(out->data(), dev_out, list.size() * 8, hipMemcpyDeviceToHost, hs),
+                      "hipMemcpyAsync totals")))
+    return st;
+  return check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+}
+
+}  // namespace
+
+static int g_gen_decode = -1;
+
+int gen_decode_mode() {
+  if (g_gen_decode < 0) {
+    const char* e = getenv("FURY_GEN_DECODE");
+    g_gen_decode = e ? atoi(e) : 0;
+  }
+  return g_gen_decode;
+}
+
+void set_gen_decode_mode(int v) { g_gen_decode = v; }
+
+void lv_free(LvPlan* p) {
+  if (!p) return;
+  for (void* b : p->bufs) dev_free(b, p->stream);
+  delete p;
+}
+
+int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, int64_t nrows,
+               hipStream_t hs, LvPlan** out, std::vector<int64_t>* totals) {
+  *out = nullptr;
+  const int nn = static_cast<int>(s->nodes.size());
+  int device = 0;
+  (void)hipGetDevice(&device);
+  keep_pool(device);                                // per-level syncs must not unmap the pool
+  LvPlan* p = new LvPlan();
+  p->stream = hs;
+  p->ntop = s->num_fields;
+  p->root = s->root;
+  p->nodes.assign(nn, LvNode{});
+  std::vector<int32_t> level(nn, 0), parent(nn, -1);
+  int maxl = 0;
+  for (int i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    LvNode& n = p->nodes[i];
+    n.type = t.type_id;
+    n.first_child = t.first_child;
+    n.num_children = t.num_children;
+    n.es = 8;
+    if (i < s->num_fields) {
+      n.kind = kLvTop;
+      n.slot = i;
+      n.m = nrows;
+    } else {
+      const int32_t pt = s->nodes[parent[i]].type_id;
+      const bool in_array = pt == FURY_TYPE_LIST || pt == FURY_TYPE_MAP;
+      n.kind = host_width(t.type_id) > 0 ? kLvInline : kLvMat;
+      if (in_array && n.kind == kLvInline) n.es = host_width(t.type_id);
+    }
+    for (int j = 0; j < t.num_children; j++) {
+      parent[t.first_child + j] = i;
+      level[t.first_child + j] = level[i] + 1;
+      maxl = std::max(maxl, level[i] + 1);
+    }
+  }
+  totals->assign(2 * nn, 0);
+  int st = FURY_OK;
+  int64_t* dev_tot = nullptr;
+  if ((st = pool_alloc(p, 8 * (nn + 1), reinterpret_cast<void**>(&dev_tot)))) {
+    lv_free(p);
+    return st;
+  }
+  std::vector<int32_t> strings;                     // STRING / BINARY nodes: bytes at the end
+  for (int L = 0; L <= maxl && !st; L++) {
+    std::vector<int32_t> cnt, arrays, parents;
+    int64_t scan_n = 0;
+    for (int i = 0; i < nn; i++) {
+      LvNode& n = p->nodes[i];
+      if (level[i] != L || n.m == 0 || n.kind == kLvInline) continue;
+      if (counted(n.type)) {
+        if ((st = pool_alloc(p, 8 * (n.m + 1), reinterpret_cast<void**>(&n.start)))) break;
+        cnt.push_back(i);
+        scan_n = std::max(scan_n, n.m);
+        if (n.type == FURY_TYPE_LIST || n.type == FURY_TYPE_MAP) arrays.push_back(i);
+        else strings.push_back(i);
+      }
+    }
+    if (st) break;
+    if (!cnt.empty()) {
+      DeviceTable dt;
+      LvArgs a;
+      if ((st = upload_args(*p, cnt, rows, offs, hs, &dt, &a))) break;
+      hipLaunchKernelGGL(lv_count, grid_of(*p, cnt), dim3(kLv), 0, hs, a);
+      if ((st = check_hip(hipGetLastError(), "lv_count launch"))) break;
+      int64_t* ws = nullptr;
+      if ((st = pool_alloc(p, 8 * scan_workspace(scan_n), reinterpret_cast<void**>(&ws)))) break;
+      for (int i : cnt) {
+        LvNode& n = p->nodes[i];
+        device_scan(n.start, n.m, n.start + n.m, ws, hs);
+      }
+      if ((st = check_hip(hipGetLastError(), "scan launch"))) break;
+    }
+    // sizes of the next level: a struct's children have its entries, an array's elements its total
+    std::vector<int64_t> tot;
+    if ((st = level_totals(*p, arrays, rows, offs, hs, dev_tot, &tot))) break;
+    for (size_t j = 0; j < arrays.size(); j++) {
+      const LvNode& n = p->nodes[arrays[j]];
+      for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = tot[j];
+    }
+    for (int i = 0; i < nn; i++) {
+      const LvNode& n = p->nodes[i];
+      if (level[i] != L || n.type != FURY_TYPE_STRUCT) continue;
+      for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = n.m;
+    }
+    for (int i = 0; i < nn; i++) {
+      if (level[i] != L || p->nodes[i].m == 0 || p->nodes[i].kind == kLvInline) continue;
+      const LvNode& n = p->nodes[i];
+      bool has = false;
+      for (int c = 0; c < n.num_children && !st; c++) {
+        LvNode& ch = p->nodes[n.first_child + c];
+        if (ch.kind != kLvMat || ch.m == 0) continue;
+        st = pool_alloc(p, sizeof(LvSrc) * ch.m, reinterpret_cast<void**>(&ch.src));
+        has = true;
+      }
+      if (has) parents.push_back(i);
+    }
+    if (st || parents.empty()) continue;
+    DeviceTable dt;
+    LvArgs a;
+    if ((st = upload_args(*p, parents, rows, offs, hs, &dt, &a))) break;
+    hipLaunchKernelGGL(lv_expand, grid_of(*p, parents), dim3(kLv), 0, hs, a);
+    st = check_hip(hipGetLastError(), "lv_expand launch");
+  }
+  std::vector<int64_t> bytes;
+  if (!st) st = level_totals(*p, strings, rows, offs, hs, dev_tot, &bytes);
+  if (st) {
+    lv_free(p);
+    return st;
+  }
+  for (int i = 0; i < nn; i++) (*totals)[2 * i] = p->nodes[i].m;
+  for (size_t j = 0; j < strings.size(); j++) (*totals)[2 * strings[j] + 1] = bytes[j];
+  *out = p;
+  return FURY_OK;
+}
+
+int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
+               hipStream_t hs) {
+  LvPlan q = *p;                                   // outputs of this call into a copy
+  q.bufs.clear();
+  std::vector<int32_t> list;
+  for (size_t i = 0; i < q.nodes.size(); i++) {
+    LvNode& n = q.nodes[i];
+    n.values = outs[i].values;
+    n.validity = outs[i].validity;
+    n.offsets = outs[i].offsets;
+    if (n.kind != kLvInline && n.m > 0) list.push_back(static_cast<int32_t>(i));
+    if (n.m == 0 && n.offsets) {                   // no entries: the Arrow offsets are just [0]
+      const int st = check_hip(hipMemsetAsync(n.offsets, 0, 4, hs), "hipMemsetAsync offsets");
+      if (st) return st;
+    }
+  }
+  if (list.empty()) return FURY_OK;
+  DeviceTable dt;
+  LvArgs a;
+  int st = upload_args(q, list, rows, offs, hs, &dt, &a);
+  if (st) return st;
+  hipLaunchKernelGGL(lv_write, grid_of(q, list), dim3(kLv), 0, hs, a);
+  return check_hip(hipGetLastError(), "lv_write launch");
+}
+
+}  // namespace fury

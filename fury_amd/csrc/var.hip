@@ -47,16 +47,15 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   const int64_t nb = (n + kMeasTile - 1) / kMeasTile;
   int64_t* ws = nullptr;          // [group sums x nb][total][scan scratch]
   const int64_t wsn = nb + 1 + scan_workspace(nb);
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsn * 8, stream),
-                     "hipMallocAsync");
+  int st = dev_alloc(wsn * 8, stream, reinterpret_cast<void**>(&ws));
   if (st) return st;
   hipLaunchKernelGGL(measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, offs, ws);
   device_scan(ws, nb, ws + nb, ws + nb + 1, stream);
   hipLaunchKernelGGL(add_group_prefix, dim3(nblocks(n)), dim3(kThreads), 0, stream, offs, n, ws,
                      ws + nb);
   st = check_hip(hipGetLastError(), "measure launch");
-  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-  return st ? st : st2;
+  dev_free(ws, stream);
+  return st;
 }
 
 int var_decode_mode() { return g_var_decode; }
@@ -198,8 +197,7 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   const int64_t nb = nblocks(a.nrows);
   int64_t* ws = nullptr;
   const int64_t scr = scan_workspace(nb);
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), (nb * nseq + nseq + scr) * 8,
-                                    stream), "hipMallocAsync");
+  int st = dev_alloc((nb * nseq + nseq + scr) * 8, stream, reinterpret_cast<void**>(&ws));
   if (st) return st;
   int64_t* totals = ws + nb * nseq;
   hipLaunchKernelGGL(decode_measure_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs, ws,
@@ -207,8 +205,8 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   for (int q = 0; q < nseq; q++) device_scan(ws + q * nb, nb, totals + q, totals + nseq, stream);
   hipLaunchKernelGGL(decode_measure_fix, dim3(nb), dim3(kThreads), 0, stream, a, ws, totals, nb);
   st = check_hip(hipGetLastError(), "decode measure launch");
-  int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-  return st ? st : st2;
+  dev_free(ws, stream);
+  return st;
 }
 
 // LDS bytes of decode_var_reg's output images for tiles of `tile` rows: every variable-length
@@ -259,19 +257,19 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     // [ticket][status words: tiles x fields], zeroed per launch
     const size_t wsb = (static_cast<size_t>(nbr) * a.ncols + 1) * 8;
     uint64_t* ws = nullptr;
-    int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
+    int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     uint32_t* tk = reinterpret_cast<uint32_t*>(ws);
     const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
     if (!st) st = launch_decode_var_reg(a, rows, offs, ws + 1, tk, img, wide, nb, nbr, stream);
-    const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-    return st ? st : st2;
+    dev_free(ws, stream);
+    return st;
   }
   // look-back status words (nb x nseq) + the group ticket, zeroed per launch
   const size_t wsb = (nb * nseq + 1) * 8;
   uint64_t* ws = nullptr;
-  int st = check_hip(hipMallocAsync(reinterpret_cast<void**>(&ws), wsb, stream), "hipMallocAsync");
+  int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
   if (st) return st;
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
   if (!st) {
@@ -279,8 +277,8 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
                        ws + 1, reinterpret_cast<uint32_t*>(ws), nseq);
     st = check_hip(hipGetLastError(), "decode_var launch");
   }
-  const int st2 = check_hip(hipFreeAsync(ws, stream), "hipFreeAsync");
-  return st ? st : st2;
+  dev_free(ws, stream);
+  return st;
 }
 
 }  // namespace fury

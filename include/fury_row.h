@@ -243,6 +243,9 @@ int fury_device_status(void* stream);
  * (tile + nt loads/stores + pair-mode deep decode).
  * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
  * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles.
+ * Key "gen_decode" (nested schemas, fury_decode_prepare / _execute): 0 level-by-level engine
+ * (a thread per Arrow entry of a node, levels.hip), 1 the thread-per-row interpreter
+ * (generic.hip).  Results are identical.
  * Key "unframe": 0 speculative parallel stream parse (a stream that does not verify -- a payload
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk

@@ -444,6 +444,39 @@ static void fo_read_array(const uint8_t* base, const fury_field* elem, fury_colu
   *count = (int32_t)n;
 }
 
+/* A null entry out_i of node `node` (ArrowWriter appendNull, FMT/vectorized/ArrowWriter.java:
+ * 205-215 and the writers' appendNull): validity 0, values zeroed, a zero-length string / list /
+ * map, and for a struct one null entry in EVERY child, recursively (StructWriter.appendNull
+ * :577-584 calls each child writer's appendNull). */
+static void fo_null_entry(const fury_field* f, fury_column* c, int64_t out_i, int64_t* cur,
+                          int32_t node) {
+  fo_set_valid(c, out_i, 0);
+  const int32_t w = fo_type_width(f->type_id);
+  switch (f->type_id) {
+    case FURY_TYPE_BOOL:
+      if (c->values) ((uint8_t*)c->values)[out_i >> 3] &= (uint8_t)~(1u << (out_i & 7));
+      return;
+    case FURY_TYPE_DECIMAL:
+      if (c->values) memset((uint8_t*)c->values + out_i * 16, 0, 16);
+      return;
+    case FURY_TYPE_STRING: case FURY_TYPE_BINARY: case FURY_TYPE_LIST: case FURY_TYPE_MAP:
+      c->offsets[out_i] = (int32_t)cur[node];
+      c->offsets[out_i + 1] = (int32_t)cur[node];
+      return;
+    case FURY_TYPE_STRUCT: {
+      int32_t child_node = node + 1;
+      for (int k = 0; k < f->num_children; k++) {
+        fo_null_entry(&f->children[k], &c->child[k], out_i, cur, child_node);
+        child_node += fo_node_count(&f->children[k]);
+      }
+      return;
+    }
+    default:
+      if (w > 0 && c->values) memset((uint8_t*)c->values + out_i * w, 0, (size_t)w);
+      return;
+  }
+}
+
 static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f,
                           fury_column* c, int64_t out_i, int64_t* cur, int32_t node) {
   int is_null = fo_view_is_null(v, ordinal);
@@ -503,21 +536,9 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
     case FURY_TYPE_STRUCT: {                  /* getStruct :148-166 */
       /* child columns are row-aligned with the parent (Arrow struct) */
       int32_t child_node = node + 1;
-      if (is_null) {
+      if (is_null) {                          /* StructWriter.appendNull :577-584 */
         for (int k = 0; k < f->num_children; k++) {
-          fury_column* cc = &c->child[k];
-          fo_set_valid(cc, out_i, 0);
-          int32_t w2 = fo_type_width(f->children[k].type_id);
-          if (f->children[k].type_id == FURY_TYPE_BOOL) {
-            ((uint8_t*)cc->values)[out_i >> 3] &= (uint8_t)~(1u << (out_i & 7));
-          } else if (w2 > 0) {
-            memset((uint8_t*)cc->values + out_i * w2, 0, (size_t)w2);
-          } else if (f->children[k].type_id == FURY_TYPE_DECIMAL) {
-            memset((uint8_t*)cc->values + out_i * 16, 0, 16);
-          } else if (cc->offsets) {
-            cc->offsets[out_i] = (int32_t)cur[child_node];
-            cc->offsets[out_i + 1] = (int32_t)cur[child_node];
-          }
+          fo_null_entry(&f->children[k], &c->child[k], out_i, cur, child_node);
           child_node += fo_node_count(&f->children[k]);
         }
         return;

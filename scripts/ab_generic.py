@@ -60,9 +60,42 @@ def main():
         return statistics.median(xs)
     enc_ms = t(lambda: enc.encode_batch(cols, n))
     dec_ms = t(lambda: enc.decode_batch(batch))
+    # the pieces: measure (row sizes + scan), encode into sized rows, decode count pass
+    # (fury_decode_prepare incl. its host read of the node totals), decode execute alone
+    import ctypes
+    from fury_amd import _native as N
+    from fury_amd.encoder import _bfs, _c_columns, _ptr
+    L = N.lib()
+    h = enc._schema.handle
+    sh = torch.cuda.current_stream().cuda_stream
+    offs = batch.row_offsets
+    meas_ms = t(lambda: enc.measure_into(cols, n, offs))
+    enc_only_ms = t(lambda: enc.encode_into(cols, n, batch.rows, offs))
+    nn = L.fury_schema_num_nodes(h)
+    e = (ctypes.c_int64 * nn)()
+    b = (ctypes.c_int64 * nn)()
+
+    def prep():
+        p = ctypes.c_void_p()
+        assert L.fury_decode_prepare(h, _ptr(batch.rows), _ptr(offs), n, e, b,
+                                     ctypes.byref(p), sh) == 0
+        return p
+
+    def prep_destroy():
+        L.fury_decode_plan_destroy(prep())
+
+    prep_ms = t(prep_destroy)
+    plan = prep()
+    keep: list = []
+    cc = _c_columns(out, keep)
+    exec_ms = t(lambda: L.fury_decode_execute(plan, cc, 0, sh))
+    L.fury_decode_plan_destroy(plan)
     cb = _bytes(cols)
     rb = batch.rows.numel() + 8 * (n + 1)
-    print(json.dumps({"schema": "tests _nested_fields (7 fields, depth 3)", "rows": n,
+    print(json.dumps({"pieces_ms": {"measure": round(meas_ms, 3), "encode": round(enc_only_ms, 3),
+                                    "decode_prepare": round(prep_ms, 3),
+                                    "decode_execute": round(exec_ms, 3)},
+                      "execute_GBps": round((cb + rb) / exec_ms / 1e6, 1),"schema": "tests _nested_fields (7 fields, depth 3)", "rows": n,
                       "column_bytes": cb, "row_bytes": rb,
                       "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
                       "encode_GBps": round((cb + rb) / enc_ms / 1e6, 1),

@@ -227,3 +227,20 @@ def test_array_encoder_restatement_matches_row_restatement(oracle):
         got = B.encode_array(elem, vals)
         assert rows[16:offs[1]].tobytes() == got
         assert B.decode_array(elem, got) == vals
+
+
+def test_null_struct_chain_decode(oracle):
+    """A null struct appends a null entry to EVERY descendant (StructWriter.appendNull,
+    ArrowWriter.java:577-584, recursive through child StructWriters): decode of struct-in-struct
+    chains with strings / binary / decimal / lists under them equals the Arrow columns built from
+    the beans."""
+    from tests.test_device import _engine_schemas, _random_value
+    from fury_amd.beans import beans_to_columns
+    for name in ("struct_chain", "nested7", "maps"):
+        fields = _engine_schemas()[name]
+        rng = np.random.default_rng(3)
+        n = 400
+        beans = [{f.name: _random_value(f, rng) for f in fields} for _ in range(n)]
+        cols = beans_to_columns(fields, beans)
+        rows, offs = oracle.encode(fields, cols, n)
+        assert_columns_equal(fields, oracle.decode(fields, rows, offs, n), cols, n)
