@@ -229,9 +229,10 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
 // top-level BinaryArray (root 1) / BinaryMap [int64 keyBytes][keys][values] (root 2) of node 0's
 // entry r, written at the buffer start exactly as inside a row (element offsets are relative to
 // the array itself).
-template <bool W>
-__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf, int root = 0) {
-  if (root) {
+template <bool W, int kRoot>
+__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf) {
+  constexpr int root = kRoot;
+  if constexpr (kRoot != 0) {
     const GenNode& n = nodes[0];
     const int64_t b = n.offsets[r];
     const int64_t m = n.offsets[r + 1] - b;
@@ -265,15 +266,18 @@ __device__ __forceinline__ const GenNode* stage_nodes(const GenArgs& g, GenNode*
   return lds;
 }
 
-template <bool kWide>
+// kRoot (fury_schema.root) is a template parameter so the row kernels do not carry the
+// collection code: inlining both into one kernel raised its scratch from 192 to 1200 B per lane
+// and doubled the encode time.
+template <bool kWide, int kRoot>
 __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int64_t* __restrict__ sizes) {
   __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
   const GenNode* nodes = stage_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows) sizes[r] = put_row<false>(nodes, g.ntop, r, nullptr, g.root);
+  if (r < g.nrows) sizes[r] = put_row<false, kRoot>(nodes, g.ntop, r, nullptr);
 }
 
-template <bool kWide>
+template <bool kWide, int kRoot>
 __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
                                                                  uint8_t* __restrict__ rows,
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
   __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
   const GenNode* nodes = stage_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows && offs[r + 1] <= cap) put_row<true>(nodes, g.ntop, r, rows + offs[r], g.root);
+  if (r < g.nrows && offs[r + 1] <= cap) put_row<true, kRoot>(nodes, g.ntop, r, rows + offs[r]);
 }
 
 // ---- decode ----------------------------------------------------------------------------------
@@ -550,24 +554,38 @@ __global__ void gen_offsets_zero(GenArgs g) {
 
 }  // namespace
 
-int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
+template <bool kWide, int kRoot>
+void gen_encode_pass(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
+                     int64_t cap, hipStream_t stream) {
   const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  if (g.tab)
-    hipLaunchKernelGGL(gen_measure_kernel<true>, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
+  if (sizes)
+    hipLaunchKernelGGL((gen_measure_kernel<kWide, kRoot>), dim3(blocks), dim3(kEncThreads), 0,
+                       stream, g, sizes);
   else
-    hipLaunchKernelGGL(gen_measure_kernel<false>, dim3(blocks), dim3(kEncThreads), 0, stream, g, sizes);
+    hipLaunchKernelGGL((gen_encode_kernel<kWide, kRoot>), dim3(blocks), dim3(kEncThreads), 0,
+                       stream, g, offs, rows, cap);
+}
+
+template <bool kWide>
+void gen_encode_root(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
+                     int64_t cap, hipStream_t stream) {
+  switch (g.root) {
+    case 1: return gen_encode_pass<kWide, 1>(g, offs, sizes, rows, cap, stream);
+    case 2: return gen_encode_pass<kWide, 2>(g, offs, sizes, rows, cap, stream);
+    default: return gen_encode_pass<kWide, 0>(g, offs, sizes, rows, cap, stream);
+  }
+}
+
+int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
+  if (g.tab) gen_encode_root<true>(g, nullptr, sizes, nullptr, 0, stream);
+  else gen_encode_root<false>(g, nullptr, sizes, nullptr, 0, stream);
   return check_hip(hipGetLastError(), "gen_measure launch");
 }
 
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
-  const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  if (g.tab)
-    hipLaunchKernelGGL(gen_encode_kernel<true>, dim3(blocks), dim3(kEncThreads), 0, stream, g,
-                       offs, rows, cap);
-  else
-    hipLaunchKernelGGL(gen_encode_kernel<false>, dim3(blocks), dim3(kEncThreads), 0, stream, g,
-                       offs, rows, cap);
+  if (g.tab) gen_encode_root<true>(g, offs, nullptr, rows, cap, stream);
+  else gen_encode_root<false>(g, offs, nullptr, rows, cap, stream);
   return check_hip(hipGetLastError(), "gen_encode launch");
 }
 

@@ -58,6 +58,7 @@ struct LvNode {
 
 struct LvPlan {
   std::vector<LvNode> nodes;        // device pointers (src, start) and entry counts
+  int64_t nrows = 0;
   std::vector<void*> bufs;          // stream-pool allocations owned by the plan
   hipStream_t stream = nullptr;     // the stream they were allocated on (freed on it)
   int32_t ntop = 0;
@@ -74,8 +75,10 @@ struct LvArgs {
   const uint8_t* rows;
   const int64_t* offs;
   int64_t* out;                               // lv_gather output
+  int64_t nrows;
   int32_t ntop;
   int32_t root;
+  int32_t nlist;                              // row-major launches: nodes in the list
 };
 
 __device__ __forceinline__ bool lbit(const uint8_t* b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
@@ -172,10 +175,7 @@ __device__ __forceinline__ const uint8_t* lv_var(const LvArgs& a, const LvVal& v
 }
 
 // Pass 1 of a level: per entry, elements (LIST / MAP) or payload bytes (STRING / BINARY).
-__global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
-  const LvNode& n = a.nodes[a.list[blockIdx.y]];
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
-  if (e >= n.m) return;
+__device__ __forceinline__ void count_entry(const LvArgs& a, const LvNode& n, int64_t e) {
   const LvVal v = lv_source(a, n, e);
   int64_t c = 0;
   if (!v.null) {
@@ -188,22 +188,98 @@ __global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
   n.start[e] = c;
 }
 
-// Sources of the entries of an array's elements [p0, p0 + m) (non-scalar element node c).
-__device__ __forceinline__ void expand_array(const LvArgs& a, const LvNode& c, const uint8_t* arr,
-                                             int64_t m, int64_t p0) {
-  const int64_t ab = arr - a.rows;
-  const int64_t hb = 8 + lbm(m);
-  for (int64_t j = 0; j < m; j++)
-    c.src[p0 + j] = lbit(arr + 8, j) ? LvSrc{-1, 0} : LvSrc{ab, hb + 8 * j};
+// Launch shapes: kRows = the listed nodes are top-level fields (entry = row) and one thread per
+// row walks all of them, so a row's null bitmap and slots are fetched once for every field;
+// otherwise blockIdx.y = node, a thread per entry.
+template <bool kRows>
+__global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
+  const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
+  if (kRows) {
+    if (e >= a.nrows) return;
+    for (int j = 0; j < a.nlist; j++) count_entry(a, a.nodes[a.list[j]], e);
+  } else {
+    const LvNode& n = a.nodes[a.list[blockIdx.y]];
+    if (e < n.m) count_entry(a, n, e);
+  }
 }
 
-// Pass 3 of a level: the sources of the next level's materialised entries.
-__global__ __launch_bounds__(kLv) void lv_expand(LvArgs a) {
-  const LvNode& n = a.nodes[a.list[blockIdx.y]];
-  const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
-  if (e >= n.m) return;
-  const LvVal v = lv_source(a, n, e);
+// Elements / payload bytes of a non-null variable-length value whose slot is at rows + slot in
+// the container at rows + base (what lv_count computes, here for the next level's entries).
+__device__ __forceinline__ int64_t var_count(const LvArgs& a, int type, int64_t base, int64_t slot) {
+  const uint64_t oas = lld8(a.rows + slot);
+  const uint8_t* vp = a.rows + base + static_cast<int32_t>(oas >> 32);
+  if (type == FURY_TYPE_LIST) return static_cast<int32_t>(lld8(vp));
+  if (type == FURY_TYPE_MAP) return static_cast<int32_t>(lld8(vp + 8));
+  return static_cast<uint32_t>(oas);
+}
+
+// The elements of the 64 entries of a wave (one LIST / MAP node) are one contiguous range of the
+// child entries: [st[0], st[64]) with st = the entries' exclusive starts.  Lanes take the
+// elements round-robin (q = st[0] + lane + 64 i), each finding its owner entry by a binary search
+// over st in LDS, so element work is spread evenly over the lanes whatever the list lengths and
+// consecutive lanes write consecutive child entries (coalesced stores, ballot-able bits).
+struct WaveLists {
+  int64_t st[65];          // exclusive starts of the wave's entries (clamped at m), st[64] = end
+  int64_t arr[64];         // element array of the entry (LIST / MAP keys), rows-relative
+  int64_t arr2[64];        // MAP values array
+};
+
+__device__ __forceinline__ void wave_lists_fill(const LvArgs& a, const LvNode& n, int64_t e,
+                                                WaveLists& W) {
+  const int lane = threadIdx.x & 63;
+  const bool live = e < n.m;
+  LvVal v{true, 0, -1};
+  if (live) v = lv_source(a, n, e);
+  int64_t ab = -1, ab2 = -1;
+  if (live && !v.null) {
+    uint32_t size;
+    const uint8_t* vp = lv_var(a, v, &size);
+    if (n.type == FURY_TYPE_LIST) {
+      ab = vp - a.rows;
+    } else {                                             // MAP: [keyBytes][keys][values]
+      ab = vp + 8 - a.rows;
+      ab2 = vp + 8 + static_cast<int64_t>(lld8(vp)) - a.rows;
+    }
+  }
+  W.st[lane] = n.start[live ? e : n.m];
+  if (lane == 63) W.st[64] = n.start[min(e + 1, n.m)];
+  W.arr[lane] = ab;
+  W.arr2[lane] = ab2;
+}
+
+// Owner lane of child entry q: the last l with st[l] <= q.
+__device__ __forceinline__ int wave_owner(const WaveLists& W, int64_t q) {
+  int l = 0;
+#pragma unroll
+  for (int b = 32; b; b >>= 1)
+    if (W.st[l + b] <= q && l + b < 64) l += b;
+  return l;
+}
+
+// Sources (and, for counted element nodes, counts) of the elements of a wave's arrays, into the
+// non-scalar element node c; `second` selects a MAP's values array.
+__device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, const WaveLists& W,
+                                            bool second) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t q = W.st[0] + lane; q < W.st[64]; q += 64) {
+    const int l = wave_owner(W, q);
+    const int64_t j = q - W.st[l];
+    const int64_t m = W.st[l + 1] - W.st[l];
+    const int64_t ab = second ? W.arr2[l] : W.arr[l];
+    const int64_t hb = 8 + lbm(m);
+    const bool nul = lbit(a.rows + ab + 8, j);
+    c.src[q] = nul ? LvSrc{-1, 0} : LvSrc{ab, hb + 8 * j};
+    if (c.start && !nul) c.start[q] = var_count(a, c.type, ab, ab + hb + 8 * j);
+  }
+}
+
+// Pass 3 of a level: the sources (and counts) of the next level's materialised entries.  Every
+// thread of the workgroup calls it for the same node (LDS + barriers for lists / maps).
+__device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, int64_t e,
+                                            WaveLists& W) {
   if (n.type == FURY_TYPE_STRUCT) {
+    if (e >= n.m) return;
+    const LvVal v = lv_source(a, n, e);
     uint32_t size;
     const uint8_t* vp = v.null ? nullptr : lv_var(a, v, &size);
     const int64_t vb = v.null ? -1 : vp - a.rows;
@@ -211,23 +287,35 @@ __global__ __launch_bounds__(kLv) void lv_expand(LvArgs a) {
     for (int k = 0; k < nc; k++) {
       const LvNode& c = a.nodes[n.first_child + k];
       if (c.kind != kLvMat) continue;
-      c.src[e] = (v.null || lbit(vp, k)) ? LvSrc{-1, 0} : LvSrc{vb, lbm(nc) + 8 * k};
+      const bool nul = v.null || lbit(vp, k);
+      c.src[e] = nul ? LvSrc{-1, 0} : LvSrc{vb, lbm(nc) + 8 * k};
+      if (c.start && !nul) c.start[e] = var_count(a, c.type, vb, vb + lbm(nc) + 8 * k);
     }
     return;
   }
-  if (v.null) return;                                    // a null list / map has no elements
-  uint32_t size;
-  const uint8_t* vp = lv_var(a, v, &size);
-  const int64_t p0 = n.start[e];
-  const int64_t m = n.start[e + 1] - p0;
-  if (n.type == FURY_TYPE_LIST) {
-    const LvNode& c = a.nodes[n.first_child];
-    if (c.kind == kLvMat) expand_array(a, c, vp, m, p0);
-  } else {                                               // MAP: [keyBytes][keys][values]
-    const LvNode& k = a.nodes[n.first_child];
-    const LvNode& w = a.nodes[n.first_child + 1];
-    if (k.kind == kLvMat) expand_array(a, k, vp + 8, m, p0);
-    if (w.kind == kLvMat) expand_array(a, w, vp + 8 + static_cast<int64_t>(lld8(vp)), m, p0);
+  wave_lists_fill(a, n, e, W);
+  __syncthreads();
+  const LvNode& c0 = a.nodes[n.first_child];
+  if (c0.kind == kLvMat) expand_wave(a, c0, W, false);
+  if (n.type == FURY_TYPE_MAP) {
+    const LvNode& c1 = a.nodes[n.first_child + 1];
+    if (c1.kind == kLvMat) expand_wave(a, c1, W, true);
+  }
+  __syncthreads();
+}
+
+template <bool kRows>
+__global__ __launch_bounds__(kLv) void lv_expand(LvArgs a) {
+  __shared__ WaveLists wl[kLv / 64];
+  WaveLists& W = wl[threadIdx.x >> 6];
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
+  const int64_t e = e0 + threadIdx.x;
+  if (kRows) {
+    if (e0 >= a.nrows) return;
+    for (int j = 0; j < a.nlist; j++) expand_node(a, a.nodes[a.list[j]], e, W);
+  } else {
+    const LvNode& n = a.nodes[a.list[blockIdx.y]];
+    if (e0 < n.m) expand_node(a, n, e, W);
   }
 }
 
@@ -239,35 +327,66 @@ __global__ void lv_gather(LvArgs a, int32_t count) {
   a.out[j] = n.start[n.m];
 }
 
-// Array elements of a scalar element node c: entries [p0, p0 + m) from arr (elements es = w
-// bytes after [int64 n][bitmap]); bits through atomics (words shared with other owners).
-__device__ __forceinline__ void write_elements(const LvNode& c, const uint8_t* arr, int64_t m,
-                                               int64_t p0) {
-  const int w = lwidth(c.type);
-  const uint8_t* el = arr + 8 + lbm(m);
-  uint8_t* dst = const_cast<uint8_t*>(c.values);
-  for (int64_t j = 0; j < m; j++) {
-    const bool valid = !lbit(arr + 8, j);
-    const int64_t idx = p0 + j;
-    if (c.validity && valid) atomic_bit(c.validity, idx);
-    if (!dst) continue;
-    const uint64_t x = valid ? load_w(el + j * w, w) : 0;
-    if (c.type == FURY_TYPE_BOOL) {
-      if (x & 0xff) atomic_bit(dst, idx);
-    } else {
-      store_w(dst + idx * w, w, x);
-    }
+// Segmented scan of a level's count buffer: after one exclusive scan over the concatenated
+// segments ([m_j counts][0] per counted node j), every segment minus its first prefix.
+__global__ void lv_seg_bases(const int64_t* __restrict__ buf, int64_t* tab, int32_t nseg) {
+  const int j = threadIdx.x + blockIdx.x * blockDim.x;
+  if (j < nseg) tab[nseg + 1 + j] = buf[tab[j]];          // tab = [offsets nseg + 1][bases nseg]
+}
+
+__global__ __launch_bounds__(kLv) void lv_seg_sub(int64_t* __restrict__ buf, const int64_t* tab,
+                                                   int32_t nseg) {
+  const int j = blockIdx.y;
+  const int64_t i = tab[j] + static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
+  if (i < tab[j + 1]) buf[i] -= tab[nseg + 1 + j];
+}
+
+// ORs a ballot (bit i = child entry base + i, base not aligned) into a bitmap whose words other
+// waves share: at most three 32-bit atomics per 64 entries.
+__device__ __forceinline__ void ballot_or(uint8_t* bits, int64_t base, bool pred) {
+  const uint64_t b = __ballot(pred);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  const int sh = static_cast<int>(base & 31);
+  const uint64_t lo = b << sh;
+  const uint32_t hi = sh ? static_cast<uint32_t>(b >> (64 - sh)) : 0u;
+  if (lane < 3) {
+    const uint32_t part = lane == 0 ? static_cast<uint32_t>(lo)
+                        : lane == 1 ? static_cast<uint32_t>(lo >> 32) : hi;
+    if (part) atomicOr(reinterpret_cast<uint32_t*>(bits) + (base >> 5) + lane, part);
   }
 }
 
-// The write pass: every entry of every listed node (kLvTop / kLvMat), plus the scalar children
-// its thread owns.  Types are uniform per workgroup (blockIdx.y = node), so the ballots below
-// are reached by whole waves.
-__global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
-  const LvNode& n = a.nodes[a.list[blockIdx.y]];
-  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
-  if (e0 >= n.m) return;
-  const int64_t e = e0 + threadIdx.x;
+// Scalar elements (node c, element width w) of a wave's arrays: lanes take consecutive child
+// entries, so values are coalesced stores and bits one ballot per 64 entries.
+__device__ __forceinline__ void write_wave(const LvArgs& a, const LvNode& c, const WaveLists& W,
+                                           bool second) {
+  const int lane = threadIdx.x & 63;
+  const int w = lwidth(c.type);
+  uint8_t* dst = const_cast<uint8_t*>(c.values);
+  const int64_t end = W.st[64];
+  for (int64_t base = W.st[0]; base < end; base += 64) {
+    const int64_t q = base + lane;
+    bool valid = false;
+    uint64_t x = 0;
+    if (q < end) {
+      const int l = wave_owner(W, q);
+      const int64_t j = q - W.st[l];
+      const int64_t m = W.st[l + 1] - W.st[l];
+      const uint8_t* arr = a.rows + (second ? W.arr2[l] : W.arr[l]);
+      valid = !lbit(arr + 8, j);
+      if (valid) x = load_w(arr + 8 + lbm(m) + j * w, w);
+      if (dst && c.type != FURY_TYPE_BOOL) store_w(dst + q * w, w, x);
+    }
+    if (c.validity) ballot_or(c.validity, base, valid);
+    if (dst && c.type == FURY_TYPE_BOOL) ballot_or(dst, base, valid && (x & 0xff));
+  }
+}
+
+// The write pass: entry e of node n (kLvTop / kLvMat), plus the scalar children its thread
+// owns.  Every lane of the wave calls it for the same node (the ballots below).
+__device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, int64_t e,
+                                            WaveLists& W) {
   const bool live = e < n.m;
   LvVal v{true, 0, -1};
   if (live) v = lv_source(a, n, e);
@@ -306,22 +425,19 @@ __global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
     }
     case FURY_TYPE_LIST:
     case FURY_TYPE_MAP: {
-      if (!live) return;
-      const int64_t p0 = n.start[e];
-      const int64_t p1 = n.start[e + 1];
-      n.offsets[e + 1] = static_cast<int32_t>(p1);
-      if (e == 0) n.offsets[0] = 0;
-      if (!valid) return;
-      if (t == FURY_TYPE_LIST) {
-        const LvNode& c = a.nodes[n.first_child];
-        if (c.kind == kLvInline) write_elements(c, vp, p1 - p0, p0);
-      } else {
-        const LvNode& k = a.nodes[n.first_child];
-        const LvNode& x = a.nodes[n.first_child + 1];
-        if (k.kind == kLvInline) write_elements(k, vp + 8, p1 - p0, p0);
-        if (x.kind == kLvInline)
-          write_elements(x, vp + 8 + static_cast<int64_t>(lld8(vp)), p1 - p0, p0);
+      if (live) {
+        n.offsets[e + 1] = static_cast<int32_t>(n.start[e + 1]);
+        if (e == 0) n.offsets[0] = 0;
       }
+      const LvNode& c0 = a.nodes[n.first_child];
+      const bool s0 = c0.kind == kLvInline;
+      const bool s1 = t == FURY_TYPE_MAP && a.nodes[n.first_child + 1].kind == kLvInline;
+      if (!s0 && !s1) return;
+      wave_lists_fill(a, n, e, W);                         // every lane of the workgroup
+      __syncthreads();
+      if (s0) write_wave(a, c0, W, false);
+      if (s1) write_wave(a, a.nodes[n.first_child + 1], W, true);
+      __syncthreads();
       return;
     }
     case FURY_TYPE_STRUCT: {                             // scalar fields: entry index = e
@@ -342,6 +458,21 @@ __global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
     }
     default:
       return;
+  }
+}
+
+template <bool kRows>
+__global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
+  __shared__ WaveLists wl[kLv / 64];
+  WaveLists& W = wl[threadIdx.x >> 6];
+  const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
+  const int64_t e = e0 + threadIdx.x;
+  if (kRows) {
+    if (e0 >= a.nrows) return;
+    for (int j = 0; j < a.nlist; j++) write_entry(a, a.nodes[a.list[j]], e, W);
+  } else {
+    const LvNode& n = a.nodes[a.list[blockIdx.y]];
+    if (e0 < n.m) write_entry(a, n, e, W);
   }
 }
 
@@ -376,6 +507,8 @@ int upload_args(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t
   a->out = nullptr;
   a->ntop = p.ntop;
   a->root = p.root;
+  a->nrows = p.nrows;
+  a->nlist = static_cast<int32_t>(list.size());
   return FURY_OK;
 }
 
@@ -388,6 +521,27 @@ int64_t max_m(const LvPlan& p, const std::vector<int32_t>& list) {
 dim3 grid_of(const LvPlan& p, const std::vector<int32_t>& list) {
   return dim3(static_cast<unsigned>((max_m(p, list) + kLv - 1) / kLv),
               static_cast<unsigned>(list.size()));
+}
+
+// Launches kernel K<true> row-major over the listed top-level nodes and K<false> node-major over
+// the others (each with its own uploaded list).
+template <typename F>
+int launch_split(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t* rows,
+                 const int64_t* offs, hipStream_t hs, F launch) {
+  std::vector<int32_t> top, deep;
+  for (int i : list) (p.nodes[i].kind == kLvTop ? top : deep).push_back(i);
+  for (int pass = 0; pass < 2; pass++) {
+    const std::vector<int32_t>& l = pass == 0 ? top : deep;
+    if (l.empty()) continue;
+    DeviceTable dt;
+    LvArgs a;
+    int st = upload_args(p, l, rows, offs, hs, &dt, &a);
+    if (st) return st;
+    launch(pass == 0, a, pass == 0 ? dim3(static_cast<unsigned>((p.nrows + kLv - 1) / kLv))
+                                   : grid_of(p, l));
+    if ((st = check_hip(hipGetLastError(), "level kernel launch"))) return st;
+  }
+  return FURY_OK;
 }
 
 int pool_alloc(LvPlan* p, int64_t bytes, void** out) {
@@ -448,6 +602,7 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
   p->ntop = s->num_fields;
   p->root = s->root;
   p->nodes.assign(nn, LvNode{});
+  p->nrows = nrows;
   std::vector<int32_t> level(nn, 0), parent(nn, -1);
   int maxl = 0;
   for (int i = 0; i < nn; i++) {
@@ -480,36 +635,63 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
     lv_free(p);
     return st;
   }
+  // The counted nodes of level L (m > 0) share one buffer of segments [m_j counts][0], zeroed:
+  // lv_count (level 0) or the parent level's lv_expand fills the counts, one segmented scan
+  // turns them into starts.
+  auto counted_at = [&](int L) {
+    std::vector<int32_t> v;
+    for (int i = 0; i < nn; i++)
+      if (level[i] == L && p->nodes[i].m > 0 && p->nodes[i].kind != kLvInline && counted(p->nodes[i].type))
+        v.push_back(i);
+    return v;
+  };
+  std::vector<int64_t> seg;                         // segment offsets of the current level
+  auto alloc_level = [&](const std::vector<int32_t>& cnt) -> int {
+    seg.assign(1, 0);
+    for (int i : cnt) seg.push_back(seg.back() + p->nodes[i].m + 1);
+    if (cnt.empty()) return FURY_OK;
+    int64_t* buf = nullptr;
+    int r = pool_alloc(p, 8 * (seg.back() + 1), reinterpret_cast<void**>(&buf));
+    if (r) return r;
+    for (size_t j = 0; j < cnt.size(); j++) p->nodes[cnt[j]].start = buf + seg[j];
+    return check_hip(hipMemsetAsync(buf, 0, 8 * (seg.back() + 1), hs), "hipMemsetAsync counts");
+  };
+  auto scan_level = [&](const std::vector<int32_t>& cnt) -> int {
+    if (cnt.empty()) return FURY_OK;
+    int64_t* buf = p->nodes[cnt[0]].start;
+    const int64_t len = seg.back();
+    int64_t* ws = nullptr;
+    int r = pool_alloc(p, 8 * scan_workspace(len), reinterpret_cast<void**>(&ws));
+    if (r) return r;
+    device_scan(buf, len, buf + len, ws, hs);
+    if (cnt.size() == 1) return check_hip(hipGetLastError(), "scan launch");
+    const int32_t nseg = static_cast<int32_t>(cnt.size());
+    std::vector<int64_t> tab(seg.begin(), seg.end());
+    tab.resize(2 * nseg + 1, 0);
+    DeviceTable dt;
+    if ((r = upload_table(tab.data(), tab.size() * 8, hs, &dt))) return r;
+    int64_t* dtab = static_cast<int64_t*>(dt.dev);
+    hipLaunchKernelGGL(lv_seg_bases, dim3(static_cast<unsigned>((nseg + 255) / 256)), dim3(256), 0, hs,
+                       buf, dtab, nseg);
+    int64_t maxlen = 0;
+    for (int32_t j = 0; j < nseg; j++) maxlen = std::max(maxlen, seg[j + 1] - seg[j]);
+    hipLaunchKernelGGL(lv_seg_sub, dim3(static_cast<unsigned>((maxlen + kLv - 1) / kLv), nseg),
+                       dim3(kLv), 0, hs, buf, dtab, nseg);
+    return check_hip(hipGetLastError(), "segmented scan launch");
+  };
   std::vector<int32_t> strings;                     // STRING / BINARY nodes: bytes at the end
+  std::vector<int32_t> cnt = counted_at(0);
+  if (!(st = alloc_level(cnt)) && !cnt.empty())
+    st = launch_split(*p, cnt, rows, offs, hs, [&](bool by_row, const LvArgs& a, dim3 g) {
+      if (by_row) hipLaunchKernelGGL(lv_count<true>, g, dim3(kLv), 0, hs, a);
+      else hipLaunchKernelGGL(lv_count<false>, g, dim3(kLv), 0, hs, a);
+    });
   for (int L = 0; L <= maxl && !st; L++) {
-    std::vector<int32_t> cnt, arrays, parents;
-    int64_t scan_n = 0;
-    for (int i = 0; i < nn; i++) {
-      LvNode& n = p->nodes[i];
-      if (level[i] != L || n.m == 0 || n.kind == kLvInline) continue;
-      if (counted(n.type)) {
-        if ((st = pool_alloc(p, 8 * (n.m + 1), reinterpret_cast<void**>(&n.start)))) break;
-        cnt.push_back(i);
-        scan_n = std::max(scan_n, n.m);
-        if (n.type == FURY_TYPE_LIST || n.type == FURY_TYPE_MAP) arrays.push_back(i);
-        else strings.push_back(i);
-      }
-    }
-    if (st) break;
-    if (!cnt.empty()) {
-      DeviceTable dt;
-      LvArgs a;
-      if ((st = upload_args(*p, cnt, rows, offs, hs, &dt, &a))) break;
-      hipLaunchKernelGGL(lv_count, grid_of(*p, cnt), dim3(kLv), 0, hs, a);
-      if ((st = check_hip(hipGetLastError(), "lv_count launch"))) break;
-      int64_t* ws = nullptr;
-      if ((st = pool_alloc(p, 8 * scan_workspace(scan_n), reinterpret_cast<void**>(&ws)))) break;
-      for (int i : cnt) {
-        LvNode& n = p->nodes[i];
-        device_scan(n.start, n.m, n.start + n.m, ws, hs);
-      }
-      if ((st = check_hip(hipGetLastError(), "scan launch"))) break;
-    }
+    if ((st = scan_level(cnt))) break;
+    std::vector<int32_t> arrays, parents;
+    for (int i : cnt)
+      (p->nodes[i].type == FURY_TYPE_LIST || p->nodes[i].type == FURY_TYPE_MAP ? arrays : strings)
+          .push_back(i);
     // sizes of the next level: a struct's children have its entries, an array's elements its total
     std::vector<int64_t> tot;
     if ((st = level_totals(*p, arrays, rows, offs, hs, dev_tot, &tot))) break;
@@ -522,6 +704,9 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
       if (level[i] != L || n.type != FURY_TYPE_STRUCT) continue;
       for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = n.m;
     }
+    if (L == maxl) break;
+    cnt = counted_at(L + 1);
+    if ((st = alloc_level(cnt))) break;
     for (int i = 0; i < nn; i++) {
       if (level[i] != L || p->nodes[i].m == 0 || p->nodes[i].kind == kLvInline) continue;
       const LvNode& n = p->nodes[i];
@@ -535,11 +720,10 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
       if (has) parents.push_back(i);
     }
     if (st || parents.empty()) continue;
-    DeviceTable dt;
-    LvArgs a;
-    if ((st = upload_args(*p, parents, rows, offs, hs, &dt, &a))) break;
-    hipLaunchKernelGGL(lv_expand, grid_of(*p, parents), dim3(kLv), 0, hs, a);
-    st = check_hip(hipGetLastError(), "lv_expand launch");
+    st = launch_split(*p, parents, rows, offs, hs, [&](bool by_row, const LvArgs& a, dim3 g) {
+      if (by_row) hipLaunchKernelGGL(lv_expand<true>, g, dim3(kLv), 0, hs, a);
+      else hipLaunchKernelGGL(lv_expand<false>, g, dim3(kLv), 0, hs, a);
+    });
   }
   std::vector<int64_t> bytes;
   if (!st) st = level_totals(*p, strings, rows, offs, hs, dev_tot, &bytes);
@@ -570,12 +754,10 @@ int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const 
     }
   }
   if (list.empty()) return FURY_OK;
-  DeviceTable dt;
-  LvArgs a;
-  int st = upload_args(q, list, rows, offs, hs, &dt, &a);
-  if (st) return st;
-  hipLaunchKernelGGL(lv_write, grid_of(q, list), dim3(kLv), 0, hs, a);
-  return check_hip(hipGetLastError(), "lv_write launch");
+  return launch_split(q, list, rows, offs, hs, [&](bool by_row, const LvArgs& a, dim3 g) {
+    if (by_row) hipLaunchKernelGGL(lv_write<true>, g, dim3(kLv), 0, hs, a);
+    else hipLaunchKernelGGL(lv_write<false>, g, dim3(kLv), 0, hs, a);
+  });
 }
 
 }  // namespace fury
