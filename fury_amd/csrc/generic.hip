@@ -277,14 +277,34 @@ __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int
   if (r < g.nrows) sizes[r] = put_row<false, kRoot>(nodes, g.ntop, r, nullptr);
 }
 
+// The workgroup's 256 rows are one contiguous byte range of the output: each thread builds its
+// row in an LDS image of that range (put_row writes every byte of a row: zeroed bitmaps and
+// slots, zero-padded variable parts), then the workgroup stores the range with coalesced 8-byte
+// stores.  Thread-per-row stores straight to HBM wrote ~5x the row bytes (WRITE_SIZE of the
+// depth-3 schema at 4M rows: partial lines of 64 rows at a time, evicted before they filled).
+// A tile larger than the image (or past `cap`) takes the direct path.
+constexpr int64_t kGenImg = 96 * 1024;
+
 template <bool kWide, int kRoot>
 __global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
                                                                  uint8_t* __restrict__ rows,
                                                                  int64_t cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t img[];
   __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
   const GenNode* nodes = stage_nodes<kWide>(g, sn);
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kEncThreads;
+  const int64_t r = r0 + threadIdx.x;
+  const int64_t rend = min(r0 + kEncThreads, g.nrows);
+  const int64_t b0 = offs[r0], b1 = offs[rend];
+  if (b1 - b0 <= kGenImg && b1 <= cap) {
+    if (r < g.nrows) put_row<true, kRoot>(nodes, g.ntop, r, img + (offs[r] - b0));
+    __syncthreads();
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
+    uint64_t* d = reinterpret_cast<uint64_t*>(rows + b0);
+    for (int64_t i = threadIdx.x; i < (b1 - b0) >> 3; i += kEncThreads) d[i] = s[i];
+    return;
+  }
   if (r < g.nrows && offs[r + 1] <= cap) put_row<true, kRoot>(nodes, g.ntop, r, rows + offs[r]);
 }
 
@@ -558,12 +578,17 @@ template <bool kWide, int kRoot>
 void gen_encode_pass(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
                      int64_t cap, hipStream_t stream) {
   const int64_t blocks = (g.nrows + kEncThreads - 1) / kEncThreads;
-  if (sizes)
+  if (sizes) {
     hipLaunchKernelGGL((gen_measure_kernel<kWide, kRoot>), dim3(blocks), dim3(kEncThreads), 0,
                        stream, g, sizes);
-  else
-    hipLaunchKernelGGL((gen_encode_kernel<kWide, kRoot>), dim3(blocks), dim3(kEncThreads), 0,
-                       stream, g, offs, rows, cap);
+    return;
+  }
+  static const bool lds_ok = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(gen_encode_kernel<kWide, kRoot>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kGenImg)) == hipSuccess;
+  (void)lds_ok;
+  hipLaunchKernelGGL((gen_encode_kernel<kWide, kRoot>), dim3(blocks), dim3(kEncThreads), kGenImg,
+                     stream, g, offs, rows, cap);
 }
 
 template <bool kWide>

@@ -196,7 +196,34 @@ __global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
   if (kRows) {
     if (e >= a.nrows) return;
-    for (int j = 0; j < a.nlist; j++) count_entry(a, a.nodes[a.list[j]], e);
+    // batches of kB fields: all their loads are issued before any count is stored (a store to
+    // the count buffers may alias the row bytes for the compiler, which would serialise them)
+    constexpr int kB = 8;
+    const int64_t base = a.offs[e];
+    const uint8_t* row = a.rows + base;
+    const int64_t slots = lbm(a.ntop);
+    for (int j0 = 0; j0 < a.nlist; j0 += kB) {
+      int64_t c[kB];
+#pragma unroll
+      for (int u = 0; u < kB; u++) {
+        c[u] = 0;
+        if (j0 + u >= a.nlist) continue;
+        const LvNode& n = a.nodes[a.list[j0 + u]];
+        if (a.root) {                                  // a top-level array / map at the row
+          c[u] = static_cast<int32_t>(lld8(row + (n.type == FURY_TYPE_MAP ? 8 : 0)));
+          continue;
+        }
+        if (lbit(row, n.slot)) continue;
+        const uint64_t oas = lld8(row + slots + 8 * n.slot);
+        const uint8_t* vp = row + static_cast<int32_t>(oas >> 32);
+        c[u] = n.type == FURY_TYPE_LIST ? static_cast<int32_t>(lld8(vp))
+             : n.type == FURY_TYPE_MAP ? static_cast<int32_t>(lld8(vp + 8))
+             : static_cast<int64_t>(static_cast<uint32_t>(oas));
+      }
+#pragma unroll
+      for (int u = 0; u < kB; u++)
+        if (j0 + u < a.nlist) a.nodes[a.list[j0 + u]].start[e] = c[u];
+    }
   } else {
     const LvNode& n = a.nodes[a.list[blockIdx.y]];
     if (e < n.m) count_entry(a, n, e);
