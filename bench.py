@@ -219,19 +219,24 @@ def run(args):
     dec_bytes = row_bytes + col_bytes           # read rows, write columns
     step_bytes = enc_bytes + dec_bytes
 
+    # the same calls as encode_measured_into / encode_into / decode_into, argument blocks built
+    # once (RowEncoder.bind_*): per-call Python work must not starve the GPU between launches
+    if offs is not None:           # variable-length rows: one pass computes sizes + rows
+        encode = enc.bind_encode(cols, n, batch.rows, offs, stream=stream, measured=True)
+    else:
+        encode = enc.bind_encode(cols, n, batch.rows, None, stream=stream)
+    # fixed width: the decode into preallocated columns; C4 names row->Arrow conversion
+    # (ArrowWriter's fury_rows_to_arrow)
+    decode = enc.bind_decode(batch, out_cols if out_cols is not None else var_out, stream=stream,
+                             arrow=args.workload == "nested")
+
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        if offs is not None:       # variable-length rows: one pass computes sizes + rows
-            enc.encode_measured_into(cols, n, batch.rows, offs, stream=stream)
-        else:
-            enc.encode_into(cols, n, batch.rows, None, stream=stream)
+        encode()
         if ev is not None:
             ev[1].record(stream)
-        if out_cols is not None:
-            enc.decode_batch(batch, validity=False, stream=stream, out=out_cols)
-        else:       # C4 names row->Arrow conversion: ArrowWriter's fury_rows_to_arrow
-            enc.decode_into(batch, var_out, stream=stream, arrow=args.workload == "nested")
+        decode()
         if ev is not None:
             ev[2].record(stream)
 

@@ -1280,3 +1280,30 @@ def test_nested_decode_engines_oracle_exact(oracle, dev, name, mode):
     for f, c in zip(fields, empty):
         if c.offsets is not None:
             assert int(c.offsets[0].item()) == 0, f.name
+
+
+def test_bound_calls_match(oracle, dev):
+    """RowEncoder.bind_encode / bind_decode (argument blocks built once) issue the same calls as
+    encode_measured_into / decode_into: oracle-exact rows and columns, repeatable."""
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = SCHEMAS["mixed"]
+    n = 5000
+    host = gen_columns("mixed", fields, n, seed=4)
+    enc = Encoders.bean(fields, device=dev)
+    cols = _dev_cols(host, dev)
+    batch = enc.encode_batch(cols, n)
+    want, want_offs = oracle.encode(fields, host, n)
+    rows = torch.zeros_like(batch.rows)
+    offs = torch.zeros_like(batch.row_offsets)
+    call = enc.bind_encode(cols, n, rows, offs, measured=True)
+    call()
+    call()
+    assert np.array_equal(rows.cpu().numpy(), want) and np.array_equal(offs.cpu().numpy(), want_offs)
+    out = enc.decode_batch(batch)
+    ref = [column_to_host(c) for c in out]
+    for c in out:
+        for t in (c.values, c.validity, c.offsets):
+            if t is not None:
+                t.zero_()
+    enc.bind_decode(batch, out)()
+    assert_columns_equal(fields, [column_to_host(c) for c in out], ref, n)
