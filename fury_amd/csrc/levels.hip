@@ -579,10 +579,30 @@ int pool_alloc(LvPlan* p, int64_t bytes, void** out) {
 }
 
 // start[m] of the listed nodes -> host (one gather kernel, one copy, one sync).
+// Pinned landing buffer of the level totals, per thread, grown on demand (a copy into pageable
+// memory takes the runtime's staged path).
+int64_t* pinned_totals(size_t n) {
+  thread_local int64_t* buf = nullptr;
+  thread_local size_t cap = 0;
+  if (n > cap) {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    cap = 0;
+    const size_t c = std::max<size_t>(n, 4096);
+    void* p = nullptr;
+    if (hipHostMalloc(&p, c * 8, hipHostMallocDefault) != hipSuccess) return nullptr;
+    buf = static_cast<int64_t*>(p);
+    cap = c;
+  }
+  return buf;
+}
+
 int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t* rows,
                  const int64_t* offs, hipStream_t hs, int64_t* dev_out, std::vector<int64_t>* out) {
   out->assign(list.size(), 0);
   if (list.empty()) return FURY_OK;
+  int64_t* host = pinned_totals(list.size());
+  if (!host) return set_error(FURY_ERR_DEVICE, "hipHostMalloc (decode plan totals)");
   DeviceTable dt;
   LvArgs a;
   int st = upload_args(p, list, rows, offs, hs, &dt, &a);
@@ -591,10 +611,12 @@ int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_
   hipLaunchKernelGGL(lv_gather, dim3(static_cast<unsigned>((list.size() + 255) / 256)), dim3(256), 0,
                      hs, a, static_cast<int32_t>(list.size()));
   if ((st = check_hip(hipGetLastError(), "lv_gather launch"))) return st;
-  if ((st = check_hip(hipMemcpyAsync(out->data(), dev_out, list.size() * 8, hipMemcpyDeviceToHost, hs),
+  if ((st = check_hip(hipMemcpyAsync(host, dev_out, list.size() * 8, hipMemcpyDeviceToHost, hs),
                       "hipMemcpyAsync totals")))
     return st;
-  return check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+  if ((st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) return st;
+  out->assign(host, host + list.size());
+  return FURY_OK;
 }
 
 }  // namespace
@@ -720,8 +742,17 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
       (p->nodes[i].type == FURY_TYPE_LIST || p->nodes[i].type == FURY_TYPE_MAP ? arrays : strings)
           .push_back(i);
     // sizes of the next level: a struct's children have its entries, an array's elements its total
+    // one gather + copy + sync per level that holds lists / maps; string totals found so far
+    // ride along (bytes), so the last sync is needed only for strings below the last array level
     std::vector<int64_t> tot;
-    if ((st = level_totals(*p, arrays, rows, offs, hs, dev_tot, &tot))) break;
+    std::vector<int32_t> ask(arrays);
+    if (!arrays.empty()) ask.insert(ask.end(), strings.begin(), strings.end());
+    if ((st = level_totals(*p, ask, rows, offs, hs, dev_tot, &tot))) break;
+    if (!arrays.empty()) {
+      for (size_t j = 0; j < strings.size(); j++)
+        (*totals)[2 * strings[j] + 1] = tot[arrays.size() + j];
+      strings.clear();
+    }
     for (size_t j = 0; j < arrays.size(); j++) {
       const LvNode& n = p->nodes[arrays[j]];
       for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = tot[j];

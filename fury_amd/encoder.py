@@ -439,9 +439,7 @@ class RowEncoder:
             order = _bfs(self._schema.fields)
             cols: List[Column] = []
             with _on(stream):
-                for i, (f, first) in enumerate(order):
-                    cols.append(_alloc_node(f, int(entries[i]), int(nbytes[i]), validity or arrow,
-                                            self.device))
+                cols = _alloc_nodes(order, entries, nbytes, validity or arrow, self.device)
             for i, (f, first) in enumerate(order):
                 if f.children:
                     cols[i].child = [cols[first + j] for j in range(len(f.children))]
@@ -790,29 +788,57 @@ def _alloc_host_node(f: Field, m: int, nbytes: int) -> Column:
     raise UnsupportedOperationException(f"no device decode for {f}")
 
 
-def _alloc_node(f: Field, m: int, nbytes: int, validity: bool, device) -> Column:
-    """Output buffers for one schema node with m Arrow entries (validity / bool bitmaps zeroed:
-    the decode kernel only sets bits)."""
-    def zeros(k):
-        return torch.zeros(k, dtype=torch.uint8, device=device)
-
-    def empty(k, dt=torch.uint8):
-        return torch.empty(k, dtype=dt, device=device)
-    vb = zeros((m + 7) // 8 + 4) if validity else None
-    t = f.type_id
-    if t == BOOL:
-        return Column(values=zeros((m + 7) // 8 + 4), validity=vb)
-    if type_width(t) > 0:
-        return Column(values=empty(m * type_width(t) + 8), validity=vb)
-    if t in (STRING, BINARY):
-        return Column(values=empty(max(nbytes, 1)), validity=vb, offsets=empty(m + 1, torch.int32))
-    if t == DECIMAL:
-        return Column(values=empty(16 * m + 16), validity=vb)
-    if t in (LIST, MAP):
-        return Column(validity=vb, offsets=empty(m + 1, torch.int32))
-    if t == STRUCT:
-        return Column(validity=vb)
-    raise UnsupportedOperationException(f"no device decode for {f}")
+def _alloc_nodes(order, entries, nbytes, validity: bool, device) -> List[Column]:
+    """The output buffers of every schema node (breadth-first ``order``) carved from ONE device
+    allocation: bitmaps (validity, BOOL values; zeroed -- the decode only sets bits of shared
+    words) first, so a single memset clears them, then values / payloads / offsets, each 256-B
+    aligned.  One allocation and one memset instead of a few
+    per node (~17 nodes: the per-tensor cost was a third of a 400k-row decode's wall time)."""
+    def al(x):
+        return (x + 255) & ~255
+    plan = []            # per node: list of (kind, nbytes) in node order
+    zero_total = 0
+    rest_total = 0
+    for i, (f, _first) in enumerate(order):
+        m, nb, t = int(entries[i]), int(nbytes[i]), f.type_id
+        parts = {}
+        if validity:
+            parts["validity"] = ("z", (m + 7) // 8 + 4)
+        if t == BOOL:
+            parts["values"] = ("z", (m + 7) // 8 + 4)
+        elif type_width(t) > 0:
+            parts["values"] = ("e", m * type_width(t) + 8)
+        elif t in (STRING, BINARY):
+            parts["values"] = ("e", max(nb, 1))
+            parts["offsets"] = ("e", 4 * (m + 1))
+        elif t == DECIMAL:
+            parts["values"] = ("e", 16 * m + 16)
+        elif t in (LIST, MAP):
+            parts["offsets"] = ("e", 4 * (m + 1))
+        elif t != STRUCT:
+            raise UnsupportedOperationException(f"no device decode for {f}")
+        for kind, n in parts.values():
+            if kind == "z":
+                zero_total += al(n)
+            else:
+                rest_total += al(n)
+        plan.append(parts)
+    arena = torch.empty(max(zero_total + rest_total, 256), dtype=torch.uint8, device=device)
+    if zero_total:
+        arena[:zero_total].zero_()
+    zo, ro = 0, zero_total
+    cols = []
+    for parts in plan:
+        views = {}
+        for name, (kind, n) in parts.items():
+            if kind == "z":
+                v, zo = arena[zo:zo + n], zo + al(n)
+            else:
+                v, ro = arena[ro:ro + n], ro + al(n)
+            views[name] = v.view(torch.int32) if name == "offsets" else v
+        cols.append(Column(values=views.get("values"), validity=views.get("validity"),
+                           offsets=views.get("offsets")))
+    return cols
 
 
 class _CollectionEncoder(RowEncoder):
