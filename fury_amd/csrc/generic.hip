@@ -283,10 +283,10 @@ __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int
 // stores.  Thread-per-row stores straight to HBM wrote ~5x the row bytes (WRITE_SIZE of the
 // depth-3 schema at 4M rows: partial lines of 64 rows at a time, evicted before they filled).
 // A tile larger than the image (or past `cap`) takes the direct path.
-constexpr int64_t kGenImg = 96 * 1024;
+constexpr int64_t kGenImg = 76 * 1024;
 
 template <bool kWide, int kRoot>
-__global__ __launch_bounds__(kEncThreads) void gen_encode_kernel(GenArgs g,
+__global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
                                                                  uint8_t* __restrict__ rows,
                                                                  int64_t cap) {
