@@ -53,7 +53,6 @@ struct LvNode {
   int32_t num_children;
   int32_t kind;            // kLvTop / kLvInline / kLvMat
   int32_t slot;            // top-level field index (kLvTop)
-  int32_t es;              // element bytes in its container (8: a slot; w: array element)
 };
 
 struct LvPlan {
@@ -652,7 +651,7 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
   p->root = s->root;
   p->nodes.assign(nn, LvNode{});
   p->nrows = nrows;
-  std::vector<int32_t> level(nn, 0), parent(nn, -1);
+  std::vector<int32_t> level(nn, 0);
   int maxl = 0;
   for (int i = 0; i < nn; i++) {
     const GenTpl& t = s->nodes[i];
@@ -660,19 +659,15 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
     n.type = t.type_id;
     n.first_child = t.first_child;
     n.num_children = t.num_children;
-    n.es = 8;
     if (i < s->num_fields) {
       n.kind = kLvTop;
       n.slot = i;
       n.m = nrows;
     } else {
-      const int32_t pt = s->nodes[parent[i]].type_id;
-      const bool in_array = pt == FURY_TYPE_LIST || pt == FURY_TYPE_MAP;
+      // scalars are written by their parent's thread (struct field) or wave (array element)
       n.kind = host_width(t.type_id) > 0 ? kLvInline : kLvMat;
-      if (in_array && n.kind == kLvInline) n.es = host_width(t.type_id);
     }
     for (int j = 0; j < t.num_children; j++) {
-      parent[t.first_child + j] = i;
       level[t.first_child + j] = level[i] + 1;
       maxl = std::max(maxl, level[i] + 1);
     }
