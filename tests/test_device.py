@@ -1307,3 +1307,21 @@ def test_bound_calls_match(oracle, dev):
                 t.zero_()
     enc.bind_decode(batch, out)()
     assert_columns_equal(fields, [column_to_host(c) for c in out], ref, n)
+
+
+def test_nested_large_batch_level_engine(oracle, dev):
+    """600k depth-3 rows (several thousand workgroups per level, multi-block scans of every
+    level's segments): device rows == C restatement, level-engine decode == its decode."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_host
+    fields = _nested_fields()
+    base = _nested_beans(20_000, seed=8)
+    n = 600_000
+    host = beans_to_columns(fields, (base * (n // len(base) + 1))[:n])
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(_dev_cols(host, dev), n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.row_offsets.cpu().numpy(), want_offs)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    assert_columns_equal(fields, dec, oracle.decode(fields, want, want_offs, n), n)
