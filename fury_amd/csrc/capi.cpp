@@ -81,15 +81,15 @@ std::vector<RingUse> g_ring_pending;
 // Per-call workspaces (scan scratch, column tables, decode plans) come from power-of-two size
 // classes cached per device instead of hipMallocAsync / hipFreeAsync: on the box hipFreeAsync
 // took ~110 us of host time per call (HIP API trace of scripts/ab_generic.py), more than most of
-// the kernels it serves.  A freed block records an event on its stream; reuse on the same stream
-// is ordered by the stream, on another stream it waits for that event (hipStreamWaitEvent, no host
-// sync).  Cached free bytes are capped (kCacheCap); beyond that blocks go back to the pool.
+// the kernels it serves.  A freed block records an event on its stream; its next user's stream
+// waits for that event on the device (hipStreamWaitEvent, no host sync) -- also when the handles
+// are equal, since a destroyed stream's handle can be reused.  Cached free bytes are capped
+// (kCacheCap); beyond that blocks go back to the pool.
 namespace {
 struct CacheBlock {
   void* p;
   size_t cls;
   int device;
-  hipStream_t stream;
   hipEvent_t ev;
 };
 std::mutex g_cache_mu;
@@ -113,7 +113,9 @@ int dev_alloc(int64_t bytes, hipStream_t stream, void** out) {
       g_cache_free[i] = g_cache_free.back();
       g_cache_free.pop_back();
       g_cache_bytes -= cls;
-      if (b.stream != stream) (void)hipStreamWaitEvent(stream, b.ev, 0);
+      // always wait on the device (free when already ordered): a stream handle can be reused
+      // by a new stream after the old one is destroyed with work pending
+      (void)hipStreamWaitEvent(stream, b.ev, 0);
       (void)hipEventDestroy(b.ev);
       g_cache_live[b.p] = {cls, device};
       *out = b.p;
@@ -143,7 +145,7 @@ void dev_free(void* p, hipStream_t stream) {
     return;
   }
   (void)hipEventRecord(ev, stream);
-  g_cache_free.push_back(CacheBlock{p, cls, device, stream, ev});
+  g_cache_free.push_back(CacheBlock{p, cls, device, ev});
   g_cache_bytes += cls;
 }
 
