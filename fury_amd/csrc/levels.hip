@@ -78,6 +78,7 @@ struct LvArgs {
   int32_t ntop;
   int32_t root;
   int32_t nlist;                              // row-major launches: nodes in the list
+  int32_t dbg;                                // DIAGNOSTIC phase bits (FURY_LV_DBG), else 0
 };
 
 __device__ __forceinline__ bool lbit(const uint8_t* b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
@@ -250,6 +251,14 @@ struct WaveLists {
   int64_t arr2[64];        // MAP values array
 };
 
+// The WaveLists of a wave are written and read by that wave only: a wave-scope LDS fence and a
+// scheduling barrier order them (a workgroup barrier made all four waves wait for the slowest,
+// twice per list / map node).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ void wave_lists_fill(const LvArgs& a, const LvNode& n, int64_t e,
                                                 WaveLists& W) {
   const int lane = threadIdx.x & 63;
@@ -300,7 +309,7 @@ __device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, co
 }
 
 // Pass 3 of a level: the sources (and counts) of the next level's materialised entries.  Every
-// thread of the workgroup calls it for the same node (LDS + barriers for lists / maps).
+// lane of the wave calls it for the same node (per-wave LDS for lists / maps).
 __device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, int64_t e,
                                             WaveLists& W) {
   if (n.type == FURY_TYPE_STRUCT) {
@@ -320,14 +329,14 @@ __device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, in
     return;
   }
   wave_lists_fill(a, n, e, W);
-  __syncthreads();
+  wave_sync();
   const LvNode& c0 = a.nodes[n.first_child];
   if (c0.kind == kLvMat) expand_wave(a, c0, W, false);
   if (n.type == FURY_TYPE_MAP) {
     const LvNode& c1 = a.nodes[n.first_child + 1];
     if (c1.kind == kLvMat) expand_wave(a, c1, W, true);
   }
-  __syncthreads();
+  wave_sync();
 }
 
 template <bool kRows>
@@ -437,7 +446,7 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
     case FURY_TYPE_BINARY: {
       if (!live) return;
       const int64_t pos = n.start[e];
-      if (valid && n.values) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
+      if (valid && n.values && !(a.dbg & 1)) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
       n.offsets[e + 1] = static_cast<int32_t>(pos + (valid ? size : 0));
       if (e == 0) n.offsets[0] = 0;
       return;
@@ -458,12 +467,12 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
       const LvNode& c0 = a.nodes[n.first_child];
       const bool s0 = c0.kind == kLvInline;
       const bool s1 = t == FURY_TYPE_MAP && a.nodes[n.first_child + 1].kind == kLvInline;
-      if (!s0 && !s1) return;
-      wave_lists_fill(a, n, e, W);                         // every lane of the workgroup
-      __syncthreads();
+      if ((!s0 && !s1) || (a.dbg & 2)) return;
+      wave_lists_fill(a, n, e, W);                         // every lane of the wave
+      wave_sync();
       if (s0) write_wave(a, c0, W, false);
       if (s1) write_wave(a, a.nodes[n.first_child + 1], W, true);
-      __syncthreads();
+      wave_sync();
       return;
     }
     case FURY_TYPE_STRUCT: {                             // scalar fields: entry index = e
@@ -494,11 +503,11 @@ __global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
   const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
   const int64_t e = e0 + threadIdx.x;
   if (kRows) {
-    if (e0 >= a.nrows) return;
+    if (e0 >= a.nrows || (a.dbg & 4)) return;
     for (int j = 0; j < a.nlist; j++) write_entry(a, a.nodes[a.list[j]], e, W);
   } else {
     const LvNode& n = a.nodes[a.list[blockIdx.y]];
-    if (e0 < n.m) write_entry(a, n, e, W);
+    if (e0 < n.m && !(a.dbg & 8)) write_entry(a, n, e, W);
   }
 }
 
@@ -514,6 +523,18 @@ int host_width(int32_t t) {
     case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
     default: return -1;
   }
+}
+
+// DIAGNOSTIC (timing only, outputs wrong when set; honoured only with FURY_DIAGNOSTIC=1):
+// FURY_LV_DBG bit 1 skips string payload copies, 2 scalar array elements, 4 the row-major write
+// launch, 8 the node-major write launch.
+int lv_dbg() {
+  static const int v = [] {
+    const char* e = getenv("FURY_LV_DBG");
+    const char* d = getenv("FURY_DIAGNOSTIC");
+    return e && d && atoi(d) == 1 ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 // The node table + launch list for one kernel, uploaded stream-ordered (kept alive by dt until
@@ -535,6 +556,7 @@ int upload_args(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t
   a->root = p.root;
   a->nrows = p.nrows;
   a->nlist = static_cast<int32_t>(list.size());
+  a->dbg = lv_dbg();
   return FURY_OK;
 }
 
