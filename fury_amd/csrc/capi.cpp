@@ -724,7 +724,7 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "var_decode") {
-    if (value < 0 || value > 3) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..3");
+    if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..4");
     set_var_decode_mode(value);
     return FURY_OK;
   }

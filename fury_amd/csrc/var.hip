@@ -5,6 +5,9 @@
 #define FURY_VAR_MAIN
 #include "var_dev.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace fury {
 
 namespace {
@@ -14,7 +17,8 @@ const VarCol& hcol(const VarArgs& a, int k) { return a.htab ? a.htab[k] : a.col[
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
 int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back (tile rows by sequence
-                          // count), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256 rows
+                          // count), 1 sizing pass + decode, 2 / 3 register-staged one-pass with
+                          // 512 / 256 rows, 4 LDS-staged one-pass (var_lds.hip)
 
 }  // namespace
 
@@ -233,6 +237,56 @@ uint32_t dec_img_bytes(const VarArgs& a, int tile) {
   return static_cast<uint32_t>(need < cap ? need : cap);
 }
 
+// LDS plan of the LDS-staged decode (var_lds.hip): per workgroup the tile's row range (stage),
+// its output images and the nseq x NT in-tile offsets, within kLdsBudget so three workgroups
+// share a CU.  Row bytes are estimated from the output capacities (exact after
+// fury_row_decode_measure, over-estimates under bound sizing); a tile whose rows exceed the stage
+// reads them from HBM, so the estimate only moves speed.  FURY_LDS_BUDGET (bytes) overrides the
+// budget for A/B.
+int decode_var_lds_plan(const VarArgs& a, const uint8_t* rows, const int64_t* offs, int nseq,
+                        int nt, hipStream_t stream) {
+  static const int64_t budget = [] {
+    const char* e = getenv("FURY_LDS_BUDGET");
+    const int64_t v = e ? atoll(e) : 0;
+    return v >= 16384 && v <= 150 * 1024 ? v : int64_t(51) * 1024;
+  }();
+  double row = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = hcol(a, k);
+    const double per = c.values && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
+    if (c.kind == kDecimal) row += 16;
+    else if (c.kind == kBytes) row += per + 4;
+    else if (c.kind == kListFixed) row += 12 + per * (c.width == 0 ? 1 : c.width) + per / 8;
+  }
+  const int64_t pos = int64_t(nseq) * nt * 4;
+  int64_t img = dec_img_bytes(a, nt);
+  int64_t stage = r16(static_cast<int64_t>(row * nt * 1.2) + 64);
+  if (stage < 4096) stage = 4096;
+  // many string / list columns: the per-row offsets alone may fill the budget -- exceed it
+  // (fewer workgroups per CU) rather than leave no stage
+  const int64_t avail = (budget > pos + 16384 ? budget : pos + 16384) - pos;
+  if (stage + img > avail) {
+    // keep at least 3/4 of the stage estimate (at most avail - 1 KB), then trim the images
+    const int64_t keep = stage * 3 / 4 < avail - 1024 ? stage * 3 / 4 : avail - 1024;
+    stage = avail - img > keep ? avail - img : keep;
+    img = avail - stage;
+  }
+  stage = stage & ~int64_t(15);
+  img = img & ~int64_t(15);
+  const int64_t ntiles = (a.nrows + nt - 1) / nt;
+  const size_t wsb = (static_cast<size_t>(ntiles) * nseq + 1) * 8;    // [ticket][status words]
+  uint64_t* ws = nullptr;
+  int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
+  if (st) return st;
+  st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+  if (!st)
+    st = launch_decode_var_lds(a, rows, offs, ws + 1, reinterpret_cast<uint32_t*>(ws), nseq, nt,
+                               static_cast<uint32_t>(stage), static_cast<uint32_t>(img), ntiles,
+                               stream);
+  dev_free(ws, stream);
+  return st;
+}
+
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                       hipStream_t stream, bool arrow) {
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
@@ -247,6 +301,14 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     hipLaunchKernelGGL(decode_var_kernel<false>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
                        nullptr, nullptr, nseq);
     return check_hip(hipGetLastError(), "decode_var launch");
+  }
+  if (g_var_decode == 4 && nseq <= lds_decode_max_seq() && !a.tab) {
+    static const int nt = [] {
+      const char* e = getenv("FURY_LDS_ROWS");       // A/B: 128 / 256 / 512-row tiles
+      const int v = e ? atoi(e) : 0;
+      return v == 128 || v == 512 ? v : kThreads;
+    }();
+    return decode_var_lds_plan(a, rows, offs, nseq, nt, stream);
   }
   if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
     // 512-row tiles halve the look-back chain links: faster with several string / list

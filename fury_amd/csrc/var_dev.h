@@ -44,8 +44,21 @@ constexpr int kStrStage = 8 * 1024;           // LDS image of one column's Arrow
 
 // Column record k: from the kernel argument block, or -- schemas wider than kMaxVarCols -- from
 // the device table the host uploaded for the call (VarArgs.tab).  Uniform branch, scalar loads.
-__device__ __forceinline__ const VarCol& vc(const VarArgs& a, int k) {
-  return a.tab ? a.tab[k] : a.col[k];
+// Both live in the constant address space (kernarg segment / a read-only device table), so the
+// record's fields are scalar loads; a select of the kernarg and the table pointers as generic
+// pointers compiled to flat (vector) loads, each waited with vmcnt and lgkmcnt.
+using CVarCol = __attribute__((address_space(4))) const VarCol;
+__device__ __forceinline__ CVarCol& vc(const VarArgs& a, int k) {
+  CVarCol* base = a.tab ? (CVarCol*)(a.tab) : (CVarCol*)(a.col);
+  return base[k];
+}
+
+// The same pointer in the global address space: stores through it are global_store, not
+// flat_store (a flat store also counts against lgkmcnt, so every later LDS wait would wait for
+// it to complete).  Only for pointers into device / host memory, never LDS.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gl(T* p) {
+  return (__attribute__((address_space(1))) T*)(p);
 }
 
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
@@ -365,7 +378,7 @@ template <int NT, class MM>
 __device__ __forceinline__ uint32_t stage_meta(const VarArgs& a, int64_t r0, int64_t nr,
                                                uint8_t* pool, MM& mm, uint32_t at = 0) {
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     uint32_t fix = kNone, val = kNone, off = kNone;
     if (c.validity) val = stage_range<NT>(pool, at, c.validity + (r0 >> 3), c.validity + ((r0 + nr + 7) >> 3));
     switch (c.kind) {
@@ -400,7 +413,7 @@ __device__ __forceinline__ int64_t tile_row_size(const VarArgs& a, const MM& mm,
                                                  const uint8_t* pool, int t) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind < kBytes) continue;
     if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) continue;
     if (c.kind == kDecimal) {
@@ -420,7 +433,7 @@ __device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MM& mm,
                                                  const uint8_t* pool, int nr) {
   uint64_t need = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
     if (e <= b) continue;
@@ -440,7 +453,7 @@ __device__ __forceinline__ void stage_payloads(const VarArgs& a, MM& mm, uint8_t
                                                uint32_t at, int nr) {
   const bool iss = !(a.dbg & 1);
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = lds_i32(pool, mm.off[k]), e = lds_i32(pool, mm.off[k] + 4 * nr);
     uint32_t pay = kNone, pvb = kNone;
@@ -470,7 +483,7 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MM& mm,
   int64_t cursor = a.fixed_size;
   uint64_t nullbits = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     uint64_t slot = 0;
     if (mm.val[k] != kNone && !lds_bit(pool, mm.val[k], t)) {
       nullbits |= 1ull << (k & 63);
@@ -568,7 +581,7 @@ __device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MM& 
   }
 #pragma unroll
   for (int k = 0; k < S::n; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     uint64_t slot = 0;
     if (!ok[k]) {
       nullbits |= 1ull << k;
@@ -927,7 +940,7 @@ __device__ __forceinline__ void pipe_issue(const VarArgs& a, const int64_t* __re
   stage_meta<NT>(a, r0, nr, meta, ps.mm, at);        // sets every mm.pay / mm.pvb to kNone
   uint32_t pat = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
     if (e <= b) continue;
@@ -1022,7 +1035,7 @@ constexpr int kMeasTile = kThreads * kMeasRows;                // rows per workg
 __device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   int64_t sz = a.fixed_size;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind < kBytes) continue;
     if (c.validity && !bit_at(c.validity, r)) continue;          // null: setNullAt only
     if (c.kind == kDecimal) {
@@ -1047,7 +1060,7 @@ __global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* _
 #pragma unroll
     for (int j = 0; j < kMeasRows; j++) sz[j] = a.fixed_size;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = vc(a, k);
+      CVarCol& c = vc(a, k);
       if (c.kind < kBytes) continue;
       const uint32_t vb = c.validity ? (c.validity[r >> 3] >> (r & 7)) : 0xffu;
       if (c.kind == kDecimal) {
@@ -1099,7 +1112,8 @@ __global__ __launch_bounds__(kThreads) void add_group_prefix(int64_t* __restrict
 // --- decode side -------------------------------------------------------------------------------
 
 // Per row and var field: STRING/BINARY -> unpadded size; LIST -> numElements; else 0.
-__device__ __forceinline__ int64_t var_count(const VarArgs& a, const VarCol& c, int k,
+template <class Col>
+__device__ __forceinline__ int64_t var_count(const VarArgs& a, const Col& c, int k,
                                              const uint8_t* row) {
   if ((row[k >> 3] >> (k & 7)) & 1) return 0;                  // null
   const uint64_t slot = *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k);
@@ -1137,7 +1151,7 @@ __global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
       r < a.nrows ? (staged ? stage + d0 + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     const int64_t cnt = row ? var_count(a, c, k, row) : 0;
     int64_t total;
@@ -1157,7 +1171,7 @@ __global__ __launch_bounds__(kThreads) void decode_measure_fix(VarArgs a,
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
     if (r < a.nrows) c.offsets[r] += static_cast<int32_t>(sums[seq * nb + blockIdx.x]);
     if (r == a.nrows - 1) c.offsets[a.nrows] = static_cast<int32_t>(totals[seq]);
@@ -1214,7 +1228,8 @@ __device__ __forceinline__ void copy_bytes_range(uint8_t* g, const uint8_t* l, i
                                 reinterpret_cast<v4*>(g + i));
 }
 
-__device__ __forceinline__ bool is_seq(const VarCol& c) {
+template <class Col>
+__device__ __forceinline__ bool is_seq(const Col& c) {
   return c.kind == kBytes || c.kind == kListFixed;
 }
 
@@ -1237,6 +1252,9 @@ constexpr int kDecImg = 24 * 1024;
 // against hardware faults; a look-back that gives up raises the host-visible device error word
 // (`err`), which the next API call / fury_device_status() reports as FURY_ERR_DEVICE -- its
 // outputs are never passed off as valid.
+// Polling is economical: a lane re-reads its status word only while it is unpublished, and the
+// wave waits only for the lanes nearer than the nearest inclusive prefix (status reads go to the
+// cross-XCD coherence point; thousands of spinning waves re-reading 64 words each congested it).
 __device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q,
                                      uint32_t* err) {
   const int lane = threadIdx.x & 63;
@@ -1244,18 +1262,21 @@ __device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq
   uint32_t spins = 0;
   for (int64_t j = b - 1;; j -= 64) {
     const int64_t idx = j - lane;
-    uint64_t v;
+    uint64_t v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
+    uint64_t inc;
+    int stop;
     for (;;) {
-      v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
-      if (__ballot((v >> 62) == 0) == 0) break;
+      inc = __ballot((v >> 62) == 2);
+      stop = inc ? __builtin_ctzll(inc) : 63;
+      const uint64_t upto = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+      if ((__ballot((v >> 62) == 0) & upto) == 0) break;
       if (++spins > (1u << 24)) {
         if (lane == 0 && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return 0;
       }
       __builtin_amdgcn_s_sleep(1);
+      if ((v >> 62) == 0 && lane <= stop) v = ld_status(status + idx * nseq + q);
     }
-    const uint64_t inc = __ballot((v >> 62) == 2);
-    const int stop = inc ? __builtin_ctzll(inc) : 63;
     excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
     if (inc) return excl;
   }
@@ -1271,8 +1292,8 @@ __device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, in
   const int64_t head = min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
   const int64_t body = (n - head) >> 4;
   const int64_t t0 = head + 16 * body;
-  if (threadIdx.x < head) g[threadIdx.x] = img[threadIdx.x];
-  if (threadIdx.x < n - t0) g[t0 + threadIdx.x] = img[t0 + threadIdx.x];
+  if (threadIdx.x < head) gl(g)[threadIdx.x] = img[threadIdx.x];
+  if (threadIdx.x < n - t0) gl(g)[t0 + threadIdx.x] = img[t0 + threadIdx.x];
   const uint64_t* i64 = reinterpret_cast<const uint64_t*>(img);
   const int sh = static_cast<int>(head & 7) * 8;
   for (int64_t m = threadIdx.x; m < body; m += NT) {
@@ -1290,7 +1311,7 @@ __device__ __forceinline__ void store_shifted(uint8_t* g, const uint8_t* img, in
     v4 vv;
     vv.x = static_cast<uint32_t>(x); vv.y = static_cast<uint32_t>(x >> 32);
     vv.z = static_cast<uint32_t>(y); vv.w = static_cast<uint32_t>(y >> 32);
-    __builtin_nontemporal_store(vv, reinterpret_cast<v4*>(g + head + 16 * m));
+    __builtin_nontemporal_store(vv, gl(reinterpret_cast<v4*>(g + head + 16 * m)));
   }
 }
 
@@ -1318,7 +1339,7 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
     if (w == w0) m &= ~0u << (gbit0 & 31);
     if (w == w1 - 1 && (end & 31)) m &= (1u << (end & 31)) - 1;
     if (m == ~0u) {
-      g[w] = x;
+      gl(g)[w] = x;
     } else {
       atomicAnd(g + w, ~m);
       atomicOr(g + w, x & m);
@@ -1687,7 +1708,7 @@ __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row
                                             int nseq) {
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     if (!is_seq(c)) continue;
     const int q = seq++ - cbase;
     if (q < 0) continue;
@@ -1752,7 +1773,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
 
   // fixed-width fields and every field's validity: no dependency on other groups
   for (int k = 0; k < ((a.dbg & 8) ? 0 : a.ncols); k++) {
-    const VarCol& c = vc(a, k);
+    CVarCol& c = vc(a, k);
     const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
     const uint64_t slot =
         (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
@@ -1794,7 +1815,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
     chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq);
     int seq = 0;
     for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = vc(a, k);
+      CVarCol& c = vc(a, k);
       if (!is_seq(c)) continue;
       const int q = seq++ - cbase;
       if (q < 0) continue;
@@ -1913,6 +1934,10 @@ int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, 
 int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                           uint64_t* status, uint32_t* ticket, uint32_t img, bool wide,
                           int64_t nb, int64_t nbr, hipStream_t stream);
+int lds_decode_max_seq();
+int launch_decode_var_lds(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
+                          uint64_t* status, uint32_t* ticket, int nseq, int nt, uint32_t stage,
+                          uint32_t img, int64_t ntiles, hipStream_t stream);
 int launch_decode_var_reg_hi(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                              uint64_t* status, uint32_t* ticket, uint32_t img, bool wide,
                              int64_t nb, int64_t nbr, hipStream_t stream);

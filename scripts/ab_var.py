@@ -73,7 +73,11 @@ def main():
                                os.environ.__setitem__("FURY_VAR_DBG", "1024"),
                                enc.decode_into(batch, out),
                                os.environ.__setitem__("FURY_VAR_DBG", "0")),
+        # round 2: LDS-staged decode (var_lds.hip)
+        "decode_lds_tile": lambda: (L.fury_set_tuning(b"var_decode", 4), enc.decode_into(batch, out)),
     }
+    if os.environ.get("AB_LEGS"):
+        legs = {k: v for k, v in legs.items() if k in os.environ["AB_LEGS"].split(",")}
     times = {k: [] for k in legs}
     for _ in range(2):
         for f in legs.values():
@@ -97,9 +101,7 @@ def main():
     med = {k: round(statistics.median(v), 4) for k, v in times.items()}
     res = {"workload": name, "rows": n, "ms": med,
            "GBps": {k: round((col_bytes + row_bytes) / (med[k] * 1e-3) / 1e9, 1)
-                    for k in ("encode", "encode_tile", "encode_measured", "decode_1pass", "decode_2pass",
-                              "decode_512", "decode_ticket", "decode_order", "decode_lds",
-                              "decode_maximg")}}
+                    for k in med if k != "measure" and k != "decode_measure"}}
     print(json.dumps(res), flush=True)
 
 

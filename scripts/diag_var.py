@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--workload", default="mixed")
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--mode", type=int, default=0, help="tuning var_decode for the decode legs")
+    ap.add_argument("--decode-only", action="store_true")
     args = ap.parse_args()
     os.environ["FURY_DIAGNOSTIC"] = "1"      # the phase-skipping bits are diagnostic only
     import torch
@@ -53,13 +55,16 @@ def main():
         return round(statistics.median(xs) * 1e3, 1)
 
     res = {"workload": args.workload, "rows": n, "encode_us": {}, "decode_us": {}}
-    for d in (0, 2, 4, 6, 64):
+    for d in (() if args.decode_only else (0, 2, 4, 6, 64)):
         os.environ["FURY_VAR_DBG"] = str(d)
         res["encode_us"][d] = t(lambda: enc.encode_into(cols, n, batch.rows, batch.row_offsets))
     os.environ["FURY_VAR_DBG"] = "0"          # restore valid rows before the decode legs
     enc.encode_into(cols, n, batch.rows, batch.row_offsets)
     torch.cuda.synchronize()
-    for d in (0, 8, 16, 32, 56, 128, 4096, 4096 + 32):
+    from fury_amd import _native as N
+    N.lib().fury_set_tuning(b"var_decode", args.mode)
+    res["mode"] = args.mode
+    for d in (0, 8, 16, 32, 56, 128) + (() if args.mode >= 4 else (4096, 4096 + 32)):
         os.environ["FURY_VAR_DBG"] = str(d)
         res["decode_us"][d] = t(lambda: enc.decode_into(batch, out))
     os.environ["FURY_VAR_DBG"] = "0"

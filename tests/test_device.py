@@ -203,10 +203,11 @@ def test_fixed_variants_bit_exact(oracle, dev, variant):
         N.lib().fury_set_tuning(b"fixed_variant", old)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 def test_var_decode_modes_bit_exact(oracle, dev, mode):
     """Every variable-length decode mode (tuning 'var_decode': one-pass look-back with 256- or
-    512-row tiles, sizing pass + decode) decodes to the oracle's columns."""
+    512-row tiles, register- or LDS-staged, sizing pass + decode) decodes to the oracle's
+    columns."""
     from fury_amd import _native as N
     old = N.lib().fury_get_tuning(b"var_decode")
     assert N.lib().fury_set_tuning(b"var_decode", mode) == 0
