@@ -77,8 +77,12 @@ __device__ __forceinline__ uint8_t* values_of(const FixedArgs& a, int c, int lan
 }
 
 // Column record c of the general path: argument block, or the device table of a wide schema.
-__device__ __forceinline__ const FixedCol& fcol(const FixedArgs& a, int c) {
-  return a.tab ? a.tab[c] : a.col[c];
+// Both are constant address space (kernarg / read-only table): scalar loads of the record (as
+// generic pointers, the select compiled to flat vector loads).
+using CFixedCol = __attribute__((address_space(4))) const FixedCol;
+__device__ __forceinline__ CFixedCol& fcol(const FixedArgs& a, int c) {
+  CFixedCol* base = a.tab ? (CFixedCol*)(a.tab) : (CFixedCol*)(a.col);
+  return base[c];
 }
 
 // Tile of workgroup b.  Workgroups are dealt round-robin to the 8 XCDs (b % 8); tile_order 1
@@ -284,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
         if (kFast) {
           v[u] = ld8<NT>(values_of<R>(a, c, lane) + row * 8);
         } else {
-          const FixedCol& fc = fcol(a, c);
+          CFixedCol& fc = fcol(a, c);
           const uint8_t* vb = fc.validity;
           if (vb && !((vb[row >> 3] >> (row & 7)) & 1)) {
             isnull[u] = true;
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
       bool isnull = live && ((rowp[c >> 3] >> (c & 7)) & 1);
       uint64_t v = 0;
       if (live && !isnull) v = *reinterpret_cast<const uint64_t*>(rowp + bm + 8 * c);
-      const FixedCol& fc = fcol(a, c);
+      CFixedCol& fc = fcol(a, c);
       const int w = fc.width;
       uint8_t* dst = const_cast<uint8_t*>(fc.values);
       // rows [rbase, rbase + 64) of this wave; rbase % 64 == 0 and R % 64 == 0

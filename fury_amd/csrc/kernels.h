@@ -10,6 +10,15 @@
 
 namespace fury {
 
+// The same pointer in the global address space: accesses through it are global_load /
+// global_store, not flat (a flat access also counts against lgkmcnt, so every later LDS or scalar
+// wait waits for it too).  Pointers loaded from argument blocks or tables are generic to the
+// compiler.  Only for pointers into device / host memory, never LDS.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gl(T* p) {
+  return (__attribute__((address_space(1))) T*)(p);
+}
+
 // Columns per fixed-tile launch: the pointer table travels in the kernel argument block
 // (scalar-loaded, no per-call device upload).  Wider schemas are rejected.
 constexpr int kMaxFixedCols = 128;

@@ -81,9 +81,20 @@ struct LvArgs {
   int32_t dbg;                                // DIAGNOSTIC phase bits (FURY_LV_DBG), else 0
 };
 
-__device__ __forceinline__ bool lbit(const uint8_t* b, int64_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
+// LvSrc records through the global address space (one 16-B load / store)
+__device__ __forceinline__ LvSrc ld_src(const LvSrc* p, int64_t i) {
+  const auto q = gl(reinterpret_cast<const int64_t*>(p + i));
+  return LvSrc{q[0], q[1]};
+}
+__device__ __forceinline__ void st_src(LvSrc* p, int64_t i, int64_t base, int64_t off) {
+  const auto q = gl(reinterpret_cast<int64_t*>(p + i));
+  q[0] = base;
+  q[1] = off;
+}
+
+__device__ __forceinline__ bool lbit(const uint8_t* b, int64_t i) { return (gl(b)[i >> 3] >> (i & 7)) & 1; }
 __device__ __forceinline__ int64_t lbm(int64_t n) { return ((n + 63) >> 6) << 3; }
-__device__ __forceinline__ uint64_t lld8(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+__device__ __forceinline__ uint64_t lld8(const uint8_t* p) { return *gl(reinterpret_cast<const uint64_t*>(p)); }
 
 __device__ __forceinline__ int lwidth(int t) {
   switch (t) {
@@ -98,18 +109,18 @@ __device__ __forceinline__ int lwidth(int t) {
 __device__ __forceinline__ uint64_t load_w(const uint8_t* p, int w) {
   switch (w) {
     case 8: return lld8(p);
-    case 4: return *reinterpret_cast<const uint32_t*>(p);
-    case 2: return *reinterpret_cast<const uint16_t*>(p);
-    default: return *p;
+    case 4: return *gl(reinterpret_cast<const uint32_t*>(p));
+    case 2: return *gl(reinterpret_cast<const uint16_t*>(p));
+    default: return *gl(p);
   }
 }
 
 __device__ __forceinline__ void store_w(uint8_t* p, int w, uint64_t v) {
   switch (w) {
-    case 8: *reinterpret_cast<uint64_t*>(p) = v; break;
-    case 4: *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(v); break;
-    case 2: *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v); break;
-    default: *p = static_cast<uint8_t>(v); break;
+    case 8: *gl(reinterpret_cast<uint64_t*>(p)) = v; break;
+    case 4: *gl(reinterpret_cast<uint32_t*>(p)) = static_cast<uint32_t>(v); break;
+    case 2: *gl(reinterpret_cast<uint16_t*>(p)) = static_cast<uint16_t>(v); break;
+    default: *gl(p) = static_cast<uint8_t>(v); break;
   }
 }
 
@@ -120,7 +131,7 @@ __device__ __forceinline__ void ballot_bits(uint8_t* bits, int64_t e, bool pred,
   const int lane = threadIdx.x & 63;
   const int64_t w0 = (e - lane) >> 5;
   if (lane < 2 && (w0 + lane) * 32 < m)
-    reinterpret_cast<uint32_t*>(bits)[w0 + lane] = static_cast<uint32_t>(b >> (32 * lane));
+    gl(reinterpret_cast<uint32_t*>(bits))[w0 + lane] = static_cast<uint32_t>(b >> (32 * lane));
 }
 
 // One bit of a bitmap shared with other threads (array elements of different owners).
@@ -134,16 +145,16 @@ __device__ __forceinline__ void atomic_bit(uint8_t* bits, int64_t i) {
 __device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, int64_t len) {
   if (len <= 0) return;
   const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
-  for (int64_t t = 0; t < head; t++) dst[t] = src[t];
+  for (int64_t t = 0; t < head; t++) gl(dst)[t] = gl(src)[t];
   const int64_t body = (len - head) >> 3;
-  const uint64_t* s64 = reinterpret_cast<const uint64_t*>(src);
+  const auto s64 = gl(reinterpret_cast<const uint64_t*>(src));
   const int sh = static_cast<int>(head) * 8;
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst + head);
+  const auto d64 = gl(reinterpret_cast<uint64_t*>(dst + head));
   for (int64_t w = 0; w < body; w++) {
     const uint64_t lo = s64[w];
     d64[w] = sh ? (lo >> sh) | (s64[w + 1] << (64 - sh)) : lo;
   }
-  for (int64_t t = head + 8 * body; t < len; t++) dst[t] = src[t];
+  for (int64_t t = head + 8 * body; t < len; t++) gl(dst)[t] = gl(src)[t];
 }
 
 // The value of entry e of node n: null flag, its container base, and for variable-length types
@@ -156,11 +167,11 @@ struct LvVal {
 
 __device__ __forceinline__ LvVal lv_source(const LvArgs& a, const LvNode& n, int64_t e) {
   if (n.kind == kLvTop) {
-    const int64_t base = a.offs[e];
+    const int64_t base = gl(a.offs)[e];
     if (a.root) return {false, base, -1};                       // a top-level array / map
     return {lbit(a.rows + base, n.slot), base, base + lbm(a.ntop) + 8 * n.slot};
   }
-  const LvSrc s = n.src[e];
+  const LvSrc s = ld_src(n.src, e);
   return {s.base < 0, s.base, s.off < 0 ? -1 : s.base + s.off};
 }
 
@@ -185,7 +196,7 @@ __device__ __forceinline__ void count_entry(const LvArgs& a, const LvNode& n, in
     else if (n.type == FURY_TYPE_MAP) c = static_cast<int32_t>(lld8(vp + 8));
     else c = size;
   }
-  n.start[e] = c;
+  gl(n.start)[e] = c;
 }
 
 // Launch shapes: kRows = the listed nodes are top-level fields (entry = row) and one thread per
@@ -199,7 +210,7 @@ __global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
     // batches of kB fields: all their loads are issued before any count is stored (a store to
     // the count buffers may alias the row bytes for the compiler, which would serialise them)
     constexpr int kB = 8;
-    const int64_t base = a.offs[e];
+    const int64_t base = gl(a.offs)[e];
     const uint8_t* row = a.rows + base;
     const int64_t slots = lbm(a.ntop);
     for (int j0 = 0; j0 < a.nlist; j0 += kB) {
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < kB; u++)
-        if (j0 + u < a.nlist) a.nodes[a.list[j0 + u]].start[e] = c[u];
+        if (j0 + u < a.nlist) gl(a.nodes[a.list[j0 + u]].start)[e] = c[u];
     }
   } else {
     const LvNode& n = a.nodes[a.list[blockIdx.y]];
@@ -276,8 +287,8 @@ __device__ __forceinline__ void wave_lists_fill(const LvArgs& a, const LvNode& n
       ab2 = vp + 8 + static_cast<int64_t>(lld8(vp)) - a.rows;
     }
   }
-  W.st[lane] = n.start[live ? e : n.m];
-  if (lane == 63) W.st[64] = n.start[min(e + 1, n.m)];
+  W.st[lane] = gl(n.start)[live ? e : n.m];
+  if (lane == 63) W.st[64] = gl(n.start)[min(e + 1, n.m)];
   W.arr[lane] = ab;
   W.arr2[lane] = ab2;
 }
@@ -303,8 +314,8 @@ __device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, co
     const int64_t ab = second ? W.arr2[l] : W.arr[l];
     const int64_t hb = 8 + lbm(m);
     const bool nul = lbit(a.rows + ab + 8, j);
-    c.src[q] = nul ? LvSrc{-1, 0} : LvSrc{ab, hb + 8 * j};
-    if (c.start && !nul) c.start[q] = var_count(a, c.type, ab, ab + hb + 8 * j);
+    st_src(c.src, q, nul ? -1 : ab, nul ? 0 : hb + 8 * j);
+    if (c.start && !nul) gl(c.start)[q] = var_count(a, c.type, ab, ab + hb + 8 * j);
   }
 }
 
@@ -323,8 +334,8 @@ __device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, in
       const LvNode& c = a.nodes[n.first_child + k];
       if (c.kind != kLvMat) continue;
       const bool nul = v.null || lbit(vp, k);
-      c.src[e] = nul ? LvSrc{-1, 0} : LvSrc{vb, lbm(nc) + 8 * k};
-      if (c.start && !nul) c.start[e] = var_count(a, c.type, vb, vb + lbm(nc) + 8 * k);
+      st_src(c.src, e, nul ? -1 : vb, nul ? 0 : lbm(nc) + 8 * k);
+      if (c.start && !nul) gl(c.start)[e] = var_count(a, c.type, vb, vb + lbm(nc) + 8 * k);
     }
     return;
   }
@@ -388,7 +399,9 @@ __device__ __forceinline__ void ballot_or(uint8_t* bits, int64_t base, bool pred
   if (lane < 3) {
     const uint32_t part = lane == 0 ? static_cast<uint32_t>(lo)
                         : lane == 1 ? static_cast<uint32_t>(lo >> 32) : hi;
-    if (part) atomicOr(reinterpret_cast<uint32_t*>(bits) + (base >> 5) + lane, part);
+    if (part)
+      __hip_atomic_fetch_or(gl(reinterpret_cast<uint32_t*>(bits)) + (base >> 5) + lane, part,
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -445,15 +458,15 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
     case FURY_TYPE_STRING:
     case FURY_TYPE_BINARY: {
       if (!live) return;
-      const int64_t pos = n.start[e];
+      const int64_t pos = gl(n.start)[e];
       if (valid && n.values && !(a.dbg & 1)) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
-      n.offsets[e + 1] = static_cast<int32_t>(pos + (valid ? size : 0));
-      if (e == 0) n.offsets[0] = 0;
+      gl(n.offsets)[e + 1] = static_cast<int32_t>(pos + (valid ? size : 0));
+      if (e == 0) gl(n.offsets)[0] = 0;
       return;
     }
     case FURY_TYPE_DECIMAL: {
       if (!live || !n.values) return;
-      uint64_t* d = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(n.values) + 16 * e);
+      const auto d = gl(reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(n.values) + 16 * e));
       d[0] = valid ? lld8(vp) : 0;
       d[1] = valid ? lld8(vp + 8) : 0;
       return;
@@ -461,8 +474,8 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
     case FURY_TYPE_LIST:
     case FURY_TYPE_MAP: {
       if (live) {
-        n.offsets[e + 1] = static_cast<int32_t>(n.start[e + 1]);
-        if (e == 0) n.offsets[0] = 0;
+        gl(n.offsets)[e + 1] = static_cast<int32_t>(gl(n.start)[e + 1]);
+        if (e == 0) gl(n.offsets)[0] = 0;
       }
       const LvNode& c0 = a.nodes[n.first_child];
       const bool s0 = c0.kind == kLvInline;

@@ -53,14 +53,6 @@ __device__ __forceinline__ CVarCol& vc(const VarArgs& a, int k) {
   return base[k];
 }
 
-// The same pointer in the global address space: stores through it are global_store, not
-// flat_store (a flat store also counts against lgkmcnt, so every later LDS wait would wait for
-// it to complete).  Only for pointers into device / host memory, never LDS.
-template <class T>
-__device__ __forceinline__ __attribute__((address_space(1))) T* gl(T* p) {
-  return (__attribute__((address_space(1))) T*)(p);
-}
-
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
 }
