@@ -38,7 +38,7 @@ constexpr int kThreads = 64;          // decode keeps per-thread node counters i
 constexpr int kEncThreads = 256;
 
 __device__ __forceinline__ bool gbit(const uint8_t* bits, int64_t i) {
-  return (bits[i >> 3] >> (i & 7)) & 1;
+  return (gl(bits)[i >> 3] >> (i & 7)) & 1;
 }
 __device__ __forceinline__ int64_t g8(int64_t n) { return (n + 7) & ~int64_t(7); }
 __device__ __forceinline__ int64_t gbm(int64_t n) { return ((n + 63) >> 6) << 3; }
@@ -53,13 +53,28 @@ __device__ __forceinline__ int gwidth(int t) {
   }
 }
 
-__device__ __forceinline__ void st8(uint8_t* p, uint64_t v) {
-  memcpy(p, &v, 8);   // p is 8-byte aligned by construction; memcpy keeps it a single store
+// Typed accesses.  Row images are built in LDS (LdsU8) or, past the image, straight in HBM
+// (uint8_t*: always device memory here); input columns and rows are device memory.  With the
+// address space explicit the compiler emits ds_* / global_* instead of flat_* (a flat access
+// counts against both vmcnt and lgkmcnt, so each wait waited for both).
+template <class T>
+using Lds = __attribute__((address_space(3))) T;
+using LdsU8 = Lds<uint8_t>;
+
+__device__ __forceinline__ void st8(uint8_t* p, uint64_t v) {   // p 8-aligned by construction
+  *gl(reinterpret_cast<uint64_t*>(p)) = v;
 }
+__device__ __forceinline__ void st8(LdsU8* p, uint64_t v) { *reinterpret_cast<Lds<uint64_t>*>(p) = v; }
+__device__ __forceinline__ void st4(uint8_t* p, uint32_t v) { *gl(reinterpret_cast<uint32_t*>(p)) = v; }
+__device__ __forceinline__ void st4(LdsU8* p, uint32_t v) { *reinterpret_cast<Lds<uint32_t>*>(p) = v; }
+__device__ __forceinline__ void st2(uint8_t* p, uint16_t v) { *gl(reinterpret_cast<uint16_t*>(p)) = v; }
+__device__ __forceinline__ void st2(LdsU8* p, uint16_t v) { *reinterpret_cast<Lds<uint16_t>*>(p) = v; }
+__device__ __forceinline__ void st1(uint8_t* p, uint8_t v) { *gl(p) = v; }
+__device__ __forceinline__ void st1(LdsU8* p, uint8_t v) { *p = v; }
+__device__ __forceinline__ void or1(uint8_t* p, uint8_t v) { *gl(p) |= v; }
+__device__ __forceinline__ void or1(LdsU8* p, uint8_t v) { *p |= v; }
 __device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
-  uint64_t v;
-  memcpy(&v, p, 8);
-  return v;
+  return *gl(reinterpret_cast<const uint64_t*>(p));
 }
 
 // Copies len bytes from an 8-byte aligned source (a row's var section) to any destination:
@@ -84,16 +99,18 @@ __device__ __forceinline__ void copy_to_unaligned(uint8_t* dst, const uint8_t* s
 
 // ---- encode ----------------------------------------------------------------------------------
 
-__device__ __forceinline__ void zero_bytes(uint8_t* p, int64_t n) {
+template <class P>
+__device__ __forceinline__ void zero_bytes(P p, int64_t n) {
   // 8-byte aligned start; n multiple of 8 in every use
   for (int64_t i = 0; i < n; i += 8) st8(p + i, 0);
 }
 
 // Appends len bytes (unaligned source) at dst (8-aligned), zero-padding to 8.
-__device__ __forceinline__ void append_unaligned(uint8_t* dst, const uint8_t* src, int64_t len) {
+template <class P>
+__device__ __forceinline__ void append_unaligned(P dst, const uint8_t* src, int64_t len) {
   // aligned source words funnel-shifted into place; no word past the last source byte is read
   const uintptr_t so = reinterpret_cast<uintptr_t>(src) & 7;
-  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - so);
+  const auto ap = gl(reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - so));
   const int64_t nw = (len + 7) >> 3;
   const int64_t nsrc = (static_cast<int64_t>(so) + len + 7) >> 3;
   const int sh = static_cast<int>(so) * 8;
@@ -108,16 +125,16 @@ __device__ __forceinline__ void append_unaligned(uint8_t* dst, const uint8_t* sr
   }
 }
 
-template <int D, bool W>
-__device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+template <int D, bool W, class P, class NP>
+__device__ void put_value(NP nodes, int ni, int64_t idx, P buf, int64_t container,
                           int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
                           int64_t& cursor);
 
 // BinaryArrayWriter image of elements [b, b + m) of node `ei` at buf + cursor.
-template <int D, bool W>
-__device__ void put_array(const GenNode* nodes, int ei, int64_t b, int64_t m, uint8_t* buf,
+template <int D, bool W, class P, class NP>
+__device__ void put_array(NP nodes, int ei, int64_t b, int64_t m, P buf,
                           int64_t& cursor) {
-  const GenNode& e = nodes[ei];
+  const auto& e = nodes[ei];
   const int w = gwidth(e.type);
   const int es = w > 0 ? w : 8;
   const int64_t start = cursor;
@@ -133,17 +150,17 @@ __device__ void put_array(const GenNode* nodes, int ei, int64_t b, int64_t m, ui
   cursor = c2;
 }
 
-template <int D, bool W>
-__device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* buf, int64_t container,
+template <int D, bool W, class P, class NP>
+__device__ void put_value(NP nodes, int ni, int64_t idx, P buf, int64_t container,
                           int64_t slot, int es, bool in_array, int64_t bitmap, int64_t ordinal,
                           int64_t& cursor) {
   if constexpr (D >= kGenMaxDepth) {
     (void)nodes;
     return;
   } else {
-    const GenNode& n = nodes[ni];
+    const auto& n = nodes[ni];
     if (n.validity && !gbit(n.validity, idx)) {      // setNullAt: bit only, slot stays 0
-      if (W) buf[bitmap + (ordinal >> 3)] |= static_cast<uint8_t>(1u << (ordinal & 7));
+      if (W) or1(buf + bitmap + (ordinal >> 3), static_cast<uint8_t>(1u << (ordinal & 7)));
       return;
     }
     const int w = gwidth(n.type);
@@ -152,17 +169,17 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
         uint64_t v;
         if (n.type == FURY_TYPE_BOOL) v = gbit(n.values, idx);
         else if (w == 8) v = ld8(n.values + idx * 8);
-        else if (w == 4) v = *reinterpret_cast<const uint32_t*>(n.values + idx * 4);
-        else if (w == 2) v = *reinterpret_cast<const uint16_t*>(n.values + idx * 2);
-        else v = n.values[idx];
+        else if (w == 4) v = *gl(reinterpret_cast<const uint32_t*>(n.values + idx * 4));
+        else if (w == 2) v = *gl(reinterpret_cast<const uint16_t*>(n.values + idx * 2));
+        else v = gl(n.values)[idx];
         if (!in_array) {
           st8(buf + slot, v);                           // putInt64(0) + narrow put
         } else {
           switch (es) {
             case 8: st8(buf + slot, v); break;
-            case 4: *reinterpret_cast<uint32_t*>(buf + slot) = static_cast<uint32_t>(v); break;
-            case 2: *reinterpret_cast<uint16_t*>(buf + slot) = static_cast<uint16_t>(v); break;
-            default: buf[slot] = static_cast<uint8_t>(v); break;
+            case 4: st4(buf + slot, static_cast<uint32_t>(v)); break;
+            case 2: st2(buf + slot, static_cast<uint16_t>(v)); break;
+            default: st1(buf + slot, static_cast<uint8_t>(v)); break;
           }
         }
       }
@@ -172,8 +189,8 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
     switch (n.type) {
       case FURY_TYPE_STRING:
       case FURY_TYPE_BINARY: {
-        const int64_t b = n.offsets[idx];
-        const int64_t len = n.offsets[idx + 1] - b;
+        const int64_t b = gl(n.offsets)[idx];
+        const int64_t len = gl(n.offsets)[idx + 1] - b;
         if (W) append_unaligned(buf + start, n.values + b, len);
         cursor = start + g8(len);
         if (W) st8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
@@ -189,8 +206,8 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
         return;
       }
       case FURY_TYPE_LIST: {
-        const int64_t b = n.offsets[idx];
-        put_array<D, W>(nodes, n.first_child, b, n.offsets[idx + 1] - b, buf, cursor);
+        const int64_t b = gl(n.offsets)[idx];
+        put_array<D, W>(nodes, n.first_child, b, gl(n.offsets)[idx + 1] - b, buf, cursor);
         break;
       }
       case FURY_TYPE_STRUCT: {
@@ -206,8 +223,8 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
         break;
       }
       case FURY_TYPE_MAP: {
-        const int64_t b = n.offsets[idx];
-        const int64_t m = n.offsets[idx + 1] - b;
+        const int64_t b = gl(n.offsets)[idx];
+        const int64_t m = gl(n.offsets)[idx + 1] - b;
         int64_t c2 = start + 8;                         // writeDirectly(-1) placeholder
         put_array<D, W>(nodes, n.first_child, b, m, buf, c2);
         if (W) st8(buf + start, static_cast<uint64_t>(c2 - (start + 8)));   // key array size
@@ -229,13 +246,13 @@ __device__ void put_value(const GenNode* nodes, int ni, int64_t idx, uint8_t* bu
 // top-level BinaryArray (root 1) / BinaryMap [int64 keyBytes][keys][values] (root 2) of node 0's
 // entry r, written at the buffer start exactly as inside a row (element offsets are relative to
 // the array itself).
-template <bool W, int kRoot>
-__device__ int64_t put_row(const GenNode* nodes, int ntop, int64_t r, uint8_t* buf) {
+template <bool W, int kRoot, class P, class NP>
+__device__ int64_t put_row(NP nodes, int ntop, int64_t r, P buf) {
   constexpr int root = kRoot;
   if constexpr (kRoot != 0) {
-    const GenNode& n = nodes[0];
-    const int64_t b = n.offsets[r];
-    const int64_t m = n.offsets[r + 1] - b;
+    const auto& n = nodes[0];
+    const int64_t b = gl(n.offsets)[r];
+    const int64_t m = gl(n.offsets)[r + 1] - b;
     int64_t cursor = root == 2 ? 8 : 0;
     put_array<1, W>(nodes, n.first_child, b, m, buf, cursor);
     if (root == 2) {
@@ -266,15 +283,25 @@ __device__ __forceinline__ const GenNode* stage_nodes(const GenArgs& g, GenNode*
   return lds;
 }
 
+// The encode side's node table with its address space explicit (LDS copy / uploaded table).
+using GNodes = __attribute__((address_space(1))) const GenNode*;
+using LNodes = Lds<const GenNode>*;
+template <bool kWide>
+__device__ __forceinline__ auto enc_nodes(const GenArgs& g, GenNode* lds) {
+  const GenNode* p = stage_nodes<kWide>(g, lds);
+  if constexpr (kWide) return (GNodes)(p);
+  else return (LNodes)(p);
+}
+
 // kRoot (fury_schema.root) is a template parameter so the row kernels do not carry the
 // collection code: inlining both into one kernel raised its scratch from 192 to 1200 B per lane
 // and doubled the encode time.
 template <bool kWide, int kRoot>
 __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int64_t* __restrict__ sizes) {
   __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
-  const GenNode* nodes = stage_nodes<kWide>(g, sn);
+  const auto nodes = enc_nodes<kWide>(g, sn);
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kEncThreads + threadIdx.x;
-  if (r < g.nrows) sizes[r] = put_row<false, kRoot>(nodes, g.ntop, r, nullptr);
+  if (r < g.nrows) sizes[r] = put_row<false, kRoot>(nodes, g.ntop, r, static_cast<uint8_t*>(nullptr));
 }
 
 // The workgroup's 256 rows are one contiguous byte range of the output: each thread builds its
@@ -292,13 +319,13 @@ __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
                                                                  int64_t cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t img[];
   __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
-  const GenNode* nodes = stage_nodes<kWide>(g, sn);
+  const auto nodes = enc_nodes<kWide>(g, sn);
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kEncThreads;
   const int64_t r = r0 + threadIdx.x;
   const int64_t rend = min(r0 + kEncThreads, g.nrows);
   const int64_t b0 = offs[r0], b1 = offs[rend];
   if (b1 - b0 <= kGenImg && b1 <= cap) {
-    if (r < g.nrows) put_row<true, kRoot>(nodes, g.ntop, r, img + (offs[r] - b0));
+    if (r < g.nrows) put_row<true, kRoot>(nodes, g.ntop, r, (LdsU8*)(img + (offs[r] - b0)));
     __syncthreads();
     const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
     uint64_t* d = reinterpret_cast<uint64_t*>(rows + b0);
