@@ -56,17 +56,22 @@ __device__ __forceinline__ CVarCol& vc(const VarArgs& a, int k) {
 __device__ __forceinline__ bool bit_at(const uint8_t* bits, int64_t i) {
   return (bits[i >> 3] >> (i & 7)) & 1;
 }
+// bit_at of a bitmap in device memory (global loads, never flat)
+__device__ __forceinline__ bool bit_at_g(const uint8_t* bits, int64_t i) {
+  return (gl(bits)[i >> 3] >> (i & 7)) & 1;
+}
 __device__ __forceinline__ int64_t rnd8(int64_t n) { return (n + 7) & ~int64_t(7); }
 __host__ __device__ __forceinline__ int64_t r16(int64_t x) { return (x + 15) & ~int64_t(15); }
 __device__ __forceinline__ int64_t bm_bytes(int64_t n) { return ((n + 63) >> 6) << 3; }
 
+// Element i of a device-memory column (global loads).
 __device__ __forceinline__ uint64_t load_fixed(const uint8_t* p, int64_t i, int w) {
   switch (w) {
-    case 8: return *reinterpret_cast<const uint64_t*>(p + i * 8);
-    case 4: return *reinterpret_cast<const uint32_t*>(p + i * 4);
-    case 2: return *reinterpret_cast<const uint16_t*>(p + i * 2);
-    case 1: return p[i];
-    default: return bit_at(p, i);
+    case 8: return *gl(reinterpret_cast<const uint64_t*>(p + i * 8));
+    case 4: return *gl(reinterpret_cast<const uint32_t*>(p + i * 4));
+    case 2: return *gl(reinterpret_cast<const uint16_t*>(p + i * 2));
+    case 1: return gl(p)[i];
+    default: return bit_at_g(p, i);
   }
 }
 
@@ -726,7 +731,7 @@ template <typename D>
 __device__ __forceinline__ void put_string(D* dst, const uint8_t* src, int64_t len) {
   if (len <= 0) return;
   const uintptr_t s = reinterpret_cast<uintptr_t>(src) & 7;
-  const uint64_t* ap = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s);
+  const auto ap = gl(reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - s));
   const int64_t nw = (len + 7) >> 3;
   const int64_t nsrc = (static_cast<int64_t>(s) + len + 7) >> 3;
   for (int64_t k0 = 0; k0 < nw; k0 += 4) {
@@ -750,7 +755,7 @@ __device__ __forceinline__ void put_string(D* dst, const uint8_t* src, int64_t l
 // (bits past `lim` are garbage).
 __device__ __forceinline__ uint64_t load_bits64(const uint8_t* bits, int64_t i, int lim) {
   const uintptr_t addr = reinterpret_cast<uintptr_t>(bits) + (i >> 3);
-  const uint64_t* a = reinterpret_cast<const uint64_t*>(addr & ~uintptr_t(7));
+  const auto a = gl(reinterpret_cast<const uint64_t*>(addr & ~uintptr_t(7)));    // device memory
   const int sh = static_cast<int>((addr & 7) * 8 + (i & 7));
   const uint64_t lo = a[0];
   if (sh == 0) return lo;
@@ -774,7 +779,7 @@ __device__ __forceinline__ int64_t put_array(D* d64, int width, const uint8_t* v
   }
   D* out = d64 + 1 + nbw;
   if (ew == 8) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(vals);
+    const auto src = gl(reinterpret_cast<const uint64_t*>(vals));
     for (int64_t j0 = 0; j0 < n; j0 += 8) {
       const int lim = static_cast<int>(min<int64_t>(8, n - j0));
       const uint64_t vm = vbits ? load_bits64(vbits, vbit0 + j0, lim) : ~0ull;
@@ -798,10 +803,10 @@ __device__ __forceinline__ int64_t put_array(D* d64, int width, const uint8_t* v
       if (!((vm >> t) & 1)) continue;                  // null element stays 0
       uint64_t x;
       switch (width) {
-        case 4: x = reinterpret_cast<const uint32_t*>(vals)[j]; break;
-        case 2: x = reinterpret_cast<const uint16_t*>(vals)[j]; break;
-        case 1: x = vals[j]; break;
-        default: x = bit_at(vals, vbit0 + j); break;   // bool: bit-packed, same bit origin
+        case 4: x = gl(reinterpret_cast<const uint32_t*>(vals))[j]; break;
+        case 2: x = gl(reinterpret_cast<const uint16_t*>(vals))[j]; break;
+        case 1: x = gl(vals)[j]; break;
+        default: x = bit_at_g(vals, vbit0 + j); break;   // bool: bit-packed, same bit origin
       }
       word |= x << (8 * ew * t);
     }
@@ -832,7 +837,7 @@ __device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const
       slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
       cursor += rnd8(len);
     } else if (c.kind == kDecimal) {
-      const uint64_t* s = reinterpret_cast<const uint64_t*>(c.values) + 2 * r;
+      const auto s = gl(reinterpret_cast<const uint64_t*>(c.values)) + 2 * r;
       d64[cursor >> 3] = s[0];
       d64[(cursor >> 3) + 1] = s[1];
       slot = (static_cast<uint64_t>(cursor) << 32) | 16u;
@@ -872,16 +877,16 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    const bool ok = !c.validity || ((c.validity[r >> 3] >> (r & 7)) & 1);
+    const bool ok = !c.validity || bit_at_g(c.validity, r);
     valid |= static_cast<uint64_t>(ok) << k;
     uint64_t x = 0;
     switch (c.kind) {
       case kFixed: x = load_fixed(c.values, r, c.width); break;
-      case kBool: x = bit_at(c.values, r); break;
+      case kBool: x = bit_at_g(c.values, r); break;
       case kBytes:
       case kListFixed:
-        x = static_cast<uint32_t>(c.offsets[r]) |
-            (static_cast<uint64_t>(static_cast<uint32_t>(c.offsets[r + 1])) << 32);
+        x = static_cast<uint32_t>(gl(c.offsets)[r]) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(gl(c.offsets)[r + 1])) << 32);
         break;
       default: break;
     }
