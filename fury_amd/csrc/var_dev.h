@@ -1373,12 +1373,28 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   const bool live = tid < nr;
   const int64_t r = live ? r0 + tid : r0;
   const uint8_t* row = rows + offs[r];
-  const uint64_t* row64 = reinterpret_cast<const uint64_t*>(row);
-  // null word + slots: one batch of loads
-  const uint64_t nullw = live ? row64[0] : ~0ull;
+  // null word + slots: one batch of 16-byte loads of the aligned blocks covering them (rows are
+  // only 8-aligned; selecting words afterwards costs cndmasks, while 8-byte loads took 1 + K
+  // instructions, each touching one cache line per lane -- the vector memory pipeline's cost).
+  // Blocks past the header's last word are not loaded.
+  using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
+  constexpr int kNch = (K + 3) / 2;
+  const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
+  const int mis = static_cast<int>((ra >> 3) & 1);
+  const int need = (mis + K + 2) / 2;
+  const auto blk = gl(reinterpret_cast<const u64x2*>(ra & ~uintptr_t(15)));
+  uint64_t hw[2 * kNch];
+#pragma unroll
+  for (int c = 0; c < kNch; c++) {
+    u64x2 x = {0, 0};
+    if (c < need) x = blk[c];
+    hw[2 * c] = x.x;
+    hw[2 * c + 1] = x.y;
+  }
+  const uint64_t nullw = live ? (mis ? hw[1] : hw[0]) : ~0ull;
   uint64_t slot[K];
 #pragma unroll
-  for (int k = 0; k < K; k++) slot[k] = row64[1 + k];
+  for (int k = 0; k < K; k++) slot[k] = mis ? hw[k + 2] : hw[k + 1];
   // element counts of LIST fields (dependent load of the array header)
   uint32_t cnt[K];
 #pragma unroll
