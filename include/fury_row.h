@@ -242,7 +242,9 @@ int fury_device_status(void* stream);
  * padded LDS rows in the encode.  Results are bit-identical across variants.  Default 54
  * (tile + nt loads/stores + pair-mode deep decode).
  * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
- * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles.
+ * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles,
+ * 4 one-pass LDS-staged decode (var_lds.hip: tiles' row ranges staged by LDS-DMA; at most 32
+ * STRING / BINARY / LIST columns and 64 fields, else as 0).
  * Key "gen_decode" (nested schemas, fury_decode_prepare / _execute): 0 level-by-level engine
  * (a thread per Arrow entry of a node, levels.hip), 1 the thread-per-row interpreter
  * (generic.hip).  Results are identical.

@@ -65,6 +65,7 @@ def main():
     L.fury_set_tuning(b"var_decode", 0)
     nbytes = _nbytes(cols) + batch.rows.numel() + batch.row_offsets.numel() * 8
     res = {"workload": args.workload, "rows": n, "bytes": nbytes,
+           "env": {k: v for k, v in os.environ.items() if k.startswith("FURY_LDS_")},
            "us": {f"{m}:{d}": round(statistics.median(v), 1) for (m, d), v in times.items()}}
     print(json.dumps(res), flush=True)
 
