@@ -1279,6 +1279,72 @@ __device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq
   }
 }
 
+// Count (string bytes / list elements) of column k summed over the rows of tile j, by one wave,
+// straight from the rows: the aggregate tile j publishes, for a look-back that stopped waiting.
+template <int NT>
+__device__ int64_t tile_count(const VarArgs& a, int k, const uint8_t* rows, const int64_t* offs,
+                              int64_t j) {
+  const int lane = threadIdx.x & 63;
+  const VarCol& c = a.col[k];
+  int64_t sum = 0;
+  const int64_t i1 = min<int64_t>((j + 1) * NT, a.nrows);
+  for (int64_t i = j * NT + lane; i < i1; i += 64) {
+    const uint8_t* row = rows + gl(offs)[i];
+    if ((gl(row)[k >> 3] >> (k & 7)) & 1) continue;
+    const uint64_t slot = *gl(reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k));
+    if (c.kind == kBytes)
+      sum += static_cast<uint32_t>(slot);
+    else
+      sum += static_cast<uint32_t>(*gl(reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot >> 32))));
+  }
+  return wave_sum(sum);
+}
+
+// look_back_bounded for blockIdx-ordered tiles: when the nearest unpublished predecessor inside
+// the window has not published for kHelpSpins polls, the wave computes that tile's aggregate
+// itself (tile_count) and goes on, so the look-back finishes whatever the dispatch order.  The
+// helped values are exactly what the tile publishes later.  FURY_VAR_DBG bit 32768 helps at once
+// (exercises this path in the tests; results are identical).
+constexpr uint32_t kHelpSpins = 1u << 14;
+template <int NT>
+__device__ int64_t look_back_help(const VarArgs& a, int k, const uint8_t* rows,
+                                  const int64_t* offs, const uint64_t* status, int64_t b, int nseq,
+                                  int q, uint32_t* err) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t limit = (a.dbg & 32768) ? 0u : kHelpSpins;
+  int64_t excl = 0;
+  for (int64_t j = b - 1;; j -= 64) {
+    const int64_t idx = j - lane;
+    uint64_t v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
+    uint64_t inc;
+    int stop;
+    uint32_t spins = 0, helped = 0;
+    for (;;) {
+      inc = __ballot((v >> 62) == 2);
+      stop = inc ? __builtin_ctzll(inc) : 63;
+      const uint64_t upto = stop == 63 ? ~0ull : ((2ull << stop) - 1);
+      const uint64_t pend = __ballot((v >> 62) == 0) & upto;
+      if (pend == 0) break;
+      if (spins >= limit) {                      // help the nearest silent predecessor
+        const int l = __builtin_ctzll(pend);
+        const int64_t agg = tile_count<NT>(a, k, rows, offs, j - l);
+        if (lane == l) v = kAgg | static_cast<uint64_t>(agg);
+        spins = 0;
+        if (++helped > 64 && err) {              // cannot happen: at most 64 lanes to help
+          if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          return 0;
+        }
+        continue;
+      }
+      ++spins;
+      __builtin_amdgcn_s_sleep(1);
+      if ((v >> 62) == 0 && lane <= stop) v = ld_status(status + idx * nseq + q);
+    }
+    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
+    if (inc) return excl;
+  }
+}
+
 // Stores image bytes img[0, n) to g[0, n) (g any alignment, img 16-aligned LDS with >= 16 bytes
 // of readable padding past n): byte stores up to g's 16-byte boundary, then 16-B non-temporal
 // stores whose data is funnel-shifted out of aligned image words, then the byte tail.
@@ -1359,15 +1425,18 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   __shared__ int64_t sbase[K];
   __shared__ int64_t stile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // Tiles are numbered in the order workgroups START (a ticket), not by blockIdx: dispatch order
-  // is not guaranteed, and the look-back below only waits on tiles with smaller numbers, which
-  // therefore are already running -- every wait ends.  (FURY_VAR_DBG bit 4096: blockIdx order,
-  // for A/B only.)
-  if (!(a.dbg & 4096)) {
+  // Tile = blockIdx.  A ticket (tiles numbered in start order) made every look-back wait end by
+  // construction, but its one device-scope atomic per tile serialises at the cross-XCD coherence
+  // point (~12 ns each: the C4 decode's loads alone took 202 us with it, 83 us without).  Instead
+  // the look-back helps itself (look_back_help): a predecessor that has published nothing for a
+  // long time -- not dispatched yet, under any dispatch order -- has its aggregate computed from
+  // its rows by the waiting wave, so no wait depends on a workgroup that is not running.
+  // FURY_VAR_DBG bit 4096: the ticket (A/B).
+  if (a.dbg & 4096) {
     if (tid == 0) stile = atomicAdd(ticket, 1u);
     __syncthreads();
   }
-  const int64_t b = (a.dbg & 4096) ? static_cast<int64_t>(blockIdx.x) : stile, nb = gridDim.x;
+  const int64_t b = (a.dbg & 4096) ? stile : static_cast<int64_t>(blockIdx.x), nb = gridDim.x;
   const int64_t r0 = b * NT;
   const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
@@ -1579,7 +1648,8 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     for (int k = 0; k < K; k++) {
       if (!is_seq(a.col[k])) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0 : look_back_bounded(status, b, K, k, a.err);
+      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0
+                          : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err);
       if (lane == 0) {
         sbase[k] = pre;
         if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));

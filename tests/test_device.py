@@ -222,6 +222,21 @@ def test_var_decode_modes_bit_exact(oracle, dev, mode):
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
+@pytest.mark.parametrize("bits", ["32768", "4096"])
+def test_var_decode_tile_order_bit_exact(oracle, dev, bits, monkeypatch):
+    """The register-staged decode numbers tiles by blockIdx and lets a look-back compute a silent
+    predecessor's aggregate from its rows (look_back_help).  FURY_VAR_DBG 32768 makes every
+    look-back help at once -- the path a late-dispatched predecessor takes -- and 4096 restores
+    the ticket; both must decode to the oracle's columns."""
+    from fury_amd import _native as N
+    monkeypatch.setenv("FURY_VAR_DBG", bits)
+    for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
+                    ("nested", 4097), ("beanb", 700)):
+        _roundtrip(oracle, name, n, dev, seed=n + int(bits))
+    _roundtrip(oracle, "mixed", 3000, dev, seed=7, str_max=600)
+    assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
+
+
 def _walks():
     from fury_amd import _native as N
     return N.lib().fury_get_tuning(b"unframe_walks")
