@@ -230,7 +230,8 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
  * (on any stream of this process) could not produce a valid result -- a decoupled look-back of
  * the variable-length decode that gave up waiting -- and clears that state; FURY_OK otherwise.
  * Every entry point also reports such a failure (without synchronising) the next time it is
- * called.  By construction (ticket-ordered tiles) it is never raised on working hardware. */
+ * called.  By construction (a look-back computes a silent predecessor's aggregate itself) it is
+ * never raised on working hardware. */
 int fury_device_status(void* stream);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
