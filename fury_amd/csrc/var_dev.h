@@ -1285,7 +1285,7 @@ template <int NT>
 __device__ int64_t tile_count(const VarArgs& a, int k, const uint8_t* rows, const int64_t* offs,
                               int64_t j) {
   const int lane = threadIdx.x & 63;
-  const VarCol& c = a.col[k];
+  CVarCol& c = vc(a, k);
   int64_t sum = 0;
   const int64_t i1 = min<int64_t>((j + 1) * NT, a.nrows);
   for (int64_t i = j * NT + lane; i < i1; i += 64) {
@@ -1306,6 +1306,16 @@ __device__ int64_t tile_count(const VarArgs& a, int k, const uint8_t* rows, cons
 // helped values are exactly what the tile publishes later.  FURY_VAR_DBG bit 32768 helps at once
 // (exercises this path in the tests; results are identical).
 constexpr uint32_t kHelpSpins = 1u << 14;
+// Column index of the q-th STRING / BINARY / LIST column (the kernels' sequence numbering).
+__device__ __forceinline__ int seq_col(const VarArgs& a, int q) {
+  int seq = 0;
+  for (int k = 0; k < a.ncols; k++) {
+    if (!is_seq(vc(a, k))) continue;
+    if (seq++ == q) return k;
+  }
+  return 0;
+}
+
 template <int NT>
 __device__ int64_t look_back_help(const VarArgs& a, int k, const uint8_t* rows,
                                   const int64_t* offs, const uint64_t* status, int64_t b, int nseq,
@@ -1811,7 +1821,8 @@ __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row
 
 template <bool kLookBack>
 __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh, int cbase,
-                                              int nchunk, int64_t b, uint64_t* status, int nseq) {
+                                              int nchunk, int64_t b, uint64_t* status, int nseq,
+                                              const uint8_t* rows, const int64_t* offs) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (!kLookBack) {     // offsets precomputed by the sizing pass (fury_row_decode_measure)
     if (threadIdx.x < nchunk) {
@@ -1828,7 +1839,9 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
     return;
   }
   for (int q = w; q < nchunk; q += kThreads / 64) {
-    const int64_t ex = (b == 0 || (a.dbg & 32)) ? 0 : look_back(status, b, nseq, cbase + q);
+    const int64_t ex = (b == 0 || (a.dbg & 32)) ? 0
+                       : look_back_help<kThreads>(a, seq_col(a, cbase + q), rows, offs, status, b,
+                                                  nseq, cbase + q, a.err);
     if (lane == 0) {
       sh.base[q] = ex;
       if (b > 0)
@@ -1842,7 +1855,8 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
 template <bool kStaged, bool kLookBack>
 __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* src, uint8_t* oimg,
                                              DecodeShared& sh, int64_t b, int64_t nb, int nr,
-                                             uint64_t* status, int nseq) {
+                                             uint64_t* status, int nseq, const uint8_t* rows,
+                                             const int64_t* offs) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t r0 = b * kThreads;
   const int64_t r = r0 + tid;
@@ -1895,7 +1909,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
   for (int cbase = 0; cbase < nseq; cbase += kSeqChunk) {
     const int nchunk = min(kSeqChunk, nseq - cbase);
     if (cbase > 0 || !kLookBack) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
-    chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq);
+    chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq, rows, offs);
     int seq = 0;
     for (int k = 0; k < a.ncols; k++) {
       CVarCol& c = vc(a, k);
@@ -1987,11 +2001,13 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
   __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
   __shared__ DecodeShared sh;
-  if (kLookBack && !(a.dbg & 64)) {
+  // tile = blockIdx; the look-back helps itself (look_back_help), as in decode_var_reg.
+  // FURY_VAR_DBG bit 4096: a ticket (tiles numbered in start order), for A/B.
+  if (kLookBack && (a.dbg & 4096)) {
     if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
     __syncthreads();
   }
-  const int64_t b = (kLookBack && !(a.dbg & 64)) ? sh.blk : blockIdx.x;
+  const int64_t b = (kLookBack && (a.dbg & 4096)) ? sh.blk : static_cast<int64_t>(blockIdx.x);
   const int64_t r0 = b * kThreads;
   const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
   const int64_t rbeg = offs[r0];
@@ -2001,10 +2017,12 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
     uint32_t at = 0;
     const uint32_t d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
     __syncthreads();
-    decode_group<true, kLookBack>(a, stage + d0, oimg, sh, b, gridDim.x, nr, status, nseq);
+    decode_group<true, kLookBack>(a, stage + d0, oimg, sh, b, gridDim.x, nr, status, nseq, rows,
+                                  offs);
   } else {
     __syncthreads();
-    decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq);
+    decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq, rows,
+                                   offs);
   }
 }
 #endif  // FURY_VAR_MAIN

@@ -224,7 +224,7 @@ def test_var_decode_modes_bit_exact(oracle, dev, mode):
 
 @pytest.mark.parametrize("bits", ["32768", "4096"])
 def test_var_decode_tile_order_bit_exact(oracle, dev, bits, monkeypatch):
-    """The register-staged decode numbers tiles by blockIdx and lets a look-back compute a silent
+    """The variable-length decodes number tiles by blockIdx and let a look-back compute a silent
     predecessor's aggregate from its rows (look_back_help).  FURY_VAR_DBG 32768 makes every
     look-back help at once -- the path a late-dispatched predecessor takes -- and 4096 restores
     the ticket; both must decode to the oracle's columns."""
@@ -234,6 +234,10 @@ def test_var_decode_tile_order_bit_exact(oracle, dev, bits, monkeypatch):
                     ("nested", 4097), ("beanb", 700)):
         _roundtrip(oracle, name, n, dev, seed=n + int(bits))
     _roundtrip(oracle, "mixed", 3000, dev, seed=7, str_max=600)
+    for ncols, n in ((33, 2049), (17, 20_001)):    # the 17-256-field kernel (decode_var_kernel)
+        fields = _wide_fields(ncols)
+        host = gen_columns("wide", fields, n, seed=ncols, null_pct=10, str_max=40, list_max=8)
+        _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
@@ -788,7 +792,7 @@ def test_wide_var_schemas_bit_exact(oracle, dev, ncols, n, str_max):
 
 
 def test_wide_var_schema_large_batch(oracle, dev):
-    """A 40-field schema over 300k rows (>1,000 workgroups chained by the ticketed look-back)."""
+    """A 40-field schema over 300k rows (>1,000 workgroups chained by the look-back)."""
     fields = _wide_fields(40)
     n = 300_000
     host = gen_columns("wide", fields, n, seed=4, null_pct=10, str_max=20, list_max=6)
