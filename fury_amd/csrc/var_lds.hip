@@ -369,11 +369,15 @@ __global__ __launch_bounds__(NT) void decode_var_lds(VarArgs a, const uint8_t* _
   uint8_t* stage = reinterpret_cast<uint8_t*>(dyn) + static_cast<uint32_t>(nseq) * NT * 4;
   uint8_t* img = stage + stage_cap;
   const int tid = threadIdx.x;
-  if (!(a.dbg & 4096)) {      // DIAGNOSTIC bit 4096: blockIdx order (A/B of the ticket's cost)
+  // tiles numbered by a ticket (start order), so every look-back wait ends; blockIdx order
+  // (FURY_VAR_DBG 4096 | 128 with FURY_DIAGNOSTIC=1) is for timing only: this kernel's look-back
+  // does not help itself
+  const bool order = (a.dbg & 4096) && (a.dbg & 128);
+  if (!order) {
     if (tid == 0) sh.tile = atomicAdd(ticket, 1u);
     __syncthreads();
   }
-  const int64_t b = (a.dbg & 4096) ? static_cast<int64_t>(blockIdx.x) : sh.tile, nb = gridDim.x;
+  const int64_t b = order ? static_cast<int64_t>(blockIdx.x) : sh.tile, nb = gridDim.x;
   const int64_t r0 = b * NT;
   const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
