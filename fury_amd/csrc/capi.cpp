@@ -345,14 +345,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     a->tile_rows = encode_tile_rows(*a);
   }
   a->err = device_error_word();
-  // FURY_VAR_DBG selects kernel variants for A/B (bits 512 / 1024 / 2048: all correct).  Bits
-  // 1-64 switch phases OFF for timing (scripts/diag_var.py) and leave wrong outputs, so they
-  // are honoured only with FURY_DIAGNOSTIC=1.
-  if (const char* e = getenv("FURY_VAR_DBG")) {
-    a->dbg = atoi(e);
-    const char* d = getenv("FURY_DIAGNOSTIC");
-    if (!d || std::string(d) != "1") a->dbg &= ~255;
-  }
+  a->help_now = lookback_help_mode();
   return FURY_OK;
 }
 
@@ -617,57 +610,12 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   p->offs = row_offsets;
   p->nrows = nrows;
   std::vector<int64_t> totals(2 * nn, 0);
-  if (nrows > 0 && gen_decode_mode() == 0) {
+  if (nrows > 0) {
     const int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
     if (st) {
       delete p;
       return st;
     }
-  } else if (nrows > 0) {
-    // Count pass: the column tree is not needed (null columns everywhere).
-    std::vector<fury_column> dummy(nn);
-    std::vector<fury_column> top(s->num_fields);
-    GenArgs g{};
-    g.nnodes = nn;
-    g.ntop = s->num_fields;
-    g.nrows = nrows;
-    g.root = s->root;
-    const bool wide = nn > kGenMaxNodes;
-    std::vector<GenNode> tab(wide ? nn : 0);
-    GenNode* nodes = wide ? tab.data() : g.node;
-    for (int i = 0; i < nn; i++) {
-      nodes[i].type = s->nodes[i].type_id;
-      nodes[i].first_child = s->nodes[i].first_child;
-      nodes[i].num_children = s->nodes[i].num_children;
-    }
-    DeviceTable dt;
-    if (wide) {
-      const int st0 = upload_table(tab.data(), tab.size() * sizeof(GenNode), hs, &dt);
-      if (st0) { delete p; return st0; }
-      g.tab = static_cast<const GenNode*>(dt.dev);
-    }
-    const int64_t cells = 2 * static_cast<int64_t>(nn) * nrows;
-    int64_t* dev = nullptr;
-    // [counts cells][totals 2 nn][scan workspace][wide schemas: cursor scratch cells]
-    const int64_t words = cells + 2 * nn + scan_workspace(cells) + 2 * nn + 1 + (wide ? cells : 0);
-    // stream-ordered pool memory: a hipMalloc / hipFree pair of this size per call cost
-    // milliseconds (hipFree synchronises the device), more than the count pass itself
-    int device = 0;
-    (void)hipGetDevice(&device);
-    keep_pool(device);
-    int st = dev_alloc(words * 8, hs, reinterpret_cast<void**>(&dev));
-    if (st) { delete p; return st; }
-    p->cnt = dev;
-    p->cnt_stream = hs;
-    p->scratch = wide ? dev + (words - cells) : nullptr;
-    st = launch_gen_count(g, p->rows, row_offsets, dev, hs);
-    int64_t* tot = dev + cells;
-    int64_t* ws = tot + 2 * nn;
-    if (!st) st = device_scan_batched(dev, 2 * nn, nrows, tot, ws, hs);
-    if (!st) st = check_hip(hipMemcpyAsync(totals.data(), tot, 2 * nn * 8, hipMemcpyDeviceToHost, hs),
-                            "hipMemcpyAsync");
-    if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
-    if (st) { fury_decode_plan_destroy(p); return st; }
   }
   for (int i = 0; i < nn; i++) {
     if (node_entries) node_entries[i] = totals[2 * i];
@@ -692,16 +640,12 @@ int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, v
         st = check_hip(hipMemsetAsync(nodes[i].offsets, 0, 4, hs), "hipMemsetAsync offsets");
     return st;
   }
-  if (p->lv) {
-    const GenNode* outs = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
-    return lv_execute(p->lv, outs, p->rows, p->offs, hs);
-  }
-  return launch_gen_decode(g, p->rows, p->offs, p->cnt, p->scratch, hs);
+  const GenNode* outs = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
+  return lv_execute(p->lv, outs, p->rows, p->offs, hs);
 }
 
 void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
-  if (p->cnt) dev_free(p->cnt, static_cast<hipStream_t>(p->cnt_stream));
   if (p->lv) lv_free(p->lv);
   if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
   if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
@@ -717,20 +661,9 @@ int fury_device_status(void* stream) {
 
 int fury_set_tuning(const char* key, int32_t value) {
   if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
-  if (std::string(key) == "fixed_variant") {
-    if (value < 0 || value > 1023)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_variant: 0..1023");
-    set_fixed_variant(value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "var_decode") {
-    if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_decode: 0..4");
-    set_var_decode_mode(value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "gen_decode") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "gen_decode: 0..1");
-    set_gen_decode_mode(value);
+  if (std::string(key) == "lookback_help") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "lookback_help: 0..1");
+    set_lookback_help_mode(value);
     return FURY_OK;
   }
   if (std::string(key) == "unframe") {
@@ -742,14 +675,12 @@ int fury_set_tuning(const char* key, int32_t value) {
 }
 
 int32_t fury_get_tuning(const char* key) {
-  if (key && std::string(key) == "fixed_variant") return fixed_variant();
-  if (key && std::string(key) == "var_decode") return var_decode_mode();
+  if (key && std::string(key) == "lookback_help") return lookback_help_mode();
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "lookback_timeouts")
     return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")
     return static_cast<int32_t>(unframe_walk_count());
-  if (key && std::string(key) == "gen_decode") return gen_decode_mode();
   if (key && std::string(key) == "host_direct")
     return static_cast<int32_t>(host_direct_count());
   if (key && std::string(key) == "unframe_repairs")

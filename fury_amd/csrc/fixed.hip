@@ -85,16 +85,6 @@ __device__ __forceinline__ CFixedCol& fcol(const FixedArgs& a, int c) {
   return base[c];
 }
 
-// Tile of workgroup b.  Workgroups are dealt round-robin to the 8 XCDs (b % 8); tile_order 1
-// gives each XCD one contiguous eighth of the tiles (b -> (b % 8) * (nb / 8) + b / 8 on the
-// largest multiple of 8, identity on the tail), so an XCD's L2 and TLB see one address range.
-__device__ __forceinline__ int64_t tile_of(const FixedArgs& a) {
-  const int64_t b = blockIdx.x, nb = gridDim.x;
-  if (!a.tile_order) return b;
-  const int64_t q = nb >> 3;
-  return b < 8 * q ? (b & 7) * q + (b >> 3) : b;
-}
-
 // Global access helpers; NT bit 0 = non-temporal loads, bit 1 = non-temporal stores (streamed
 // bytes are touched once, so keeping them out of L2/MALL leaves room for the other stream).
 using v4u = __attribute__((ext_vector_type(4))) uint32_t;
@@ -165,62 +155,20 @@ __device__ __forceinline__ void copy_tile(uint8_t* __restrict__ g, uint8_t* __re
   }
 }
 
-// LDS row stride of the padded encode: an odd number of 8-B words.
-__host__ __device__ __forceinline__ int lds_row_stride(int rs) { return ((rs >> 3) & 1) ? rs : rs + 8; }
-
-// Row tile LDS -> global.  Unpadded: one contiguous copy.  Padded (LDS row stride ls != rs):
-// each lane's 16-B output chunk is read as two 8-B words from their padded LDS rows; the chunk's
-// (row, offset) advances incrementally by the loop stride, so there is no division per chunk.
-template <int NT, int DS, bool PAD>
-__device__ __forceinline__ void store_tile(uint8_t* __restrict__ g, uint8_t* __restrict__ lds,
-                                           int nr, int rs, int ls) {
-  const int64_t bytes = static_cast<int64_t>(nr) * rs;
-  if (!PAD || ls == rs) {
-    copy_tile<true, NT, DS>(g, lds, bytes);
-    return;
-  }
-  const int n16 = static_cast<int>(bytes >> 4);
-  constexpr int kStep = 16 * kThreads;
-  const int q = kStep / rs, rm = kStep - q * rs;
-  int o = 16 * threadIdx.x;
-  int row = o / rs, w = o - row * rs;
-  for (int i = threadIdx.x; i < n16; i += kThreads) {
-    const uint64_t lo = *reinterpret_cast<const uint64_t*>(lds + row * ls + w);
-    int row2 = row, w2 = w + 8;
-    if (w2 >= rs) { w2 -= rs; row2++; }
-    const uint64_t hi = *reinterpret_cast<const uint64_t*>(lds + row2 * ls + w2);
-    st16<NT>(g + 16 * static_cast<int64_t>(i),
-             v4u{static_cast<uint32_t>(lo), static_cast<uint32_t>(lo >> 32),
-                 static_cast<uint32_t>(hi), static_cast<uint32_t>(hi >> 32)});
-    row += q;
-    w += rm;
-    if (w >= rs) { w -= rs; row++; }
-  }
-  if ((bytes & 15) && threadIdx.x == 0) {       // a last 8-B word (rs % 16 == 8, nr odd)
-    const int64_t o8 = static_cast<int64_t>(n16) << 4;
-    const int r8 = static_cast<int>(o8 / rs);
-    *reinterpret_cast<uint64_t*>(g + o8) =
-        *reinterpret_cast<const uint64_t*>(lds + r8 * ls + (o8 - static_cast<int64_t>(r8) * rs));
-  }
-}
-
 // kFast: every column is 8 bytes wide and no column carries validity.
 // U = column loads per lane in flight in the gather (8 default, 16 "deep"); P = pair mode
 // (fast path only): a lane moves rows 2q and 2q + 1 of one column with ONE 16-B load, so a
 // wave-instruction covers 128 rows (R >= 128) or two columns x 64 rows (R = 64).
-// PAD: LDS rows are laid out with an odd number of 8-B words (row size + 8 when row_size / 8 is
-// even) so the 64 lanes of a column write hit 64 distinct LDS banks; the copy-out then maps
-// each 16-B output chunk back to its padded LDS address.
-template <int R, bool kFast, int NT, int U = kUnroll, int DS = 4, bool P = false, bool PAD = false>
+template <int R, bool kFast, int NT, int U = kUnroll, int DS = 4, bool P = false>
 __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
                                                                  uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t r0 = tile_of(a) * R;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
   const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
   const int bw = bm >> 3;
-  const int ls = PAD ? lds_row_stride(rs) : rs;     // LDS bytes per row
+  const int ls = rs;                                // LDS bytes per row
 
   // BinaryRowWriter.reset(): zero the bitmap words of every row of the tile.
   for (int i = threadIdx.x; i < R * bw; i += kThreads) {
@@ -267,7 +215,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
       }
     }
     __syncthreads();
-    store_tile<NT, DS, PAD>(rows + r0 * rs, lds, nr, rs, ls);
+    copy_tile<true, NT, DS>(rows + r0 * rs, lds, static_cast<int64_t>(nr) * rs);
     return;
   }
 
@@ -313,7 +261,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
     }
   }
   __syncthreads();
-  store_tile<NT, DS, PAD>(rows + r0 * rs, lds, nr, rs, ls);
+  copy_tile<true, NT, DS>(rows + r0 * rs, lds, static_cast<int64_t>(nr) * rs);
 }
 
 // D = 16-B row-tile loads per lane in flight (4 default, 16 "deep": the whole 64-row Struct-100
@@ -322,7 +270,7 @@ template <int R, bool kFast, int NT, int D = 4, bool P = false>
 __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
                                                                  const uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int64_t r0 = tile_of(a) * R;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
   const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
   const int rs = a.row_size;
   const int bm = a.bitmap_bytes;
@@ -401,179 +349,15 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
   }
 }
 
-// ---- pipelined persistent variants (fast path: all 8-byte columns, no validity) ------------
-// One workgroup walks tiles blockIdx.x, +gridDim.x, ...; while tile t's LDS image streams out to
-// HBM, tile t+1's global loads are already in flight (register staging).  Barriers only order
-// LDS (lgkmcnt(0) + s_barrier): no vmcnt(0) drain, so the prefetch survives them.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-template <int MAXU, int NT>
-__global__ __launch_bounds__(kThreads) void encode_fixed_pipe(FixedArgs a,
-                                                              uint8_t* __restrict__ rows,
-                                                              int64_t ntiles) {
-  constexpr int R = 64;   // lane == row of the tile; wave w owns columns w, w+4, ...
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  const int rs = a.row_size;
-  const int bm = a.bitmap_bytes;
-  const int bw = bm >> 3;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ncols = a.ncols;
-  for (int i = threadIdx.x; i < R * bw; i += kThreads) {
-    const int r = i / bw, w = i - r * bw;
-    *reinterpret_cast<uint64_t*>(lds + r * rs + 8 * w) = 0;   // never nulls on this path
-  }
-  // Column pointers are loop invariant and wave uniform: load them once into SGPRs (the
-  // record table always has kMaxFixedCols entries, so reading past ncols is in bounds).
-  static_assert(4 * MAXU <= kMaxFixedCols, "column table");
-  const uint8_t* p[MAXU];
-#pragma unroll
-  for (int u = 0; u < MAXU; u++) p[u] = a.col[wid + 4 * u].values;
-  uint64_t v[MAXU];
-  int64_t tile = blockIdx.x;
-  auto load = [&](int64_t t) {
-    const int64_t row = t * R + lane;
-    const bool ok = row < a.nrows;
-#pragma unroll
-    for (int u = 0; u < MAXU; u++) {
-      const int c = wid + 4 * u;
-      if (c < ncols && ok) v[u] = ld8<NT>(p[u] + row * 8);
-    }
-  };
-  if (tile < ntiles) load(tile);
-  while (tile < ntiles) {
-    const int64_t r0 = tile * R;
-    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
-#pragma unroll
-    for (int u = 0; u < MAXU; u++) {
-      const int c = wid + 4 * u;
-      if (c < ncols && lane < nr) *reinterpret_cast<uint64_t*>(lds + lane * rs + bm + 8 * c) = v[u];
-    }
-    lds_barrier();
-    const int64_t next = tile + gridDim.x;
-    if (next < ntiles) load(next);
-    const int64_t bytes = static_cast<int64_t>(nr) * rs;
-    uint8_t* g = rows + r0 * rs;
-    const int n16 = static_cast<int>(bytes >> 4);
-    for (int i = threadIdx.x; i < n16; i += kThreads)
-      st16<NT>(g + 16 * i, *reinterpret_cast<const v4*>(lds + 16 * i));
-    if ((bytes & 15) && threadIdx.x == 0)
-      *reinterpret_cast<uint64_t*>(g + 16 * n16) = *reinterpret_cast<const uint64_t*>(lds + 16 * n16);
-    lds_barrier();
-    tile = next;
-  }
-}
-
-template <int MAXL, int NT>
-__global__ __launch_bounds__(kThreads) void decode_fixed_pipe(FixedArgs a,
-                                                              const uint8_t* __restrict__ rows,
-                                                              int64_t ntiles) {
-  constexpr int R = 64;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
-  const int rs = a.row_size;
-  const int bm = a.bitmap_bytes;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ncols = a.ncols;
-  const uint8_t* q[32];
-#pragma unroll
-  for (int u = 0; u < 32; u++) q[u] = a.col[wid + 4 * u].values;
-  v4 t16[MAXL];
-  int64_t tile = blockIdx.x;
-  auto load = [&](int64_t t) {
-    const int64_t r0 = t * R;
-    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
-    const int n16 = (nr * rs) >> 4;
-    const v4* g = reinterpret_cast<const v4*>(rows + r0 * rs);
-#pragma unroll
-    for (int k = 0; k < MAXL; k++) {
-      const int i = threadIdx.x + k * kThreads;
-      if (i < n16) t16[k] = ld16<NT>(reinterpret_cast<const uint8_t*>(g + i));
-    }
-  };
-  if (tile < ntiles) load(tile);
-  while (tile < ntiles) {
-    const int64_t r0 = tile * R;
-    const int nr = static_cast<int>(min(static_cast<int64_t>(R), a.nrows - r0));
-    const int64_t bytes = static_cast<int64_t>(nr) * rs;
-    const int n16 = static_cast<int>(bytes >> 4);
-#pragma unroll
-    for (int k = 0; k < MAXL; k++) {
-      const int i = threadIdx.x + k * kThreads;
-      if (i < n16) *reinterpret_cast<v4*>(lds + 16 * i) = t16[k];
-    }
-    if ((bytes & 15) && threadIdx.x == 0)
-      *reinterpret_cast<uint64_t*>(lds + 16 * n16) =
-          *reinterpret_cast<const uint64_t*>(rows + r0 * rs + 16 * n16);
-    lds_barrier();
-    const int64_t next = tile + gridDim.x;
-    if (next < ntiles) load(next);
-    const int64_t row = r0 + lane;
-    if (lane < nr) {
-#pragma unroll
-      for (int u = 0; u < 32; u++) {
-        const int c = wid + 4 * u;
-        if (c < ncols) {
-          const uint64_t x = *reinterpret_cast<const uint64_t*>(lds + lane * rs + bm + 8 * c);
-          uint64_t* dst = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(q[u])) + row;
-          st8<NT>(reinterpret_cast<uint8_t*>(dst), x);
-        }
-      }
-    }
-    lds_barrier();
-    tile = next;
-  }
-}
-
 }  // namespace
 
-// Kernel variant for fixed-width fast-path schemas (fury_set_tuning("fixed_variant", v) or env
-// FURY_FIXED_VARIANT), a bit set: 1 = pipelined persistent kernel, 2 = nt stores, 4 = nt loads.
-static int g_variant = -1;
-static thread_local int t_variant = -1;      // the calling thread's override (host direct path)
-
-int fixed_variant() {
-  if (t_variant >= 0) return t_variant;
-  if (g_variant < 0) {
-    const char* e = getenv("FURY_FIXED_VARIANT");
-    // tile kernel + nt loads + nt stores + pair-mode deep decode (A/B: profiles/r01_ab_fixed*.json)
-    g_variant = e ? atoi(e) : 54;
-  }
-  return g_variant;
-}
-
-void set_fixed_variant(int v) { g_variant = v; }
-void set_thread_fixed_variant(int v) { t_variant = v; }
+// Host-direct mode of the calling thread (hostpath.cpp): the kernels run on pinned host memory
+// over PCIe, where plain loads / stores measured faster than non-temporal ones (95 / 89 vs
+// 92 / 88 GB/s encode / decode, profiles/r02_host_direct.json).
+static thread_local bool t_host_direct = false;
+void set_thread_host_direct(bool on) { t_host_direct = on; }
 
 namespace {
-
-template <typename K>
-int launch_pipe(K kernel, int row_size, int64_t nrows, hipStream_t stream, const FixedArgs& a,
-                uint8_t* rows) {
-  const size_t lds = static_cast<size_t>(64) * row_size;
-  if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(lds));
-    if (e != hipSuccess) return check_hip(e, "hipFuncSetAttribute");
-  }
-  const int64_t ntiles = (nrows + 63) / 64;
-  int dev = 0, cus = 256, per_cu = 0;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel),
-                                                     kThreads, lds);
-  if (per_cu < 1) per_cu = 1;
-  const int64_t cap = static_cast<int64_t>(cus) * per_cu;
-  const int64_t grid = ntiles < cap ? ntiles : cap;
-  hipLaunchKernelGGL(kernel, dim3(static_cast<unsigned>(grid)), dim3(kThreads), lds, stream, a,
-                     rows, ntiles);
-  return check_hip(hipGetLastError(), "fixed pipelined kernel launch");
-}
 
 int pick_rows_per_tile(int row_size) {
   if (row_size * 256 <= 48 * 1024) return 256;
@@ -583,8 +367,8 @@ int pick_rows_per_tile(int row_size) {
 
 template <typename K>
 int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t stream,
-                       const FixedArgs& a, uint8_t* rows, int lds_row = 0) {
-  const size_t lds = static_cast<size_t>(R) * (lds_row ? lds_row : row_size);
+                       const FixedArgs& a, uint8_t* rows) {
+  const size_t lds = static_cast<size_t>(R) * row_size;
   static_assert(sizeof(FixedArgs) < 4096, "kernel argument block too large");
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
@@ -599,93 +383,37 @@ int launch_tile_kernel(K kernel, int R, int row_size, int64_t nrows, hipStream_t
   return check_hip(hipGetLastError(), "fixed kernel launch");
 }
 
-// Fast-path tile kernels (nt loads + stores) with the variant bits 3 (deep encode gather: 16
-// column loads per lane in flight), 4 (pair mode: 16-B column accesses) and 5 (deep decode:
-// 16 tile loads per lane in flight).
-template <int R, bool kEnc, bool P>
-int launch_fast_tile(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool deep, bool pad) {
-  const int ls = lds_row_stride(a.row_size);
-  if (kEnc) {
-    if (pad)
-      return deep ? launch_tile_kernel(encode_fixed_kernel<R, true, 3, 16, 4, P, true>, R,
-                                       a.row_size, a.nrows, stream, a, rows, ls)
-                  : launch_tile_kernel(encode_fixed_kernel<R, true, 3, 8, 4, P, true>, R,
-                                       a.row_size, a.nrows, stream, a, rows, ls);
-    return deep ? launch_tile_kernel(encode_fixed_kernel<R, true, 3, 16, 4, P>, R, a.row_size,
-                                     a.nrows, stream, a, rows)
-                : launch_tile_kernel(encode_fixed_kernel<R, true, 3, 8, 4, P>, R, a.row_size,
-                                     a.nrows, stream, a, rows);
-  }
-  return deep ? launch_tile_kernel(decode_fixed_kernel<R, true, 3, 16, P>, R, a.row_size, a.nrows,
-                                   stream, a, rows)
-              : launch_tile_kernel(decode_fixed_kernel<R, true, 3, 4, P>, R, a.row_size, a.nrows,
-                                   stream, a, rows);
-}
-
-template <bool kEnc>
-int launch_fast_tile_variant(const FixedArgs& a0, uint8_t* rows, hipStream_t stream, int var) {
-  FixedArgs a = a0;
-  a.tile_order = (var & 512) ? 1 : 0;          // bit 9: XCD-contiguous tile ranges
-  int R = pick_rows_per_tile(a.row_size);
-  // bit 8: tall tiles (twice the rows: longer contiguous column runs, fewer workgroups per CU)
-  if ((var & 256) && R < 256 && static_cast<int64_t>(2 * R) * a.row_size <= 160 * 1024) R *= 2;
-  const bool deep = (var & (kEnc ? 8 : 32)) != 0;
-  const bool pad = kEnc && (var & 128) != 0;
-  // pad only where it fits the LDS budget of the unpadded tile's occupancy class
-  const bool pad_ok = pad && static_cast<int64_t>(R) * lds_row_stride(a.row_size) <= 64 * 1024;
-  bool pair = (var & (kEnc ? 64 : 16)) != 0;
-  for (int c = 0; c < a.ncols && pair; c++)       // 16-B column accesses need 16-B aligned columns
-    pair = (reinterpret_cast<uintptr_t>(a.col[c].values) & 15) == 0;
-#define FURY_FT(RR)                                                              \
-  if (R == RR)                                                                   \
-    return pair ? launch_fast_tile<RR, kEnc, true>(a, rows, stream, deep, pad_ok) \
-                : launch_fast_tile<RR, kEnc, false>(a, rows, stream, deep, pad_ok);
-  FURY_FT(256)
-  FURY_FT(128)
-  FURY_FT(64)
-#undef FURY_FT
-  return set_error(FURY_ERR_UNSUPPORTED, "row size");
+// 16-B column accesses of the pair mode need 16-B aligned columns.
+bool pair_ok(const FixedArgs& a) {
+  for (int c = 0; c < a.ncols; c++)
+    if (reinterpret_cast<uintptr_t>(a.col[c].values) & 15) return false;
+  return true;
 }
 
 }  // namespace
 
-// Variant bits (fury_set_tuning("fixed_variant")): bit 0 = pipelined persistent kernel,
-// bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode gather, bit 4 =
-// pair-mode decode, bit 5 = deep decode loads, bit 6 = pair-mode encode, bit 7 = padded LDS rows
-// in the encode, bit 8 = tall tiles (bits 3-8 with nt loads + stores only).  A column-strip
-// encode (a workgroup per 256 rows x 20 columns: 2 KB contiguous column reads, 160-B strided row
-// strips written) measured 2.77 vs 5.80 TB/s in one process and was removed: partial-row
-// writes cost far more than the longer reads gain.  Only the fast path (8-byte columns,
-// no validity) has variants; the general path always runs the tile kernel.
+// Kernel choice (round-1/2 A/B sweeps, profiles/r01_ab_fixed*.json, r02_host_direct*.json; the
+// measured-slower pipelined persistent kernels, padded LDS rows, deep encode gather, pair-mode
+// encode and XCD-contiguous tile order were removed in round 3):
+//   fast path (8-byte columns, no validity): non-temporal loads + stores; the encode gathers 8
+//     column loads per lane; the decode keeps the whole tile in flight (16 loads per lane) and
+//     stores pairs of rows as 16-B column accesses;
+//   general path (narrow types, validity, > 128 fields): the same tile kernels with per-column
+//     width / validity handling;
+//   host-direct calls: plain loads / stores (see t_host_direct).
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
-  const int var = fixed_variant();
-  const int nt = ((var >> 2) & 1) | (var & 2);          // NT bit0 loads, bit1 stores
-  if (fast && (var & 1) && a.ncols <= 128) {
-    switch (nt) {
-      case 1: return launch_pipe(encode_fixed_pipe<32, 1>, a.row_size, a.nrows, stream, a, rows);
-      case 2: return launch_pipe(encode_fixed_pipe<32, 2>, a.row_size, a.nrows, stream, a, rows);
-      case 3: return launch_pipe(encode_fixed_pipe<32, 3>, a.row_size, a.nrows, stream, a, rows);
-      default: return launch_pipe(encode_fixed_pipe<32, 0>, a.row_size, a.nrows, stream, a, rows);
-    }
-  }
-  if (fast && (var & 1016) && nt == 3) return launch_fast_tile_variant<true>(a, rows, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                          \
   if (R == RR) {                                                                              \
     if (!fast)                                                                                \
       return launch_tile_kernel(encode_fixed_kernel<RR, false, 0>, RR, a.row_size, a.nrows,   \
                                 stream, a, rows);                                             \
-    switch (nt) {                                                                             \
-      case 1: return launch_tile_kernel(encode_fixed_kernel<RR, true, 1>, RR, a.row_size,     \
-                                        a.nrows, stream, a, rows);                            \
-      case 2: return launch_tile_kernel(encode_fixed_kernel<RR, true, 2>, RR, a.row_size,     \
-                                        a.nrows, stream, a, rows);                            \
-      case 3: return launch_tile_kernel(encode_fixed_kernel<RR, true, 3>, RR, a.row_size,     \
-                                        a.nrows, stream, a, rows);                            \
-      default: return launch_tile_kernel(encode_fixed_kernel<RR, true, 0>, RR, a.row_size,    \
-                                         a.nrows, stream, a, rows);                           \
-    }                                                                                         \
+    if (t_host_direct)                                                                        \
+      return launch_tile_kernel(encode_fixed_kernel<RR, true, 0>, RR, a.row_size, a.nrows,    \
+                                stream, a, rows);                                             \
+    return launch_tile_kernel(encode_fixed_kernel<RR, true, 3>, RR, a.row_size, a.nrows,      \
+                              stream, a, rows);                                               \
   }
   FURY_ENC(256)
   FURY_ENC(128)
@@ -697,42 +425,20 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
 int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
   uint8_t* r = const_cast<uint8_t*>(rows);
-  const int var = fixed_variant();
-  const int nt = ((var >> 2) & 1) | (var & 2);
-  const int64_t tile_bytes = static_cast<int64_t>(a.row_size) * 64;
-  if (fast && (var & 1) && tile_bytes <= 17 * 16 * kThreads) {
-    if (tile_bytes <= 13 * 16 * kThreads) {
-      switch (nt) {
-        case 1: return launch_pipe(decode_fixed_pipe<13, 1>, a.row_size, a.nrows, stream, a, r);
-        case 2: return launch_pipe(decode_fixed_pipe<13, 2>, a.row_size, a.nrows, stream, a, r);
-        case 3: return launch_pipe(decode_fixed_pipe<13, 3>, a.row_size, a.nrows, stream, a, r);
-        default: return launch_pipe(decode_fixed_pipe<13, 0>, a.row_size, a.nrows, stream, a, r);
-      }
-    }
-    switch (nt) {
-      case 1: return launch_pipe(decode_fixed_pipe<17, 1>, a.row_size, a.nrows, stream, a, r);
-      case 2: return launch_pipe(decode_fixed_pipe<17, 2>, a.row_size, a.nrows, stream, a, r);
-      case 3: return launch_pipe(decode_fixed_pipe<17, 3>, a.row_size, a.nrows, stream, a, r);
-      default: return launch_pipe(decode_fixed_pipe<17, 0>, a.row_size, a.nrows, stream, a, r);
-    }
-  }
-  if (fast && (var & 1016) && nt == 3) return launch_fast_tile_variant<false>(a, r, stream, var);
   const int R = pick_rows_per_tile(a.row_size);
+  const bool pair = fast && !t_host_direct && pair_ok(a);
 #define FURY_DEC(RR)                                                                          \
   if (R == RR) {                                                                              \
     if (!fast)                                                                                \
       return launch_tile_kernel(decode_fixed_kernel<RR, false, 0>, RR, a.row_size, a.nrows,   \
                                 stream, a, r);                                                \
-    switch (nt) {                                                                             \
-      case 1: return launch_tile_kernel(decode_fixed_kernel<RR, true, 1>, RR, a.row_size,     \
-                                        a.nrows, stream, a, r);                               \
-      case 2: return launch_tile_kernel(decode_fixed_kernel<RR, true, 2>, RR, a.row_size,     \
-                                        a.nrows, stream, a, r);                               \
-      case 3: return launch_tile_kernel(decode_fixed_kernel<RR, true, 3>, RR, a.row_size,     \
-                                        a.nrows, stream, a, r);                               \
-      default: return launch_tile_kernel(decode_fixed_kernel<RR, true, 0>, RR, a.row_size,    \
-                                         a.nrows, stream, a, r);                              \
-    }                                                                                         \
+    if (t_host_direct)                                                                        \
+      return launch_tile_kernel(decode_fixed_kernel<RR, true, 0>, RR, a.row_size, a.nrows,    \
+                                stream, a, r);                                                \
+    return pair ? launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, true>, RR,          \
+                                     a.row_size, a.nrows, stream, a, r)                       \
+                : launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, false>, RR,         \
+                                     a.row_size, a.nrows, stream, a, r);                      \
   }
   FURY_DEC(256)
   FURY_DEC(128)

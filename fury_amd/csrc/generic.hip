@@ -16,11 +16,9 @@
 //
 // MI355X design: the flattened schema and the per-call column pointers travel in the kernel
 // argument block (scalar-loaded).  Encode is one thread per row (measure pass -> device scan ->
-// build pass).  Decode counts, per row and per schema node, the Arrow entries and payload bytes
-// the row contributes; device scans turn those into each row's starting positions in every
-// output buffer, and a second thread-per-row pass writes them.  Validity bits go through 32-bit
-// atomics on buffers the host zeroes; everything else is plain stores into disjoint ranges.
-// Recursion is depth-unrolled (template<int D>), at most kMaxDepth levels of nesting.
+// build pass).  Recursion is depth-unrolled (template<int D>), at most kMaxDepth levels of
+// nesting.  Decode is levels.hip (level by level, a thread per Arrow entry); the round-1/2
+// thread-per-row decode interpreter that lived here was removed in round 3.
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -34,7 +32,6 @@ namespace fury {
 
 namespace {
 
-constexpr int kThreads = 64;          // decode keeps per-thread node counters in LDS
 constexpr int kEncThreads = 256;
 
 __device__ __forceinline__ bool gbit(const uint8_t* bits, int64_t i) {
@@ -335,270 +332,6 @@ __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
   if (r < g.nrows && offs[r + 1] <= cap) put_row<true, kRoot>(nodes, g.ntop, r, rows + offs[r]);
 }
 
-// ---- decode ----------------------------------------------------------------------------------
-// Per thread, per node: running Arrow entry index and payload byte position -- in LDS (stride 1,
-// bytes after the nnodes entries), or, for schemas wider than the LDS budget, in the plan's
-// per-(node, row) count array itself (stride 2 * nrows: the row's own slots).
-struct Cursors {
-  int64_t* base;
-  int64_t sn;        // stride between nodes
-  int64_t ob;        // offset of the byte cursors
-  uint64_t* vmask;   // row-aligned nodes: validity bit of this row's entry, by node index
-  uint64_t* bmask;   // row-aligned BOOL nodes: value bit of this row's entry
-  __device__ __forceinline__ int64_t& e(int ni) const { return base[ni * sn]; }
-  __device__ __forceinline__ int64_t& b(int ni) const { return base[ni * sn + ob]; }
-};
-
-template <int D, bool W>
-__device__ void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
-                          int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
-                          int64_t ordinal, Cursors cur);
-
-// Elements of a BinaryArray at `arr` into node ei's Arrow column (m entries).
-template <int D, bool W>
-__device__ void get_array(const GenNode* nodes, int ei, const uint8_t* arr, int64_t m, Cursors cur) {
-  const GenNode& e = nodes[ei];
-  const int w = gwidth(e.type);
-  const int es = w > 0 ? w : 8;
-  const int64_t hb = 8 + gbm(m);
-  for (int64_t j = 0; j < m; j++)
-    get_value<D + 1, W>(nodes, ei, true, arr, hb + j * es, es, true, arr + 8, j, cur);
-}
-
-// A null (or absent) entry for node ni and, for structs, one null entry in every child.
-template <int D, bool W>
-__device__ void null_entry(const GenNode* nodes, int ni, Cursors cur) {
-  if constexpr (D >= kGenMaxDepth) {
-    return;
-  } else {
-    const GenNode& n = nodes[ni];
-    const int64_t e = cur.e(ni)++;
-    if (W) {
-      const int w = gwidth(n.type);
-      if (w > 0 && n.type != FURY_TYPE_BOOL && n.values) {
-        uint8_t* p = const_cast<uint8_t*>(n.values) + e * w;
-        for (int t = 0; t < w; t++) p[t] = 0;
-      } else if (n.type == FURY_TYPE_DECIMAL && n.values) {
-        st8(const_cast<uint8_t*>(n.values) + 16 * e, 0);
-        st8(const_cast<uint8_t*>(n.values) + 16 * e + 8, 0);
-      } else if (n.offsets) {                          // zero-length string / list / map
-        const int64_t pos = (n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY)
-                                ? cur.b(ni) : cur.e(n.first_child);
-        n.offsets[e + 1] = static_cast<int32_t>(pos);
-      }
-    }
-    if (n.type == FURY_TYPE_STRUCT)
-      for (int k = 0; k < n.num_children; k++) null_entry<D + 1, W>(nodes, n.first_child + k, cur);
-  }
-}
-
-__device__ __forceinline__ void set_valid_bit(uint8_t* bits, int64_t i) {
-  uint32_t* wp = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits + (i >> 3)) & ~uintptr_t(3));
-  const int sh = static_cast<int>((reinterpret_cast<uintptr_t>(bits + (i >> 3)) & 3) * 8 + (i & 7));
-  atomicOr(wp, 1u << sh);
-}
-
-template <int D, bool W>
-__device__ void get_value(const GenNode* nodes, int ni, bool present, const uint8_t* base,
-                          int64_t slot_addr, int es, bool in_array, const uint8_t* bitmap,
-                          int64_t ordinal, Cursors cur) {
-  if constexpr (D >= kGenMaxDepth) {
-    return;
-  } else {
-    const GenNode& n = nodes[ni];
-    const bool isnull = !present || ((bitmap[ordinal >> 3] >> (ordinal & 7)) & 1);
-    if (isnull) {
-      null_entry<D, W>(nodes, ni, cur);
-      return;
-    }
-    const int64_t e = cur.e(ni)++;
-    if (W && n.validity) {
-      if (n.row_aligned && ni < 64) *cur.vmask |= 1ull << ni;   // a wave ballot (entry = row)
-      else set_valid_bit(n.validity, e);
-    }
-    const uint8_t* sp = base + slot_addr;
-    const int w = gwidth(n.type);
-    if (w > 0) {
-      if (!W) return;
-      uint64_t v;
-      if (es == 8) v = ld8(sp);
-      else if (es == 4) v = *reinterpret_cast<const uint32_t*>(sp);
-      else if (es == 2) v = *reinterpret_cast<const uint16_t*>(sp);
-      else v = *sp;
-      uint8_t* dst = const_cast<uint8_t*>(n.values);
-      if (!dst) return;
-      if (n.type == FURY_TYPE_BOOL) {
-        if (v & 0xff) {
-          if (n.row_aligned && ni < 64) *cur.bmask |= 1ull << ni;
-          else set_valid_bit(dst, e);
-        }
-      } else if (w == 8) {
-        st8(dst + 8 * e, v);
-      } else if (w == 4) {
-        *reinterpret_cast<uint32_t*>(dst + 4 * e) = static_cast<uint32_t>(v);
-      } else if (w == 2) {
-        *reinterpret_cast<uint16_t*>(dst + 2 * e) = static_cast<uint16_t>(v);
-      } else {
-        dst[e] = static_cast<uint8_t>(v);
-      }
-      return;
-    }
-    const uint64_t oas = ld8(sp);
-    const uint8_t* vp = base + static_cast<int32_t>(oas >> 32);
-    const int64_t size = static_cast<uint32_t>(oas);
-    switch (n.type) {
-      case FURY_TYPE_STRING:
-      case FURY_TYPE_BINARY: {
-        const int64_t pos = cur.b(ni);
-        cur.b(ni) = pos + size;
-        if (W) {
-          uint8_t* dst = const_cast<uint8_t*>(n.values);
-          if (dst) copy_to_unaligned(dst + pos, vp, size);
-          n.offsets[e + 1] = static_cast<int32_t>(pos + size);
-        }
-        return;
-      }
-      case FURY_TYPE_DECIMAL:
-        if (W && n.values) {
-          st8(const_cast<uint8_t*>(n.values) + 16 * e, ld8(vp));
-          st8(const_cast<uint8_t*>(n.values) + 16 * e + 8, ld8(vp + 8));
-        }
-        return;
-      case FURY_TYPE_LIST: {
-        const int64_t m = static_cast<int32_t>(ld8(vp));
-        get_array<D, W>(nodes, n.first_child, vp, m, cur);
-        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e(n.first_child));
-        return;
-      }
-      case FURY_TYPE_STRUCT: {
-        const int nc = n.num_children;
-        const int64_t bmb = gbm(nc);
-        for (int k = 0; k < nc; k++)
-          get_value<D + 1, W>(nodes, n.first_child + k, true, vp, bmb + 8 * k, 8, false, vp, k, cur);
-        return;
-      }
-      case FURY_TYPE_MAP: {
-        const int64_t key_bytes = static_cast<int64_t>(ld8(vp));
-        const uint8_t* ka = vp + 8;
-        const uint8_t* va = vp + 8 + key_bytes;
-        const int64_t m = static_cast<int32_t>(ld8(ka));
-        get_array<D, W>(nodes, n.first_child, ka, m, cur);
-        get_array<D, W>(nodes, n.first_child + 1, va, m, cur);
-        if (W) n.offsets[e + 1] = static_cast<int32_t>(cur.e(n.first_child));
-        return;
-      }
-      default:
-        return;
-    }
-  }
-}
-
-// Pass 1 (W = false): per row, per node, Arrow entries and payload bytes -> cnt[2*node][row],
-// cnt[2*node+1][row].  Pass 2 (W = true): cursors start at the scanned positions.
-// The per-thread cursors live in dynamic LDS sized for the schema's node count (2 x 8 B x
-// nnodes per thread), so small schemas keep many workgroups per CU (a fixed kGenMaxNodes-sized
-// array held this latency-bound interpreter to 3 waves per CU).
-template <bool W, bool kWide>
-__global__ __launch_bounds__(kThreads) void gen_decode_kernel(GenArgs g, const uint8_t* __restrict__ rows,
-                                                              const int64_t* __restrict__ offs,
-                                                              int64_t* __restrict__ cnt) {
-  static_assert(kThreads == 64, "one wave = 64 consecutive rows (ballot bitmap words)");
-  extern __shared__ int64_t cur_lds[];
-  __shared__ GenNode sn[kWide ? 1 : kGenMaxNodes];
-  const GenNode* nodes = stage_nodes<kWide>(g, sn);
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  const bool live = r < g.nrows;
-  uint64_t vmask = 0, bmask = 0;
-  if (live) {
-    Cursors cur;
-    if (kWide) {             // cursors = the row's slots of the count array (see Cursors)
-      cur = Cursors{cnt + r, 2 * g.nrows, g.nrows, &vmask, &bmask};
-      if (!W)
-        for (int i = 0; i < g.nnodes; i++) cur.e(i) = cur.b(i) = 0;
-    } else {
-      cur = Cursors{cur_lds + threadIdx.x * (2 * g.nnodes), 1, g.nnodes, &vmask, &bmask};
-      for (int i = 0; i < g.nnodes; i++) {
-        cur.e(i) = W ? cnt[(2 * i) * g.nrows + r] : 0;
-        cur.b(i) = W ? cnt[(2 * i + 1) * g.nrows + r] : 0;
-      }
-    }
-    int64_t* e = &cur.e(0);
-    const uint8_t* row = rows + offs[r];
-    const int64_t bmb = gbm(g.ntop);
-    if (g.root) {        // a top-level BinaryArray / BinaryMap: node 0's entry r
-      const GenNode& n = nodes[0];
-      const int64_t en = cur.e(0)++;
-      if (W && n.validity) vmask |= 1ull;
-      const uint8_t* ka = g.root == 2 ? row + 8 : row;
-      const int64_t m = static_cast<int32_t>(ld8(ka));
-      get_array<1, W>(nodes, n.first_child, ka, m, cur);
-      if (g.root == 2) get_array<1, W>(nodes, n.first_child + 1, row + 8 + static_cast<int64_t>(ld8(row)), m, cur);
-      if (W) n.offsets[en + 1] = static_cast<int32_t>(cur.e(n.first_child));
-    } else {
-      for (int k = 0; k < g.ntop; k++)
-        get_value<1, W>(nodes, k, true, row, bmb + 8 * k, 8, false, row, k, cur);
-    }
-    (void)e;
-    if (!W && !kWide) {
-      for (int i = 0; i < g.nnodes; i++) {
-        cnt[(2 * i) * g.nrows + r] = cur.e(i);
-        cnt[(2 * i + 1) * g.nrows + r] = cur.b(i);
-      }
-    }
-  }
-  if (!W) return;
-  // row-aligned nodes: the wave's 64 rows are 64 consecutive Arrow entries, so their validity /
-  // bool bits are two whole 32-bit words (no atomics; the host zeroes nothing for them)
-  const int lane = threadIdx.x;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
-  const int64_t left = g.nrows - r0;
-  const int nwords = left >= 64 ? 2 : static_cast<int>((left + 31) >> 5);
-  for (int i = 0; i < g.nnodes; i++) {
-    const GenNode& n = nodes[i];
-    if (!n.row_aligned || i >= 64) continue;   // nodes >= 64: per-entry atomics (get_value)
-    if (n.validity) {
-      const uint64_t bits = __ballot(live && ((vmask >> i) & 1));
-      if (lane < nwords)
-        reinterpret_cast<uint32_t*>(n.validity)[(r0 >> 5) + lane] = static_cast<uint32_t>(bits >> (32 * lane));
-    }
-    if (n.type == FURY_TYPE_BOOL && n.values) {
-      const uint64_t bits = __ballot(live && ((bmask >> i) & 1));
-      if (lane < nwords)
-        reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(n.values))[(r0 >> 5) + lane] =
-            static_cast<uint32_t>(bits >> (32 * lane));
-    }
-  }
-}
-
-__global__ void seg_bases(const int64_t* __restrict__ s, int64_t nseq, int64_t len,
-                          const int64_t* __restrict__ grand, int64_t* __restrict__ bases,
-                          int64_t* __restrict__ totals) {
-  const int64_t q = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (q >= nseq) return;
-  const int64_t b = s[q * len];
-  const int64_t e = q + 1 < nseq ? s[(q + 1) * len] : *grand;
-  bases[q] = b;
-  totals[q] = e - b;
-}
-
-__global__ void seg_unbase(int64_t* __restrict__ s, int64_t n, int64_t len,
-                           const int64_t* __restrict__ bases) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) s[i] -= bases[i / len];
-}
-
-size_t cursor_lds(const GenArgs& g) {
-  return static_cast<size_t>(kThreads) * 2 * (g.nnodes > 0 ? g.nnodes : 1) * sizeof(int64_t);
-}
-
-// Arrow offsets start at 0 for every node that has them.
-__global__ void gen_offsets_zero(GenArgs g) {
-  for (int i = threadIdx.x; i < g.nnodes; i += blockDim.x) {
-    const GenNode& n = g.tab ? g.tab[i] : g.node[i];
-    if (n.offsets) n.offsets[0] = 0;
-  }
-}
-
 }  // namespace
 
 template <bool kWide, int kRoot>
@@ -639,55 +372,6 @@ int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int6
   if (g.tab) gen_encode_root<true>(g, offs, nullptr, rows, cap, stream);
   else gen_encode_root<false>(g, offs, nullptr, rows, cap, stream);
   return check_hip(hipGetLastError(), "gen_encode launch");
-}
-
-int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                     hipStream_t stream) {
-  const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  if (g.tab)
-    hipLaunchKernelGGL((gen_decode_kernel<false, true>), dim3(blocks), dim3(kThreads), 0, stream,
-                       g, rows, offs, cnt);
-  else
-    hipLaunchKernelGGL((gen_decode_kernel<false, false>), dim3(blocks), dim3(kThreads),
-                       cursor_lds(g), stream, g, rows, offs, cnt);
-  return check_hip(hipGetLastError(), "gen_count launch");
-}
-
-// `cnt` holds the scanned start positions; a wide schema's write pass advances its cursors in
-// place, so it runs on a copy (`scratch`, same size) and the plan stays reusable.
-int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                      int64_t* scratch, hipStream_t stream) {
-  hipLaunchKernelGGL(gen_offsets_zero, dim3(1), dim3(256), 0, stream, g);
-  const int64_t blocks = (g.nrows + kThreads - 1) / kThreads;
-  if (g.tab) {
-    const int st = check_hip(hipMemcpyAsync(scratch, cnt, 2 * g.nnodes * g.nrows * 8,
-                                            hipMemcpyDeviceToDevice, stream), "cursor copy");
-    if (st) return st;
-    hipLaunchKernelGGL((gen_decode_kernel<true, true>), dim3(blocks), dim3(kThreads), 0, stream,
-                       g, rows, offs, scratch);
-  } else {
-    hipLaunchKernelGGL((gen_decode_kernel<true, false>), dim3(blocks), dim3(kThreads),
-                       cursor_lds(g), stream, g, rows, offs, cnt);
-  }
-  return check_hip(hipGetLastError(), "gen_decode launch");
-}
-
-// nseq independent exclusive scans of len entries each (s[q * len + i]), totals[q] = sequence
-// sums: ONE scan over the concatenation, then every sequence minus its starting prefix (instead
-// of a 3-kernel scan per sequence: the nested decode has 2 x nodes sequences).
-// ws: scan_workspace(nseq * len) + 2 * nseq + 1 entries.
-int device_scan_batched(int64_t* s, int64_t nseq, int64_t len, int64_t* totals, int64_t* ws,
-                        hipStream_t stream) {
-  const int64_t n = nseq * len;
-  int64_t* grand = ws;
-  int64_t* bases = ws + 1;
-  int64_t* sws = ws + 1 + nseq;
-  device_scan(s, n, grand, sws, stream);
-  hipLaunchKernelGGL(seg_bases, dim3(static_cast<unsigned>((nseq + 255) / 256)), dim3(256), 0, stream,
-                     s, nseq, len, grand, bases, totals);
-  hipLaunchKernelGGL(seg_unbase, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
-                     s, n, len, bases);
-  return check_hip(hipGetLastError(), "batched scan launch");
 }
 
 }  // namespace fury

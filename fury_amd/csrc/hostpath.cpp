@@ -103,7 +103,7 @@ int64_t stage_bytes_per_row(const fury_schema* s) {
   return per_row + s->num_fields;             // validity bits, generously
 }
 
-// Rows per chunk: kTargetChunks chunks (env FURY_HOST_CHUNKS), 64-row aligned (bitmaps slice on
+// Rows per chunk: kTargetChunks chunks, 64-row aligned (bitmaps slice on
 // 32-bit words), at most kMaxStageBytes of HBM per stage.  Measured on the MI355X box
 // (scripts/ab_host.py, profiles/r01_host_path.json): the H2D and D2H copies of different
 // streams did not overlap there, and every extra chunk adds one copy per column, so more chunks
@@ -114,7 +114,6 @@ constexpr int64_t kMaxStageBytes = 1ll << 30;
 int64_t rows_per_chunk(const fury_schema* s, int64_t n) {
   const int64_t per_row = stage_bytes_per_row(s);
   int64_t chunks = kTargetChunks;
-  if (const char* e = getenv("FURY_HOST_CHUNKS")) chunks = atoll(e) > 0 ? atoll(e) : chunks;
   int64_t c = (n + chunks - 1) / chunks;
   if (c * per_row > kMaxStageBytes) c = kMaxStageBytes / per_row;
   c = ((c + 63) / 64) * 64;
@@ -155,7 +154,6 @@ uint8_t* device_view(const void* p, int64_t bytes) {
 int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
                  bool decode, int32_t device, bool* used) {
   *used = false;
-  if (getenv("FURY_HOST_STAGED")) return FURY_OK;      // A/B switch: force the staged path
   const int nf = s->num_fields;
   // the device entry points' alignment rules (16-B rows, width-aligned values) hold for the
   // staged buffers; host buffers that miss them are staged too
@@ -203,11 +201,11 @@ int fixed_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8
   }
   *used = true;
   g_host_direct.fetch_add(1);
-  // Plain (not non-temporal) loads and stores, one tile per workgroup: over PCIe the HBM-tuned
-  // default (variant 54) measured 92 / 88 GB/s, variant 0 95 / 89 (r02_host_direct.json sweep).
-  struct VariantScope {
-    VariantScope() { set_thread_fixed_variant(getenv("FURY_FIXED_VARIANT") ? -1 : 0); }
-    ~VariantScope() { set_thread_fixed_variant(-1); }
+  // Plain (not non-temporal) loads and stores: over PCIe the HBM-tuned kernels measured 92 / 88
+  // GB/s, plain ones 95 / 89 (r02_host_direct.json sweep).
+  struct DirectScope {
+    DirectScope() { set_thread_host_direct(true); }
+    ~DirectScope() { set_thread_host_direct(false); }
   } scope;
   st = decode ? fury_row_decode(s, drows, nullptr, n, dc.data(), hs)
               : fury_row_encode(s, dc.data(), n, nullptr, drows, hs);

@@ -73,10 +73,7 @@ struct fury_decode_plan {
   const uint8_t* rows = nullptr;
   const int64_t* offs = nullptr;
   int64_t nrows = 0;
-  int64_t* cnt = nullptr;          // [2 * nodes][nrows] scanned start positions (stream pool)
-  void* cnt_stream = nullptr;      // the stream cnt was allocated on (freed on it)
-  fury::LvPlan* lv = nullptr;      // level-by-level engine (levels.hip), when it made the plan
-  int64_t* scratch = nullptr;      // wide schemas: cursor copy of cnt for the write pass
+  fury::LvPlan* lv = nullptr;      // level-by-level engine state (levels.hip); NULL when nrows = 0
   bool arrow = false;
   std::vector<int64_t> totals;     // per node: Arrow entries, payload bytes
   void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)

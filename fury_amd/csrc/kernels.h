@@ -45,12 +45,12 @@ struct FixedArgs {
   int32_t ncols;
   int32_t bitmap_bytes;
   int32_t row_size;
-  int32_t tile_order;                 // 0: tile = blockIdx; 1: XCD-contiguous tile ranges
+  int32_t pad_;
   int64_t nrows;
 };
 
-int fixed_variant();
-void set_fixed_variant(int v);
+// Host-direct mode of the calling thread (hostpath.cpp): plain instead of non-temporal accesses.
+void set_thread_host_direct(bool on);
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast);
 int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast);
 
@@ -82,7 +82,8 @@ struct VarArgs {
   int32_t nvar;
   int64_t nrows;
   int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
-  int32_t dbg;               // DIAGNOSTIC phase-skip bits (FURY_VAR_DBG), 0 in production
+  int32_t help_now;          // look-backs help a silent predecessor at once (test hook, tuning
+                             // "lookback_help"); 0 in production
   uint32_t* err;             // host-visible device error word (device_error_word()) or NULL
 };
 
@@ -121,9 +122,9 @@ int workspace_reserve(size_t bytes, void** out);
 
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
-int var_decode_mode();
 int64_t lookback_timeouts();
-void set_var_decode_mode(int v);
+int lookback_help_mode();
+void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 // Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.
 int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows, int64_t cap,
@@ -163,28 +164,18 @@ struct GenArgs {
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
-int launch_gen_count(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                     hipStream_t stream);
-int launch_gen_decode(const GenArgs& g, const uint8_t* rows, const int64_t* offs, int64_t* cnt,
-                      int64_t* scratch, hipStream_t stream);
 // Level-by-level nested decode (levels.hip): prepare = per-level count / scan / expand passes
 // (totals[2 i] entries, totals[2 i + 1] payload bytes of node i), execute = one write pass into
-// the outputs of gen_args' node table.  Tuning "gen_decode": 0 this engine (default), 1 the
-// thread-per-row interpreter of generic.hip.
+// the outputs of gen_args' node table.
 struct LvPlan;
 int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, int64_t nrows,
                hipStream_t hs, LvPlan** out, std::vector<int64_t>* totals);
 int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                hipStream_t hs);
 void lv_free(LvPlan* p);
-int gen_decode_mode();
-void set_gen_decode_mode(int v);
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);
-// nseq independent exclusive scans of len entries (ws: scan_workspace(nseq * len) + 2 nseq + 1).
-int device_scan_batched(int64_t* s, int64_t nseq, int64_t len, int64_t* totals, int64_t* ws,
-                        hipStream_t stream);
 
 int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t nrows,
                       int64_t fixed_size, int64_t schema_hash, uint8_t* out,
@@ -194,7 +185,6 @@ int launch_frame_rows(const uint8_t* rows, const int64_t* row_offsets, int64_t n
 int unframe_mode();
 void set_unframe_mode(int v);
 int64_t unframe_walk_count();
-void set_thread_fixed_variant(int v);  // fixed.hip: per-thread variant override, -1 = none
 void keep_pool(int device);      // hostpath.cpp: keep freed stream-pool memory pooled
 int64_t host_direct_count();     // hostpath.cpp: host calls run directly on pinned memory
 int64_t unframe_repair_count();      // streams parsed by the parallel repair (pointer doubling)

@@ -655,18 +655,6 @@ int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_
 
 }  // namespace
 
-static int g_gen_decode = -1;
-
-int gen_decode_mode() {
-  if (g_gen_decode < 0) {
-    const char* e = getenv("FURY_GEN_DECODE");
-    g_gen_decode = e ? atoi(e) : 0;
-  }
-  return g_gen_decode;
-}
-
-void set_gen_decode_mode(int v) { g_gen_decode = v; }
-
 void lv_free(LvPlan* p) {
   if (!p) return;
   for (void* b : p->bufs) dev_free(b, p->stream);

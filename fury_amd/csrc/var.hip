@@ -16,10 +16,6 @@ const VarCol& hcol(const VarArgs& a, int k) { return a.htab ? a.htab[k] : a.col[
 
 int64_t nblocks(int64_t n) { return (n + kThreads - 1) / kThreads; }
 
-int g_var_decode = 0;     // tuning "var_decode": 0 one-pass look-back (tile rows by sequence
-                          // count), 1 sizing pass + decode, 2 / 3 register-staged one-pass with
-                          // 512 / 256 rows, 4 LDS-staged one-pass (var_lds.hip)
-
 }  // namespace
 
 // Device exclusive scan of s[0..n) (int64) with the total written to *total; `ws` needs
@@ -62,64 +58,15 @@ int launch_measure_rows(const VarArgs& a, int64_t* offs, hipStream_t stream) {
   return st;
 }
 
-int var_decode_mode() { return g_var_decode; }
-
 // Look-back spins abandoned so far (each one would have left wrong Arrow offsets behind; never
 // observed: workgroups are dispatched in launch order).  Synchronous device read.
 int64_t lookback_timeouts() { return device_error_count(); }
-void set_var_decode_mode(int v) { g_var_decode = v; }
-// LDS plan of the pipelined encode: per workgroup 2 meta slots + 2 payload slots + 1 row image
-// within kPipeLds, so kPipeGroupsPerCU workgroups share a CU.  Payload and row sizes are
-// estimated from the input buffers' byte counts (fury_column.capacity; 32 B per string when
-// unknown) with headroom; a tile whose payload or image does not fit reads / writes global
-// memory directly for that part, so the plan affects speed only.
-constexpr int kPipeGroupsPerCU = 2;
-constexpr int64_t kPipeLds = 77 * 1024;
 
-
-bool plan_encode_pipe(const VarArgs& a, PipeLayout* L) {
-  if (a.nrows <= 0) return false;
-  double pay_row = 0, img_row = a.fixed_size;
-  int nvarc = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = hcol(a, k);
-    if (c.kind == kDecimal) img_row += 16;
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    nvarc++;
-    const double per = c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
-    if (c.kind == kBytes) {
-      pay_row += per;
-      img_row += per + 7;
-    } else {
-      const double ew = c.width == 0 ? 0.125 : c.width;
-      pay_row += per * ew + (c.elem_validity ? per / 8 : 0);
-      img_row += 16 + per * (c.width == 0 ? 1 : c.width) + 7;
-    }
-  }
-  for (int R = kEncRows; R >= 32; R -= 32) {
-    int64_t meta = 8 * int64_t(R + 1) + 32;
-    for (int k = 0; k < a.ncols; k++) {
-      const VarCol& c = hcol(a, k);
-      if (c.validity) meta += R / 8 + 32;
-      if (c.kind == kFixed) meta += int64_t(R) * c.width + 32;
-      else if (c.kind == kBool) meta += R / 8 + 32;
-      else if (c.kind == kDecimal) meta += 16 * int64_t(R) + 32;
-      else meta += 4 * int64_t(R + 1) + 32;
-    }
-    const int64_t msz = r16(meta);
-    const int64_t psz = r16(static_cast<int64_t>(R * pay_row * 1.15) + 64 * nvarc);
-    const int64_t isz = r16(static_cast<int64_t>(R * img_row * 1.10) + 64);
-    if (2 * msz + 2 * psz + isz <= kPipeLds) {
-      L->rows = R;
-      L->msz = static_cast<uint32_t>(msz);
-      L->psz = static_cast<uint32_t>(psz);
-      L->isz = static_cast<uint32_t>(isz);
-      return true;
-    }
-  }
-  return false;
-}
-
+// Test hook (tuning "lookback_help"): every look-back computes a silent predecessor's aggregate
+// at once -- the path a late-dispatched predecessor takes -- instead of polling first.
+static int g_help_now = 0;
+int lookback_help_mode() { return g_help_now; }
+void set_lookback_help_mode(int v) { g_help_now = v; }
 // Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
 // counts, as plan_encode_pipe) fit the LDS image with headroom.
 int reg_tile_rows(const VarArgs& a) {
@@ -140,23 +87,7 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
                       hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
   const int64_t nb = (a.nrows + a.tile_rows - 1) / a.tile_rows;
-  PipeLayout L;
-  if ((a.dbg & 2048) && !a.tab && plan_encode_pipe(a, &L)) {
-    VarArgs b = a;
-    b.tile_rows = L.rows;
-    const int64_t nt = (a.nrows + L.rows - 1) / L.rows;
-    const size_t lds = 2 * static_cast<size_t>(L.msz) + 2 * L.psz + L.isz;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(encode_var_pipe),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       static_cast<int>(lds));
-    if (e != hipSuccess) return check_hip(e, "hipFuncSetAttribute");
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t g = nt < int64_t(cus) * kPipeGroupsPerCU ? nt : int64_t(cus) * kPipeGroupsPerCU;
-    hipLaunchKernelGGL(encode_var_pipe, dim3(static_cast<unsigned>(g)), dim3(kEncRows), lds, stream,
-                       b, offs, rows, cap, nt, L.msz, L.psz, L.isz);
-  } else if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
+  if (a.ncols <= kRegCols) {
     VarArgs b = a;
     b.tile_rows = reg_tile_rows(a);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
@@ -164,8 +95,6 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);
-  } else if (a.dbg & 512) {
-    hipLaunchKernelGGL(encode_var_kernel_d, dim3(nb), dim3(kEncRows), 0, stream, a, offs, rows, cap);
   } else {
     hipLaunchKernelGGL(encode_var_kernel<MetaMap>, dim3(nb), dim3(kEncRows), 0, stream, a, offs,
                        rows, cap);
@@ -218,10 +147,10 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 // fury_row_decode_measure, an over-estimate under bound sizing) with 30 % headroom, the bitmap
 // images of lists, and alignment slack -- capped at the static maximum.  A tile whose payload
 // does not fit its image stores that column straight to HBM (correct, slower), so the estimate
-// only moves speed.  FURY_VAR_DBG bit 8192: always the maximum (A/B).
+// only moves speed.
 uint32_t dec_img_bytes(const VarArgs& a, int tile) {
   const int64_t cap = static_cast<int64_t>(kDecImg) * (tile / kThreads);
-  if ((a.dbg & 8192) || a.nrows <= 0) return static_cast<uint32_t>(cap);
+  if (a.nrows <= 0) return static_cast<uint32_t>(cap);
   int64_t need = 0;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = hcol(a, k);
@@ -237,56 +166,6 @@ uint32_t dec_img_bytes(const VarArgs& a, int tile) {
   return static_cast<uint32_t>(need < cap ? need : cap);
 }
 
-// LDS plan of the LDS-staged decode (var_lds.hip): per workgroup the tile's row range (stage),
-// its output images and the nseq x NT in-tile offsets, within kLdsBudget so three workgroups
-// share a CU.  Row bytes are estimated from the output capacities (exact after
-// fury_row_decode_measure, over-estimates under bound sizing); a tile whose rows exceed the stage
-// reads them from HBM, so the estimate only moves speed.  FURY_LDS_BUDGET (bytes) overrides the
-// budget for A/B.
-int decode_var_lds_plan(const VarArgs& a, const uint8_t* rows, const int64_t* offs, int nseq,
-                        int nt, hipStream_t stream) {
-  static const int64_t budget = [] {
-    const char* e = getenv("FURY_LDS_BUDGET");
-    const int64_t v = e ? atoll(e) : 0;
-    return v >= 16384 && v <= 150 * 1024 ? v : int64_t(51) * 1024;
-  }();
-  double row = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = hcol(a, k);
-    const double per = c.values && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
-    if (c.kind == kDecimal) row += 16;
-    else if (c.kind == kBytes) row += per + 4;
-    else if (c.kind == kListFixed) row += 12 + per * (c.width == 0 ? 1 : c.width) + per / 8;
-  }
-  const int64_t pos = int64_t(nseq) * nt * 4;
-  int64_t img = dec_img_bytes(a, nt);
-  int64_t stage = r16(static_cast<int64_t>(row * nt * 1.2) + 64);
-  if (stage < 4096) stage = 4096;
-  // many string / list columns: the per-row offsets alone may fill the budget -- exceed it
-  // (fewer workgroups per CU) rather than leave no stage
-  const int64_t avail = (budget > pos + 16384 ? budget : pos + 16384) - pos;
-  if (stage + img > avail) {
-    // keep at least 3/4 of the stage estimate (at most avail - 1 KB), then trim the images
-    const int64_t keep = stage * 3 / 4 < avail - 1024 ? stage * 3 / 4 : avail - 1024;
-    stage = avail - img > keep ? avail - img : keep;
-    img = avail - stage;
-  }
-  stage = stage & ~int64_t(15);
-  img = img & ~int64_t(15);
-  const int64_t ntiles = (a.nrows + nt - 1) / nt;
-  const size_t wsb = (static_cast<size_t>(ntiles) * nseq + 1) * 8;    // [ticket][status words]
-  uint64_t* ws = nullptr;
-  int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
-  if (st) return st;
-  st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-  if (!st)
-    st = launch_decode_var_lds(a, rows, offs, ws + 1, reinterpret_cast<uint32_t*>(ws), nseq, nt,
-                               static_cast<uint32_t>(stage), static_cast<uint32_t>(img), ntiles,
-                               stream);
-  dev_free(ws, stream);
-  return st;
-}
-
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                       hipStream_t stream, bool arrow) {
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
@@ -295,40 +174,24 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   for (int k = 0; k < a.ncols; k++)
     if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
   const int64_t nb = nblocks(a.nrows);
-  if (g_var_decode == 1) {       // sizing pass, then the decode kernel reads those offsets
-    int st = launch_decode_measure(a, rows, offs, stream);
-    if (st) return st;
-    hipLaunchKernelGGL(decode_var_kernel<false>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
-                       nullptr, nullptr, nseq);
-    return check_hip(hipGetLastError(), "decode_var launch");
-  }
-  if (g_var_decode == 4 && nseq <= lds_decode_max_seq() && !a.tab) {
-    static const int nt = [] {
-      const char* e = getenv("FURY_LDS_ROWS");       // A/B: 128 / 256 / 512-row tiles
-      const int v = e ? atoi(e) : 0;
-      return v == 128 || v == 512 ? v : kThreads;
-    }();
-    return decode_var_lds_plan(a, rows, offs, nseq, nt, stream);
-  }
-  if (a.ncols <= kRegCols && !(a.dbg & 1024)) {
+  if (a.ncols <= kRegCols) {
     // 512-row tiles halve the look-back chain links: faster with several string / list
     // sequences to chain (mixed, 3: 0.656 vs 0.737 ms), slower with one (nested: 0.287 vs
-    // 0.274 ms) — scripts/ab_var.py.  Mode 0 picks by sequence count, 2 / 3 force 512 / 256.
-    const bool wide = g_var_decode == 2 || (g_var_decode == 0 && nseq >= 2);
+    // 0.274 ms) -- scripts/ab_var.py.
+    const bool wide = nseq >= 2;
     const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
-    // [ticket][status words: tiles x fields], zeroed per launch
-    const size_t wsb = (static_cast<size_t>(nbr) * a.ncols + 1) * 8;
+    // status words: tiles x fields, zeroed per launch
+    const size_t wsb = static_cast<size_t>(nbr) * a.ncols * 8;
     uint64_t* ws = nullptr;
     int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-    uint32_t* tk = reinterpret_cast<uint32_t*>(ws);
     const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
-    if (!st) st = launch_decode_var_reg(a, rows, offs, ws + 1, tk, img, wide, nb, nbr, stream);
+    if (!st) st = launch_decode_var_reg(a, rows, offs, ws, img, wide, nb, nbr, stream);
     dev_free(ws, stream);
     return st;
   }
-  // look-back status words (nb x nseq) + the group ticket, zeroed per launch
+  // look-back status words (nb x nseq), zeroed per launch
   const size_t wsb = (nb * nseq + 1) * 8;
   uint64_t* ws = nullptr;
   int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
@@ -336,7 +199,7 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
   if (!st) {
     hipLaunchKernelGGL(decode_var_kernel<true>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
-                       ws + 1, reinterpret_cast<uint32_t*>(ws), nseq);
+                       ws, nseq);
     st = check_hip(hipGetLastError(), "decode_var launch");
   }
   dev_free(ws, stream);

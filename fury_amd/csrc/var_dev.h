@@ -326,11 +326,6 @@ constexpr int kEncPool = 50 * 1024;           // LDS: staged inputs + row image 
 constexpr int kMetaPool = 16 * 1024;          // bound on a tile's staged per-row inputs
 constexpr uint32_t kNone = 0xffffffffu;
 
-struct PipeLayout {
-  int rows;                   // rows per tile
-  uint32_t msz, psz, isz;     // LDS bytes: meta slot, payload slot, row image
-};
-
 // LDS byte offsets of one tile's staged inputs, per column (kNone = not present / not staged).
 template <int N>
 struct MetaMapN {
@@ -448,7 +443,7 @@ __device__ __forceinline__ uint64_t payload_need(const VarArgs& a, const MM& mm,
 template <int NT, class MM>
 __device__ __forceinline__ void stage_payloads(const VarArgs& a, MM& mm, uint8_t* pool,
                                                uint32_t at, int nr) {
-  const bool iss = !(a.dbg & 1);
+  const bool iss = true;
   for (int k = 0; k < a.ncols; k++) {
     CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
@@ -545,57 +540,6 @@ __device__ __forceinline__ void build_tile_row(const VarArgs& a, const MM& mm,
   if (a.ncols & 63) d64[(a.ncols - 1) >> 6] = nullbits;
 }
 
-// DIAGNOSTIC: build_tile_row with the column kinds known at compile time (experiment on the
-// cost of interpreting the schema at run time).
-struct SpecMixed {
-  static constexpr int n = 6;
-  static constexpr int kind[6] = {kFixed, kFixed, kFixed, kBytes, kBytes, kBytes};
-  static constexpr int width[6] = {4, 8, 8, 1, 1, 1};
-};
-template <class S, class MM>
-__device__ __forceinline__ void build_tile_row_spec(const VarArgs& a, const MM& mm,
-                                                    const uint8_t* pool, const uint8_t* pay, int t,
-                                                    uint8_t* dst) {
-  uint64_t* d64 = reinterpret_cast<uint64_t*>(dst);
-  const int nslot0 = a.bitmap_bytes >> 3;
-  int64_t cursor = a.fixed_size;
-  uint64_t nullbits = 0;
-  bool ok[S::n];
-  uint64_t fixv[S::n];
-  int32_t o0[S::n], o1[S::n], ob[S::n];
-#pragma unroll
-  for (int k = 0; k < S::n; k++) {
-    ok[k] = mm.val[k] == kNone || lds_bit(pool, mm.val[k], t);
-    if (S::kind[k] == kFixed) {
-      const uint8_t* p = pool + mm.fix[k] + t * S::width[k];
-      fixv[k] = S::width[k] == 8 ? *reinterpret_cast<const uint64_t*>(p)
-                                 : *reinterpret_cast<const uint32_t*>(p);
-    } else {
-      ob[k] = lds_i32(pool, mm.off[k]);
-      o0[k] = lds_i32(pool, mm.off[k] + 4 * t);
-      o1[k] = lds_i32(pool, mm.off[k] + 4 * (t + 1));
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < S::n; k++) {
-    CVarCol& c = vc(a, k);
-    uint64_t slot = 0;
-    if (!ok[k]) {
-      nullbits |= 1ull << k;
-    } else if (S::kind[k] == kFixed) {
-      slot = fixv[k];
-    } else {
-      const int64_t len = o1[k] - o0[k];
-      const uint8_t* src = mm.pay[k] != kNone ? pay + mm.pay[k] + (o0[k] - ob[k]) : c.values + o0[k];
-      copy_to_aligned(d64 + (cursor >> 3), src, len);
-      slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
-      cursor += rnd8(len);
-    }
-    d64[nslot0 + k] = slot;
-  }
-  d64[0] = nullbits;
-}
-
 // Encode workgroup: rows [r0, r0 + R) at the offsets fury_row_measure produced.  Bytes at or
 // past `cap` are never written.
 template <int POOL, bool kStagePay, class MM>
@@ -624,13 +568,9 @@ __device__ __forceinline__ void encode_tile(const VarArgs& a, const int64_t* __r
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (img_fits) {
     uint8_t* image = pool + img_at;
-    if (live && (a.dbg & 256)) {
-      build_tile_row_spec<SpecMixed>(a, mm, pool, pool, tid, image + ex);
-    } else if (live && !(a.dbg & 2)) {
-      build_tile_row(a, mm, pool, pool, tid, image + ex);
-    }
+    if (live) build_tile_row(a, mm, pool, pool, tid, image + ex);
     __syncthreads();
-    if (!(a.dbg & 4)) copy_range<true, kEncRows>(rows + base, image, room);
+    copy_range<true, kEncRows>(rows + base, image, room);
   } else if (live && ex + tile_row_size(a, mm, pool, tid) <= room) {
     build_tile_row(a, mm, pool, pool, tid, rows + base + ex);    // oversized tile: straight to HBM
   }
@@ -647,35 +587,6 @@ __global__ __launch_bounds__(kEncRows) void encode_var_kernel(VarArgs a,
   encode_tile<kEncPool, true>(a, offs, rows, cap, blockIdx.x, pool, mm);
 }
 #endif  // FURY_VAR_MAIN
-
-// Payloads read straight from global memory (no payload staging): a smaller LDS pool, so more
-// workgroups share a CU.
-constexpr int kEncPoolDirect = 38 * 1024;
-#ifdef FURY_VAR_MAIN
-__global__ __launch_bounds__(kEncRows) void encode_var_kernel_d(VarArgs a,
-                                                                const int64_t* __restrict__ offs,
-                                                                uint8_t* __restrict__ rows,
-                                                                int64_t cap) {
-  __shared__ __attribute__((aligned(16))) uint8_t pool[kEncPoolDirect];
-  __shared__ MetaMap mm;
-  encode_tile<kEncPoolDirect, false>(a, offs, rows, cap, blockIdx.x, pool, mm);
-}
-#endif  // FURY_VAR_MAIN
-
-__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// Waits until at most n of this wave's vector-memory operations are outstanding (n uniform).
-// The n youngest are the image stores just issued, so every older operation — the next tile's
-// LDS-DMA — has landed, while the stores keep draining.
-__device__ __forceinline__ void wait_vm_le(int n) {
-  switch (n < 0 ? 0 : (n > 15 ? 15 : n)) {
-#define FURY_VMW(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-    FURY_VMW(0) FURY_VMW(1) FURY_VMW(2) FURY_VMW(3) FURY_VMW(4) FURY_VMW(5) FURY_VMW(6)
-    FURY_VMW(7) FURY_VMW(8) FURY_VMW(9) FURY_VMW(10) FURY_VMW(11) FURY_VMW(12) FURY_VMW(13)
-    FURY_VMW(14) FURY_VMW(15)
-#undef FURY_VMW
-  }
-}
 
 // Stores img[0, bytes) to g (any alignment): each wave writes a contiguous quarter of the 16-byte
 // aligned body with 16-B non-temporal stores, wave 0 the unaligned head and wave 3 the tail by
@@ -893,132 +804,16 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
     v[k] = x;
   }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (a.dbg & 64) {         // DIAGNOSTIC: the per-row input loads only
-    uint64_t x = valid ^ static_cast<uint64_t>(ex);
-#pragma unroll
-    for (int k = 0; k < K; k++) x ^= v[k];
-    if (x == 0x123456789abcdefull) rows[0] = 1;
-    return;
-  }
   if (bytes <= kRegImg) {
-    if (live && !(a.dbg & 2)) reg_build_row<K>(a, r, v, valid, img + (ex >> 3));
+    if (live) reg_build_row<K>(a, r, v, valid, img + (ex >> 3));
     __syncthreads();
-    if (!(a.dbg & 4)) store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
+    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
     const int64_t sz = offs[r + 1] - offs[r];
     if (ex + sz <= room) reg_build_row<K>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
   }
 }
 #endif  // FURY_VAR_ENC
-
-// ---- pipelined encode ------------------------------------------------------------------------
-// A fixed grid of resident workgroups (2 per CU) walks the tiles t = blockIdx.x + i * gridDim.x.
-// Each workgroup double-buffers its inputs: while tile t is built from slot s and stored, the
-// LDS-DMA of tile t + gridDim.x (its row offsets, per-row inputs and payload ranges) is already in
-// flight into slot s ^ 1, so one HBM round trip per tile is overlapped with the build instead of
-// two being waited for.  The payload ranges of the next tile come from scalar loads of the two
-// bounding string/list offsets, so they do not wait for that tile's meta to land.
-struct PipeSlot {
-  MetaMap mm;
-  uint32_t offs_at;          // LDS offset (in the meta slot) of the staged offs[r0]
-  uint32_t pad_;
-};
-
-template <int NT>
-__device__ __forceinline__ void pipe_issue(const VarArgs& a, const int64_t* __restrict__ offs,
-                                           int64_t t, uint8_t* meta, uint8_t* pay, uint32_t psz,
-                                           PipeSlot& ps) {
-  const int R = a.tile_rows;
-  const int64_t r0 = t * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  uint32_t at = 0;
-  const uint32_t oa = stage_range<NT>(meta, at, reinterpret_cast<const uint8_t*>(offs + r0),
-                                      reinterpret_cast<const uint8_t*>(offs + r0 + nr + 1));
-  stage_meta<NT>(a, r0, nr, meta, ps.mm, at);        // sets every mm.pay / mm.pvb to kNone
-  uint32_t pat = 0;
-  for (int k = 0; k < a.ncols; k++) {
-    CVarCol& c = vc(a, k);
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t b = c.offsets[r0], e = c.offsets[r0 + nr];
-    if (e <= b) continue;
-    const uint8_t *gb, *ge;
-    if (c.kind == kBytes) { gb = c.values + b; ge = c.values + e; }
-    else if (c.width == 0) { gb = c.values + (b >> 3); ge = c.values + ((e + 7) >> 3); }
-    else { gb = c.values + b * c.width; ge = c.values + e * c.width; }
-    const bool vb = c.kind == kListFixed && c.elem_validity;
-    const uint8_t* vgb = vb ? c.elem_validity + (b >> 3) : nullptr;
-    const uint8_t* vge = vb ? c.elem_validity + ((e + 7) >> 3) : nullptr;
-    auto span = [](const uint8_t* x, const uint8_t* y) -> uint64_t {
-      return ((reinterpret_cast<uint64_t>(y) + 15) & ~uint64_t(15)) -
-             (reinterpret_cast<uint64_t>(x) & ~uint64_t(15));
-    };
-    const uint64_t need = span(gb, ge) + (vb ? span(vgb, vge) : 0);
-    if (pat + need > psz) continue;                   // this column reads global memory
-    const uint32_t pa = stage_range<NT>(pay, pat, gb, ge);
-    const uint32_t pv = vb ? stage_range<NT>(pay, pat, vgb, vge) : kNone;
-    if (threadIdx.x == 0) {
-      ps.mm.pay[k] = pa;
-      ps.mm.pvb[k] = pv;
-    }
-  }
-  if (threadIdx.x == 0) ps.offs_at = oa;
-}
-
-__device__ __forceinline__ int pipe_build_store(const VarArgs& a, uint8_t* __restrict__ rows,
-                                                 int64_t cap, int64_t t, const uint8_t* meta,
-                                                 const uint8_t* pay, uint8_t* img, uint32_t isz,
-                                                 const PipeSlot& ps) {
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;
-  const int64_t r0 = t * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t* so = reinterpret_cast<const int64_t*>(meta + ps.offs_at);
-  const int64_t base = so[0];
-  const int64_t bytes = so[nr] - base;
-  const int64_t ex = live ? so[tid] - base : 0;
-  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  if (bytes + 16 <= isz) {
-    if (live) build_tile_row(a, ps.mm, meta, pay, tid, img + ex);
-    __syncthreads();
-    return store_image(rows + base, img, room);
-  }
-  if (live && ex + tile_row_size(a, ps.mm, meta, tid) <= room)
-    build_tile_row(a, ps.mm, meta, pay, tid, rows + base + ex);   // oversized tile: straight to HBM
-  return 0;                                                       // wait for everything
-}
-
-#ifdef FURY_VAR_MAIN
-__global__ __launch_bounds__(kEncRows) void encode_var_pipe(VarArgs a,
-                                                            const int64_t* __restrict__ offs,
-                                                            uint8_t* __restrict__ rows,
-                                                            int64_t cap, int64_t ntiles,
-                                                            uint32_t msz, uint32_t psz,
-                                                            uint32_t isz) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  __shared__ PipeSlot ps[2];
-  uint8_t* img = lds + 2 * msz + 2 * psz;
-  int64_t t = blockIdx.x;
-  if (t >= ntiles) return;
-  int s = 0;
-  pipe_issue<kEncRows>(a, offs, t, lds, lds + 2 * msz, psz, ps[0]);
-  wait_dma();
-  __syncthreads();
-  for (;;) {
-    const int64_t tn = t + gridDim.x;
-    if (tn < ntiles)
-      pipe_issue<kEncRows>(a, offs, tn, lds + (s ^ 1) * msz, lds + 2 * msz + (s ^ 1) * psz, psz,
-                           ps[s ^ 1]);
-    const int nst =
-        pipe_build_store(a, rows, cap, t, lds + s * msz, lds + 2 * msz + s * psz, img, isz, ps[s]);
-    wait_vm_le(nst);
-    __syncthreads();
-    if (tn >= ntiles) break;
-    t = tn;
-    s ^= 1;
-  }
-}
-#endif  // FURY_VAR_MAIN
 
 // ---- measure: row sizes (writerIndex growth of toRow) and their exclusive scan.  Each thread
 // sizes 4 consecutive rows (one validity nibble and 5 consecutive offsets per column), so a
@@ -1321,7 +1116,7 @@ __device__ int64_t look_back_help(const VarArgs& a, int k, const uint8_t* rows,
                                   const int64_t* offs, const uint64_t* status, int64_t b, int nseq,
                                   int q, uint32_t* err) {
   const int lane = threadIdx.x & 63;
-  const uint32_t limit = (a.dbg & 32768) ? 0u : kHelpSpins;
+  const uint32_t limit = a.help_now ? 0u : kHelpSpins;
   int64_t excl = 0;
   for (int64_t j = b - 1;; j -= 64) {
     const int64_t idx = j - lane;
@@ -1425,7 +1220,6 @@ template <int K, int NT = kThreads>
 __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                            const int64_t* __restrict__ offs,
                                                            uint64_t* __restrict__ status,
-                                                           uint32_t* __restrict__ ticket,
                                                            uint32_t img_cap) {
   // dynamic LDS: the output images, sized per launch from the expected tile payload
   // (dec_img_bytes); the kernel's occupancy is register-bound (~120 VGPRs), so this only frees
@@ -1433,7 +1227,6 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   extern __shared__ __attribute__((aligned(16))) uint64_t oimg[];
   __shared__ int64_t tmp[NT / 64];
   __shared__ int64_t sbase[K];
-  __shared__ int64_t stile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // Tile = blockIdx.  A ticket (tiles numbered in start order) made every look-back wait end by
   // construction, but its one device-scope atomic per tile serialises at the cross-XCD coherence
@@ -1441,12 +1234,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   // the look-back helps itself (look_back_help): a predecessor that has published nothing for a
   // long time -- not dispatched yet, under any dispatch order -- has its aggregate computed from
   // its rows by the waiting wave, so no wait depends on a workgroup that is not running.
-  // FURY_VAR_DBG bit 4096: the ticket (A/B).
-  if (a.dbg & 4096) {
-    if (tid == 0) stile = atomicAdd(ticket, 1u);
-    __syncthreads();
-  }
-  const int64_t b = (a.dbg & 4096) ? stile : static_cast<int64_t>(blockIdx.x), nb = gridDim.x;
+  const int64_t b = static_cast<int64_t>(blockIdx.x), nb = gridDim.x;
   const int64_t r0 = b * NT;
   const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
@@ -1484,13 +1272,6 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     if (!isnull && c.kind == kBytes) cnt[k] = static_cast<uint32_t>(slot[k]);
     if (!isnull && c.kind == kListFixed)
       cnt[k] = static_cast<uint32_t>(*reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot[k] >> 32)));
-  }
-  if (a.dbg & 128) {        // DIAGNOSTIC: the loads only (a dependent store keeps them)
-    uint64_t x = nullw;
-#pragma unroll
-    for (int k = 0; k < K; k++) x ^= slot[k] + cnt[k];
-    if (x == 0x123456789abcdefull) status[0] = x;
-    return;
   }
   // in-tile exclusive scans, two columns per 64-bit scan (tile totals < 2^32)
   uint32_t ex[K], tot[K];
@@ -1543,7 +1324,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    if (img_at[k] == kNone || !live || cnt[k] == 0 || (a.dbg & 16)) continue;
+    if (img_at[k] == kNone || !live || cnt[k] == 0) continue;
     const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
     uint8_t* im = reinterpret_cast<uint8_t*>(oimg) + img_at[k];
     if (c.kind == kBytes) {
@@ -1615,7 +1396,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   const int64_t nvalid = a.nrows - rbase;
   const int nwords = nvalid >= 64 ? 2 : nvalid <= 0 ? 0 : static_cast<int>((nvalid + 31) >> 5);
 #pragma unroll
-  for (int k = 0; k < ((a.dbg & 8) ? 0 : K); k++) {
+  for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
     const bool isnull = (nullw >> k) & 1;
     if (c.validity) {
@@ -1658,8 +1439,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     for (int k = 0; k < K; k++) {
       if (!is_seq(a.col[k])) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = (b == 0 || (a.dbg & 32)) ? 0
-                          : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err);
+      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err);
       if (lane == 0) {
         sbase[k] = pre;
         if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
@@ -1839,7 +1619,7 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
     return;
   }
   for (int q = w; q < nchunk; q += kThreads / 64) {
-    const int64_t ex = (b == 0 || (a.dbg & 32)) ? 0
+    const int64_t ex = b == 0 ? 0
                        : look_back_help<kThreads>(a, seq_col(a, cbase + q), rows, offs, status, b,
                                                   nseq, cbase + q, a.err);
     if (lane == 0) {
@@ -1869,7 +1649,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
   if (kLookBack && nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
 
   // fixed-width fields and every field's validity: no dependency on other groups
-  for (int k = 0; k < ((a.dbg & 8) ? 0 : a.ncols); k++) {
+  for (int k = 0; k < a.ncols; k++) {
     CVarCol& c = vc(a, k);
     const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
     const uint64_t slot =
@@ -1922,7 +1702,7 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
       if (live) c.offsets[r] = static_cast<int32_t>(gb + sh.pos[q][tid]);
       if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot);
       uint8_t* dst = const_cast<uint8_t*>(c.values);
-      if (tot == 0 || !dst || (a.dbg & 16)) continue;
+      if (tot == 0 || !dst) continue;
       const int64_t cap = c.capacity;
       if (c.kind == kBytes) {
         const int64_t p0 = gb, p1 = gb + tot;
@@ -1996,18 +1776,12 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
                                                               const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               uint64_t* __restrict__ status,
-                                                              uint32_t* __restrict__ ticket,
                                                               int nseq) {
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
   __shared__ __attribute__((aligned(16))) uint8_t oimg[kStrStage];
   __shared__ DecodeShared sh;
   // tile = blockIdx; the look-back helps itself (look_back_help), as in decode_var_reg.
-  // FURY_VAR_DBG bit 4096: a ticket (tiles numbered in start order), for A/B.
-  if (kLookBack && (a.dbg & 4096)) {
-    if (threadIdx.x == 0) sh.blk = atomicAdd(ticket, 1u);
-    __syncthreads();
-  }
-  const int64_t b = (kLookBack && (a.dbg & 4096)) ? sh.blk : static_cast<int64_t>(blockIdx.x);
+  const int64_t b = static_cast<int64_t>(blockIdx.x);
   const int64_t r0 = b * kThreads;
   const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
   const int64_t rbeg = offs[r0];
@@ -2033,14 +1807,10 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, int64_t cap,
                           int64_t ntiles, hipStream_t stream);
 int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                          uint64_t* status, uint32_t* ticket, uint32_t img, bool wide,
-                          int64_t nb, int64_t nbr, hipStream_t stream);
-int lds_decode_max_seq();
-int launch_decode_var_lds(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                          uint64_t* status, uint32_t* ticket, int nseq, int nt, uint32_t stage,
-                          uint32_t img, int64_t ntiles, hipStream_t stream);
+                          uint64_t* status, uint32_t img, bool wide, int64_t nb, int64_t nbr,
+                          hipStream_t stream);
 int launch_decode_var_reg_hi(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                             uint64_t* status, uint32_t* ticket, uint32_t img, bool wide,
-                             int64_t nb, int64_t nbr, hipStream_t stream);
+                             uint64_t* status, uint32_t img, bool wide, int64_t nb, int64_t nbr,
+                             hipStream_t stream);
 
 }  // namespace fury

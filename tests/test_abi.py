@@ -163,12 +163,15 @@ def test_new_entry_points_reject_bad_arguments_without_touching_gpu():
     assert L.fury_unframe_rows(s.handle, None, 10, 1, None, None, None) == 1
     assert L.fury_unframe_rows(s.handle, None, -1, 1, None, None, None) == 1
     # tuning knobs: range checks, unknown keys
-    assert L.fury_set_tuning(b"fixed_variant", 1024) == 1
-    assert L.fury_set_tuning(b"var_decode", 5) == 1
+    assert L.fury_set_tuning(b"lookback_help", 2) == 1
     assert L.fury_set_tuning(b"unframe", 2) == 1
     assert L.fury_set_tuning(b"no_such_knob", 0) == 1
+    # the measured-slower kernel variants were removed in round 3: their keys are unknown now
+    assert L.fury_set_tuning(b"fixed_variant", 54) == 1
+    assert L.fury_set_tuning(b"var_decode", 0) == 1
+    assert L.fury_set_tuning(b"gen_decode", 0) == 1
     assert L.fury_get_tuning(b"no_such_knob") == -1
-    assert L.fury_get_tuning(b"fixed_variant") == 54
+    assert L.fury_get_tuning(b"lookback_help") == 0
 
 
 def test_host_decode_empty_batch_writes_arrow_offsets():

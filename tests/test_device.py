@@ -189,55 +189,62 @@ def test_frame_unframe_roundtrip(oracle, dev):
             other.unframe(stream, n)
 
 
-@pytest.mark.parametrize("variant", [6, 14, 22, 38, 54, 62, 118, 134, 182, 254, 310, 566, 7, 0])
-def test_fixed_variants_bit_exact(oracle, dev, variant):
-    """Every fixed-width kernel variant (tuning 'fixed_variant') writes the oracle's rows and
-    decodes them back, including ragged last tiles (odd row counts for the pair mode)."""
-    from fury_amd import _native as N
-    old = N.lib().fury_get_tuning(b"fixed_variant")
-    assert N.lib().fury_set_tuning(b"fixed_variant", variant) == 0
-    try:
-        for n in (1, 3, 63, 65, 129, 1001):
-            _roundtrip(oracle, "struct100", n, dev, seed=n)
-    finally:
-        N.lib().fury_set_tuning(b"fixed_variant", old)
+def test_fixed_paths_bit_exact(oracle, dev):
+    """The fixed-width kernels the library ships (fast path: 8-byte columns, no validity; pair-mode
+    decode and its fallback when a column is not 16-byte aligned; the general path: narrow types
+    and validity) write the oracle's rows and decode them back, including ragged last tiles (odd
+    row counts for the pair mode)."""
+    from fury_amd.encoder import Encoders, column_to_host
+    for n in (1, 3, 63, 65, 129, 1001):
+        _roundtrip(oracle, "struct100", n, dev, seed=n)
+        _roundtrip(oracle, "narrow", n, dev, seed=n)
+    # a column at an 8- but not 16-byte aligned address: the decode takes the non-pair kernel
+    fields = SCHEMAS["struct100"]
+    n = 257
+    host = gen_columns("struct100", fields, n, seed=5)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(_dev_cols(host, dev), n)
+    cols = enc.alloc_columns(n, validity=False)
+    pad = torch.empty(n * 8 + 8, dtype=torch.uint8, device=dev)
+    cols[3].values = pad[8:]
+    enc.decode_into(batch, cols)
+    want, _ = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, None, n)
+    assert_columns_equal(fields, [column_to_host(c) for c in cols], ref, n)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
-def test_var_decode_modes_bit_exact(oracle, dev, mode):
-    """Every variable-length decode mode (tuning 'var_decode': one-pass look-back with 256- or
-    512-row tiles, register- or LDS-staged, sizing pass + decode) decodes to the oracle's
-    columns."""
+def _roundtrips_var(oracle, dev, seed0):
+    for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
+                    ("nested", 4097), ("beanb", 700)):
+        _roundtrip(oracle, name, n, dev, seed=n + seed0)
+    _roundtrip(oracle, "mixed", 3000, dev, seed=seed0, str_max=600)   # tiles beyond the stage
+    _roundtrip(oracle, "nested", 2000, dev, seed=seed0, list_max=200)
+
+
+def test_var_decode_bit_exact(oracle, dev):
+    """The variable-length decode (one pass, Arrow offsets chained across tiles by a decoupled
+    look-back) decodes to the oracle's columns on ragged tiles and tiles beyond the LDS image."""
     from fury_amd import _native as N
-    old = N.lib().fury_get_tuning(b"var_decode")
-    assert N.lib().fury_set_tuning(b"var_decode", mode) == 0
-    try:
-        for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
-                        ("nested", 4097), ("beanb", 700)):
-            _roundtrip(oracle, name, n, dev, seed=n + mode)
-        _roundtrip(oracle, "mixed", 3000, dev, seed=mode, str_max=600)   # tiles beyond the stage
-        _roundtrip(oracle, "nested", 2000, dev, seed=mode, list_max=200)
-    finally:
-        N.lib().fury_set_tuning(b"var_decode", old)
+    _roundtrips_var(oracle, dev, 0)
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
-@pytest.mark.parametrize("bits", ["32768", "4096"])
-def test_var_decode_tile_order_bit_exact(oracle, dev, bits, monkeypatch):
+def test_var_decode_lookback_help_bit_exact(oracle, dev):
     """The variable-length decodes number tiles by blockIdx and let a look-back compute a silent
-    predecessor's aggregate from its rows (look_back_help).  FURY_VAR_DBG 32768 makes every
-    look-back help at once -- the path a late-dispatched predecessor takes -- and 4096 restores
-    the ticket; both must decode to the oracle's columns."""
+    predecessor's aggregate from its rows (look_back_help).  Tuning "lookback_help" makes every
+    look-back help at once -- the path a late-dispatched predecessor takes -- and the results must
+    still be the oracle's columns, for the register-staged (<= 16 fields) and the 17-256-field
+    kernels."""
     from fury_amd import _native as N
-    monkeypatch.setenv("FURY_VAR_DBG", bits)
-    for name, n in (("mixed", 1), ("mixed", 513), ("mixed", 20_001), ("narrow", 1025),
-                    ("nested", 4097), ("beanb", 700)):
-        _roundtrip(oracle, name, n, dev, seed=n + int(bits))
-    _roundtrip(oracle, "mixed", 3000, dev, seed=7, str_max=600)
-    for ncols, n in ((33, 2049), (17, 20_001)):    # the 17-256-field kernel (decode_var_kernel)
-        fields = _wide_fields(ncols)
-        host = gen_columns("wide", fields, n, seed=ncols, null_pct=10, str_max=40, list_max=8)
-        _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    assert N.lib().fury_set_tuning(b"lookback_help", 1) == 0
+    try:
+        _roundtrips_var(oracle, dev, 32768)
+        for ncols, n in ((33, 2049), (17, 20_001)):    # the 17-256-field kernel (decode_var_kernel)
+            fields = _wide_fields(ncols)
+            host = gen_columns("wide", fields, n, seed=ncols, null_pct=10, str_max=40, list_max=8)
+            _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    finally:
+        N.lib().fury_set_tuning(b"lookback_help", 0)
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
@@ -781,12 +788,7 @@ def test_wide_var_schemas_bit_exact(oracle, dev, ncols, n, str_max):
     w = ArrowWriter(enc)
     w.write(batch)
     assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
-    old = N.lib().fury_get_tuning(b"var_decode")
-    assert N.lib().fury_set_tuning(b"var_decode", 1) == 0
-    try:
-        dec = [column_to_host(c) for c in enc.decode_batch(batch)]
-    finally:
-        N.lib().fury_set_tuning(b"var_decode", old)
+    dec = [column_to_host(c) for c in enc.decode_batch(batch, sizing="bound")]
     assert_columns_equal(fields, dec, ref, n)
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
@@ -1264,18 +1266,16 @@ def _engine_schemas():
     }
 
 
-@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("name", ["nested7", "foo", "deep_lists", "struct_chain", "maps"])
-def test_nested_decode_engines_oracle_exact(oracle, dev, name, mode):
-    """Both nested decode engines (tuning gen_decode: 0 level-by-level, 1 thread-per-row) return
-    the oracle's columns byte for byte on schemas with lists of lists of bools, struct chains
+def test_nested_decode_oracle_exact(oracle, dev, name):
+    """The level-by-level nested decode returns the oracle's columns byte for byte on schemas with lists of lists of bools, struct chains
     with DECIMAL / BINARY / FLOAT32 / TIMESTAMP children, maps with scalar keys, lists of maps of
     structs; the plan re-executes identically; empty batch."""
     from fury_amd import _native as N
     from fury_amd.beans import beans_to_columns, columns_to_beans
     from fury_amd.encoder import Encoders, column_to_host
     fields = _engine_schemas()[name]
-    rng = np.random.default_rng(len(name) * 7 + mode)
+    rng = np.random.default_rng(len(name) * 7)
     n = 3001
     beans = [{f.name: _random_value(f, rng) for f in fields} for _ in range(n)]
     host = beans_to_columns(fields, beans)
@@ -1284,15 +1284,9 @@ def test_nested_decode_engines_oracle_exact(oracle, dev, name, mode):
     batch = enc.encode_batch(_dev_cols(host, dev), n)
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
-    L = N.lib()
-    old = L.fury_get_tuning(b"gen_decode")
-    assert L.fury_set_tuning(b"gen_decode", mode) == 0
-    try:
-        dec = enc.decode_batch(batch)
-        again = enc.decode_batch(batch)
-        empty = enc.decode_batch(type(batch)(batch.rows, batch.row_offsets[:1], 0, batch.schema_hash))
-    finally:
-        L.fury_set_tuning(b"gen_decode", old)
+    dec = enc.decode_batch(batch)
+    again = enc.decode_batch(batch)
+    empty = enc.decode_batch(type(batch)(batch.rows, batch.row_offsets[:1], 0, batch.schema_hash))
     hdec = [column_to_host(c) for c in dec]
     assert_columns_equal(fields, hdec, oracle.decode(fields, want, want_offs, n), n)
     assert_columns_equal(fields, [column_to_host(c) for c in again], hdec, n)
