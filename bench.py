@@ -28,7 +28,15 @@ sys.path.insert(0, ROOT)
 
 METRIC = "row-format encode+decode GB/s (device-resident), Struct-100, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
-CPU_THREADS = 16               # the GPU box's CPU share per GPU (nproc shows the whole machine)
+# CPU baseline threads: the GPU box's CPU share of one GPU job -- OMP_NUM_THREADS, which the box
+# sets to that share (16; nproc and the affinity mask show the whole 256-thread machine, and jobs
+# must size their pools to the share), else the affinity mask split over a node's 8 GPUs.
+def cpu_threads():
+    mine, _ = _host_cpus()
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return min(int(env), mine)
+    return max(1, mine // 8)
 DEFAULT_ROWS = {"struct100": 1_000_000, "mixed": 10_000_000, "nested": 4_000_000}
 
 
@@ -72,13 +80,9 @@ def make_device_columns(name, fields, rows, start, dev):
     """Synthetic columns resident in HBM, SplitMix64 keyed by (column, GLOBAL row index), so a
     shard holds exactly the rows a single-GPU run over the whole range would.  Struct-100 is
     generated on the device (fury_amd.workloads.gen_columns_torch, bit-identical to the host
-    generator); variable-length workloads on the host, copied once before timing."""
-    from fury_amd.encoder import column_to_device
-    from fury_amd.workloads import gen_columns, gen_columns_torch
-    if name == "struct100":
-        return gen_columns_torch(name, fields, rows, seed=1234, start=start, device=dev)
-    host = gen_columns(name, fields, rows, seed=1234, start=start)
-    return [column_to_device(c, dev) for c in host]
+    generator, tests/test_workloads.py)."""
+    from fury_amd.workloads import gen_columns_torch
+    return gen_columns_torch(name, fields, rows, seed=1234, start=start, device=dev)
 
 
 def _host_cpus():
@@ -93,13 +97,14 @@ def _host_cpus():
 
 def cpu_baseline(name, fields, budget_s, sample_rows):
     """Oracle C restatement of the Java writer/reader (kind "port") timed on this host on the
-    bench workload's own batch (``sample_rows`` rows, default = the full C2 batch of 1M rows):
-    1 thread over the whole batch, then CPU_THREADS threads each encoding + decoding a
-    contiguous slice of it (one encoder per thread, like the reference's thread-confined
-    RowEncoder; ctypes releases the GIL inside the C calls)."""
+    bench workload's own batch (``sample_rows`` rows, default = the full C2 batch of 1M rows;
+    1M rows of the mixed / nested batches): 1 thread over the whole batch, then cpu_threads()
+    threads each encoding + decoding a contiguous slice of it (one encoder per thread, like the
+    reference's thread-confined RowEncoder; variable-length slices carry rebased offsets; ctypes
+    releases the GIL inside the C calls)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
-    from fury_amd.workloads import gen_columns
+    from fury_amd.workloads import gen_columns, slice_columns
     var = name != "struct100"
     host = gen_columns(name, fields, sample_rows, seed=99)
 
@@ -126,19 +131,16 @@ def cpu_baseline(name, fields, budget_s, sample_rows):
            "sample": f"{reps} x encode+decode of the {sample_rows}-row {name} batch "
                      f"(oracle/row_oracle.c, toRow/fromRow restatement, 1 thread) in {dt:.1f} s",
            "host_cpus": {"affinity": mine, "nproc": machine}}
-    if var:
-        return out     # slicing variable-length columns per thread is not implemented
-    threads = CPU_THREADS
+    threads = cpu_threads()
     bounds = [(sample_rows * t // threads, sample_rows * (t + 1) // threads) for t in range(threads)]
-    from fury_amd.workloads import Column
-    parts = [[Column(values=c.values[b:e]) for c in host] for b, e in bounds]
+    parts = [slice_columns(fields, host, b, e) for b, e in bounds]
     stop = time.perf_counter() + budget_s / 2
 
     def work(t):
         k, m = 0, bounds[t][1] - bounds[t][0]
         while time.perf_counter() < stop:
-            r, _ = O.encode(fields, parts[t], m)
-            O.decode(fields, r, None, m, with_validity=False)
+            r, o = O.encode(fields, parts[t], m)
+            O.decode(fields, r, o if var else None, m, with_validity=False)
             k += 1
         return k
     t0 = time.perf_counter()
@@ -149,7 +151,9 @@ def cpu_baseline(name, fields, budget_s, sample_rows):
     out["threads"] = {"value": round(per_pass * done / dt / 1e9, 4), "unit": "GB/s",
                       "cores": threads,
                       "sample": f"{sum(laps)} x encode+decode of 1/{threads} slices of the "
-                                f"{sample_rows}-row batch on {threads} threads in {dt:.1f} s"}
+                                f"{sample_rows}-row batch on {threads} threads in {dt:.1f} s",
+                      "why_cores": "the box's CPU share of one GPU job (OMP_NUM_THREADS); "
+                                   "host_cpus shows the machine"}
     return out
 
 
@@ -289,9 +293,7 @@ def run(args):
     if os.path.exists(pmc_file) and n == DEFAULT_ROWS[args.workload]:
         pm = json.load(open(pmc_file))
         traffic = pm.get(f"{dominant[0]}_hbm_bytes_per_launch")
-    data = ("synthetic SplitMix64 values keyed by (column, global row) generated in HBM; "
-            "no dataset") if args.workload == "struct100" else \
-        "synthetic SplitMix64 columns keyed by (column, global row), copied to HBM once; no dataset"
+    data = "synthetic SplitMix64 columns keyed by (column, global row) generated in HBM; no dataset"
     config = {"workload": {"struct100": "Struct-100 encode+decode (configs[1])",
                            "mixed": "mixed int32/int64/double + 3 utf8 + nulls (configs[2])",
                            "nested": "id/score + list<int64>: encode + row->Arrow columns "
@@ -335,7 +337,7 @@ def run(args):
         line["e2e_pcie"] = e2e
     if world == 1 and not args.no_cpu_baseline:     # the CPU baseline is an N=1 figure
         line["cpu_baseline"] = cpu_baseline(args.workload, fields, args.cpu_seconds,
-                                            args.cpu_rows or n)
+                                            args.cpu_rows or min(n, 1_000_000))
     print(json.dumps(line), flush=True)
     orch.close()
 

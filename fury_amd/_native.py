@@ -73,8 +73,11 @@ SIGNATURES = {
     "fury_decode_execute": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I32, _P]),
     "fury_decode_plan_destroy": (None, [_P]),
     "fury_device_status": (ctypes.c_int, [_P]),
+    "fury_trim_workspace": (ctypes.c_int, [_I32]),
     "fury_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _I32]),
     "fury_get_tuning": (_I32, [ctypes.c_char_p]),
+    "fury_arrow_append": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64,
+                                         ctypes.POINTER(FuryColumn), _I64, _P]),
     "fury_frame_rows": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P]),
     "fury_unframe_rows": (ctypes.c_int, [_P, _P, _I64, _I64, _P, _P, _P]),
     "fury_host_alloc": (ctypes.c_int, [_I64, ctypes.POINTER(ctypes.c_void_p)]),

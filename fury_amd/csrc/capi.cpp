@@ -37,7 +37,7 @@ uint32_t* device_error_word() {
       (void)hipHostFree(p);
       return;
     }
-    *static_cast<volatile uint32_t*>(p) = 0;
+    std::memset(p, 0, 64);
     g_err_host = static_cast<uint32_t*>(p);
     g_err_dev = static_cast<uint32_t*>(d);
   });
@@ -48,18 +48,43 @@ std::atomic<int64_t> g_err_taken{0};
 
 int64_t device_error_count() {
   const volatile uint32_t* w = g_err_host;
-  return g_err_taken.load() + (w && *w ? 1 : 0);
+  return g_err_taken.load() + (w && w[kErrLookBack] ? 1 : 0);
+}
+
+// Where a kernel found the problem: a row index, or (bit 63 set) a nested schema node and Arrow
+// entry (err_where_entry).
+static std::string where_text(uint64_t w) {
+  if (!(w >> 63)) return "row " + std::to_string(w);
+  return "schema node " + std::to_string((w >> 40) & 0x7fffff) + ", Arrow entry " +
+         std::to_string(w & ((1ull << 40) - 1));
 }
 
 int take_device_error() {
   if (!g_err_host) return FURY_OK;
   volatile uint32_t* w = g_err_host;
-  if (*w == 0) return FURY_OK;
-  *w = 0;
-  g_err_taken.fetch_add(1);
-  return set_error(FURY_ERR_DEVICE,
-                   "an earlier asynchronous launch failed on the device (a decoupled look-back "
-                   "gave up waiting): the outputs of that call are invalid");
+  const uint32_t lb = w[kErrLookBack], oob = w[kErrBounds], map = w[kErrMapCount];
+  if (!lb && !oob && !map) return FURY_OK;
+  const uint64_t oob_at = static_cast<uint64_t>(w[kErrBounds + 1]) |
+                          (static_cast<uint64_t>(w[kErrBounds + 2]) << 32);
+  const uint64_t map_at = static_cast<uint64_t>(w[kErrMapCount + 1]) |
+                          (static_cast<uint64_t>(w[kErrMapCount + 2]) << 32);
+  for (int i = 0; i < 16; i++) w[i] = 0;
+  if (lb) {
+    g_err_taken.fetch_add(1);
+    return set_error(FURY_ERR_DEVICE,
+                     "an earlier asynchronous launch failed on the device (a decoupled look-back "
+                     "gave up waiting): the outputs of that call are invalid");
+  }
+  if (oob)
+    return set_error(FURY_ERR_OUT_OF_BOUNDS,
+                     "decode: " + where_text(oob_at) +
+                         " has a variable-length value, array or map header outside the batch's "
+                         "row bytes (MemoryBuffer bounds check); the outputs of that call are "
+                         "invalid");
+  return set_error(FURY_ERR_UNSUPPORTED,
+                   "decode: " + where_text(map_at) +
+                       ": map key and value arrays have different element counts "
+                       "(BinaryMap.pointTo); the outputs of that call are invalid");
 }
 
 // Pinned staging ring for per-call column tables: the host table is copied into the ring, then
@@ -78,13 +103,16 @@ std::vector<RingUse> g_ring_pending;
 }  // namespace
 
 // ---- device workspace cache -------------------------------------------------------------------
-// Per-call workspaces (scan scratch, column tables, decode plans) come from power-of-two size
-// classes cached per device instead of hipMallocAsync / hipFreeAsync: on the box hipFreeAsync
-// took ~110 us of host time per call (HIP API trace of scripts/ab_generic.py), more than most of
-// the kernels it serves.  A freed block records an event on its stream; its next user's stream
-// waits for that event on the device (hipStreamWaitEvent, no host sync) -- also when the handles
-// are equal, since a destroyed stream's handle can be reused.  Cached free bytes are capped
-// (kCacheCap); beyond that blocks go back to the pool.
+// Per-call workspaces (scan scratch, column tables, decode plans) come from size classes cached
+// per device instead of hipMallocAsync / hipFreeAsync: on the box hipFreeAsync took ~110 us of
+// host time per call (HIP API trace of scripts/ab_generic.py), more than most of the kernels it
+// serves.  A freed block records an event on its stream; its next user's stream waits for that
+// event on the device (hipStreamWaitEvent, no host sync) -- also when the handles are equal,
+// since a destroyed stream's handle can be reused.  Classes: powers of two up to 64 MB, 2 MB
+// multiples above (a 5.8 GB plan array is not rounded to 8 GB).  Cached free bytes are capped
+// (kCacheCap, 2 GB: the cache exists for per-call workspaces, not for whole batches); beyond that
+// blocks go back to the pool.  An allocation that fails releases every idle cached block and
+// trims the stream pool, then retries once; fury_trim_workspace() does the same on request.
 namespace {
 struct CacheBlock {
   void* p;
@@ -96,13 +124,50 @@ std::mutex g_cache_mu;
 std::vector<CacheBlock> g_cache_free;
 std::unordered_map<void*, std::pair<size_t, int>> g_cache_live;
 size_t g_cache_bytes = 0;                     // bytes in g_cache_free
-constexpr size_t kCacheCap = size_t(16) << 30;
+constexpr size_t kCacheCap = size_t(2) << 30;
+
+size_t size_class(int64_t bytes) {
+  const size_t b = static_cast<size_t>(bytes > 0 ? bytes : 1);
+  constexpr size_t kBig = size_t(64) << 20, kStep = size_t(2) << 20;
+  if (b > kBig) return (b + kStep - 1) / kStep * kStep;
+  size_t cls = 4096;
+  while (cls < b) cls <<= 1;
+  return cls;
+}
+
+// Frees every idle cached block of `device` (after the work that last used it) and trims that
+// device's stream pool.  Returns the bytes released.
+size_t release_cached(int device) {
+  std::vector<CacheBlock> drop;
+  {
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    for (size_t i = 0; i < g_cache_free.size();) {
+      if (g_cache_free[i].device == device) {
+        drop.push_back(g_cache_free[i]);
+        g_cache_bytes -= g_cache_free[i].cls;
+        g_cache_free[i] = g_cache_free.back();
+        g_cache_free.pop_back();
+      } else {
+        i++;
+      }
+    }
+  }
+  size_t bytes = 0;
+  for (CacheBlock& b : drop) {
+    (void)hipEventSynchronize(b.ev);
+    (void)hipEventDestroy(b.ev);
+    (void)hipFree(b.p);
+    bytes += b.cls;
+  }
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+  return bytes;
+}
 }  // namespace
 
 int dev_alloc(int64_t bytes, hipStream_t stream, void** out) {
   *out = nullptr;
-  size_t cls = 4096;
-  while (cls < static_cast<size_t>(bytes > 0 ? bytes : 1)) cls <<= 1;
+  const size_t cls = size_class(bytes);
   int device = 0;
   (void)hipGetDevice(&device);
   {
@@ -123,7 +188,13 @@ int dev_alloc(int64_t bytes, hipStream_t stream, void** out) {
     }
   }
   keep_pool(device);
-  const int st = check_hip(hipMallocAsync(out, cls, stream), "hipMallocAsync");
+  hipError_t e = hipMallocAsync(out, cls, stream);
+  if (e != hipSuccess) {              // idle cached blocks may be what is missing: release, retry
+    (void)hipGetLastError();
+    release_cached(device);
+    e = hipMallocAsync(out, cls, stream);
+  }
+  const int st = check_hip(e, "hipMallocAsync");
   if (st) return st;
   std::lock_guard<std::mutex> lock(g_cache_mu);
   g_cache_live[*out] = {cls, device};
@@ -602,6 +673,7 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
   if (nrows > 0 && (!rows || !row_offsets))
     return set_error(FURY_ERR_INVALID_ARGUMENT, "rows / row_offsets is null");
+  if (const int e = take_device_error()) return e;
   hipStream_t hs = static_cast<hipStream_t>(stream);
   const int nn = static_cast<int>(s->nodes.size());
   fury_decode_plan* p = new fury_decode_plan();
@@ -611,8 +683,11 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   p->nrows = nrows;
   std::vector<int64_t> totals(2 * nn, 0);
   if (nrows > 0) {
-    const int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
+    // lv_prepare synchronises `stream`: rows whose values leave the batch are reported here
+    int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
+    if (!st) st = take_device_error();
     if (st) {
+      if (p->lv) lv_free(p->lv);
       delete p;
       return st;
     }
@@ -650,6 +725,18 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
   if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
   delete p;
+}
+
+int fury_trim_workspace(int32_t device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_trim_workspace: no such device");
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  release_cached(device);
+  return check_hip(hipSetDevice(cur), "hipSetDevice");
 }
 
 int fury_device_status(void* stream) {

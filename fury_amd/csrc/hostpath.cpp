@@ -79,13 +79,14 @@ struct Streams {
     for (int g = 0; g < kStages; g++) s[g] = it->second[g];
     return FURY_OK;
   }
+  // Synchronous calls report what their kernels found (decode bounds, map counts) here.
   int sync() {
     int st = FURY_OK;
     for (auto& x : s) {
       const int e = check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
       if (!st) st = e;
     }
-    return st;
+    return st ? st : take_device_error();
   }
 };
 
@@ -654,7 +655,8 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     const int64_t vb = node_values_bytes(t.type_id, m, b);
     if (d.values && vb > 0) (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
   }
-  return check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+  st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+  return st ? st : take_device_error();
 }
 
 int fury_host_alloc(int64_t bytes, void** out) {

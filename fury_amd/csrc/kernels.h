@@ -87,10 +87,15 @@ struct VarArgs {
   uint32_t* err;             // host-visible device error word (device_error_word()) or NULL
 };
 
-// Host-visible device error word: host-pinned, mapped memory a kernel sets (system-scope store)
-// when it cannot produce a valid result (a look-back that gave up).  Allocated once per process;
-// NULL if the runtime cannot map host memory.  take_device_error() reads and clears it and sets
-// the thread's last error (FURY_ERR_DEVICE) when it was raised.
+// Host-visible device error words: host-pinned, mapped memory (16 x 32 bit) that kernels set with
+// system-scope STORES (no read-modify-write over PCIe) when they cannot produce a valid result:
+//   [kErrLookBack]            a look-back that gave up (FURY_ERR_DEVICE)
+//   [kErrBounds], [+1, +2]    a decode read that would leave the batch, and where (64-bit: a row,
+//                             or bit 63 | node << 40 | entry) (FURY_ERR_OUT_OF_BOUNDS)
+//   [kErrMapCount], [+1, +2]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
+// Allocated once per process; NULL if the runtime cannot map host memory.  take_device_error()
+// reads and clears them and sets the thread's last error when one was raised.
+constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8;
 uint32_t* device_error_word();
 int take_device_error();
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
@@ -99,6 +104,32 @@ int64_t device_error_count();        // failures raised so far (taken or pending
 // their per-call host cost.
 int dev_alloc(int64_t bytes, hipStream_t stream, void** out);
 void dev_free(void* p, hipStream_t stream);
+
+// Decode bounds (round 3).  Every byte a decode reads lies in [0, total) of the rows buffer, total
+// = the batch's row bytes (row_offsets[nrows]): the reference's getters read through MemoryBuffer,
+// whose slice / get throw IndexOutOfBoundsException for a range past the buffer (fury-core
+// memory/MemoryBuffer.java:2500-2519, through UnsafeTrait.getBuffer / getBinary,
+// format/row/binary/UnsafeTrait.java:44-51,118-129, and the getInt64 of an array header,
+// BinaryArray.pointTo :69-78).  A value that fails decodes as null, the kernel records where in the
+// error words and the call reports FURY_ERR_OUT_OF_BOUNDS; nothing outside the batch is read.
+// A negative size or element count (NegativeArraySizeException / a failed assert there) fails too.
+__device__ __forceinline__ bool span_ok(int64_t p, int64_t len, int64_t total) {
+  return p >= 0 && len >= 0 && len <= total - p;
+}
+__device__ __forceinline__ void raise_at(uint32_t* err, int slot, uint64_t where) {
+  if (!err) return;
+  __hip_atomic_store(err + slot + 1, static_cast<uint32_t>(where), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err + slot + 2, static_cast<uint32_t>(where >> 32), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void raise_oob(uint32_t* err, int64_t row) {
+  raise_at(err, kErrBounds, static_cast<uint64_t>(row));
+}
+__device__ __forceinline__ uint64_t err_where_entry(int node, int64_t entry) {
+  return (1ull << 63) | (static_cast<uint64_t>(node) << 40) | static_cast<uint64_t>(entry);
+}
 
 // Copies a host column table to device memory on `stream` (stream-ordered: through a pinned
 // staging ring, no host synchronisation); the table is freed stream-ordered when the holder goes.

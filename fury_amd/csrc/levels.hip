@@ -78,7 +78,8 @@ struct LvArgs {
   int32_t ntop;
   int32_t root;
   int32_t nlist;                              // row-major launches: nodes in the list
-  int32_t dbg;                                // DIAGNOSTIC phase bits (FURY_LV_DBG), else 0
+  int32_t pad_;
+  uint32_t* err;                              // device error words (bounds, map counts)
 };
 
 // LvSrc records through the global address space (one 16-B load / store)
@@ -165,36 +166,114 @@ struct LvVal {
   int64_t slot;            // absolute slot offset (< 0: the value is at base)
 };
 
-__device__ __forceinline__ LvVal lv_source(const LvArgs& a, const LvNode& n, int64_t e) {
+// Slot width of a node's values inside a BinaryArray (BinaryArrayWriter elementSize: the type
+// width, 8 for variable-length elements).
+__device__ __forceinline__ int64_t elem_size(int t) {
+  const int w = lwidth(t);
+  return w > 0 ? w : 8;
+}
+
+// A BinaryArray at absolute byte p whose elements are of node `en`: its header, null bits and
+// element slots lie inside the batch; returns numElements (-1: outside / negative).
+__device__ __forceinline__ int64_t array_ok(const LvArgs& a, int64_t p, int en_type, int64_t total) {
+  if (!span_ok(p, 8, total)) return -1;
+  const int64_t m = static_cast<int32_t>(lld8(a.rows + p));
+  if (m < 0 || !span_ok(p, 8 + lbm(m) + m * elem_size(en_type), total)) return -1;
+  return m;
+}
+
+// Bounds check of a non-null value (the reference reads it through MemoryBuffer's bounds checks,
+// see span_ok in kernels.h): STRING / BINARY bytes, DECIMAL's 16 bytes, a nested row's null bits
+// and slots, a LIST's array, a MAP's [key bytes][key array][value array] with equal element counts
+// (BinaryMap.pointTo, BinaryMap.java:62-77: UnsupportedOperationException otherwise).  Returns the
+// value's absolute start, or -1 (the value decodes as null; the error words record where).
+// Every pass (count, expand, write) checks through this one function, so they agree.
+__device__ __forceinline__ int64_t lv_value(const LvArgs& a, const LvNode& n, const LvVal& v,
+                                            int64_t total, uint32_t* size, uint64_t where) {
+  int64_t vp;
+  int64_t sz = 0;
+  if (v.slot < 0) {
+    vp = v.base;                                                // a top-level array / map
+  } else {
+    const uint64_t oas = lld8(a.rows + v.slot);
+    sz = static_cast<int32_t>(oas);
+    vp = v.base + static_cast<int32_t>(oas >> 32);
+  }
+  bool ok;
+  switch (n.type) {
+    case FURY_TYPE_STRING:
+    case FURY_TYPE_BINARY:
+      ok = span_ok(vp, sz, total);
+      break;
+    case FURY_TYPE_DECIMAL:
+      ok = span_ok(vp, 16, total);
+      break;
+    case FURY_TYPE_STRUCT:
+      ok = span_ok(vp, lbm(n.num_children) + 8 * n.num_children, total);
+      break;
+    case FURY_TYPE_LIST:
+      ok = array_ok(a, vp, a.nodes[n.first_child].type, total) >= 0;
+      break;
+    case FURY_TYPE_MAP: {
+      ok = span_ok(vp, 8, total);
+      if (!ok) break;
+      const int64_t kb = static_cast<int32_t>(lld8(a.rows + vp));   // getInt32 of the header
+      const int64_t nk = kb >= 0 ? array_ok(a, vp + 8, a.nodes[n.first_child].type, total) : -1;
+      const int64_t nv = kb >= 0 ? array_ok(a, vp + 8 + kb, a.nodes[n.first_child + 1].type, total) : -1;
+      ok = nk >= 0 && nv >= 0;
+      if (ok && nk != nv) {
+        raise_at(a.err, kErrMapCount, where);
+        *size = 0;
+        return -1;
+      }
+      break;
+    }
+    default:
+      ok = true;
+  }
+  if (!ok) {
+    raise_at(a.err, kErrBounds, where);
+    *size = 0;
+    return -1;
+  }
+  *size = static_cast<uint32_t>(sz);
+  return vp;
+}
+
+__device__ __forceinline__ int64_t lv_total(const LvArgs& a) { return gl(a.offs)[a.nrows]; }
+
+__device__ __forceinline__ LvVal lv_source(const LvArgs& a, const LvNode& n, int64_t e,
+                                           int64_t total) {
   if (n.kind == kLvTop) {
     const int64_t base = gl(a.offs)[e];
     if (a.root) return {false, base, -1};                       // a top-level array / map
+    if (!span_ok(base, lbm(a.ntop) + 8 * a.ntop, total)) {      // the row itself is outside
+      raise_oob(a.err, e);
+      return {true, 0, -1};
+    }
     return {lbit(a.rows + base, n.slot), base, base + lbm(a.ntop) + 8 * n.slot};
   }
   const LvSrc s = ld_src(n.src, e);
   return {s.base < 0, s.base, s.off < 0 ? -1 : s.base + s.off};
 }
 
-__device__ __forceinline__ const uint8_t* lv_var(const LvArgs& a, const LvVal& v, uint32_t* size) {
-  if (v.slot < 0) {
-    *size = 0;
-    return a.rows + v.base;
-  }
-  const uint64_t oas = lld8(a.rows + v.slot);
-  *size = static_cast<uint32_t>(oas);
-  return a.rows + v.base + static_cast<int32_t>(oas >> 32);
+// Count of a checked non-null value at absolute vp: LIST elements, MAP entries (key array
+// elements), STRING / BINARY bytes.
+__device__ __forceinline__ int64_t value_count(const LvArgs& a, int type, int64_t vp, uint32_t size) {
+  if (type == FURY_TYPE_LIST) return static_cast<int32_t>(lld8(a.rows + vp));
+  if (type == FURY_TYPE_MAP) return static_cast<int32_t>(lld8(a.rows + vp + 8));
+  return size;
 }
 
 // Pass 1 of a level: per entry, elements (LIST / MAP) or payload bytes (STRING / BINARY).
-__device__ __forceinline__ void count_entry(const LvArgs& a, const LvNode& n, int64_t e) {
-  const LvVal v = lv_source(a, n, e);
+__device__ __forceinline__ void count_entry(const LvArgs& a, const LvNode& n, int ni, int64_t e,
+                                            int64_t total) {
+  const LvVal v = lv_source(a, n, e, total);
   int64_t c = 0;
   if (!v.null) {
     uint32_t size;
-    const uint8_t* vp = lv_var(a, v, &size);
-    if (n.type == FURY_TYPE_LIST) c = static_cast<int32_t>(lld8(vp));
-    else if (n.type == FURY_TYPE_MAP) c = static_cast<int32_t>(lld8(vp + 8));
-    else c = size;
+    const int64_t vp = lv_value(a, n, v, total, &size, err_where_entry(ni, e));
+    if (vp >= 0) c = value_count(a, n.type, vp, size);
   }
   gl(n.start)[e] = c;
 }
@@ -205,50 +284,46 @@ __device__ __forceinline__ void count_entry(const LvArgs& a, const LvNode& n, in
 template <bool kRows>
 __global__ __launch_bounds__(kLv) void lv_count(LvArgs a) {
   const int64_t e = static_cast<int64_t>(blockIdx.x) * kLv + threadIdx.x;
+  const int64_t total = lv_total(a);
   if (kRows) {
     if (e >= a.nrows) return;
     // batches of kB fields: all their loads are issued before any count is stored (a store to
     // the count buffers may alias the row bytes for the compiler, which would serialise them)
     constexpr int kB = 8;
-    const int64_t base = gl(a.offs)[e];
-    const uint8_t* row = a.rows + base;
-    const int64_t slots = lbm(a.ntop);
     for (int j0 = 0; j0 < a.nlist; j0 += kB) {
       int64_t c[kB];
 #pragma unroll
       for (int u = 0; u < kB; u++) {
         c[u] = 0;
         if (j0 + u >= a.nlist) continue;
-        const LvNode& n = a.nodes[a.list[j0 + u]];
-        if (a.root) {                                  // a top-level array / map at the row
-          c[u] = static_cast<int32_t>(lld8(row + (n.type == FURY_TYPE_MAP ? 8 : 0)));
-          continue;
-        }
-        if (lbit(row, n.slot)) continue;
-        const uint64_t oas = lld8(row + slots + 8 * n.slot);
-        const uint8_t* vp = row + static_cast<int32_t>(oas >> 32);
-        c[u] = n.type == FURY_TYPE_LIST ? static_cast<int32_t>(lld8(vp))
-             : n.type == FURY_TYPE_MAP ? static_cast<int32_t>(lld8(vp + 8))
-             : static_cast<int64_t>(static_cast<uint32_t>(oas));
+        const int ni = a.list[j0 + u];
+        const LvNode& n = a.nodes[ni];
+        const LvVal v = lv_source(a, n, e, total);
+        if (v.null) continue;
+        uint32_t size;
+        const int64_t vp = lv_value(a, n, v, total, &size, err_where_entry(ni, e));
+        if (vp >= 0) c[u] = value_count(a, n.type, vp, size);
       }
 #pragma unroll
       for (int u = 0; u < kB; u++)
         if (j0 + u < a.nlist) gl(a.nodes[a.list[j0 + u]].start)[e] = c[u];
     }
   } else {
-    const LvNode& n = a.nodes[a.list[blockIdx.y]];
-    if (e < n.m) count_entry(a, n, e);
+    const int ni = a.list[blockIdx.y];
+    const LvNode& n = a.nodes[ni];
+    if (e < n.m) count_entry(a, n, ni, e, total);
   }
 }
 
-// Elements / payload bytes of a non-null variable-length value whose slot is at rows + slot in
-// the container at rows + base (what lv_count computes, here for the next level's entries).
-__device__ __forceinline__ int64_t var_count(const LvArgs& a, int type, int64_t base, int64_t slot) {
-  const uint64_t oas = lld8(a.rows + slot);
-  const uint8_t* vp = a.rows + base + static_cast<int32_t>(oas >> 32);
-  if (type == FURY_TYPE_LIST) return static_cast<int32_t>(lld8(vp));
-  if (type == FURY_TYPE_MAP) return static_cast<int32_t>(lld8(vp + 8));
-  return static_cast<uint32_t>(oas);
+// Elements / payload bytes of a non-null variable-length value of node ci (entry q) whose slot is
+// at rows + slot in the container at rows + base (what lv_count computes, here for the next
+// level's entries; 0 when the value fails its bounds check).
+__device__ __forceinline__ int64_t var_count(const LvArgs& a, int ci, int64_t q, int64_t base,
+                                             int64_t slot, int64_t total) {
+  const LvNode& c = a.nodes[ci];
+  uint32_t size;
+  const int64_t vp = lv_value(a, c, LvVal{false, base, slot}, total, &size, err_where_entry(ci, q));
+  return vp >= 0 ? value_count(a, c.type, vp, size) : 0;
 }
 
 // The elements of the 64 entries of a wave (one LIST / MAP node) are one contiguous range of the
@@ -270,21 +345,23 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void wave_lists_fill(const LvArgs& a, const LvNode& n, int64_t e,
-                                                WaveLists& W) {
+// (a value that fails its bounds check has no elements: its count and start range are empty)
+__device__ __forceinline__ void wave_lists_fill(const LvArgs& a, const LvNode& n, int ni, int64_t e,
+                                                int64_t total, WaveLists& W) {
   const int lane = threadIdx.x & 63;
   const bool live = e < n.m;
   LvVal v{true, 0, -1};
-  if (live) v = lv_source(a, n, e);
+  if (live) v = lv_source(a, n, e, total);
   int64_t ab = -1, ab2 = -1;
   if (live && !v.null) {
     uint32_t size;
-    const uint8_t* vp = lv_var(a, v, &size);
-    if (n.type == FURY_TYPE_LIST) {
-      ab = vp - a.rows;
+    const int64_t vp = lv_value(a, n, v, total, &size, err_where_entry(ni, e));
+    if (vp < 0) {
+    } else if (n.type == FURY_TYPE_LIST) {
+      ab = vp;
     } else {                                             // MAP: [keyBytes][keys][values]
-      ab = vp + 8 - a.rows;
-      ab2 = vp + 8 + static_cast<int64_t>(lld8(vp)) - a.rows;
+      ab = vp + 8;
+      ab2 = vp + 8 + static_cast<int32_t>(lld8(a.rows + vp));
     }
   }
   W.st[lane] = gl(n.start)[live ? e : n.m];
@@ -304,8 +381,8 @@ __device__ __forceinline__ int wave_owner(const WaveLists& W, int64_t q) {
 
 // Sources (and, for counted element nodes, counts) of the elements of a wave's arrays, into the
 // non-scalar element node c; `second` selects a MAP's values array.
-__device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, const WaveLists& W,
-                                            bool second) {
+__device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, int ci,
+                                            const WaveLists& W, bool second, int64_t total) {
   const int lane = threadIdx.x & 63;
   for (int64_t q = W.st[0] + lane; q < W.st[64]; q += 64) {
     const int l = wave_owner(W, q);
@@ -315,37 +392,37 @@ __device__ __forceinline__ void expand_wave(const LvArgs& a, const LvNode& c, co
     const int64_t hb = 8 + lbm(m);
     const bool nul = lbit(a.rows + ab + 8, j);
     st_src(c.src, q, nul ? -1 : ab, nul ? 0 : hb + 8 * j);
-    if (c.start && !nul) gl(c.start)[q] = var_count(a, c.type, ab, ab + hb + 8 * j);
+    if (c.start && !nul) gl(c.start)[q] = var_count(a, ci, q, ab, ab + hb + 8 * j, total);
   }
 }
 
 // Pass 3 of a level: the sources (and counts) of the next level's materialised entries.  Every
 // lane of the wave calls it for the same node (per-wave LDS for lists / maps).
-__device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, int64_t e,
-                                            WaveLists& W) {
+__device__ __forceinline__ void expand_node(const LvArgs& a, const LvNode& n, int ni, int64_t e,
+                                            int64_t total, WaveLists& W) {
   if (n.type == FURY_TYPE_STRUCT) {
     if (e >= n.m) return;
-    const LvVal v = lv_source(a, n, e);
+    const LvVal v = lv_source(a, n, e, total);
     uint32_t size;
-    const uint8_t* vp = v.null ? nullptr : lv_var(a, v, &size);
-    const int64_t vb = v.null ? -1 : vp - a.rows;
+    const int64_t vb = v.null ? -1 : lv_value(a, n, v, total, &size, err_where_entry(ni, e));
     const int nc = n.num_children;
     for (int k = 0; k < nc; k++) {
-      const LvNode& c = a.nodes[n.first_child + k];
+      const int ci = n.first_child + k;
+      const LvNode& c = a.nodes[ci];
       if (c.kind != kLvMat) continue;
-      const bool nul = v.null || lbit(vp, k);
+      const bool nul = vb < 0 || lbit(a.rows + vb, k);
       st_src(c.src, e, nul ? -1 : vb, nul ? 0 : lbm(nc) + 8 * k);
-      if (c.start && !nul) gl(c.start)[e] = var_count(a, c.type, vb, vb + lbm(nc) + 8 * k);
+      if (c.start && !nul) gl(c.start)[e] = var_count(a, ci, e, vb, vb + lbm(nc) + 8 * k, total);
     }
     return;
   }
-  wave_lists_fill(a, n, e, W);
+  wave_lists_fill(a, n, ni, e, total, W);
   wave_sync();
   const LvNode& c0 = a.nodes[n.first_child];
-  if (c0.kind == kLvMat) expand_wave(a, c0, W, false);
+  if (c0.kind == kLvMat) expand_wave(a, c0, n.first_child, W, false, total);
   if (n.type == FURY_TYPE_MAP) {
     const LvNode& c1 = a.nodes[n.first_child + 1];
-    if (c1.kind == kLvMat) expand_wave(a, c1, W, true);
+    if (c1.kind == kLvMat) expand_wave(a, c1, n.first_child + 1, W, true, total);
   }
   wave_sync();
 }
@@ -356,12 +433,14 @@ __global__ __launch_bounds__(kLv) void lv_expand(LvArgs a) {
   WaveLists& W = wl[threadIdx.x >> 6];
   const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
   const int64_t e = e0 + threadIdx.x;
+  const int64_t total = lv_total(a);
   if (kRows) {
     if (e0 >= a.nrows) return;
-    for (int j = 0; j < a.nlist; j++) expand_node(a, a.nodes[a.list[j]], e, W);
+    for (int j = 0; j < a.nlist; j++) expand_node(a, a.nodes[a.list[j]], a.list[j], e, total, W);
   } else {
-    const LvNode& n = a.nodes[a.list[blockIdx.y]];
-    if (e0 < n.m) expand_node(a, n, e, W);
+    const int ni = a.list[blockIdx.y];
+    const LvNode& n = a.nodes[ni];
+    if (e0 < n.m) expand_node(a, n, ni, e, total, W);
   }
 }
 
@@ -433,15 +512,20 @@ __device__ __forceinline__ void write_wave(const LvArgs& a, const LvNode& c, con
 
 // The write pass: entry e of node n (kLvTop / kLvMat), plus the scalar children its thread
 // owns.  Every lane of the wave calls it for the same node (the ballots below).
-__device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, int64_t e,
-                                            WaveLists& W) {
+__device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, int ni, int64_t e,
+                                            int64_t total, WaveLists& W) {
   const bool live = e < n.m;
   LvVal v{true, 0, -1};
-  if (live) v = lv_source(a, n, e);
-  const bool valid = live && !v.null;
-  if (n.validity) ballot_bits(n.validity, e, valid, n.m);
+  if (live) v = lv_source(a, n, e, total);
   const int t = n.type;
   const int w = lwidth(t);
+  // a variable-length value that fails its bounds check is written as null (as in the count and
+  // expand passes, which gave it no elements / bytes)
+  uint32_t size = 0;
+  int64_t vpa = -1;
+  if (live && !v.null && w <= 0) vpa = lv_value(a, n, v, total, &size, err_where_entry(ni, e));
+  const bool valid = live && !v.null && (w > 0 || vpa >= 0);
+  if (n.validity) ballot_bits(n.validity, e, valid, n.m);
   if (w > 0) {                                           // a top-level scalar (slot of 8 B)
     const uint64_t x = valid ? load_w(a.rows + v.slot, w) : 0;
     uint8_t* dst = const_cast<uint8_t*>(n.values);
@@ -452,14 +536,13 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
     }
     return;
   }
-  uint32_t size = 0;
-  const uint8_t* vp = valid ? lv_var(a, v, &size) : nullptr;
+  const uint8_t* vp = valid ? a.rows + vpa : nullptr;
   switch (t) {
     case FURY_TYPE_STRING:
     case FURY_TYPE_BINARY: {
       if (!live) return;
       const int64_t pos = gl(n.start)[e];
-      if (valid && n.values && !(a.dbg & 1)) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
+      if (valid && n.values) copy_bytes(const_cast<uint8_t*>(n.values) + pos, vp, size);
       gl(n.offsets)[e + 1] = static_cast<int32_t>(pos + (valid ? size : 0));
       if (e == 0) gl(n.offsets)[0] = 0;
       return;
@@ -480,8 +563,8 @@ __device__ __forceinline__ void write_entry(const LvArgs& a, const LvNode& n, in
       const LvNode& c0 = a.nodes[n.first_child];
       const bool s0 = c0.kind == kLvInline;
       const bool s1 = t == FURY_TYPE_MAP && a.nodes[n.first_child + 1].kind == kLvInline;
-      if ((!s0 && !s1) || (a.dbg & 2)) return;
-      wave_lists_fill(a, n, e, W);                         // every lane of the wave
+      if (!s0 && !s1) return;
+      wave_lists_fill(a, n, ni, e, total, W);              // every lane of the wave
       wave_sync();
       if (s0) write_wave(a, c0, W, false);
       if (s1) write_wave(a, a.nodes[n.first_child + 1], W, true);
@@ -515,12 +598,14 @@ __global__ __launch_bounds__(kLv) void lv_write(LvArgs a) {
   WaveLists& W = wl[threadIdx.x >> 6];
   const int64_t e0 = static_cast<int64_t>(blockIdx.x) * kLv;
   const int64_t e = e0 + threadIdx.x;
+  const int64_t total = lv_total(a);
   if (kRows) {
-    if (e0 >= a.nrows || (a.dbg & 4)) return;
-    for (int j = 0; j < a.nlist; j++) write_entry(a, a.nodes[a.list[j]], e, W);
+    if (e0 >= a.nrows) return;
+    for (int j = 0; j < a.nlist; j++) write_entry(a, a.nodes[a.list[j]], a.list[j], e, total, W);
   } else {
-    const LvNode& n = a.nodes[a.list[blockIdx.y]];
-    if (e0 < n.m && !(a.dbg & 8)) write_entry(a, n, e, W);
+    const int ni = a.list[blockIdx.y];
+    const LvNode& n = a.nodes[ni];
+    if (e0 < n.m) write_entry(a, n, ni, e, total, W);
   }
 }
 
@@ -536,18 +621,6 @@ int host_width(int32_t t) {
     case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
     default: return -1;
   }
-}
-
-// DIAGNOSTIC (timing only, outputs wrong when set; honoured only with FURY_DIAGNOSTIC=1):
-// FURY_LV_DBG bit 1 skips string payload copies, 2 scalar array elements, 4 the row-major write
-// launch, 8 the node-major write launch.
-int lv_dbg() {
-  static const int v = [] {
-    const char* e = getenv("FURY_LV_DBG");
-    const char* d = getenv("FURY_DIAGNOSTIC");
-    return e && d && atoi(d) == 1 ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 // The node table + launch list for one kernel, uploaded stream-ordered (kept alive by dt until
@@ -569,7 +642,7 @@ int upload_args(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t
   a->root = p.root;
   a->nrows = p.nrows;
   a->nlist = static_cast<int32_t>(list.size());
-  a->dbg = lv_dbg();
+  a->err = device_error_word();
   return FURY_OK;
 }
 

@@ -198,7 +198,7 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   if (st) return st;
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
   if (!st) {
-    hipLaunchKernelGGL(decode_var_kernel<true>, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
+    hipLaunchKernelGGL(decode_var_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
                        ws, nseq);
     st = check_hip(hipGetLastError(), "decode_var launch");
   }

@@ -903,18 +903,61 @@ __global__ __launch_bounds__(kThreads) void add_group_prefix(int64_t* __restrict
 
 // --- decode side -------------------------------------------------------------------------------
 
-// Per row and var field: STRING/BINARY -> unpadded size; LIST -> numElements; else 0.
-template <class Col>
-__device__ __forceinline__ int64_t var_count(const VarArgs& a, const Col& c, int k,
-                                             const uint8_t* row) {
-  if ((row[k >> 3] >> (k & 7)) & 1) return 0;                  // null
-  const uint64_t slot = *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k);
-  if (c.kind == kBytes) return static_cast<int64_t>(static_cast<uint32_t>(slot));
-  if (c.kind == kListFixed) {
-    const int32_t rel = static_cast<int32_t>(slot >> 32);
-    return static_cast<int32_t>(*reinterpret_cast<const int64_t*>(row + rel));
+// The count a variable-length value contributes to its Arrow column -- STRING / BINARY: the
+// unpadded size (int)slot; LIST: numElements, (int) of the array's first 8 bytes
+// (BinaryArray.pointTo, BinaryArray.java:69-78); DECIMAL and the rest: 0 -- for the slot of a
+// non-null field of the row at absolute byte `base`.  A value any of whose bytes lie outside the
+// batch [0, total) (string bytes, DECIMAL's 16, an array's header, null bits and elements), or with
+// a negative size / count, sets *bad and counts 0 (span_ok, kernels.h).  Every decode kernel and
+// the look-back's help (tile_count) count through this one function, so a helped aggregate equals
+// the one its tile publishes.
+__device__ __forceinline__ int64_t slot_count(int kind, int width, uint64_t slot, int64_t base,
+                                              const uint8_t* rows, int64_t total, bool* bad) {
+  const int64_t p = base + static_cast<int32_t>(slot >> 32);
+  switch (kind) {
+    case kBytes: {
+      const int64_t n = static_cast<int32_t>(slot);
+      if (span_ok(p, n, total)) return n;
+      *bad = true;
+      return 0;
+    }
+    case kDecimal:
+      if (!span_ok(p, 16, total)) *bad = true;
+      return 0;
+    case kListFixed: {
+      if (!span_ok(p, 8, total)) {
+        *bad = true;
+        return 0;
+      }
+      const int64_t n = static_cast<int32_t>(*gl(reinterpret_cast<const int64_t*>(rows + p)));
+      const int64_t ew = width == 0 ? 1 : width;
+      if (n >= 0 && span_ok(p, 8 + bm_bytes(n) + n * ew, total)) return n;
+      *bad = true;
+      return 0;
+    }
+    default:
+      return 0;
   }
-  return 0;
+}
+
+// The row at absolute byte `base` is inside the batch: its null bitmap and slots can be read.
+__device__ __forceinline__ bool row_ok(int64_t base, int fixed_size, int64_t total) {
+  return span_ok(base, fixed_size, total);
+}
+
+// Null-or-bad test + count of field k of the row whose header bytes are at `hdr` (LDS or HBM) and
+// which starts at absolute byte `base`.  Returns the count; *null = null field or bad value.
+template <class Col>
+__device__ __forceinline__ int64_t field_count(const Col& c, int k, const uint8_t* hdr,
+                                               int bitmap_bytes, int64_t base, const uint8_t* rows,
+                                               int64_t total, bool* null, bool* bad) {
+  *bad = false;
+  *null = (hdr[k >> 3] >> (k & 7)) & 1;
+  if (*null || c.kind < kBytes) return 0;
+  const uint64_t slot = *reinterpret_cast<const uint64_t*>(hdr + bitmap_bytes + 8 * k);
+  const int64_t n = slot_count(c.kind, c.width, slot, base, rows, total, bad);
+  if (*bad) *null = true;
+  return n;
 }
 
 #ifdef FURY_VAR_MAIN
@@ -927,25 +970,32 @@ __global__ __launch_bounds__(kThreads) void decode_measure_kernel(VarArgs a,
   __shared__ __attribute__((aligned(16))) uint8_t stage[kDecodeStage];
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kThreads;
   const int64_t nr = min<int64_t>(kThreads, a.nrows - r0);
+  const int64_t total = offs[a.nrows];
   const int64_t rbeg = offs[r0];
   const int64_t bytes = offs[r0 + nr] - rbeg;
   const int64_t r = r0 + threadIdx.x;
   // stage the group's contiguous row range (LDS-DMA, 16-B pieces) so the per-row slot reads
-  // below hit LDS instead of scattered HBM lines
-  const bool staged = bytes + 32 <= kDecodeStage;
+  // below hit LDS instead of scattered HBM lines (only a range inside the batch)
+  const bool staged = bytes >= 0 && bytes + 32 <= kDecodeStage && span_ok(rbeg, bytes, total);
   uint32_t d0 = 0;
   if (staged) {
     uint32_t at = 0;
     d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
     __syncthreads();
   }
-  const uint8_t* row =
-      r < a.nrows ? (staged ? stage + d0 + (offs[r] - rbeg) : rows + offs[r]) : nullptr;
+  const int64_t base = r < a.nrows ? offs[r] : 0;
+  const bool rok = r < a.nrows && row_ok(base, a.fixed_size, total);
+  if (r < a.nrows && !rok) raise_oob(a.err, r);
+  // a row header inside the staged range is read from LDS
+  const bool in_stage = staged && rok && base >= rbeg && base + a.fixed_size <= rbeg + bytes;
+  const uint8_t* row = rok ? (in_stage ? stage + d0 + (base - rbeg) : rows + base) : nullptr;
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
     CVarCol& c = vc(a, k);
     if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const int64_t cnt = row ? var_count(a, c, k, row) : 0;
+    bool nul = false, bad = false;
+    const int64_t cnt = row ? field_count(c, k, row, a.bitmap_bytes, base, rows, total, &nul, &bad) : 0;
+    if (bad) raise_oob(a.err, r);
     int64_t total;
     const int64_t ex = block_excl_scan(cnt, &total, tmp);
     if (row) c.offsets[r] = static_cast<int32_t>(ex);
@@ -1039,60 +1089,27 @@ __device__ __forceinline__ bool is_seq(const Col& c) {
 constexpr int kDecImg = 24 * 1024;
 
 
-// look_back with a bounded spin.  Tiles are numbered by a ticket, so every predecessor is running
-// and publishes without waiting on anything: the wait always ends.  The bound is a safety net
-// against hardware faults; a look-back that gives up raises the host-visible device error word
-// (`err`), which the next API call / fury_device_status() reports as FURY_ERR_DEVICE -- its
-// outputs are never passed off as valid.
-// Polling is economical: a lane re-reads its status word only while it is unpublished, and the
-// wave waits only for the lanes nearer than the nearest inclusive prefix (status reads go to the
-// cross-XCD coherence point; thousands of spinning waves re-reading 64 words each congested it).
-__device__ int64_t look_back_bounded(const uint64_t* status, int64_t b, int nseq, int q,
-                                     uint32_t* err) {
-  const int lane = threadIdx.x & 63;
-  int64_t excl = 0;
-  uint32_t spins = 0;
-  for (int64_t j = b - 1;; j -= 64) {
-    const int64_t idx = j - lane;
-    uint64_t v = idx >= 0 ? ld_status(status + idx * nseq + q) : kInc;
-    uint64_t inc;
-    int stop;
-    for (;;) {
-      inc = __ballot((v >> 62) == 2);
-      stop = inc ? __builtin_ctzll(inc) : 63;
-      const uint64_t upto = stop == 63 ? ~0ull : ((2ull << stop) - 1);
-      if ((__ballot((v >> 62) == 0) & upto) == 0) break;
-      if (++spins > (1u << 24)) {
-        if (lane == 0 && err) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return 0;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      if ((v >> 62) == 0 && lane <= stop) v = ld_status(status + idx * nseq + q);
-    }
-    excl += wave_sum(lane <= stop ? static_cast<int64_t>(v & kValMask) : 0);
-    if (inc) return excl;
-  }
-}
-
 // Count (string bytes / list elements) of column k summed over the rows of tile j, by one wave,
 // straight from the rows: the aggregate tile j publishes, for a look-back that stopped waiting.
+// Same counts (slot_count) and the same 32-bit truncation as the published aggregates.
 template <int NT>
 __device__ int64_t tile_count(const VarArgs& a, int k, const uint8_t* rows, const int64_t* offs,
                               int64_t j) {
   const int lane = threadIdx.x & 63;
   CVarCol& c = vc(a, k);
+  const int64_t total = gl(offs)[a.nrows];
   int64_t sum = 0;
   const int64_t i1 = min<int64_t>((j + 1) * NT, a.nrows);
   for (int64_t i = j * NT + lane; i < i1; i += 64) {
-    const uint8_t* row = rows + gl(offs)[i];
+    const int64_t base = gl(offs)[i];
+    if (!row_ok(base, a.fixed_size, total)) continue;
+    const uint8_t* row = rows + base;
     if ((gl(row)[k >> 3] >> (k & 7)) & 1) continue;
     const uint64_t slot = *gl(reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k));
-    if (c.kind == kBytes)
-      sum += static_cast<uint32_t>(slot);
-    else
-      sum += static_cast<uint32_t>(*gl(reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot >> 32))));
+    bool bad = false;
+    sum += slot_count(c.kind, c.width, slot, base, rows, total, &bad);
   }
-  return wave_sum(sum);
+  return static_cast<uint32_t>(wave_sum(sum));
 }
 
 // look_back_bounded for blockIdx-ordered tiles: when the nearest unpublished predecessor inside
@@ -1239,16 +1256,21 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   const int nr = static_cast<int>(min<int64_t>(NT, a.nrows - r0));
   const bool live = tid < nr;
   const int64_t r = live ? r0 + tid : r0;
-  const uint8_t* row = rows + offs[r];
+  const int64_t total = offs[a.nrows];            // the batch: every read stays in [0, total)
+  const int64_t base = offs[r];
+  const bool rok = row_ok(base, a.fixed_size, total);
+  if (live && !rok) raise_oob(a.err, r);
+  const uint8_t* row = rows + (rok ? base : 0);
   // null word + slots: one batch of 16-byte loads of the aligned blocks covering them (rows are
   // only 8-aligned; selecting words afterwards costs cndmasks, while 8-byte loads took 1 + K
   // instructions, each touching one cache line per lane -- the vector memory pipeline's cost).
-  // Blocks past the header's last word are not loaded.
+  // Blocks past the header's last word are not loaded (the last block may extend 8 bytes past
+  // the header: inside the same 16-byte block, never used).
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
   constexpr int kNch = (K + 3) / 2;
   const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
   const int mis = static_cast<int>((ra >> 3) & 1);
-  const int need = (mis + K + 2) / 2;
+  const int need = rok ? (mis + K + 2) / 2 : 0;
   const auto blk = gl(reinterpret_cast<const u64x2*>(ra & ~uintptr_t(15)));
   uint64_t hw[2 * kNch];
 #pragma unroll
@@ -1258,20 +1280,24 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     hw[2 * c] = x.x;
     hw[2 * c + 1] = x.y;
   }
-  const uint64_t nullw = live ? (mis ? hw[1] : hw[0]) : ~0ull;
+  uint64_t nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
   uint64_t slot[K];
 #pragma unroll
   for (int k = 0; k < K; k++) slot[k] = mis ? hw[k + 2] : hw[k + 1];
-  // element counts of LIST fields (dependent load of the array header)
+  // counts (LIST: dependent load of the array header), bounds-checked: a value outside the batch
+  // decodes as null and is reported (slot_count)
   uint32_t cnt[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    const bool isnull = (nullw >> k) & 1;
     cnt[k] = 0;
-    if (!isnull && c.kind == kBytes) cnt[k] = static_cast<uint32_t>(slot[k]);
-    if (!isnull && c.kind == kListFixed)
-      cnt[k] = static_cast<uint32_t>(*reinterpret_cast<const int64_t*>(row + static_cast<int32_t>(slot[k] >> 32)));
+    if (((nullw >> k) & 1) || c.kind < kBytes) continue;
+    bool bad = false;
+    cnt[k] = static_cast<uint32_t>(slot_count(c.kind, c.width, slot[k], base, rows, total, &bad));
+    if (bad) {
+      nullw |= 1ull << k;
+      raise_oob(a.err, r);
+    }
   }
   // in-tile exclusive scans, two columns per 64-bit scan (tile totals < 2^32)
   uint32_t ex[K], tot[K];
@@ -1325,6 +1351,10 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
     if (img_at[k] == kNone || !live || cnt[k] == 0) continue;
+    if (static_cast<uint64_t>(ex[k]) + cnt[k] > tot[k]) {   // the tile's 32-bit total wrapped
+      raise_oob(a.err, r);
+      continue;
+    }
     const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
     uint8_t* im = reinterpret_cast<uint8_t*>(oimg) + img_at[k];
     if (c.kind == kBytes) {
@@ -1568,17 +1598,40 @@ __device__ __forceinline__ void put_bits64(uint8_t* bits, int64_t gbit0, uint64_
 
 struct DecodeShared {
   int32_t pos[kSeqChunk][kThreads + 1];   // group-relative exclusive starts; [nr] = group total
-  int64_t rowoff[kThreads];                // row start relative to the group's first row
+  int64_t rowoff[kThreads];                // absolute row start; -1: the row is outside the batch
   int64_t base[kSeqChunk];                 // global start of the group's range, per sequence
   int64_t tmp[kThreads / 64];
-  int64_t blk;
 };
 
+// Where the group reads batch bytes [q, q + len) from: its staged row range in LDS when they lie
+// inside it, else HBM (a slot may point at bytes of another row -- the reference reads them
+// through the shared buffer, so this decode does too).
+struct TileView {
+  const uint8_t* rows;       // the batch (HBM)
+  const uint8_t* stage;      // byte `lo` of the batch in LDS, or NULL (not staged)
+  int64_t lo, hi;            // staged absolute range
+  __device__ __forceinline__ const uint8_t* at(int64_t q, int64_t len) const {
+    return (stage && q >= lo && q + len <= hi) ? stage + (q - lo) : rows + q;
+  }
+};
 
-// Counts + in-group scans of the sequences [cbase, cbase + nchunk); publishes the aggregates.
-__device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row, DecodeShared& sh,
-                                            int cbase, int nchunk, int64_t b, uint64_t* status,
-                                            int nseq) {
+// Null-or-bad test + count of field k of the row at absolute byte `base` (-1: bad row).
+__device__ __forceinline__ int64_t wide_count(const VarArgs& a, CVarCol& c, int k, const TileView& tv,
+                                              int64_t base, int64_t total, bool* null, bool* bad) {
+  if (base < 0) {
+    *null = true;
+    *bad = false;
+    return 0;
+  }
+  return field_count(c, k, tv.at(base, a.fixed_size), a.bitmap_bytes, base, tv.rows, total, null,
+                     bad);
+}
+
+// Counts + in-group scans of the sequences [cbase, cbase + nchunk); publishes the aggregates
+// (32-bit, like tile_count).
+__device__ __forceinline__ void chunk_count(const VarArgs& a, const TileView& tv, int64_t base,
+                                            int64_t total, int64_t r, DecodeShared& sh, int cbase,
+                                            int nchunk, int64_t b, uint64_t* status, int nseq) {
   int seq = 0;
   for (int k = 0; k < a.ncols; k++) {
     CVarCol& c = vc(a, k);
@@ -1586,38 +1639,25 @@ __device__ __forceinline__ void chunk_count(const VarArgs& a, const uint8_t* row
     const int q = seq++ - cbase;
     if (q < 0) continue;
     if (q >= nchunk) break;
-    const int64_t cnt = row ? var_count(a, c, k, row) : 0;
+    bool nul = false, bad = false;
+    const int64_t cnt = wide_count(a, c, k, tv, base, total, &nul, &bad);
+    if (bad) raise_oob(a.err, r);
     int64_t tot;
     const int64_t ex = block_excl_scan(cnt, &tot, sh.tmp);
     sh.pos[q][threadIdx.x] = static_cast<int32_t>(ex);
     if (threadIdx.x == 0) {
       sh.pos[q][kThreads] = static_cast<int32_t>(tot);
-      if (status)
-        st_status(status + b * nseq + cbase + q, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot));
+      st_status(status + b * nseq + cbase + q,
+                (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(static_cast<uint32_t>(tot)));
     }
   }
   __syncthreads();
 }
 
-template <bool kLookBack>
 __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh, int cbase,
                                               int nchunk, int64_t b, uint64_t* status, int nseq,
                                               const uint8_t* rows, const int64_t* offs) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (!kLookBack) {     // offsets precomputed by the sizing pass (fury_row_decode_measure)
-    if (threadIdx.x < nchunk) {
-      int seq = 0;
-      for (int k = 0; k < a.ncols; k++) {
-        if (!is_seq(vc(a, k))) continue;
-        if (seq++ == cbase + static_cast<int>(threadIdx.x)) {
-          sh.base[threadIdx.x] = vc(a, k).offsets[b * kThreads];
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    return;
-  }
   for (int q = w; q < nchunk; q += kThreads / 64) {
     const int64_t ex = b == 0 ? 0
                        : look_back_help<kThreads>(a, seq_col(a, cbase + q), rows, offs, status, b,
@@ -1626,34 +1666,35 @@ __device__ __forceinline__ void chunk_resolve(const VarArgs& a, DecodeShared& sh
       sh.base[q] = ex;
       if (b > 0)
         st_status(status + b * nseq + cbase + q,
-                  kInc | static_cast<uint64_t>(ex + sh.pos[q][kThreads]));
+                  kInc | static_cast<uint64_t>(ex + static_cast<uint32_t>(sh.pos[q][kThreads])));
     }
   }
   __syncthreads();
 }
 
-template <bool kStaged, bool kLookBack>
-__device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* src, uint8_t* oimg,
-                                             DecodeShared& sh, int64_t b, int64_t nb, int nr,
-                                             uint64_t* status, int nseq, const uint8_t* rows,
+__device__ __forceinline__ void decode_group(const VarArgs& a, const TileView& tv, int64_t total,
+                                             uint8_t* oimg, DecodeShared& sh, int64_t b, int64_t nb,
+                                             int nr, uint64_t* status, int nseq,
                                              const int64_t* offs) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t r0 = b * kThreads;
   const int64_t r = r0 + tid;
   const bool live = tid < nr;
-  const uint8_t* row = live ? src + sh.rowoff[tid] : nullptr;
+  const int64_t base = live ? sh.rowoff[tid] : -1;
+  const uint8_t* row = base >= 0 ? tv.at(base, a.fixed_size) : nullptr;
   const int64_t rbase = r - lane;                               // this wave's first row
   const int64_t nvalid = a.nrows - rbase;
   const int nbytes = nvalid >= 64 ? 8 : static_cast<int>((nvalid + 7) >> 3);
 
-  if (kLookBack && nseq > 0) chunk_count(a, row, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
+  if (nseq > 0) chunk_count(a, tv, base, total, r, sh, 0, min(kSeqChunk, nseq), b, status, nseq);
 
   // fixed-width fields and every field's validity: no dependency on other groups
   for (int k = 0; k < a.ncols; k++) {
     CVarCol& c = vc(a, k);
-    const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
+    bool isnull = true, bad = false;
+    if (row) (void)wide_count(a, c, k, tv, base, total, &isnull, &bad);
     const uint64_t slot =
-        (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
+        !isnull ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
     if (c.validity) {
       const uint64_t ok = __ballot(live && !isnull);
       if (lane < nbytes) c.validity[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));
@@ -1675,8 +1716,9 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
       if (live && dst) {
         uint64_t* d = reinterpret_cast<uint64_t*>(dst + 16 * r);
         uint64_t lo = 0, hi = 0;
-        if (!isnull) {
-          const uint8_t* s = row + static_cast<int32_t>(slot >> 32);
+        if (!isnull) {                                  // [p, p + 16) checked by wide_count
+          const int64_t p = base + static_cast<int32_t>(slot >> 32);
+          const uint8_t* s = tv.at(p, 16);
           lo = reinterpret_cast<const uint64_t*>(s)[0];
           hi = reinterpret_cast<const uint64_t*>(s)[1];
         }
@@ -1688,8 +1730,8 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
 
   for (int cbase = 0; cbase < nseq; cbase += kSeqChunk) {
     const int nchunk = min(kSeqChunk, nseq - cbase);
-    if (cbase > 0 || !kLookBack) chunk_count(a, row, sh, cbase, nchunk, b, status, nseq);
-    chunk_resolve<kLookBack>(a, sh, cbase, nchunk, b, status, nseq, rows, offs);
+    if (cbase > 0) chunk_count(a, tv, base, total, r, sh, cbase, nchunk, b, status, nseq);
+    chunk_resolve(a, sh, cbase, nchunk, b, status, nseq, tv.rows, offs);
     int seq = 0;
     for (int k = 0; k < a.ncols; k++) {
       CVarCol& c = vc(a, k);
@@ -1706,25 +1748,29 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
       const int64_t cap = c.capacity;
       if (c.kind == kBytes) {
         const int64_t p0 = gb, p1 = gb + tot;
-        const bool isnull = live && ((row[k >> 3] >> (k & 7)) & 1);
-        const uint64_t slot =
-            (live && !isnull) ? *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k) : 0;
-        const int64_t len = (live && !isnull) ? static_cast<uint32_t>(slot) : 0;
-        const uint8_t* s = live ? row + static_cast<int32_t>(slot >> 32) : nullptr;
+        bool isnull = true, bad = false;
+        const int64_t len = row ? wide_count(a, c, k, tv, base, total, &isnull, &bad) : 0;
+        const uint8_t* s = nullptr;
+        if (!isnull && len > 0) {
+          const uint64_t slot = *reinterpret_cast<const uint64_t*>(row + a.bitmap_bytes + 8 * k);
+          const int64_t p = base + static_cast<int32_t>(slot >> 32);
+          s = tv.at(p, len);
+        }
         const int64_t pos = p0 + sh.pos[q][tid];
         // LDS byte i <-> global byte a0 + i, a0 = 16-aligned address of payload byte p0
         const int64_t a0 = p0 - static_cast<int64_t>(reinterpret_cast<uintptr_t>(dst + p0) & 15);
         if (p1 - a0 <= kStrStage) {
-          put_bytes(oimg, pos - a0, s, len);
+          if (s) put_bytes(oimg, pos - a0, s, len);
           __syncthreads();
           if (cap > p0) copy_bytes_range<true>(dst, oimg, p0, min<int64_t>(p1, cap), a0);
           __syncthreads();
-        } else {
+        } else if (s) {
           put_bytes(dst, pos, s, max<int64_t>(0, min<int64_t>(len, cap - pos)));
         }
         continue;
       }
-      // LIST of fixed-width elements -> Arrow child values + element validity
+      // LIST of fixed-width elements -> Arrow child values + element validity.  A row owns
+      // elements only when its array passed the bounds check (else its count is 0).
       const int ew = c.width == 0 ? 1 : c.width;
       const int sh0 = static_cast<int>(gb & 63);
       const int64_t span = sh0 + tot;
@@ -1735,10 +1781,12 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
         uint64_t v = 0;
         if (act) {
           const int t = find_row(sh.pos[q], nr, static_cast<int32_t>(i));
-          const uint8_t* rw = src + sh.rowoff[t];
-          const uint64_t sl = *reinterpret_cast<const uint64_t*>(rw + a.bitmap_bytes + 8 * k);
-          const uint8_t* arr = rw + static_cast<int32_t>(sl >> 32);
-          const int64_t n = *reinterpret_cast<const int64_t*>(arr);
+          const int64_t bt = sh.rowoff[t];
+          const uint64_t sl = *reinterpret_cast<const uint64_t*>(tv.at(bt, a.fixed_size) +
+                                                                 a.bitmap_bytes + 8 * k);
+          const int64_t pa = bt + static_cast<int32_t>(sl >> 32);
+          const int64_t n = static_cast<int32_t>(*gl(reinterpret_cast<const int64_t*>(tv.rows + pa)));
+          const uint8_t* arr = tv.at(pa, 8 + bm_bytes(n) + n * ew);
           const int64_t j = i - sh.pos[q][t];
           valid = !((arr[8 + (j >> 3)] >> (j & 7)) & 1);
           if (valid) {
@@ -1771,7 +1819,6 @@ __device__ __forceinline__ void decode_group(const VarArgs& a, const uint8_t* sr
 }
 
 #ifdef FURY_VAR_MAIN
-template <bool kLookBack>
 __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
                                                               const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
@@ -1784,20 +1831,24 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
   const int64_t b = static_cast<int64_t>(blockIdx.x);
   const int64_t r0 = b * kThreads;
   const int nr = static_cast<int>(min<int64_t>(kThreads, a.nrows - r0));
+  const int64_t total = offs[a.nrows];
   const int64_t rbeg = offs[r0];
   const int64_t bytes = offs[r0 + nr] - rbeg;
-  if (threadIdx.x < nr) sh.rowoff[threadIdx.x] = offs[r0 + threadIdx.x] - rbeg;
-  if (bytes + 32 <= kDecodeStage) {          // LDS-DMA: every piece in flight at once
+  if (threadIdx.x < nr) {
+    const int64_t base = offs[r0 + threadIdx.x];
+    const bool ok = row_ok(base, a.fixed_size, total);
+    if (!ok) raise_oob(a.err, r0 + threadIdx.x);
+    sh.rowoff[threadIdx.x] = ok ? base : -1;
+  }
+  TileView tv{rows, nullptr, 0, 0};
+  // LDS-DMA of the tile's row range (every piece in flight at once), when it is inside the batch
+  if (bytes >= 0 && bytes + 32 <= kDecodeStage && span_ok(rbeg, bytes, total)) {
     uint32_t at = 0;
     const uint32_t d0 = stage_range<kThreads>(stage, at, rows + rbeg, rows + rbeg + bytes);
-    __syncthreads();
-    decode_group<true, kLookBack>(a, stage + d0, oimg, sh, b, gridDim.x, nr, status, nseq, rows,
-                                  offs);
-  } else {
-    __syncthreads();
-    decode_group<false, kLookBack>(a, rows + rbeg, oimg, sh, b, gridDim.x, nr, status, nseq, rows,
-                                   offs);
+    tv = TileView{rows, stage + d0, rbeg, rbeg + bytes};
   }
+  __syncthreads();
+  decode_group(a, tv, total, oimg, sh, b, gridDim.x, nr, status, nseq, offs);
 }
 #endif  // FURY_VAR_MAIN
 

@@ -355,7 +355,9 @@ class RowEncoder:
 
         def call():
             _check(fn(*args))
-        call.keep = (keep, columns, rows, row_offsets)
+        # the schema handle in args lives as long as the Schema object: keep it (and this
+        # encoder) alive with the callable, or a dropped encoder would free it under the call
+        call.keep = (keep, columns, rows, row_offsets, self, self._schema)
         return call
 
     def bind_decode(self, batch: RowBatch, cols: List[Column], stream=None, arrow: bool = False):
@@ -368,7 +370,7 @@ class RowEncoder:
 
         def call():
             _check(fn(*args))
-        call.keep = (keep, batch, cols)
+        call.keep = (keep, batch, cols, self, self._schema)
         return call
 
     def encode_batch(self, columns: Sequence[Column], nrows: int, stream=None) -> RowBatch:
@@ -767,6 +769,29 @@ def _bfs(fields: Sequence[Field]):
     return out
 
 
+def _node_sizes(order, cols: List[Column], n: int, stream=None):
+    """Arrow entries and STRING / BINARY payload bytes of every schema node (breadth-first
+    ``order``) of decoded columns ``cols`` with n top-level entries (device offsets read back)."""
+    nodes: List[Optional[Column]] = [None] * len(order)
+    m = [0] * len(order)
+    b = [0] * len(order)
+    ntop = len(cols)
+    for k in range(ntop):
+        nodes[k] = cols[k]
+        m[k] = n
+    with _on(stream):
+        for i, (f, first) in enumerate(order):
+            c = nodes[i]
+            t = f.type_id
+            end = int(c.offsets[m[i]].item()) if (t in (STRING, BINARY, LIST, MAP) and m[i]) else 0
+            if t in (STRING, BINARY):
+                b[i] = end
+            for j in range(len(f.children)):
+                nodes[first + j] = c.child[j]
+                m[first + j] = m[i] if t == STRUCT else end
+    return m, b
+
+
 def _alloc_host_node(f: Field, m: int, nbytes: int) -> Column:
     """Host (numpy) buffers for one schema node with m Arrow entries (fury_decode_host_execute
     contract: exact sizes)."""
@@ -952,21 +977,88 @@ class Encoders:
 
 
 class ArrowWriter:
-    """``ArrowWriter`` (ArrowWriter.java:55-99) over a RowBatch: ``write(batch)`` converts a
-    whole batch on the device; ``finish()`` returns device Arrow columns and
-    ``finish_as_record_batch()`` a pyarrow.RecordBatch on the host."""
+    """``ArrowWriter`` (ArrowWriter.java:55-99) over RowBatches: ``write(batch)`` converts a whole
+    batch on the device and APPENDS it after everything written since ``reset()`` -- the
+    reference's write(row) appends at the vectors' rowCount -- so two writes then
+    ``finish_as_record_batch()`` give the concatenation.  ``finish()`` returns the accumulated
+    device Arrow columns; ``finish_as_record_batch()`` a pyarrow.RecordBatch on the host.
+
+    The accumulated buffers grow like Arrow's setSafe (capacity doubling, amortised O(1) per
+    row): a batch that does not fit moves the accumulation into buffers of twice the size first.
+    Appends run on the device (``fury_arrow_append``: copies, offset rebasing, bit shifting)."""
 
     def __init__(self, encoder: RowEncoder):
         self._enc = encoder
-        self._cols: Optional[List[Column]] = None
-        self._n = 0
+        self.reset()
 
     def write(self, batch: RowBatch, stream=None) -> None:
-        self._cols = self._enc._decode(batch, True, True, stream)
-        self._n = batch.nrows
+        """Synchronous like the reference's write(row): a row whose values lie outside the batch
+        raises IndexOutOfBoundsException here (nothing of the batch is appended then)."""
+        cols = self._enc._decode(batch, True, True, stream)
+        self._enc.device_status(stream)
+        n = batch.nrows
+        order = _bfs(self._enc.schema().fields)
+        m, b = _node_sizes(order, cols, n, stream)
+        if self._acc is None or self._n == 0:
+            self._acc, self._m, self._b = cols, m, b
+            self._cap_m, self._cap_b = list(m), list(b)
+        else:
+            need_m = [x + y for x, y in zip(self._m, m)]
+            need_b = [x + y for x, y in zip(self._b, b)]
+            if any(x > c for x, c in zip(need_m, self._cap_m)) or \
+                    any(x > c for x, c in zip(need_b, self._cap_b)):
+                self._grow(order, need_m, need_b, stream)
+            keep: list = []
+            _check(N.lib().fury_arrow_append(self._enc.schema().handle,
+                                             _c_columns(self._acc[:len(cols)], keep), self._n,
+                                             _c_columns(cols, keep), n, _stream_handle(stream)))
+            self._m, self._b = need_m, need_b
+        self._n += n
+
+    def _grow(self, order, need_m, need_b, stream) -> None:
+        cap_m = [max(2 * c, x) for c, x in zip(self._cap_m, need_m)]
+        cap_b = [max(2 * c, x) for c, x in zip(self._cap_b, need_b)]
+        with _on(stream):
+            nodes = _alloc_nodes(order, cap_m, cap_b, True, self._enc.device)
+        for i, (f, first) in enumerate(order):
+            if f.children:
+                nodes[i].child = [nodes[first + j] for j in range(len(f.children))]
+        top = nodes[:len(self._enc.schema().fields)]
+        keep: list = []
+        _check(N.lib().fury_arrow_append(self._enc.schema().handle, _c_columns(top, keep), 0,
+                                         _c_columns(self._acc, keep), self._n,
+                                         _stream_handle(stream)))
+        self._acc, self._cap_m, self._cap_b = top, cap_m, cap_b
 
     def finish(self) -> List[Column]:
-        return self._cols or []
+        """The device Arrow columns of every row written since reset() (views trimmed to the
+        written entries)."""
+        if self._acc is None:
+            return []
+        order = _bfs(self._enc.schema().fields)
+        flat: List[Column] = []
+
+        def walk(c: Column, i: int):
+            f, first = order[i]
+            m, nb = self._m[i], self._b[i]
+            t = f.type_id
+            out = Column(validity=None if c.validity is None else c.validity[:((m + 31) // 32) * 4])
+            if t == BOOL:
+                out.values = c.values[:((m + 31) // 32) * 4]
+            elif type_width(t) > 0:
+                out.values = c.values[:m * type_width(t)]
+            elif t == DECIMAL:
+                out.values = c.values[:16 * m]
+            elif t in (STRING, BINARY):
+                out.values = c.values[:max(nb, 1)]
+                out.offsets = c.offsets[:m + 1]
+            elif t in (LIST, MAP):
+                out.offsets = c.offsets[:m + 1]
+            if f.children:
+                out.child = [walk(c.child[j], first + j) for j in range(len(f.children))]
+            return out
+
+        return [walk(c, i) for i, c in enumerate(self._acc)]
 
     def finish_as_record_batch(self):
         from .arrow import columns_to_record_batch
@@ -991,8 +1083,13 @@ class ArrowWriter:
         return self.ipc_schema() + body + IPC_EOS
 
     def reset(self) -> None:
-        self._cols = None
+        """ArrowWriter.reset(): the next write starts a new batch (ArrowWriter.java:95-99)."""
+        self._acc: Optional[List[Column]] = None
         self._n = 0
+        self._m: List[int] = []
+        self._b: List[int] = []
+        self._cap_m: List[int] = []
+        self._cap_b: List[int] = []
 
 
 IPC_EOS = b"\xff\xff\xff\xff\x00\x00\x00\x00"

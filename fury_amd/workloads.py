@@ -217,6 +217,44 @@ def gen_columns(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
     return [gen_column(f, seed, k, start, n, **knobs) for k, f in enumerate(fields)]
 
 
+def slice_columns(fields: Sequence[Field], cols: Sequence[Column], b: int, e: int) -> List[Column]:
+    """Rows [b, e) of host columns as columns of their own: fixed values sliced, bitmaps re-packed
+    from bit b, STRING / BINARY / LIST offsets rebased to 0 with their payload / child slices
+    (the CPU baseline's per-thread batches)."""
+    def bits(a, lo, hi):
+        if a is None:
+            return None
+        u = np.unpackbits(np.asarray(a, np.uint8), bitorder="little")[lo:hi]
+        return np.packbits(u, bitorder="little")
+
+    out = []
+    for f, c in zip(fields, cols):
+        t = f.type_id
+        if t == BOOL:
+            out.append(Column(values=bits(c.values, b, e), validity=bits(c.validity, b, e)))
+        elif type_width(t) > 0:
+            out.append(Column(values=c.values[b:e], validity=bits(c.validity, b, e)))
+        elif t == DECIMAL:
+            out.append(Column(values=c.values[16 * b:16 * e], validity=bits(c.validity, b, e)))
+        elif t in (STRING, BINARY):
+            o = np.asarray(c.offsets)
+            out.append(Column(values=c.values[o[b]:o[e]], validity=bits(c.validity, b, e),
+                              offsets=(o[b:e + 1] - o[b]).astype(np.int32)))
+        elif t == LIST:
+            o = np.asarray(c.offsets)
+            ch = c.child[0]
+            if f.children[0].type_id == BOOL:
+                cv = bits(ch.values, o[b], o[e])
+            else:
+                cv = ch.values[o[b]:o[e]]
+            out.append(Column(validity=bits(c.validity, b, e),
+                              offsets=(o[b:e + 1] - o[b]).astype(np.int32),
+                              child=[Column(values=cv, validity=bits(ch.validity, o[b], o[e]))]))
+        else:
+            raise ValueError(f"no slice for type {t}")
+    return out
+
+
 def _u64_const(c: int):
     """A uint64 constant as the int64 with the same bits (torch has no uint64 arithmetic)."""
     c &= 0xFFFFFFFFFFFFFFFF
@@ -235,36 +273,116 @@ def _t_splitmix64(x):
     return z ^ _t_shr(z, 31)
 
 
-def gen_columns_torch(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
-                      start: int = 0, device=None) -> List[Column]:
-    """``gen_columns`` for all-fixed-width, non-null schemas (Struct-100) computed with torch on
-    ``device`` (the GPU for the bench, so 12.5M-row shards need no host copy): the same SplitMix64
-    values keyed by (seed, column, GLOBAL row index), bit for bit."""
+def _t_keys(seed: int, col: int, rows):
+    k = (seed * 0x9E3779B97F4A7C15 + (col + 1) * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
+    return _t_splitmix64(rows ^ _u64_const(k))
+
+
+def _t_umod(x, m: int):
+    """x mod m for int64 tensors holding uint64 bits (numpy's uint64 %)."""
+    hi = _t_shr(x, 32)
+    lo = x & 0xFFFFFFFF
+    return ((hi % m) * ((1 << 32) % m) + lo % m) % m
+
+
+def _t_packbits(mask):
+    """numpy.packbits(mask, bitorder="little") of a bool tensor."""
     import torch
-    if _KNOBS.get(name, {}).get("null_pct", 10) != 0:
-        raise ValueError(f"{name}: the torch generator covers non-null schemas only")
+    n = mask.numel()
+    pad = (-n) % 8
+    m = torch.nn.functional.pad(mask.to(torch.uint8), (0, pad)).view(-1, 8)
+    w = (1 << torch.arange(8, device=mask.device, dtype=torch.int32))
+    return (m.to(torch.int32) * w).sum(1).to(torch.uint8)
+
+
+def _t_gen_fixed(t: int, h):
+    import torch
+    if t == FLOAT64:
+        return _t_shr(h, 11).to(torch.float64) * (1.0 / (1 << 53))
+    if t == FLOAT32:
+        return _t_shr(h, 40).to(torch.float32) * (1.0 / (1 << 24))
+    if t in (INT64, TIMESTAMP):
+        return h
+    if t in (INT32, DATE32):
+        return _t_trunc(h, 32, torch.int32)
+    if t == INT16:
+        return _t_trunc(h, 16, torch.int16)
+    if t == INT8:
+        return _t_trunc(h, 8, torch.int8)
+    raise ValueError(f"no torch generator for type {t}")
+
+
+def gen_column_torch(f: Field, seed: int, col: int, start: int, n: int, null_pct: int,
+                     str_max: int = 32, list_max: int = 16, list_null_pct: int = 5,
+                     elem_null_pct: int = 0, device=None) -> Column:
+    """``gen_column`` computed with torch on ``device``, bit for bit (the same SplitMix64 keys of
+    (seed, column, GLOBAL row index)); for the configuration-size GPU tests and the bench, whose
+    10M-row batches would take the numpy generator minutes."""
+    import torch
     rows = torch.arange(start, start + n, dtype=torch.int64, device=device)
-    out = []
-    for col, f in enumerate(fields):
-        k = (seed * 0x9E3779B97F4A7C15 + (col + 1) * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF
-        h = _t_splitmix64(rows ^ _u64_const(k))
-        t = f.type_id
-        if t == FLOAT64:
-            v = _t_shr(h, 11).to(torch.float64) * (1.0 / (1 << 53))
-        elif t == FLOAT32:
-            v = _t_shr(h, 40).to(torch.float32) * (1.0 / (1 << 24))
-        elif t in (INT64, TIMESTAMP):
-            v = h
-        elif t in (INT32, DATE32):
-            v = _t_trunc(h, 32, torch.int32)
-        elif t == INT16:
-            v = _t_trunc(h, 16, torch.int16)
-        elif t == INT8:
-            v = _t_trunc(h, 8, torch.int8)
+    h = _t_keys(seed, col, rows)
+    validity = None
+    valid = torch.ones(n, dtype=torch.bool, device=device)
+    pct = list_null_pct if f.type_id == LIST else null_pct
+    if f.nullable and pct > 0:
+        valid = (_t_shr(h, 7) % 100) >= pct
+        validity = _t_packbits(valid)
+    t = f.type_id
+    if t == BOOL:
+        return Column(values=_t_packbits(((_t_shr(h, 3) & 1) != 0) & valid), validity=validity)
+    if type_width(t) > 0:
+        v = _t_gen_fixed(t, h)
+        if f.nullable and pct > 0:
+            v = torch.where(valid, v, torch.zeros_like(v))
+        return Column(values=v.contiguous(), validity=validity)
+    if t == DECIMAL:
+        h2 = _t_keys(seed, col + 1000, rows) >> 3                  # arithmetic, as numpy's int64
+        v = torch.stack([h, h2], 1).contiguous().view(torch.uint8).reshape(n, 16).clone()
+        v[~valid] = 0
+        return Column(values=v.reshape(-1), validity=validity)
+    if t in (STRING, BINARY, LIST):
+        mod = (str_max + 1) if t != LIST else (list_max + 1)
+        lens = _t_shr(h, 17 if t != LIST else 19) % mod
+        lens = torch.where(valid, lens, torch.zeros_like(lens))
+        offsets = torch.zeros(n + 1, dtype=torch.int64, device=device)
+        torch.cumsum(lens, 0, out=offsets[1:])
+        total = int(offsets[-1].item())
+        rid = torch.repeat_interleave(rows, lens, output_size=total)
+        pos = torch.arange(total, dtype=torch.int64, device=device) - \
+            torch.repeat_interleave(offsets[:-1], lens, output_size=total)
+        if t != LIST:
+            hb = _t_splitmix64(_t_keys(seed, col + 2000, rid) ^ pos)
+            if t == STRING:
+                data = (32 + _t_umod(hb, 95)).to(torch.uint8)      # printable ASCII
+            else:
+                data = (_t_shr(hb, 13) & 0xFF).to(torch.uint8)
+            return Column(values=data, validity=validity, offsets=offsets.to(torch.int32))
+        elem = f.children[0]
+        eh = _t_splitmix64(_t_keys(seed, col + 3000, rid) ^ (pos << 32))
+        evalid = torch.ones(total, dtype=torch.bool, device=device)
+        evalidity = None
+        if elem.nullable and elem_null_pct > 0:
+            evalid = (_t_shr(eh, 5) % 100) >= elem_null_pct
+            evalidity = _t_packbits(evalid)
+        if elem.type_id == BOOL:
+            ev = _t_packbits(((_t_shr(eh, 3) & 1) != 0) & evalid)
         else:
-            raise ValueError(f"{name}: no torch generator for type {t}")
-        out.append(Column(values=v.contiguous()))
-    return out
+            ev = _t_gen_fixed(elem.type_id, eh)
+            ev = torch.where(evalid, ev, torch.zeros_like(ev))
+        child = Column(values=ev.contiguous(), validity=evalidity)
+        return Column(validity=validity, offsets=offsets.to(torch.int32), child=[child])
+    raise ValueError(f"no torch generator for type {t}")
+
+
+def gen_columns_torch(name: str, fields: Sequence[Field], n: int, seed: int = 1234,
+                      start: int = 0, device=None, **over) -> List[Column]:
+    """``gen_columns`` computed with torch on ``device`` (the GPU for the bench, so 10M-row
+    batches and 12.5M-row shards need no host generation or copy): bit for bit the same columns
+    (tests/test_workloads.py checks it against the numpy generator)."""
+    knobs = dict(_KNOBS.get(name, dict(null_pct=10)))
+    knobs.update(over)
+    return [gen_column_torch(f, seed, k, start, n, device=device, **knobs)
+            for k, f in enumerate(fields)]
 
 
 def _t_trunc(h, bits: int, dtype):

@@ -31,6 +31,8 @@
  *                            FMT/row/binary/BinaryArray.java:69-78,157-197)
  *   fury_rows_to_arrow      ArrowWriter.write(row)* + finishAsRecordBatch
  *                           (FMT/vectorized/ArrowWriter.java:74-99,205-225,519-540)
+ *   fury_arrow_append       ArrowWriter.write(row) appending at rowCount until finish() / reset()
+ *                           (FMT/vectorized/ArrowWriter.java:74-99)
  *   fury_frame_rows /       RowEncoder.encode(MemoryBuffer, T) / decode(MemoryBuffer) stream
  *   fury_unframe_rows       framing [int32 len][int64 schemaHash][row]
  *                           (FMT/encoder/Encoders.java:165-182,201-213)
@@ -192,6 +194,20 @@ int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* 
 int fury_rows_to_arrow(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* columns, void* stream);
 
+/* Appends the Arrow columns `src` (src_rows top-level entries, e.g. fury_rows_to_arrow /
+ * fury_decode_execute output) at entry dst_rows of the columns `dst` -- ArrowWriter.write(row)
+ * appending at rowCount until finish() / reset() (FMT/vectorized/ArrowWriter.java:74-99): values
+ * and STRING/BINARY payloads are copied after the destination's, offsets rebased on its end
+ * (offsets[dst_rows]), validity / BOOL bits shifted to its bit position, LIST / MAP child entries
+ * appended after its child entries, STRUCT children entry-aligned.  Every node's destination
+ * buffers must hold the combined entries (validity / BOOL bitmaps as 32-bit words: 4-byte aligned,
+ * padded to a multiple of 4 bytes; offsets entries + 1); fury_column.capacity, when > 0, bounds a
+ * node's values / payload bytes (FURY_ERR_CAPACITY).  Child offsets of `src` must start at 0.
+ * Reads the destination's and source's end offsets from the device, so the call synchronises
+ * `stream`; the copies themselves are one launch on it. */
+int fury_arrow_append(const fury_schema* schema, fury_column* dst, int64_t dst_rows,
+                      const fury_column* src, int64_t src_rows, void* stream);
+
 /* ---- ArrayEncoder / MapEncoder batches (Encoders.arrayEncoder / mapEncoder,
  *      FMT/encoder/Encoders.java:230-600, ArrayEncoderBuilder.java:118-140,
  *      MapEncoderBuilder.java:152-208) ----------------------------------------------------- */
@@ -233,6 +249,13 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
  * called.  By construction (a look-back computes a silent predecessor's aggregate itself) it is
  * never raised on working hardware. */
 int fury_device_status(void* stream);
+
+/* ---- workspace (no reference equivalent) ------------------------------------------------- */
+/* The library caches the device workspaces of its calls (scan scratch, decode plans, column
+ * tables; at most 2 GB of idle blocks per process).  Releases every idle cached block of `device`
+ * (after the work that last used it, so the call may wait for it) and trims the device's stream
+ * memory pool.  An allocation that fails does the same by itself before it reports. */
+int fury_trim_workspace(int32_t device);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
 /* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,

@@ -141,6 +141,21 @@ public final class GpuRowEncoder<T> implements RowEncoder<T> {
         }
       }
       nativeDecodeHostExecute(schemaHandle, plan, describe(out, true));
+      // A MapVector's entries struct is not a schema node (fury_row.h): the native side writes
+      // no validity for it, and every entry of a map is a defined (key, value) struct, as the
+      // reference's MapWriter marks them through startEntry / endEntry (ArrowWriter.java:623-630).
+      for (int i = 0; i < nodes.size(); i++) {
+        FieldVector v = nodes.get(i);
+        if (v instanceof MapVector) {
+          int entries = (int) counts[2 * i];
+          int children = entries == 0 ? 0 : v.getOffsetBuffer().getInt((long) entries * 4);
+          StructVector kv = (StructVector) ((MapVector) v).getDataVector();
+          for (int j = 0; j < children; j++) {
+            kv.setIndexDefined(j);
+          }
+          kv.setValueCount(children);
+        }
+      }
       for (int i = nodes.size() - 1; i >= 0; i--) {     // children first
         FieldVector v = nodes.get(i);
         int entries = (int) counts[2 * i];

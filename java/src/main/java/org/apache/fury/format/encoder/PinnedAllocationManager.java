@@ -26,8 +26,9 @@ public final class PinnedAllocationManager extends AllocationManager {
         }
       };
 
-  private static final ArrowBuf EMPTY =
-      new ArrowBuf(ReferenceManager.NO_OP, null, 0, GpuRowEncoder.hostAlloc(64));
+  // zero capacity at address 0, as Arrow's own managers do: loading the class needs neither the
+  // native library nor a GPU, and nothing is allocated that would never be freed
+  private static final ArrowBuf EMPTY = new ArrowBuf(ReferenceManager.NO_OP, null, 0, 0);
 
   private final long address;
   private final long size;

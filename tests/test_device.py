@@ -873,38 +873,47 @@ def test_side_stream_encode_decode(oracle, dev, sizing):
                          oracle.decode(fields, want, want_offs, n), n)
 
 
-def test_bound_decode_falls_back_on_slot_outside_row(dev):
-    """A string slot whose size runs far past its row (malformed rows) makes the column's payload
-    larger than the row-byte bound: decode_batch(sizing="bound") must not hand back offsets that
-    point past the values buffer -- it re-decodes with exact sizes.  (The bytes read past the row
-    stay inside a zero-padded allocation here.)"""
-    from fury_amd.encoder import Encoders, RowBatch
+def test_bound_decode_falls_back_when_payload_exceeds_rows(oracle, dev):
+    """Slots may point at any bytes of the batch (the reference reads the shared buffer): ten rows
+    whose s1 covers the WHOLE batch make the column's payload ten times the row bytes, past the
+    "bound" sizing -- decode_batch(sizing="bound") must re-decode with exact sizes and equal
+    "measure" and the oracle.  A slot running past the batch raises IndexOutOfBoundsException
+    under both sizings (test_bounds.py covers the rest)."""
+    from fury_amd.encoder import Encoders, IndexOutOfBoundsException, RowBatch, column_to_host
     fields = SCHEMAS["mixed"]
     n = 1000
     host = gen_columns("mixed", fields, n, seed=2)
     enc = Encoders.bean(fields, device=dev)
     b = enc.encode_batch(_dev_cols(host, dev), n)
     total = b.rows.numel()
-    big = torch.zeros(total + (1 << 20), dtype=torch.uint8, device=dev)
-    big[:total] = b.rows
     offs = b.row_offsets.cpu().numpy()
-    r = 500
-    row = big[int(offs[r]):int(offs[r + 1])].cpu().numpy().copy()
+    rows = b.rows.cpu().numpy().copy()
     slot_at = 8 + 8 * 3                               # s1's slot (field 3)
-    row[0] &= ~np.uint8(1 << 3)                       # s1 not null
-    rel = 56                                          # start of the var section
-    size = total                                      # runs past the batch's row bytes
-    row[slot_at:slot_at + 8] = np.frombuffer(np.array([(rel << 32) | size], np.uint64).tobytes(),
-                                             np.uint8)
-    big[int(offs[r]):int(offs[r + 1])] = torch.from_numpy(row).to(dev)
-    bad = RowBatch(big[:total], b.row_offsets, n, enc.schema_hash)
-    got = enc.decode_batch(bad, sizing="bound")
-    ref = enc.decode_batch(bad, sizing="measure")
-    torch.cuda.synchronize()
+    for r in range(500, 510):
+        base = int(offs[r])
+        rows[base] &= ~np.uint8(1 << 3)               # s1 not null
+        rel = (-base) & 0xFFFFFFFF
+        rows[base + slot_at:base + slot_at + 8] = np.frombuffer(
+            np.array([(rel << 32) | total], np.uint64).tobytes(), np.uint8)
+    batch = RowBatch(torch.from_numpy(rows).to(dev), b.row_offsets, n, enc.schema_hash)
+    got = enc.decode_batch(batch, sizing="bound")
+    ref = enc.decode_batch(batch, sizing="measure")
     need = int(got[3].offsets[n])
-    assert need > total and got[3].values.numel() >= need
+    assert need > 10 * total - 1 and got[3].values.numel() >= need
     assert torch.equal(got[3].offsets, ref[3].offsets)
     assert torch.equal(got[3].values[:need], ref[3].values[:need])
+    assert_columns_equal(fields, [column_to_host(c) for c in got],
+                         oracle.decode(fields, rows, offs, n), n)
+    r = 700
+    base = int(offs[r])
+    rows2 = rows.copy()
+    rows2[base] &= ~np.uint8(1 << 3)
+    rows2[base + slot_at:base + slot_at + 8] = np.frombuffer(
+        np.array([(56 << 32) | total], np.uint64).tobytes(), np.uint8)   # runs past the batch
+    bad = RowBatch(torch.from_numpy(rows2).to(dev), b.row_offsets, n, enc.schema_hash)
+    for sizing in ("bound", "measure"):
+        with pytest.raises(IndexOutOfBoundsException, match="row 700 "):
+            enc.decode_batch(bad, sizing=sizing)
 
 
 def test_c5_shard_size_property(oracle, dev):
