@@ -119,7 +119,7 @@ def cpu_baseline(name, fields, budget_s, sample_rows):
     reps = 0
     while True:
         r, o = O.encode(fields, host, sample_rows)
-        O.decode(fields, r, o if var else None, sample_rows, with_validity=False)
+        O.decode(fields, r, o if var else None, sample_rows, with_validity=False, sizing="bound")
         del r, o
         reps += 1
         if time.perf_counter() - t0 >= budget_s:
@@ -140,7 +140,7 @@ def cpu_baseline(name, fields, budget_s, sample_rows):
         k, m = 0, bounds[t][1] - bounds[t][0]
         while time.perf_counter() < stop:
             r, o = O.encode(fields, parts[t], m)
-            O.decode(fields, r, o if var else None, m, with_validity=False)
+            O.decode(fields, r, o if var else None, m, with_validity=False, sizing="bound")
             k += 1
         return k
     t0 = time.perf_counter()

@@ -91,6 +91,10 @@ def lib():
         L.fo_decode_batch.restype = ctypes.c_int
         L.fo_decode_batch.argtypes = [ctypes.POINTER(_CField), ctypes.c_int32, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(_CColumn)]
+        L.fo_decode_batch_cur.restype = ctypes.c_int
+        L.fo_decode_batch_cur.argtypes = [ctypes.POINTER(_CField), ctypes.c_int32, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.POINTER(_CColumn), ctypes.c_void_p]
         L.fo_encode_fixed_inplace.restype = ctypes.c_int64
         L.fo_encode_fixed_inplace.argtypes = [ctypes.POINTER(_CField), ctypes.c_int32,
                                               ctypes.POINTER(_CColumn), ctypes.c_int64,
@@ -227,11 +231,77 @@ def _trim(f: F, c: Col, n: int) -> Col:
     raise ValueError(t)
 
 
+def _shape_only(f: F) -> Col:
+    """A column tree with every buffer None (the sizing pass writes nothing)."""
+    return Col(child=[_shape_only(c) for c in f.children] if f.children else None)
+
+
+def _nodes_dfs(fields: Sequence[F]):
+    out = []
+
+    def walk(f):
+        out.append(f)
+        for c in f.children:
+            walk(c)
+    for f in fields:
+        walk(f)
+    return out
+
+
+def _alloc_exact(f: F, n: int, cur: np.ndarray, node: int, with_validity: bool):
+    """Output column of node `node` (depth-first id) with n entries, sized from the sizing pass's
+    cursors; returns (column, next node id)."""
+    vb = np.zeros((n + 7) // 8 + 1, np.uint8) if with_validity else None
+    t = f.type_id
+    if t == BOOL:
+        return Col(values=np.zeros((n + 7) // 8 + 1, np.uint8), validity=vb), node + 1
+    if t in WIDTH:
+        return Col(values=np.zeros(n * WIDTH[t] + 8, np.uint8), validity=vb), node + 1
+    if t in (STRING, BINARY):
+        return Col(values=np.zeros(int(cur[node]) + 8, np.uint8), validity=vb,
+                   offsets=np.zeros(n + 1, np.int32)), node + 1
+    if t == DECIMAL:
+        return Col(values=np.zeros(n * 16 + 8, np.uint8), validity=vb), node + 1
+    m = n if t == STRUCT else int(cur[node])
+    kids, nxt = [], node + 1
+    for c in f.children:
+        k, nxt = _alloc_exact(c, m, cur, nxt, with_validity)
+        kids.append(k)
+    if t == STRUCT:
+        return Col(validity=vb, child=kids), nxt
+    if t in (LIST, MAP):
+        return Col(validity=vb, offsets=np.zeros(n + 1, np.int32), child=kids), nxt
+    raise ValueError(f"unsupported type {t}")
+
+
 def decode(fields: Sequence[F], rows: np.ndarray, row_offsets: Optional[np.ndarray], nrows: int,
-           with_validity: bool = True) -> List[Col]:
+           with_validity: bool = True, sizing: str = "exact") -> List[Col]:
+    """Two passes, as fo_decode_batch prescribes: a sizing pass (nothing written) whose cursors
+    give every node's exact payload / child-entry count -- slots may share bytes of the batch, so
+    no bound from the row bytes holds -- then the decode into buffers of those sizes.
+    sizing="bound" (the CPU baseline, rows written by an encoder: every value inside its own row)
+    skips the sizing pass and sizes outputs by the row bytes, as the reference's fromRow has no
+    sizing pass either."""
     keep: list = []
-    outs = [_alloc_out(f, nrows, int(rows.nbytes), with_validity) for f in fields]
-    st = lib().fo_decode_batch(_c_fields(fields, keep), len(fields), _ptr(rows),
+    cf = _c_fields(fields, keep)
+    if sizing == "bound":
+        outs = [_alloc_out(f, nrows, int(rows.nbytes), with_validity) for f in fields]
+        st = lib().fo_decode_batch(cf, len(fields), _ptr(rows), _ptr(row_offsets), nrows,
+                                   _c_columns(outs, keep))
+        if st != 0:
+            raise RuntimeError(f"oracle decode failed with status {st}")
+        return [_trim(f, c, nrows) for f, c in zip(fields, outs)]
+    cur = np.zeros(len(_nodes_dfs(fields)) + 1, np.int64)
+    st = lib().fo_decode_batch_cur(cf, len(fields), _ptr(rows), _ptr(row_offsets), nrows,
+                                   _c_columns([_shape_only(f) for f in fields], keep),
+                                   cur.ctypes.data)
+    if st != 0:
+        raise RuntimeError(f"oracle decode failed with status {st}")
+    outs, node = [], 0
+    for f in fields:
+        c, node = _alloc_exact(f, nrows, cur, node, with_validity)
+        outs.append(c)
+    st = lib().fo_decode_batch(cf, len(fields), _ptr(rows),
                                _ptr(row_offsets), nrows, _c_columns(outs, keep))
     if st != 0:
         raise RuntimeError(f"oracle decode failed with status {st}")

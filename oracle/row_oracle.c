@@ -460,8 +460,10 @@ static void fo_null_entry(const fury_field* f, fury_column* c, int64_t out_i, in
       if (c->values) memset((uint8_t*)c->values + out_i * 16, 0, 16);
       return;
     case FURY_TYPE_STRING: case FURY_TYPE_BINARY: case FURY_TYPE_LIST: case FURY_TYPE_MAP:
-      c->offsets[out_i] = (int32_t)cur[node];
-      c->offsets[out_i + 1] = (int32_t)cur[node];
+      if (c->offsets) {
+        c->offsets[out_i] = (int32_t)cur[node];
+        c->offsets[out_i + 1] = (int32_t)cur[node];
+      }
       return;
     case FURY_TYPE_STRUCT: {
       int32_t child_node = node + 1;
@@ -510,8 +512,10 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
         size = (int32_t)oas;
         if (c->values) memcpy((uint8_t*)c->values + start, v->base + rel, (size_t)size);
       }
-      c->offsets[out_i] = (int32_t)start;
-      c->offsets[out_i + 1] = (int32_t)(start + size);
+      if (c->offsets) {
+        c->offsets[out_i] = (int32_t)start;
+        c->offsets[out_i + 1] = (int32_t)(start + size);
+      }
       cur[node] = start + size;
       return;
     }
@@ -524,13 +528,13 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
     }
     case FURY_TYPE_LIST: {                    /* getArray :168-178 */
       int32_t count = 0;
-      c->offsets[out_i] = (int32_t)cur[node];
+      if (c->offsets) c->offsets[out_i] = (int32_t)cur[node];
       if (!is_null) {
         int64_t oas = fo_get_i64(slot);
         fo_read_array(v->base + (int32_t)(oas >> 32), &f->children[0], c->child, cur, node + 1,
                       node, &count);
       }
-      c->offsets[out_i + 1] = (int32_t)cur[node];
+      if (c->offsets) c->offsets[out_i + 1] = (int32_t)cur[node];
       return;
     }
     case FURY_TYPE_STRUCT: {                  /* getStruct :148-166 */
@@ -558,7 +562,7 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
     case FURY_TYPE_MAP: {                     /* getMap + BinaryMap.pointTo :62-77 */
       int32_t key_node = node + 1;
       int32_t val_node = key_node + fo_node_count(&f->children[0]);
-      c->offsets[out_i] = (int32_t)cur[node];
+      if (c->offsets) c->offsets[out_i] = (int32_t)cur[node];
       if (!is_null) {
         int64_t oas = fo_get_i64(slot);
         const uint8_t* mb = v->base + (int32_t)(oas >> 32);
@@ -570,7 +574,7 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
         fo_read_array(mb + 8 + key_bytes, &f->children[1], &c->child[1], cur, val_node, node, &nv);
         if (nk != nv) g_err = FURY_ERR_UNSUPPORTED;   /* BinaryMap.java:73-75 */
       }
-      c->offsets[out_i + 1] = (int32_t)cur[node];
+      if (c->offsets) c->offsets[out_i + 1] = (int32_t)cur[node];
       return;
     }
     default:
@@ -581,10 +585,21 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
 }
 
 /* Decode rows [row_offsets[i], row_offsets[i+1]) (or i * fixed_size when row_offsets is NULL)
- * into columns.  Variable-length outputs must be large enough (callers size them from a first
- * pass with values == NULL for STRING/BINARY, which only fills offsets). */
+ * into columns.  Variable-length outputs must be large enough: callers size them from a first
+ * pass over a column tree with every buffer NULL (nothing is written), whose final cursors
+ * (cur_out, one per schema node in depth-first order) are the exact sizes -- STRING / BINARY:
+ * payload bytes; LIST / MAP: child entries. */
+int fo_decode_batch_cur(const fury_field* fields, int32_t nfields, const uint8_t* rows,
+                        const int64_t* row_offsets, int64_t nrows, fury_column* cols,
+                        int64_t* cur_out);
 int fo_decode_batch(const fury_field* fields, int32_t nfields, const uint8_t* rows,
                     const int64_t* row_offsets, int64_t nrows, fury_column* cols) {
+  return fo_decode_batch_cur(fields, nfields, rows, row_offsets, nrows, cols, NULL);
+}
+
+int fo_decode_batch_cur(const fury_field* fields, int32_t nfields, const uint8_t* rows,
+                        const int64_t* row_offsets, int64_t nrows, fury_column* cols,
+                        int64_t* cur_out) {
   g_err = 0;
   int32_t nodes = 0;
   for (int k = 0; k < nfields; k++) nodes += fo_node_count(&fields[k]);
@@ -603,6 +618,7 @@ int fo_decode_batch(const fury_field* fields, int32_t nfields, const uint8_t* ro
       node += fo_node_count(&fields[k]);
     }
   }
+  if (cur_out) memcpy(cur_out, cur, (size_t)nodes * sizeof(int64_t));
   free(cur);
   return g_err;
 }
