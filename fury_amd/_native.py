@@ -90,6 +90,15 @@ SIGNATURES = {
     "fury_decode_host_prepare": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(_I64),
                                                 ctypes.POINTER(_I64), ctypes.POINTER(_P), _I32]),
     "fury_decode_host_execute": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn)]),
+    "fury_jni_exception_class": (ctypes.c_char_p, [ctypes.c_int]),
+    "fury_jni_schema_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(_I32),
+                                              _I32, _I32, ctypes.POINTER(_P)]),
+    "fury_jni_encode_host": (ctypes.c_int, [_P, ctypes.POINTER(_I64), _I64, _I64, _P, _I64, _P,
+                                            ctypes.POINTER(_I64), _I32]),
+    "fury_jni_decode_host": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(_I64), _I64, _I32]),
+    "fury_jni_decode_host_prepare": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(_I64),
+                                                    ctypes.POINTER(_P), _I32]),
+    "fury_jni_decode_host_execute": (ctypes.c_int, [_P, _P, ctypes.POINTER(_I64), _I64]),
     "fury_arrow_ipc_schema": (ctypes.c_int, [_P, _P, _I64, ctypes.POINTER(_I64)]),
     "fury_arrow_ipc_record_batch": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _I64,
                                                    ctypes.POINTER(_I64), _P]),
@@ -106,6 +115,8 @@ def lib():
                               "`python -c 'import __graft_entry__ as g; g.build()'`")
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("FURY_ROW_LIB") and not hasattr(L, name):
+                continue          # an older build for A/B: entry points it predates stay unbound
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

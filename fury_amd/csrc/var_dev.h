@@ -1133,7 +1133,7 @@ __device__ int64_t look_back_help(const VarArgs& a, int k, const uint8_t* rows,
                                   const int64_t* offs, const uint64_t* status, int64_t b, int nseq,
                                   int q, uint32_t* err) {
   const int lane = threadIdx.x & 63;
-  const uint32_t limit = a.help_now ? 0u : kHelpSpins;
+  const uint32_t limit = (a.help_now & 1) ? 0u : kHelpSpins;
   int64_t excl = 0;
   for (int64_t j = b - 1;; j -= 64) {
     const int64_t idx = j - lane;

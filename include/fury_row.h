@@ -341,6 +341,31 @@ int fury_decode_host_prepare(const fury_schema* schema, const void* rows, const 
                              fury_decode_plan** plan, int32_t device);
 int fury_decode_host_execute(fury_decode_plan* plan, fury_column* columns);
 
+/* ---- JNI core (java/.../GpuRowEncoder.java's native methods, minus the JNIEnv marshalling) ---
+ * The exact arrays GpuRowEncoder builds, decoded in this library (fury_row_jni.cc only copies Java
+ * arrays in and out and throws fury_jni_exception_class(status)).  Reference surface:
+ * Encoders.bean(...) / RowEncoder (FMT/encoder/Encoders.java:60-219, RowEncoder.java:26-32).
+ *   names / meta: flattenField in pre-order -- names[i] and meta[3 i .. 3 i + 2] = {typeId,
+ *     nullable, numChildren} of node i (a MAP's children are key and value; `nodes` entries, the
+ *     first `top` subtrees are the bean's fields in slot order);
+ *   desc: describe() in pre-order -- 5 int64 per schema node {values address, validity address,
+ *     offsets address, values capacity, numChildren} (host addresses); its child counts must
+ *     match the schema's (FURY_ERR_INVALID_ARGUMENT otherwise);
+ *   counts: 2 int64 per node (breadth-first, fury_decode_prepare order): entries, payload bytes. */
+const char* fury_jni_exception_class(int status);   /* Java class name of a status, NULL for OK */
+int fury_jni_schema_create(const char* const* names, const int32_t* meta, int32_t nodes,
+                           int32_t top, fury_schema** out);
+int fury_jni_encode_host(const fury_schema* schema, const int64_t* desc, int64_t desc_len,
+                         int64_t nrows, void* rows, int64_t rows_capacity, int64_t* row_offsets,
+                         int64_t* row_bytes, int32_t device);
+int fury_jni_decode_host(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
+                         int64_t nrows, const int64_t* desc, int64_t desc_len, int32_t device);
+int fury_jni_decode_host_prepare(const fury_schema* schema, const void* rows,
+                                 const int64_t* row_offsets, int64_t nrows, int64_t* counts,
+                                 fury_decode_plan** plan, int32_t device);
+int fury_jni_decode_host_execute(const fury_schema* schema, fury_decode_plan* plan,
+                                 const int64_t* desc, int64_t desc_len);
+
 /* ---- Arrow IPC (ArrowUtils.serializeRecordBatch, FMT/vectorized/ArrowUtils.java:63-72;
  *      ArrowSerializers stream writers, FMT/vectorized/ArrowSerializers.java:128-167) --------- */
 /* Encapsulated IPC Schema message of the schema, in HOST memory:
