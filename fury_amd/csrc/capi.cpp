@@ -416,7 +416,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     a->tile_rows = encode_tile_rows(*a);
   }
   a->err = device_error_word();
-  a->help_now = lookback_help_mode() | (var_diag_bits() << 8);   // DIAG (temporary)
+  a->help_now = lookback_help_mode();
   return FURY_OK;
 }
 
@@ -748,15 +748,6 @@ int fury_device_status(void* stream) {
 
 int fury_set_tuning(const char* key, int32_t value) {
   if (!key) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_set_tuning: key is null");
-  if (std::string(key) == "var_tile") {
-    if (value != 256 && value != 512) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_tile: 256 or 512");
-    set_var_tile_rows(value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "var_diag") {   // DIAG (temporary, round-3 study)
-    set_var_diag_bits(value);
-    return FURY_OK;
-  }
   if (std::string(key) == "lookback_help") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "lookback_help: 0..1");
     set_lookback_help_mode(value);
@@ -772,7 +763,6 @@ int fury_set_tuning(const char* key, int32_t value) {
 
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "lookback_help") return lookback_help_mode();
-  if (key && std::string(key) == "var_tile") return var_tile_rows();
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "lookback_timeouts")
     return static_cast<int32_t>(lookback_timeouts());

@@ -155,8 +155,6 @@ int workspace_reserve(size_t bytes, void** out);
 int encode_tile_rows(const VarArgs& a);
 int64_t lookback_timeouts();
 int lookback_help_mode();
-int var_diag_bits();          // DIAG (temporary)
-void set_var_diag_bits(int v);
 void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 // Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.
@@ -168,13 +166,6 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 // and writes payloads clipped to each column's capacity.
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                       hipStream_t stream, bool arrow);
-// The decode kernel (var_dec.hip): NT-row tiles, per-wave LDS-staged rows; row_hint = expected
-// mean row bytes (sizes the stage).
-int launch_decode_var_ws(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                         uint64_t* status, int nseq, int64_t nb, int nt, double row_hint,
-                         hipStream_t stream);
-int var_tile_rows();
-void set_var_tile_rows(int v);
 // ---- generic (nested) schema engine: generic.hip --------------------------------------------
 constexpr int kGenMaxNodes = 48;      // schema tree nodes in the argument block
 constexpr int kGenMaxWideNodes = 4096;  // beyond 48: node table uploaded per call (GenArgs.tab)

@@ -66,9 +66,6 @@ int64_t lookback_timeouts() { return device_error_count(); }
 // at once -- the path a late-dispatched predecessor takes -- instead of polling first.
 static int g_help_now = 0;
 int lookback_help_mode() { return g_help_now; }
-static int g_diag = 0;
-int var_diag_bits() { return g_diag; }
-void set_var_diag_bits(int v) { g_diag = v; }
 void set_lookback_help_mode(int v) { g_help_now = v; }
 // Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
 // counts, as plan_encode_pipe) fit the LDS image with headroom.
@@ -169,26 +166,6 @@ uint32_t dec_img_bytes(const VarArgs& a, int tile) {
   return static_cast<uint32_t>(need < cap ? need : cap);
 }
 
-// Mean row bytes the decode expects, from the output capacities (exact after
-// fury_row_decode_measure or an earlier decode of the same batch; an over-estimate under "bound"
-// sizing): it sizes the decode's per-wave LDS stage, so it moves speed only.
-double decode_row_hint(const VarArgs& a) {
-  double row = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = hcol(a, k);
-    const double per = c.values && c.capacity > 0 && a.nrows > 0
-                           ? static_cast<double>(c.capacity) / a.nrows : 32.0;
-    if (c.kind == kDecimal) row += 16;
-    else if (c.kind == kBytes) row += per + 4;
-    else if (c.kind == kListFixed) row += 12 + per * (c.width == 0 ? 1 : c.width);
-  }
-  return row;
-}
-
-static int g_var_tile = 512;      // tuning "var_tile": rows per decode tile (256 / 512)
-int var_tile_rows() { return g_var_tile; }
-void set_var_tile_rows(int v) { g_var_tile = v; }
-
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                       hipStream_t stream, bool arrow) {
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
@@ -196,15 +173,35 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   int nseq = 0;
   for (int k = 0; k < a.ncols; k++)
     if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
-  const int nt = g_var_tile;
-  const int64_t nb = (a.nrows + nt - 1) / nt;
-  // look-back status words (tiles x sequences), zeroed per launch
-  const size_t wsb = static_cast<size_t>(nb) * (nseq > 0 ? nseq : 1) * 8;
+  const int64_t nb = nblocks(a.nrows);
+  if (a.ncols <= kRegCols) {
+    // 512-row tiles halve the look-back chain links: faster with several string / list
+    // sequences to chain (mixed, 3: 0.656 vs 0.737 ms), slower with one (nested: 0.287 vs
+    // 0.274 ms) -- scripts/ab_var.py.
+    const bool wide = nseq >= 2;
+    const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
+    // status words: tiles x fields, zeroed per launch
+    const size_t wsb = static_cast<size_t>(nbr) * a.ncols * 8;
+    uint64_t* ws = nullptr;
+    int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
+    if (st) return st;
+    st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+    const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
+    if (!st) st = launch_decode_var_reg(a, rows, offs, ws, img, wide, nb, nbr, stream);
+    dev_free(ws, stream);
+    return st;
+  }
+  // look-back status words (nb x nseq), zeroed per launch
+  const size_t wsb = (nb * nseq + 1) * 8;
   uint64_t* ws = nullptr;
   int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
   if (st) return st;
   st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-  if (!st) st = launch_decode_var_ws(a, rows, offs, ws, nseq, nb, nt, decode_row_hint(a), stream);
+  if (!st) {
+    hipLaunchKernelGGL(decode_var_kernel, dim3(nb), dim3(kThreads), 0, stream, a, rows, offs,
+                       ws, nseq);
+    st = check_hip(hipGetLastError(), "decode_var launch");
+  }
   dev_free(ws, stream);
   return st;
 }

@@ -1257,10 +1257,13 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   const bool live = tid < nr;
   const int64_t r = live ? r0 + tid : r0;
   const int64_t total = offs[a.nrows];            // the batch: every read stays in [0, total)
-  const int64_t base = offs[r];
-  const bool rok = row_ok(base, a.fixed_size, total);
-  if (live && !rok) raise_oob(a.err, r);
-  const uint8_t* row = rows + (rok ? base : 0);
+  const int64_t lim = total - a.fixed_size;       // last byte a row header may start at
+  const int64_t base0 = offs[r];
+  // the header is read at a clamped (always readable) start; a row outside the batch decodes as
+  // all-null and is reported
+  const int64_t base = min<int64_t>(max<int64_t>(base0, 0), max<int64_t>(lim, 0));
+  const bool rok = lim >= 0 && base == base0;
+  const uint8_t* row = rows + base;
   // null word + slots: one batch of 16-byte loads of the aligned blocks covering them (rows are
   // only 8-aligned; selecting words afterwards costs cndmasks, while 8-byte loads took 1 + K
   // instructions, each touching one cache line per lane -- the vector memory pipeline's cost).
@@ -1270,7 +1273,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   constexpr int kNch = (K + 3) / 2;
   const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
   const int mis = static_cast<int>((ra >> 3) & 1);
-  const int need = rok ? (mis + K + 2) / 2 : 0;
+  const int need = lim >= 0 ? (mis + K + 2) / 2 : 0;
   const auto blk = gl(reinterpret_cast<const u64x2*>(ra & ~uintptr_t(15)));
   uint64_t hw[2 * kNch];
 #pragma unroll
@@ -1287,6 +1290,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   // counts (LIST: dependent load of the array header), bounds-checked: a value outside the batch
   // decodes as null and is reported (slot_count)
   uint32_t cnt[K];
+  uint64_t badw = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
@@ -1294,11 +1298,10 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     if (((nullw >> k) & 1) || c.kind < kBytes) continue;
     bool bad = false;
     cnt[k] = static_cast<uint32_t>(slot_count(c.kind, c.width, slot[k], base, rows, total, &bad));
-    if (bad) {
-      nullw |= 1ull << k;
-      raise_oob(a.err, r);
-    }
+    badw |= static_cast<uint64_t>(bad) << k;
   }
+  nullw |= badw;
+  if (live && (badw || !rok)) raise_oob(a.err, r);
   // in-tile exclusive scans, two columns per 64-bit scan (tile totals < 2^32)
   uint32_t ex[K], tot[K];
 #pragma unroll
