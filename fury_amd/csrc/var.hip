@@ -171,8 +171,15 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
   if (a.nrows == 0) return FURY_OK;
   int nseq = 0;
-  for (int k = 0; k < a.ncols; k++)
-    if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
+  bool bytes = false, lists = false, other = false;   // -> the register-staged instance's mode
+  for (int k = 0; k < a.ncols; k++) {
+    const int kd = hcol(a, k).kind;
+    if (kd == kBytes || kd == kListFixed) nseq++;
+    bytes |= kd == kBytes;
+    lists |= kd == kListFixed;
+    other |= kd != kFixed && kd != kBool && kd != kBytes && kd != kListFixed;
+  }
+  const int mode = other || (bytes && lists) ? kSeqAll : lists ? kSeqLists : kSeqBytes;
   const int64_t nb = nblocks(a.nrows);
   if (a.ncols <= kRegCols) {
     // 512-row tiles halve the look-back chain links: faster with several string / list
@@ -180,14 +187,14 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     // 0.274 ms) -- scripts/ab_var.py.
     const bool wide = nseq >= 2;
     const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
-    // status words: tiles x fields, zeroed per launch
-    const size_t wsb = static_cast<size_t>(nbr) * a.ncols * 8;
+    // status words: tiles x K (the instance's column count), zeroed per launch
+    const size_t wsb = static_cast<size_t>(nbr) * reg_dec_k(a.ncols) * 8;
     uint64_t* ws = nullptr;
     int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
-    if (!st) st = launch_decode_var_reg(a, rows, offs, ws, img, wide, nb, nbr, stream);
+    if (!st) st = launch_decode_var_reg(a, rows, offs, ws, img, wide, mode, nb, nbr, stream);
     dev_free(ws, stream);
     return st;
   }

@@ -635,6 +635,8 @@ __device__ __forceinline__ int store_image(uint8_t* g, const uint8_t* img, int64
 // round trip, issued for all columns at once).  LDS holds only the image, so five workgroups
 // share a CU.
 constexpr int kRegCols = 16;
+// kind modes of the register-staged decode instances (kind_of)
+constexpr int kSeqBytes = 0, kSeqLists = 1, kSeqAll = 2;
 constexpr int kRegImg = 30 * 1024;
 
 // Copies len bytes at global src to 8-byte aligned dst (LDS or global) as whole words, zero pad.
@@ -1233,7 +1235,26 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 }
 
 #ifdef FURY_VAR_DEC
-template <int K, int NT = kThreads>
+// The kind of column k as the kernel instance sees it.  Instances for schemas of fixed-width, bool
+// and STRING / BINARY fields only (kSeqBytes) or of fixed-width, bool and LIST fields (kSeqLists),
+// as the host checks, map every kind onto those three, so the compiler drops the other kinds' code
+// from the unrolled K-column body (mixed, K = 6: 7.1k instead of 18k instructions; the full body
+// cost the mixed decode ~10 % in instruction-cache misses).
+template <int M>
+__device__ __forceinline__ int kind_of(const VarCol& c) {
+  const int kd = c.kind;
+  if (M == kSeqAll) return kd;
+  const int seq = M == kSeqBytes ? kBytes : kListFixed;
+  return kd == seq ? seq : (kd == kBool ? kBool : kFixed);
+}
+// a sequence column's payload is bytes (else list elements)
+template <int M>
+__device__ __forceinline__ bool bytes_seq(const VarCol& c) {
+  return M == kSeqBytes || (M == kSeqAll && c.kind == kBytes);
+}
+__device__ __forceinline__ bool seq_kind(int kd) { return kd == kBytes || kd == kListFixed; }
+
+template <int K, int NT, int M>
 __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                            const int64_t* __restrict__ offs,
                                                            uint64_t* __restrict__ status,
@@ -1273,7 +1294,9 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   constexpr int kNch = (K + 3) / 2;
   const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
   const int mis = static_cast<int>((ra >> 3) & 1);
-  const int need = lim >= 0 ? (mis + K + 2) / 2 : 0;
+  // K may exceed the schema's field count (instances for K in {2, 4, 6, 8, 12, 16}): the columns
+  // past a.ncols are zeroed records (no outputs, null) and their slots are not loaded
+  const int need = lim >= 0 ? (mis + a.ncols + 2) / 2 : 0;
   const auto blk = gl(reinterpret_cast<const u64x2*>(ra & ~uintptr_t(15)));
   uint64_t hw[2 * kNch];
 #pragma unroll
@@ -1284,6 +1307,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     hw[2 * c + 1] = x.y;
   }
   uint64_t nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
+  nullw |= a.ncols >= 64 ? 0ull : (~0ull << a.ncols);
   uint64_t slot[K];
 #pragma unroll
   for (int k = 0; k < K; k++) slot[k] = mis ? hw[k + 2] : hw[k + 1];
@@ -1294,10 +1318,11 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
+    const int kd = kind_of<M>(c);
     cnt[k] = 0;
-    if (((nullw >> k) & 1) || c.kind < kBytes) continue;
+    if (((nullw >> k) & 1) || kd < kBytes) continue;
     bool bad = false;
-    cnt[k] = static_cast<uint32_t>(slot_count(c.kind, c.width, slot[k], base, rows, total, &bad));
+    cnt[k] = static_cast<uint32_t>(slot_count(kd, c.width, slot[k], base, rows, total, &bad));
     badw |= static_cast<uint64_t>(bad) << k;
   }
   nullw |= badw;
@@ -1306,8 +1331,8 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   uint32_t ex[K], tot[K];
 #pragma unroll
   for (int k = 0; k < K; k += 2) {
-    const bool s0 = is_seq(a.col[k]);
-    const bool s1 = k + 1 < K && is_seq(a.col[k + 1]);
+    const bool s0 = seq_kind(kind_of<M>(a.col[k]));
+    const bool s1 = k + 1 < K && seq_kind(kind_of<M>(a.col[k + 1]));
     ex[k] = tot[k] = 0;
     if (k + 1 < K) ex[k + 1] = tot[k + 1] = 0;
     if (!s0 && !s1) continue;
@@ -1324,7 +1349,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
   if (tid == 0) {
 #pragma unroll
     for (int k = 0; k < K; k++)
-      if (is_seq(a.col[k]))
+      if (seq_kind(kind_of<M>(a.col[k])))
         st_status(status + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
   }
   // tile-relative LDS images of every variable-length column (image byte / bit i = the tile's
@@ -1335,13 +1360,14 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
+    const int kd = kind_of<M>(c);
     img_at[k] = kNone;
-    if (!is_seq(c) || !c.values || tot[k] == 0) continue;
+    if (!seq_kind(kd) || !c.values || tot[k] == 0) continue;
     int64_t need;
-    if (c.kind == kBytes) need = r16(tot[k] + 16);
+    if (kd == kBytes) need = r16(tot[k] + 16);
     else if (c.width == 0) need = r16((((tot[k] + 31) >> 5) + 1) * 4);
     else need = r16(int64_t(tot[k]) * c.width + 16);
-    if (c.kind == kListFixed && c.elem_validity) need += r16((((tot[k] + 31) >> 5) + 1) * 4);
+    if (kd == kListFixed && c.elem_validity) need += r16((((tot[k] + 31) >> 5) + 1) * 4);
     if (used + need <= img_cap) {
       img_at[k] = used;
       used += static_cast<uint32_t>(need);
@@ -1360,7 +1386,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     }
     const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
     uint8_t* im = reinterpret_cast<uint8_t*>(oimg) + img_at[k];
-    if (c.kind == kBytes) {
+    if (bytes_seq<M>(c)) {
       const int64_t len = cnt[k];
       const int64_t d = ex[k];
       uint64_t* iw = reinterpret_cast<uint64_t*>(im) + (d >> 3);
@@ -1440,7 +1466,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     uint8_t* dst = const_cast<uint8_t*>(c.values);
     if (!dst) continue;
     const uint64_t x = isnull ? 0 : slot[k];
-    if (c.kind == kFixed) {
+    if (kind_of<M>(c) == kFixed) {
       if (live) {
         switch (c.width) {
           case 8: __builtin_nontemporal_store(x, reinterpret_cast<uint64_t*>(dst) + r); break;
@@ -1449,11 +1475,11 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
           default: dst[r] = static_cast<uint8_t>(x); break;
         }
       }
-    } else if (c.kind == kBool) {
+    } else if (kind_of<M>(c) == kBool) {
       const uint64_t bits = __ballot(live && (x & 0xff) != 0);
       if (lane < nwords)
         reinterpret_cast<uint32_t*>(dst)[(rbase >> 5) + lane] = static_cast<uint32_t>(bits >> (32 * lane));
-    } else if (c.kind == kDecimal && live) {
+    } else if (kind_of<M>(c) == kDecimal && live) {
       uint64_t lo = 0, hi = 0;
       if (!isnull) {
         const uint64_t* s = reinterpret_cast<const uint64_t*>(row + static_cast<int32_t>(x >> 32));
@@ -1470,7 +1496,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     int q = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      if (!is_seq(a.col[k])) continue;
+      if (!seq_kind(kind_of<M>(a.col[k]))) continue;
       if ((q++ % (NT / 64)) != wave) continue;
       const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err);
       if (lane == 0) {
@@ -1484,7 +1510,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    if (!is_seq(c)) continue;
+    if (!seq_kind(kind_of<M>(c))) continue;
     const int64_t gb = sbase[k];
     if (live) c.offsets[r] = static_cast<int32_t>(gb + ex[k]);
     if (b == nb - 1 && tid == nr - 1) c.offsets[a.nrows] = static_cast<int32_t>(gb + tot[k]);
@@ -1493,7 +1519,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     const int64_t cap = c.capacity;
     const int64_t pos = gb + ex[k];
     const uint8_t* src = row + static_cast<int32_t>(slot[k] >> 32);
-    if (c.kind == kBytes) {
+    if (bytes_seq<M>(c)) {
       put_bytes(dst, pos, src, max<int64_t>(0, min<int64_t>(cnt[k], cap - pos)));
       continue;
     }
@@ -1540,7 +1566,7 @@ __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* _
     uint8_t* dst = const_cast<uint8_t*>(c.values);
     const uint8_t* im = reinterpret_cast<const uint8_t*>(oimg) + img_at[k];
     const int64_t n = max<int64_t>(0, min<int64_t>(tot[k], c.capacity - gb));
-    if (c.kind == kBytes) {
+    if (bytes_seq<M>(c)) {
       store_shifted<NT>(dst + gb, im, n);
       continue;
     }
@@ -1860,11 +1886,19 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 // Dispatchers of the register-staged kernels (var_reg_enc.hip / var_reg_dec_*.hip).
 int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, int64_t cap,
                           int64_t ntiles, hipStream_t stream);
+// The decode instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded up;
+// look-back status words are tiles x K); mode = kSeqBytes / kSeqLists / kSeqAll (kind_of).
+inline int reg_dec_k(int ncols) {
+  return ncols <= 4 ? (ncols < 2 ? 2 : ncols) : ncols <= 6 ? 6 : ncols <= 8 ? 8 : ncols <= 12 ? 12 : 16;
+}
 int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                          uint64_t* status, uint32_t img, bool wide, int64_t nb, int64_t nbr,
-                          hipStream_t stream);
+                          uint64_t* status, uint32_t img, bool wide, int mode, int64_t nb,
+                          int64_t nbr, hipStream_t stream);
+int launch_decode_var_reg_mid(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
+                              uint64_t* status, uint32_t img, bool wide, int mode, int64_t nb,
+                              int64_t nbr, hipStream_t stream);
 int launch_decode_var_reg_hi(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                             uint64_t* status, uint32_t img, bool wide, int64_t nb, int64_t nbr,
-                             hipStream_t stream);
+                             uint64_t* status, uint32_t img, bool wide, int mode, int64_t nb,
+                             int64_t nbr, hipStream_t stream);
 
 }  // namespace fury

@@ -1,4 +1,4 @@
-// var_reg_dec_lo.hip — instances of the register-staged decode for K = 2, 3 (reg_dec_k), every
+// var_reg_dec_mid.hip — instances of the register-staged decode for K = 4, 6 (reg_dec_k), every
 // kind mode (kind_of).
 #define FURY_VAR_DEC
 #include "var_dev.h"
@@ -19,11 +19,11 @@ namespace fury {
     else { FURY_DREG_M(KK, kSeqAll) }                                                          \
     break;
 
-int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs, uint64_t* status,
-                          uint32_t img, bool wide, int mode, int64_t nb, int64_t nbr, hipStream_t stream) {
+int launch_decode_var_reg_mid(const VarArgs& a, const uint8_t* rows, const int64_t* offs, uint64_t* status,
+                              uint32_t img, bool wide, int mode, int64_t nb, int64_t nbr, hipStream_t stream) {
   switch (reg_dec_k(a.ncols)) {
-    FURY_DREG(2) FURY_DREG(3)
-    default: return launch_decode_var_reg_mid(a, rows, offs, status, img, wide, mode, nb, nbr, stream);
+    FURY_DREG(4) FURY_DREG(6)
+    default: return launch_decode_var_reg_hi(a, rows, offs, status, img, wide, mode, nb, nbr, stream);
   }
   return check_hip(hipGetLastError(), "decode_var_reg launch");
 }

@@ -793,6 +793,34 @@ def test_wide_var_schemas_bit_exact(oracle, dev, ncols, n, str_max):
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
+_REG_MODES = {"bytes": [T.INT32, T.STRING, T.BOOL, T.INT64, T.STRING, T.FLOAT64],
+              "lists": [T.INT64, "list", T.BOOL, T.FLOAT32, "list"],
+              "all": [T.INT32, T.STRING, "list", T.BOOL, T.INT16]}
+
+
+@pytest.mark.parametrize("mode", sorted(_REG_MODES))
+@pytest.mark.parametrize("ncols", list(range(1, 17)))
+def test_reg_decode_every_width_and_kind_mode(oracle, dev, mode, ncols):
+    """The register-staged decode instances: K rounded up to {2, 3, 4, 6, 8, 12, 16} (padding
+    columns), the kind modes strings-only / lists-only / all (var_dev.h kind_of), and both tile
+    sizes (one vs several sequence columns) -- decode and rows->Arrow oracle-exact."""
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    kinds = _REG_MODES[mode]
+    fields = []
+    for i in range(ncols):
+        k = kinds[i % len(kinds)]
+        fields.append(T.array_field(f"f{i:02d}", T.INT64) if k == "list" else T.field(f"f{i:02d}", k))
+    n = 1300
+    host = gen_columns("wide", fields, n, seed=ncols * 7 + len(mode), null_pct=10, str_max=40,
+                       list_max=9, list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
+
+
 def test_wide_var_schema_large_batch(oracle, dev):
     """A 40-field schema over 300k rows (>1,000 workgroups chained by the look-back)."""
     fields = _wide_fields(40)
