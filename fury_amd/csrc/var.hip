@@ -83,6 +83,18 @@ int reg_tile_rows(const VarArgs& a) {
   return 64;
 }
 
+// Kind mode of a schema's register-staged instances (kind_of): strings-only, lists-only or all.
+int reg_mode(const VarArgs& a) {
+  bool bytes = false, lists = false, other = false;
+  for (int k = 0; k < a.ncols; k++) {
+    const int kd = hcol(a, k).kind;
+    bytes |= kd == kBytes;
+    lists |= kd == kListFixed;
+    other |= kd != kFixed && kd != kBool && kd != kBytes && kd != kListFixed;
+  }
+  return other || (bytes && lists) ? kSeqAll : lists ? kSeqLists : kSeqBytes;
+}
+
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
@@ -91,7 +103,7 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     VarArgs b = a;
     b.tile_rows = reg_tile_rows(a);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
-    return launch_encode_var_reg(b, offs, rows, cap, nt, stream);
+    return launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), stream);
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);
@@ -171,15 +183,9 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   (void)arrow;   // Arrow output differs only in requiring validity buffers (checked on host)
   if (a.nrows == 0) return FURY_OK;
   int nseq = 0;
-  bool bytes = false, lists = false, other = false;   // -> the register-staged instance's mode
-  for (int k = 0; k < a.ncols; k++) {
-    const int kd = hcol(a, k).kind;
-    if (kd == kBytes || kd == kListFixed) nseq++;
-    bytes |= kd == kBytes;
-    lists |= kd == kListFixed;
-    other |= kd != kFixed && kd != kBool && kd != kBytes && kd != kListFixed;
-  }
-  const int mode = other || (bytes && lists) ? kSeqAll : lists ? kSeqLists : kSeqBytes;
+  for (int k = 0; k < a.ncols; k++)
+    if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
+  const int mode = reg_mode(a);
   const int64_t nb = nblocks(a.nrows);
   if (a.ncols <= kRegCols) {
     // 512-row tiles halve the look-back chain links: faster with several string / list

@@ -635,8 +635,27 @@ __device__ __forceinline__ int store_image(uint8_t* g, const uint8_t* img, int64
 // round trip, issued for all columns at once).  LDS holds only the image, so five workgroups
 // share a CU.
 constexpr int kRegCols = 16;
-// kind modes of the register-staged decode instances (kind_of)
+// kind modes of the register-staged instances (kind_of)
 constexpr int kSeqBytes = 0, kSeqLists = 1, kSeqAll = 2;
+// The kind of column k as a register-staged kernel instance sees it.  Instances for schemas of
+// fixed-width, bool and STRING / BINARY fields only (kSeqBytes) or of fixed-width, bool and LIST
+// fields (kSeqLists), as the host checks (reg_mode), map every kind onto those three, so the
+// compiler drops the other kinds' code from the unrolled K-column bodies (mixed decode, K = 6:
+// 7.1k instead of 18k instructions; the full body cost it ~10 % in instruction-cache misses).
+template <int M>
+__device__ __forceinline__ int kind_of(const VarCol& c) {
+  const int kd = c.kind;
+  if (M == kSeqAll) return kd;
+  const int seq = M == kSeqBytes ? kBytes : kListFixed;
+  return kd == seq ? seq : (kd == kBool ? kBool : kFixed);
+}
+// a sequence column's payload is bytes (else list elements)
+template <int M>
+__device__ __forceinline__ bool bytes_seq(const VarCol& c) {
+  return M == kSeqBytes || (M == kSeqAll && c.kind == kBytes);
+}
+__device__ __forceinline__ bool seq_kind(int kd) { return kd == kBytes || kd == kListFixed; }
+
 constexpr int kRegImg = 30 * 1024;
 
 // Copies len bytes at global src to 8-byte aligned dst (LDS or global) as whole words, zero pad.
@@ -729,7 +748,7 @@ __device__ __forceinline__ int64_t put_array(D* d64, int width, const uint8_t* v
 }
 
 // Builds row r (tile thread t) at d64 from the register-staged inputs.
-template <int K, typename D>
+template <int K, int M, typename D>
 __device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const uint64_t* v,
                                               uint64_t valid, D* d64) {
   const int nslot0 = a.bitmap_bytes >> 3;
@@ -737,19 +756,21 @@ __device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const
   uint64_t nullbits = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
+    if (k >= a.ncols) continue;              // K rounded up past the schema's fields
     const VarCol& c = a.col[k];
+    const int kd = kind_of<M>(c);
     uint64_t slot = 0;
     if (!((valid >> k) & 1)) {
       nullbits |= 1ull << k;
-    } else if (c.kind == kFixed || c.kind == kBool) {
+    } else if (kd == kFixed || kd == kBool) {
       slot = v[k];
-    } else if (c.kind == kBytes) {
+    } else if (kd == kBytes) {
       const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
       const int64_t len = o1 - o0;
       put_string(d64 + (cursor >> 3), c.values + o0, len);
       slot = (static_cast<uint64_t>(cursor) << 32) | static_cast<uint32_t>(len);
       cursor += rnd8(len);
-    } else if (c.kind == kDecimal) {
+    } else if (kd == kDecimal) {
       const auto s = gl(reinterpret_cast<const uint64_t*>(c.values)) + 2 * r;
       d64[cursor >> 3] = s[0];
       d64[(cursor >> 3) + 1] = s[1];
@@ -770,7 +791,7 @@ __device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const
 }
 
 #ifdef FURY_VAR_ENC
-template <int K>
+template <int K, int M>
 __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
                                                            const int64_t* __restrict__ offs,
                                                            uint8_t* __restrict__ rows, int64_t cap) {
@@ -789,11 +810,13 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
   uint64_t valid = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
+    v[k] = 0;
+    if (k >= a.ncols) continue;
     const VarCol& c = a.col[k];
     const bool ok = !c.validity || bit_at_g(c.validity, r);
     valid |= static_cast<uint64_t>(ok) << k;
     uint64_t x = 0;
-    switch (c.kind) {
+    switch (kind_of<M>(c)) {
       case kFixed: x = load_fixed(c.values, r, c.width); break;
       case kBool: x = bit_at_g(c.values, r); break;
       case kBytes:
@@ -807,12 +830,12 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
   }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (bytes <= kRegImg) {
-    if (live) reg_build_row<K>(a, r, v, valid, img + (ex >> 3));
+    if (live) reg_build_row<K, M>(a, r, v, valid, img + (ex >> 3));
     __syncthreads();
     store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
     const int64_t sz = offs[r + 1] - offs[r];
-    if (ex + sz <= room) reg_build_row<K>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
+    if (ex + sz <= room) reg_build_row<K, M>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
   }
 }
 #endif  // FURY_VAR_ENC
@@ -1235,25 +1258,6 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 }
 
 #ifdef FURY_VAR_DEC
-// The kind of column k as the kernel instance sees it.  Instances for schemas of fixed-width, bool
-// and STRING / BINARY fields only (kSeqBytes) or of fixed-width, bool and LIST fields (kSeqLists),
-// as the host checks, map every kind onto those three, so the compiler drops the other kinds' code
-// from the unrolled K-column body (mixed, K = 6: 7.1k instead of 18k instructions; the full body
-// cost the mixed decode ~10 % in instruction-cache misses).
-template <int M>
-__device__ __forceinline__ int kind_of(const VarCol& c) {
-  const int kd = c.kind;
-  if (M == kSeqAll) return kd;
-  const int seq = M == kSeqBytes ? kBytes : kListFixed;
-  return kd == seq ? seq : (kd == kBool ? kBool : kFixed);
-}
-// a sequence column's payload is bytes (else list elements)
-template <int M>
-__device__ __forceinline__ bool bytes_seq(const VarCol& c) {
-  return M == kSeqBytes || (M == kSeqAll && c.kind == kBytes);
-}
-__device__ __forceinline__ bool seq_kind(int kd) { return kd == kBytes || kd == kListFixed; }
-
 template <int K, int NT, int M>
 __global__ __launch_bounds__(NT) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                            const int64_t* __restrict__ offs,
@@ -1885,9 +1889,9 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 
 // Dispatchers of the register-staged kernels (var_reg_enc.hip / var_reg_dec_*.hip).
 int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, int64_t cap,
-                          int64_t ntiles, hipStream_t stream);
-// The decode instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded up;
-// look-back status words are tiles x K); mode = kSeqBytes / kSeqLists / kSeqAll (kind_of).
+                          int64_t ntiles, int mode, hipStream_t stream);
+// The register-staged instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded
+// up; the decode's look-back status words are tiles x K) x mode (kind_of, from reg_mode).
 inline int reg_dec_k(int ncols) {
   return ncols <= 4 ? (ncols < 2 ? 2 : ncols) : ncols <= 6 ? 6 : ncols <= 8 ? 8 : ncols <= 12 ? 12 : 16;
 }
