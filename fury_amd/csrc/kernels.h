@@ -18,6 +18,16 @@ template <class T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* gl(T* p) {
   return (__attribute__((address_space(1))) T*)(p);
 }
+// Pointer casts that keep the operand's address space (global via gl(), or a generic pointer the
+// compiler resolves, e.g. into LDS), for code instantiated once per address space.
+template <class T, class U>
+__device__ __forceinline__ __attribute__((address_space(1))) T* cast_as(__attribute__((address_space(1))) U* p) {
+  return (__attribute__((address_space(1))) T*)(p);
+}
+template <class T, class U>
+__device__ __forceinline__ T* cast_as(U* p) {
+  return (T*)(p);
+}
 
 // Columns per fixed-tile launch: the pointer table travels in the kernel argument block
 // (scalar-loaded, no per-call device upload).  Wider schemas are rejected.

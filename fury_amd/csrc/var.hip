@@ -154,28 +154,41 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   return st;
 }
 
-// LDS bytes of decode_var_reg's output images for tiles of `tile` rows: every variable-length
-// column's expected tile payload (its output capacity / nrows: the exact size after
-// fury_row_decode_measure, an over-estimate under bound sizing) with 30 % headroom, the bitmap
-// images of lists, and alignment slack -- capped at the static maximum.  A tile whose payload
-// does not fit its image stores that column straight to HBM (correct, slower), so the estimate
-// only moves speed.
-uint32_t dec_img_bytes(const VarArgs& a, int tile) {
-  const int64_t cap = static_cast<int64_t>(kDecImg) * (tile / kThreads);
-  if (a.nrows <= 0) return static_cast<uint32_t>(cap);
-  int64_t need = 0;
+// Tile plan of decode_var_reg: rows per tile (a multiple of 64, <= kDecThreads), LDS bytes of the
+// output images and of the row stage, within the LDS of two workgroups per CU.  Per-row sizes are
+// estimated from the output capacities (exact after fury_row_decode_measure, an over-estimate under
+// bound sizing); a tile whose payload outgrows its image stores that column straight to HBM and
+// rows past the stage are read from HBM (both correct, slower), so the estimate only moves speed.
+// mixed (C3): 448-row tiles, C4: 384.
+void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) {
+  constexpr int64_t kBudget = 80 * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
+  double row = a.fixed_size, img_row = 0, img_fix = 0;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = hcol(a, k);
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    if (!c.values) continue;
-    const double per = static_cast<double>(c.capacity) / static_cast<double>(a.nrows);
-    const double bytes = c.kind == kBytes ? per : per * (c.width == 0 ? 0.125 : c.width);
-    need += r16(static_cast<int64_t>(bytes * tile * 1.3) + 64);
-    if (c.kind == kListFixed && c.elem_validity) need += r16(static_cast<int64_t>(per * tile * 1.3 / 8) + 64);
+    const double per = a.nrows > 0 && c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 16.0;
+    if (c.kind == kDecimal) row += 16;
+    if (c.kind == kBytes) {
+      row += per + 4;
+      if (c.values) { img_row += per; img_fix += 80; }
+    }
+    if (c.kind == kListFixed) {
+      row += 12 + per * (c.width == 0 ? 1 : c.width) + 4;
+      if (c.values) {
+        img_row += per * (c.width == 0 ? 0.125 : c.width) + (c.elem_validity ? per / 8 : 0);
+        img_fix += c.elem_validity ? 160 : 80;
+      }
+    }
   }
-  need = (need + 1023) & ~int64_t(1023);
-  if (need < 4096) need = 4096;
-  return static_cast<uint32_t>(need < cap ? need : cap);
+  for (int R = kDecThreads; R >= 64; R -= 64) {
+    const int64_t im = (static_cast<int64_t>(img_row * R * 1.15 + img_fix) + 1023) & ~int64_t(1023);
+    const int64_t st = (kBudget - im) & ~int64_t(15);
+    if (st >= static_cast<int64_t>(row * R * 1.05) + 64 || R == 64) {
+      *tile = R;
+      *img = static_cast<uint32_t>(std::min<int64_t>(im, kBudget / 2));
+      *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
+      return;
+    }
+  }
 }
 
 int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
@@ -188,19 +201,17 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   const int mode = reg_mode(a);
   const int64_t nb = nblocks(a.nrows);
   if (a.ncols <= kRegCols) {
-    // 512-row tiles halve the look-back chain links: faster with several string / list
-    // sequences to chain (mixed, 3: 0.656 vs 0.737 ms), slower with one (nested: 0.287 vs
-    // 0.274 ms) -- scripts/ab_var.py.
-    const bool wide = nseq >= 2;
-    const int64_t nbr = wide ? (a.nrows + 511) / 512 : nb;
+    VarArgs b = a;
+    uint32_t img = 0, stage = 0;
+    dec_tile_plan(a, &b.tile_rows, &img, &stage);
+    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     // status words: tiles x K (the instance's column count), zeroed per launch
-    const size_t wsb = static_cast<size_t>(nbr) * reg_dec_k(a.ncols) * 8;
+    const size_t wsb = static_cast<size_t>(nt) * reg_dec_k(a.ncols) * 8;
     uint64_t* ws = nullptr;
     int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-    const uint32_t img = dec_img_bytes(a, wide ? 512 : kThreads);
-    if (!st) st = launch_decode_var_reg(a, rows, offs, ws, img, wide, mode, nb, nbr, stream);
+    if (!st) st = launch_decode_var_reg(b, rows, offs, ws, img, stage, mode, nt, stream);
     dev_free(ws, stream);
     return st;
   }

@@ -6,12 +6,8 @@
 namespace fury {
 
 #define FURY_DREG_M(KK, M)                                                                     \
-  if (wide)                                                                                    \
-    hipLaunchKernelGGL((decode_var_reg<KK, 512, M>), dim3(nbr), dim3(512), img, stream, a,     \
-                       rows, offs, status, img);                                               \
-  else                                                                                         \
-    hipLaunchKernelGGL((decode_var_reg<KK, kThreads, M>), dim3(nb), dim3(kThreads), img,       \
-                       stream, a, rows, offs, status, img);
+  hipLaunchKernelGGL((decode_var_reg<KK, M>), dim3(nt), dim3(kDecThreads), img + stage, stream, a, \
+                     rows, offs, status, img, stage);
 #define FURY_DREG(KK)                                                                          \
   case KK:                                                                                     \
     if (mode == kSeqBytes) { FURY_DREG_M(KK, kSeqBytes) }                                      \
@@ -20,10 +16,10 @@ namespace fury {
     break;
 
 int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs, uint64_t* status,
-                          uint32_t img, bool wide, int mode, int64_t nb, int64_t nbr, hipStream_t stream) {
+                          uint32_t img, uint32_t stage, int mode, int64_t nt, hipStream_t stream) {
   switch (reg_dec_k(a.ncols)) {
     FURY_DREG(2) FURY_DREG(3)
-    default: return launch_decode_var_reg_mid(a, rows, offs, status, img, wide, mode, nb, nbr, stream);
+    default: return launch_decode_var_reg_mid(a, rows, offs, status, img, stage, mode, nt, stream);
   }
   return check_hip(hipGetLastError(), "decode_var_reg launch");
 }

@@ -1376,3 +1376,32 @@ def test_nested_large_batch_level_engine(oracle, dev):
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     dec = [column_to_host(c) for c in enc.decode_batch(batch)]
     assert_columns_equal(fields, dec, oracle.decode(fields, want, want_offs, n), n)
+
+
+@pytest.mark.parametrize("order", ["short_first", "long_first", "alternating_blocks"])
+def test_decode_skewed_row_sizes(oracle, dev, order):
+    """Row sizes far from the batch average: the row-staged decode sizes its tiles, row stage and
+    output images from the average (dec_tile_plan), so tiles of long rows read their tail rows from
+    HBM and store columns that outgrow their image straight to HBM -- still bit-exact."""
+    from fury_amd.beans import beans_to_columns
+    fields = [T.field("a", T.INT32), T.field("s1", T.STRING), T.array_field("l", T.INT64),
+              T.field("s2", T.BINARY)]
+    rng = np.random.default_rng(11)
+    n_short, n_long = 6000, 2500
+    lengths = [0] * n_short + [1] * n_long
+    if order == "long_first":
+        lengths = lengths[::-1]
+    elif order == "alternating_blocks":
+        lengths = ([0] * 1500 + [1] * 600) * 4
+    beans = []
+    for i, longrow in enumerate(lengths):
+        m = int(rng.integers(150, 400)) if longrow else int(rng.integers(0, 3))
+        k = int(rng.integers(40, 90)) if longrow else int(rng.integers(0, 2))
+        beans.append({
+            "a": None if i % 13 == 5 else i,
+            "s1": None if i % 17 == 2 else "".join(chr(97 + (i + j) % 26) for j in range(m)),
+            "l": None if i % 19 == 4 else [None if j % 11 == 3 else i * 1000 + j for j in range(k)],
+            "s2": bytes((i * 7 + j) & 0xFF for j in range(m // 2)),
+        })
+    cols = beans_to_columns(fields, beans)
+    _roundtrip(oracle, None, len(beans), dev, fields=fields, cols=cols)
