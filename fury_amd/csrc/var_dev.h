@@ -1283,8 +1283,9 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 }
 
 #ifdef FURY_VAR_DEC
+// (K <= 4: at most 128 VGPRs, so two 512-thread workgroups share a CU -- the LDS plan assumes two)
 template <int K, int M>
-__global__ __launch_bounds__(kDecThreads) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
+__global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <= 4 ? 4 : 1))) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               uint64_t* __restrict__ status,
                                                               uint32_t img_cap, uint32_t stage_cap) {
