@@ -1165,7 +1165,7 @@ __device__ int64_t tile_count(const VarArgs& a, int k, const uint8_t* rows, cons
 // look_back_bounded for blockIdx-ordered tiles: when the nearest unpublished predecessor inside
 // the window has not published for kHelpSpins polls, the wave computes that tile's aggregate
 // itself (tile_count) and goes on, so the look-back finishes whatever the dispatch order.  The
-// helped values are exactly what the tile publishes later.  FURY_VAR_DBG bit 32768 helps at once
+// helped values are exactly what the tile publishes later.  Tuning "lookback_help" 1 helps at once
 // (exercises this path in the tests; results are identical).
 constexpr uint32_t kHelpSpins = 1u << 14;
 // Column index of the q-th STRING / BINARY / LIST column (the kernels' sequence numbering).

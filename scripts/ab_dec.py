@@ -1,4 +1,4 @@
-"""A/B timing of the variable-length decode under fury_set_tuning legs (or one leg), HIP events
+"""A/B timing of the variable-length decode (or, --encode, the measured encode) under fury_set_tuning legs (or one leg), HIP events
 over bound calls, interleaved rounds in one process; every leg's output is checked equal to leg 0's.
 
     python scripts/ab_dec.py --workload mixed [--key lookback_help --legs 0,1]
@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-check", action="store_true", help="timing-only legs (outputs differ)")
+    ap.add_argument("--encode", action="store_true",
+                    help="time the measured encode (rows + row offsets checked) instead")
     args = ap.parse_args()
     import torch
     from bench import DEFAULT_ROWS, make_device_columns
@@ -36,6 +38,10 @@ def main():
     batch = enc.encode_batch(cols, n)
     out = enc.decode_batch(batch)
     call = enc.bind_decode(batch, out)
+    if args.encode:
+        from fury_amd.encoder import Column
+        out = [Column(values=batch.rows), Column(values=batch.row_offsets)]
+        call = enc.bind_encode(cols, n, batch.rows, batch.row_offsets, measured=True)
     L = N.lib()
     key = args.key.encode()
 
