@@ -281,6 +281,8 @@ def run(args):
     e2e = None
     if world == 1 and not args.no_e2e and args.workload == "struct100":
         e2e = end_to_end(enc, cols, n, dev, stream)
+    elif world == 1 and not args.no_e2e:
+        e2e = end_to_end_var(enc, cols, n, int(offs[n].item()))
 
     # every rank's bytes and rows (shards may differ by one row under strong scaling)
     all_bytes = sum(orch.gather_ints(int(step_bytes)))
@@ -403,6 +405,59 @@ def end_to_end(enc, cols, n, dev, stream):
                     "fury_row_encode_host -> host rows -> fury_row_decode_host -> host columns, "
                     "direct (kernels on host memory over PCIe); registered_*: the same with "
                     "malloc'd buffers pinned by fury_host_register (4 KB pages)"}
+
+
+def end_to_end_var(enc, cols, n, total_rows):
+    """The variable-length workloads' host-memory round trip: host columns -> fury_row_encode_host
+    -> host rows + row offsets -> fury_row_decode_host -> host columns, every buffer a
+    fury_host_alloc (pinned) allocation of exactly the size the batch needs.  PCIe-inclusive, for
+    DESIGN.md; never `value`."""
+    import numpy as np
+    import torch
+    from fury_amd.encoder import host_empty
+    from fury_amd.workloads import Column
+
+    def pinned(t, dtype=np.uint8):
+        if t is None:
+            return None
+        a = host_empty(t.numel() * t.element_size())
+        a[:] = t.contiguous().view(torch.uint8).cpu().numpy()
+        return a.view(dtype)
+
+    def tree(c, fill):
+        ch = [tree(x, fill) for x in c.child] if c.child else None
+        if fill:
+            return Column(values=pinned(c.values), validity=pinned(c.validity),
+                          offsets=pinned(c.offsets, np.int32), child=ch)
+        def empty(t, dtype=np.uint8):
+            return None if t is None else host_empty(t.numel() * t.element_size()).view(dtype)
+        return Column(values=empty(c.values), validity=empty(c.validity),
+                      offsets=empty(c.offsets, np.int32), child=ch)
+
+    host_cols = [tree(c, True) for c in cols]
+    out = [tree(c, False) for c in cols]
+    rows = host_empty(total_rows)
+    roffs = host_empty(8 * (n + 1)).view(np.int64)
+    enc.encode_host(host_cols, n, rows=rows, row_offsets=roffs)          # warm-up
+    enc.decode_host(rows, roffs, n, out=out)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc.encode_host(host_cols, n, rows=rows, row_offsets=roffs)
+        enc.decode_host(rows, roffs, n, out=out)
+    dt = (time.perf_counter() - t0) / reps
+
+    def same(a, b):
+        if a.child:
+            if not all(same(x, y) for x, y in zip(a.child, b.child)):
+                return False
+        return all((x is None) == (y is None) and (x is None or np.array_equal(x, y))
+                   for x, y in ((a.offsets, b.offsets), (a.values, b.values)))
+    assert all(same(a, b) for a, b in zip(host_cols, out)), "host-path round trip"
+    alg = 2 * (_nbytes(cols) + total_rows)
+    return {"GBps_algorithmic": round(alg / dt / 1e9, 2), "ms_per_step": round(dt * 1e3, 2),
+            "what": "host columns in fury_host_alloc (pinned) buffers -> fury_row_encode_host -> "
+                    "host rows -> fury_row_decode_host -> host columns (variable-length path)"}
 
 
 if __name__ == "__main__":
