@@ -6,8 +6,9 @@
 // Fixed-width schemas (Struct-100) whose buffers are all pinned run the kernel directly on the
 // host memory (fixed_direct: both PCIe directions busy at once, no HBM staging).  Otherwise
 // they are streamed in 64-row-aligned chunks on three HIP streams (chunk k's H2D copies, chunk
-// k-1's kernel, chunk k-2's D2H copies).  Variable-length schemas are staged whole: their row
-// offsets are a scan over the whole batch.  Pinning (hipHostRegister) is the caller's choice
+// k-1's kernel, chunk k-2's D2H copies).  Flat variable-length schemas on pinned buffers run
+// their kernels on host memory too (var_encode_direct / var_decode_direct); otherwise they are
+// staged whole: their row offsets are a scan over the whole batch.  Pinning (hipHostRegister) is the caller's choice
 // (fury_host_register): pinned buffers DMA at the link rate, pageable ones are bounced through
 // the runtime's staging buffers.
 #include <hip/hip_runtime.h>
@@ -356,10 +357,242 @@ int stage_column(const OwnedField& f, const fury_column& h, int64_t n, DeviceAre
   }
 }
 
+// ---- variable-length flat schemas on pinned buffers: kernels on host memory -----------------
+// As fixed_direct: when every host buffer is pinned (fury_host_alloc / fury_host_register) and
+// meets the device entry points' alignment, the measure / encode / decode kernels read and write
+// host memory over PCIe, both link directions at once, instead of staging the batch through HBM.
+// Every kernel read of an input is either exact or an aligned 8- or 16-byte word holding at least
+// one byte of the buffer -- inside the same page, so inside the pinned mapping.  Outputs written
+// as whole bitmap words or with atomics (validity, BOOL values, list element bitmaps) go to HBM
+// and are copied back; Arrow offsets, payloads, element values and rows are written exactly.
+bool aligned_to(const void* q, int64_t a) { return (reinterpret_cast<uintptr_t>(q) & (a - 1)) == 0; }
+
+// Device views of a flat variable-length schema's host input columns (encode); false when a
+// buffer is pageable or misaligned (the call is then staged).
+bool view_inputs(const fury_schema* s, const fury_column* host, int64_t n,
+                 std::vector<fury_column>& d, std::vector<fury_column>& dchild) {
+  const int nf = s->num_fields;
+  d.assign(nf, fury_column{});
+  dchild.assign(nf, fury_column{});
+  auto need = [](const void* p, int64_t bytes, uint8_t** out) {
+    *out = nullptr;
+    if (!p) return true;
+    if (bytes <= 0) bytes = 1;
+    *out = device_view(p, bytes);
+    return *out != nullptr;
+  };
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    const fury_column& h = host[k];
+    fury_column& c = d[k];
+    if (!need(h.validity, (n + 7) / 8, &c.validity)) return false;
+    uint8_t* v = nullptr;
+    switch (p.kind) {
+      case kFixed:
+        if (!need(h.values, n * p.width, &v) || !aligned_to(v, p.width)) return false;
+        c.values = v;
+        break;
+      case kBool:
+        if (!need(h.values, (n + 7) / 8, &v)) return false;
+        c.values = v;
+        break;
+      case kDecimal:
+        if (!need(h.values, 16 * n, &v) || !aligned_to(v, 8)) return false;
+        c.values = v;
+        break;
+      case kBytes:
+      case kListFixed: {
+        if (!h.offsets) return false;
+        if (!need(h.offsets, (n + 1) * 4, &v) || !aligned_to(v, 4)) return false;
+        c.offsets = reinterpret_cast<int32_t*>(v);
+        const int64_t m = h.offsets[n];
+        if (p.kind == kBytes) {
+          if (!need(h.values, m, &v)) return false;
+          c.values = v;
+          break;
+        }
+        const fury_column* hc = h.child;
+        if (!hc) return false;
+        fury_column& e = dchild[k];
+        const bool bits = p.elem_type == FURY_TYPE_BOOL;
+        if (!need(hc->values, bits ? (m + 7) / 8 : m * p.elem_width, &v) ||
+            (!bits && !aligned_to(v, p.elem_width)))
+          return false;
+        e.values = v;
+        if (!need(hc->validity, (m + 7) / 8, &e.validity)) return false;
+        c.child = &e;
+        break;
+      }
+      default:
+        return false;
+    }
+  }
+  return true;
+}
+
+int var_encode_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
+                      int64_t cap, int64_t* row_offsets, int64_t* row_bytes, int32_t device,
+                      bool* used) {
+  *used = false;
+  if (s->generic || n == 0 || cap <= 0) return FURY_OK;
+  std::vector<fury_column> d, dchild;
+  if (!view_inputs(s, host, n, d, dchild)) return FURY_OK;
+  uint8_t* drows = device_view(rows, cap);
+  if (!drows || !aligned_to(drows, 16) || !device_view(row_offsets, (n + 1) * 8)) return FURY_OK;
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  Streams ss;
+  if ((st = ss.create(device))) return st;
+  hipStream_t hs = ss.s[0];
+  DeviceArena arena(hs);
+  void* doffs = nullptr;
+  if ((st = arena.alloc((n + 1) * 8, &doffs))) return st;
+  int64_t* dof = static_cast<int64_t*>(doffs);
+  *used = true;
+  g_host_direct.fetch_add(1);
+  // the row offsets are a scan: measured into HBM (its passes re-read them), copied out once
+  if ((st = fury_row_measure(s, d.data(), n, dof, hs))) return st;
+  int64_t total = 0;
+  if ((st = check_hip(hipMemcpyAsync(&total, dof + n, 8, hipMemcpyDeviceToHost, hs), "D2H total")))
+    return st;
+  if ((st = ss.sync())) return st;
+  *row_bytes = total;
+  if (total > cap)
+    return set_error(FURY_ERR_CAPACITY, "rows need " + std::to_string(total) +
+                                            " bytes, capacity is " + std::to_string(cap));
+  if ((st = fury_row_encode(s, d.data(), n, dof, drows, hs))) return st;
+  (void)hipMemcpyAsync(row_offsets, dof, (n + 1) * 8, hipMemcpyDeviceToHost, hs);
+  return ss.sync();
+}
+
+// Host rows -> host columns with the decode kernel on host memory: payloads and offsets are
+// written straight into the host buffers, bounded by their capacities (no sizing pass over the
+// rows: the kernel never writes past a capacity and offsets[n] holds what a column needed, checked
+// after the kernel -- FURY_ERR_CAPACITY when short, as the staged path reports).
+int var_decode_direct(const fury_schema* s, const uint8_t* rows, const int64_t* row_offsets,
+                      int64_t n, fury_column* host, int32_t device, bool* used) {
+  *used = false;
+  if (s->generic || n == 0) return FURY_OK;
+  const int64_t total = row_offsets[n];
+  const uint8_t* drows = total > 0 ? device_view(rows, total) : nullptr;
+  const uint8_t* doff = device_view(row_offsets, (n + 1) * 8);
+  if (!drows || !doff || !aligned_to(drows, 16) || !aligned_to(doff, 8)) return FURY_OK;
+  const int nf = s->num_fields;
+  std::vector<fury_column> d(nf, fury_column{}), dchild(nf, fury_column{});
+  // HBM bitmaps: (host destination, device buffer, bits) -- copied back after the kernel
+  struct Bits { uint8_t* host; int64_t off; int64_t bits; int64_t cap_bits; int kind; int k; };
+  std::vector<Bits> bits;
+  int64_t ws_bytes = 0;
+  auto bitmap = [&](uint8_t* h, int64_t nb, int kind, int k) {
+    bits.push_back(Bits{h, ws_bytes, nb, nb, kind, k});
+    ws_bytes += ((bitmap_alloc(nb) + 255) / 256) * 256;
+  };
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    fury_column& h = host[k];
+    fury_column& c = d[k];
+    if (h.validity) bitmap(h.validity, n, 0, k);
+    uint8_t* v = nullptr;
+    switch (p.kind) {
+      case kFixed:
+        if (!(v = device_view(h.values, n * p.width)) || !aligned_to(v, p.width)) return FURY_OK;
+        c.values = v;
+        break;
+      case kBool:
+        bitmap(static_cast<uint8_t*>(h.values), n, 1, k);
+        break;
+      case kDecimal:
+        if (!(v = device_view(h.values, 16 * n)) || !aligned_to(v, 8)) return FURY_OK;
+        c.values = v;
+        break;
+      case kBytes:
+      case kListFixed: {
+        if (!h.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "output offsets is null");
+        if (!(v = device_view(h.offsets, (n + 1) * 4)) || !aligned_to(v, 4)) return FURY_OK;
+        c.offsets = reinterpret_cast<int32_t*>(v);
+        if (p.kind == kBytes) {
+          if (h.capacity > 0 && !(c.values = device_view(h.values, h.capacity))) return FURY_OK;
+          c.capacity = c.values ? h.capacity : 0;
+          break;
+        }
+        fury_column* hc = h.child;
+        if (!hc) return set_error(FURY_ERR_INVALID_ARGUMENT, "output element column is null");
+        fury_column& e = dchild[k];
+        const bool bool_elems = p.elem_type == FURY_TYPE_BOOL;
+        const int64_t cap_elems = bool_elems ? hc->capacity * 8 : hc->capacity / p.elem_width;
+        if (bool_elems) {
+          bitmap(static_cast<uint8_t*>(hc->values), cap_elems, 2, k);
+        } else if (hc->capacity > 0) {
+          if (!(e.values = device_view(hc->values, hc->capacity)) || !aligned_to(e.values, p.elem_width))
+            return FURY_OK;
+        }
+        e.capacity = hc->capacity;
+        if (hc->validity) bitmap(hc->validity, cap_elems, 3, k);
+        c.child = &e;
+        break;
+      }
+      default:
+        return FURY_OK;
+    }
+  }
+  int st = check_hip(hipSetDevice(device), "hipSetDevice");
+  if (st) return st;
+  Streams ss;
+  if ((st = ss.create(device))) return st;
+  hipStream_t hs = ss.s[0];
+  DeviceArena arena(hs);
+  uint8_t* ws = nullptr;
+  if (ws_bytes > 0) {
+    void* w = nullptr;
+    if ((st = arena.alloc(ws_bytes, &w))) return st;
+    ws = static_cast<uint8_t*>(w);
+    if ((st = check_hip(hipMemsetAsync(ws, 0, ws_bytes, hs), "hipMemsetAsync bitmaps"))) return st;
+  }
+  for (const Bits& b : bits) {
+    uint8_t* dv = ws + b.off;
+    if (b.kind == 0) d[b.k].validity = dv;
+    else if (b.kind == 1) d[b.k].values = dv;
+    else if (b.kind == 2) dchild[b.k].values = dv;
+    else dchild[b.k].validity = dv;
+  }
+  *used = true;
+  g_host_direct.fetch_add(1);
+  if ((st = fury_row_decode(s, drows, const_cast<int64_t*>(reinterpret_cast<const int64_t*>(doff)),
+                            n, d.data(), hs)))
+    return st;
+  if ((st = ss.sync())) return st;
+  // what each variable-length column needed (host offsets, now written)
+  for (int k = 0; k < nf; k++) {
+    const FieldPlan& p = s->plan[k];
+    if (p.kind != kBytes && p.kind != kListFixed) continue;
+    const int64_t m = host[k].offsets[n];
+    const int64_t bytes = p.kind == kBytes ? m
+                        : p.elem_type == FURY_TYPE_BOOL ? (m + 7) / 8 : m * p.elem_width;
+    const int64_t have = p.kind == kBytes ? host[k].capacity : host[k].child->capacity;
+    if (bytes > have)
+      return set_error(FURY_ERR_CAPACITY, "column " + s->fields[k].name + " needs " +
+                                              std::to_string(bytes) +
+                                              (p.kind == kBytes ? " payload bytes" : " element bytes"));
+  }
+  for (const Bits& b : bits) {
+    int64_t nb = b.bits;
+    if (b.kind >= 2) nb = host[b.k].offsets[n];       // element bitmaps: the elements decoded
+    if (nb > 0)
+      (void)hipMemcpyAsync(b.host, ws + b.off, (nb + 7) / 8, hipMemcpyDeviceToHost, hs);
+  }
+  if ((st = check_hip(hipGetLastError(), "hipMemcpyAsync D2H bitmaps"))) return st;
+  return ss.sync();
+}
+
 int var_encode_host(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
                     int64_t cap, int64_t* row_offsets, int64_t* row_bytes, int32_t device) {
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
+  {
+    bool used = false;
+    st = var_encode_direct(s, host, n, rows, cap, row_offsets, row_bytes, device, &used);
+    if (st || used) return st;
+  }
   Streams ss;
   if ((st = ss.create(device))) return st;
   hipStream_t hs = ss.s[0];
@@ -396,6 +629,11 @@ int var_decode_host(const fury_schema* s, const uint8_t* rows, const int64_t* ro
     return set_error(FURY_ERR_UNSUPPORTED,
                      "host-memory decode of a nested schema: its output sizes depend on the data; "
                      "use fury_decode_host_prepare / fury_decode_host_execute");
+  {
+    bool used = false;
+    const int st = var_decode_direct(s, rows, row_offsets, n, host, device, &used);
+    if (st || used) return st;
+  }
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
   Streams ss;

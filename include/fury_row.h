@@ -258,28 +258,17 @@ int fury_device_status(void* stream);
 int fury_trim_workspace(int32_t device);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
-/* Process-wide kernel selection knobs for A/B measurement.  Key "fixed_variant" (fixed-width,
- * 8-byte, no-null schemas) is a bit set: bit 0 = pipelined persistent kernel (else one tile per
- * workgroup), bit 1 = non-temporal stores, bit 2 = non-temporal loads, bit 3 = deep encode
- * gather (16 column loads per lane in flight), bit 4 = pair-mode decode (16-B column stores),
- * bit 5 = deep decode (16 tile loads per lane in flight), bit 6 = pair-mode encode, bit 7 =
- * padded LDS rows in the encode.  Results are bit-identical across variants.  Default 54
- * (tile + nt loads/stores + pair-mode deep decode).
- * Key "var_decode": 0 one-pass look-back decode (256- or 512-row tiles by the number of
- * variable-length columns), 1 sizing pass + decode, 2 / 3 one-pass with 512 / 256-row tiles,
- * 4 one-pass LDS-staged decode (var_lds.hip: tiles' row ranges staged by LDS-DMA; at most 32
- * STRING / BINARY / LIST columns and 64 fields, else as 0).
- * Key "gen_decode" (nested schemas, fury_decode_prepare / _execute): 0 level-by-level engine
- * (a thread per Arrow entry of a node, levels.hip), 1 the thread-per-row interpreter
- * (generic.hip).  Results are identical.
+/* Process-wide knobs for tests and A/B measurement (results are identical under every value).
+ * Key "lookback_help": 1 = every look-back of the variable-length decode computes a silent
+ * predecessor tile's aggregate at once (the path a late-dispatched predecessor takes).
  * Key "unframe": 0 speculative parallel stream parse (a stream that does not verify -- a payload
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
- * errors), 1 always the sequential walk.  fury_get_tuning("unframe_walks") = streams the walk
- * parsed (wholly or from the first frame the repair could not place), "unframe_repairs" =
- * streams the parallel repair parsed.  "host_direct" = fury_row_encode_host / _decode_host calls
- * on a fixed-width schema that ran the kernel directly on pinned host buffers (no staging).
- * fury_get_tuning("lookback_timeouts") = decoupled look-backs of the variable-length decode that
- * gave up waiting (must stay 0; synchronous device read). */
+ * errors), 1 always the sequential walk.
+ * fury_get_tuning only: "unframe_walks" = streams the walk parsed (wholly or from the first frame
+ * the repair could not place), "unframe_repairs" = streams the parallel repair parsed,
+ * "host_direct" = fury_row_encode_host / _decode_host calls that ran their kernels directly on
+ * pinned host buffers (fixed-width and flat variable-length schemas, no staging),
+ * "lookback_timeouts" = decoupled look-backs that gave up (must stay 0; synchronous device read). */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 
@@ -304,7 +293,8 @@ int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64
  * Fixed-width schemas whose buffers are ALL pinned (fury_host_alloc or fury_host_register) run
  * the kernel directly on host memory — loads and stores cross PCIe in both directions at once,
  * no HBM staging ("host_direct" counts these calls); otherwise they are staged through HBM
- * (chunked over three HIP streams).  Variable-length schemas are staged whole.  `device` is the
+ * (chunked over three HIP streams).  Flat variable-length schemas on pinned buffers run direct
+ * too (bitmaps through HBM); otherwise, and nested schemas always, they are staged whole.  `device` is the
  * HIP device ordinal.  Buffers from fury_host_alloc (hipHostMalloc) run fastest; registering
  * ordinary 4 KB-page memory (fury_host_register, hipHostRegister) pins it in place but the GPU
  * then walks 4 KB translations (host path). */
@@ -321,7 +311,8 @@ int fury_row_encode_host(const fury_schema* schema, const fury_column* columns, 
                          int64_t* row_bytes, int32_t device);
 /* Host rows -> host columns (fromRow semantics, like fury_row_decode).  Variable-length flat
  * schemas: STRING/BINARY payload capacity in fury_column.capacity, LIST element bytes in the
- * child's capacity (FURY_ERR_CAPACITY when short); nested schemas: FURY_ERR_UNSUPPORTED (their
+ * child's capacity (FURY_ERR_CAPACITY when short: staged calls size first and write nothing,
+ * direct calls write nothing past a capacity and leave offsets[nrows] = the size needed); nested schemas: FURY_ERR_UNSUPPORTED (their
  * output sizes depend on the data: fury_decode_host_prepare / fury_decode_host_execute below). */
 int fury_row_decode_host(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                          int64_t nrows, fury_column* columns, int32_t device);

@@ -220,3 +220,89 @@ def test_host_empty_buffers_take_direct_path(oracle):
     assert N.lib().fury_get_tuning(b"host_direct") == d0 + 2
     assert np.array_equal(got, want)
     assert all(np.array_equal(o.values, c.values.view(np.uint8)) for o, c in zip(out, host))
+
+
+def _page_tail(nbytes, dtype=np.uint8):
+    """A pinned (fury_host_alloc) buffer of exactly `nbytes` whose last byte is the last byte of
+    its allocation's last page: a kernel read past the buffer's last 16-byte block would leave the
+    mapping."""
+    from fury_amd.encoder import host_empty
+    size = max(int(nbytes), 1)
+    alloc = (size + 4095) // 4096 * 4096
+    return host_empty(alloc)[alloc - size:].view(dtype)
+
+
+def _tail_copy(a, dtype):
+    if a is None:
+        return None
+    src = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    b = _page_tail(src.nbytes)
+    b[:] = src
+    return b.view(dtype)
+
+
+def _tail_tree(c, fill: bool):
+    from fury_amd.workloads import Column
+    ch = [_tail_tree(x, fill) for x in c.child] if c.child else None
+    if fill:
+        return Column(values=_tail_copy(c.values, np.uint8), validity=_tail_copy(c.validity, np.uint8),
+                      offsets=_tail_copy(c.offsets, np.int32), child=ch)
+
+    def empty(a, dtype):
+        return None if a is None else _page_tail(np.asarray(a).nbytes, dtype)
+    return Column(values=empty(c.values, np.uint8), validity=empty(c.validity, np.uint8),
+                  offsets=empty(c.offsets, np.int32), child=ch)
+
+
+@pytest.mark.parametrize("name,n", [("mixed", 20_011), ("nested", 9_999), ("narrow", 3000),
+                                    ("beanb", 777), ("mixed", 1)])
+def test_host_direct_var_page_edge(oracle, name, n):
+    """Flat variable-length schemas on pinned buffers run their kernels on host memory
+    (host_direct counts both calls), every input and output buffer exactly its size and ending at
+    a page edge: rows, row offsets and decoded columns bit-exact vs the oracle."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS[name]
+    host = gen_columns(name, fields, n, seed=29)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    enc = Encoders.bean(fields, device="cuda:0")
+    L = N.lib()
+    d0 = L.fury_get_tuning(b"host_direct")
+    cols = [_tail_tree(c, True) for c in host]
+    rows = _page_tail((want.size + 15) // 16 * 16)      # rows must be 16-byte aligned
+    roffs = _page_tail(8 * (n + 1), np.int64)
+    got, offs = enc.encode_host(cols, n, rows=rows, row_offsets=roffs)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 1, "encode did not take the direct path"
+    assert np.array_equal(got, want) and np.array_equal(offs, want_offs)
+    out = [_tail_tree(c, False) for c in ref]
+    enc.decode_host(rows, roffs, n, out=out)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 2, "decode did not take the direct path"
+    assert_columns_equal(fields, out, ref, n)
+
+
+def test_host_direct_var_capacity_short(oracle):
+    """A payload buffer one byte short: the direct decode reports FURY_ERR_CAPACITY (it writes
+    nothing past the capacity)."""
+    from fury_amd.encoder import CapacityError, Encoders
+    fields = SCHEMAS["mixed"]
+    n = 3000
+    host = gen_columns("mixed", fields, n, seed=31)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    enc = Encoders.bean(fields, device="cuda:0")
+    rows = _page_tail((want.size + 15) // 16 * 16)
+    rows[:want.size] = want
+    roffs = _tail_copy(want_offs, np.int64)
+    from fury_amd import _native as N
+    d0 = N.lib().fury_get_tuning(b"host_direct")
+    out = [_tail_tree(c, False) for c in ref]
+    k = next(i for i, f in enumerate(fields) if ref[i].offsets is not None and len(ref[i].values) > 1)
+    full = out[k].values
+    guard = _page_tail(full.nbytes + 8)
+    guard[:] = 0xAB
+    out[k].values = guard[:full.nbytes - 1]
+    with pytest.raises(CapacityError):
+        enc.decode_host(rows, roffs, n, out=out)
+    assert N.lib().fury_get_tuning(b"host_direct") == d0 + 1, "decode did not take the direct path"
+    assert bool((guard[full.nbytes - 1:] == 0xAB).all()), "decode wrote past the capacity"
