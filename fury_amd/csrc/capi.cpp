@@ -589,6 +589,8 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
   DeviceTable dt;
   st = var_args(s, cols, nrows, false, false, &a, &dt, hs);
   if (st) return st;
+  const int one = launch_encode_measured_var(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);
+  if (one >= 0) return one;
   st = launch_measure_rows(a, row_offsets, hs);
   if (st || nrows == 0) return st;
   return launch_encode_var(a, row_offsets, static_cast<uint8_t*>(rows), capacity, hs);

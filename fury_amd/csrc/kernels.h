@@ -170,6 +170,8 @@ int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stre
 // Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.
 int launch_encode_var(const VarArgs& a, const int64_t* row_offsets, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
+int launch_encode_measured_var(const VarArgs& a, int64_t* row_offsets, uint8_t* rows, int64_t cap,
+                               hipStream_t stream);
 int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* row_offsets,
                           hipStream_t stream);
 // Single pass: computes the Arrow offsets itself (decoupled look-back scan across workgroups)

@@ -95,6 +95,28 @@ int reg_mode(const VarArgs& a) {
   return other || (bytes && lists) ? kSeqAll : lists ? kSeqLists : kSeqBytes;
 }
 
+// fury_row_encode_measured for register-staged schemas (<= kRegCols fields): the byte totals of
+// the encode's own tiles (measure_tiles, one wave per tile), their exclusive scan, then the encode
+// scans each tile's row sizes itself and writes the final row offsets once (the row-sized measure
+// wrote and the prefix pass re-read and re-wrote all 8 B/row of them).  -1: not this path.
+int launch_encode_measured_var(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
+                               hipStream_t stream) {
+  if (a.ncols > kRegCols || a.nrows <= 0) return -1;
+  VarArgs b = a;
+  b.tile_rows = reg_tile_rows(a);
+  const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
+  int64_t* ws = nullptr;          // [tile totals x nt][total][scan scratch]
+  int st = dev_alloc((nt + 1 + scan_workspace(nt)) * 8, stream, reinterpret_cast<void**>(&ws));
+  if (st) return st;
+  st = launch_measure_tiles(b, ws, nt, stream);
+  if (!st) {
+    device_scan(ws, nt, ws + nt, ws + nt + 1, stream);
+    st = launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), ws, stream);
+  }
+  dev_free(ws, stream);
+  return st;
+}
+
 int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   if (a.nrows == 0) return FURY_OK;
@@ -103,7 +125,8 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     VarArgs b = a;
     b.tile_rows = reg_tile_rows(a);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
-    return launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), stream);
+    return launch_encode_var_reg(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
+                                 stream);
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);

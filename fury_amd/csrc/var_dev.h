@@ -804,20 +804,42 @@ __device__ __forceinline__ void reg_build_row(const VarArgs& a, int64_t r, const
 }
 
 #ifdef FURY_VAR_ENC
+// Size of the row whose per-column inputs are v / valid (encode_var_reg's registers): the same
+// writerIndex growth as row_size_of.
 template <int K, int M>
-__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
-                                                           const int64_t* __restrict__ offs,
-                                                           uint8_t* __restrict__ rows, int64_t cap) {
+__device__ __forceinline__ int64_t reg_row_size(const VarArgs& a, const uint64_t* v, uint64_t valid) {
+  int64_t sz = a.fixed_size;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    if (k >= a.ncols || !((valid >> k) & 1)) continue;
+    const VarCol& c = a.col[k];
+    const int kd = kind_of<M>(c);
+    if (kd == kDecimal) {
+      sz += 16;
+    } else if (kd == kBytes || kd == kListFixed) {
+      const int64_t n = static_cast<int64_t>(static_cast<int32_t>(v[k] >> 32)) - static_cast<int32_t>(v[k]);
+      sz += kd == kBytes ? rnd8(n) : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+    }
+  }
+  return sz;
+}
+
+// tbase == nullptr: rows at the given offs.  tbase != nullptr (fury_row_encode_measured): tbase[b]
+// = the exclusive prefix of the tiles' byte totals (measure_tiles + scan); each tile scans its own
+// rows' sizes and writes their final offs -- no per-row sizes pass, no prefix-add pass.
+template <int K, int M>
+__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* __restrict__ offs,
+                                                           uint8_t* __restrict__ rows, int64_t cap,
+                                                           const int64_t* __restrict__ tbase) {
   __shared__ __attribute__((aligned(16))) uint64_t img[kRegImg / 8];
+  __shared__ int64_t tmp[kEncRows / 64];
   const int tid = threadIdx.x;
   const int R = a.tile_rows;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * R;
+  const int64_t b = blockIdx.x;
+  const int64_t r0 = b * R;
   const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
   const bool live = tid < nr;
   const int64_t r = live ? r0 + tid : r0;
-  const int64_t base = offs[r0];
-  const int64_t bytes = offs[r0 + nr] - base;
-  const int64_t ex = offs[r] - base;
   // per-row inputs of every column: one batch of independent loads
   uint64_t v[K];
   uint64_t valid = 0;
@@ -841,16 +863,29 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a,
     }
     v[k] = x;
   }
+  int64_t base, bytes, ex, sz;
+  if (tbase) {
+    sz = live ? reg_row_size<K, M>(a, v, valid) : 0;
+    base = tbase[b];
+    ex = block_excl_scan<kEncRows>(sz, &bytes, tmp);
+    if (live) offs[r] = base + ex;
+    if (r0 + nr == a.nrows && tid == nr - 1) offs[a.nrows] = base + ex + sz;
+  } else {
+    base = offs[r0];
+    bytes = offs[r0 + nr] - base;
+    ex = offs[r] - base;
+    sz = offs[r + 1] - offs[r];
+  }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (bytes <= kRegImg) {
     if (live) reg_build_row<K, M>(a, r, v, valid, img + (ex >> 3));
     __syncthreads();
     store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
-    const int64_t sz = offs[r + 1] - offs[r];
     if (ex + sz <= room) reg_build_row<K, M>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
   }
 }
+
 #endif  // FURY_VAR_ENC
 
 // ---- measure: row sizes (writerIndex growth of toRow) and their exclusive scan.  Each thread
@@ -878,6 +913,53 @@ __device__ __forceinline__ int64_t row_size_of(const VarArgs& a, int64_t r) {
   }
   return sz;
 }
+
+#ifdef FURY_VAR_ENC
+// Byte totals of encode tiles of R rows (R a multiple of 64, <= 256): one wave per tile, each lane
+// sizing R / 64 consecutive rows from one run of offsets and one or two validity bytes per column
+// (fury_row_encode_measured; the measure_kernel pattern, without the per-row output).
+__global__ __launch_bounds__(kThreads) void measure_tiles(VarArgs a, int64_t* __restrict__ tsum,
+                                                          int R, int64_t nt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = static_cast<int64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6);
+  if (t >= nt) return;
+  const int q = R >> 6;                               // rows per lane, 1..4
+  const int64_t r = t * R + static_cast<int64_t>(lane) * q;
+  int64_t s = 0;
+  if (r + q <= a.nrows) {
+    s = static_cast<int64_t>(q) * a.fixed_size;
+    for (int k = 0; k < a.ncols; k++) {
+      CVarCol& c = vc(a, k);
+      if (c.kind < kBytes) continue;
+      uint32_t vb = 0xffu;
+      if (c.validity) {
+        const int sh = static_cast<int>(r & 7);
+        vb = c.validity[r >> 3];
+        if (sh + q > 8) vb |= static_cast<uint32_t>(c.validity[(r >> 3) + 1]) << 8;
+        vb >>= sh;
+      }
+      if (c.kind == kDecimal) {
+        s += 16 * __builtin_popcount(vb & ((1u << q) - 1));
+        continue;
+      }
+      int32_t o[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) o[j] = j <= q ? c.offsets[r + j] : 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (j >= q || !((vb >> j) & 1)) continue;
+        const int64_t n = o[j + 1] - o[j];
+        s += c.kind == kBytes ? rnd8(n) : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+      }
+    }
+  } else {
+    for (int j = 0; j < q; j++)
+      if (r + j < a.nrows) s += row_size_of(a, r + j);
+  }
+  s = wave_sum(s);
+  if (lane == 0) tsum[t] = s;
+}
+#endif  // FURY_VAR_ENC
 
 #ifdef FURY_VAR_MAIN
 __global__ __launch_bounds__(kThreads) void measure_kernel(VarArgs a, int64_t* __restrict__ offs,
@@ -1986,8 +2068,9 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 }  // namespace
 
 // Dispatchers of the register-staged kernels (var_reg_enc.hip / var_reg_dec_*.hip).
-int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, int64_t cap,
-                          int64_t ntiles, int mode, hipStream_t stream);
+int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
+                          int64_t ntiles, int mode, const int64_t* tbase, hipStream_t stream);
+int launch_measure_tiles(const VarArgs& b, int64_t* tsum, int64_t ntiles, hipStream_t stream);
 // The register-staged instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded
 // up; the decode's look-back status words are tiles x K) x mode (kind_of, from reg_mode).
 inline int reg_dec_k(int ncols) {

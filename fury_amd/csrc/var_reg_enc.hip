@@ -5,10 +5,16 @@
 
 namespace fury {
 
-int launch_encode_var_reg(const VarArgs& b, const int64_t* offs, uint8_t* rows, int64_t cap,
-                          int64_t nt, int mode, hipStream_t stream) {
+int launch_measure_tiles(const VarArgs& b, int64_t* tsum, int64_t nt, hipStream_t stream) {
+  hipLaunchKernelGGL(measure_tiles, dim3(static_cast<unsigned>((nt + kThreads / 64 - 1) / (kThreads / 64))),
+                     dim3(kThreads), 0, stream, b, tsum, b.tile_rows, nt);
+  return check_hip(hipGetLastError(), "measure_tiles launch");
+}
+
+int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
+                          int64_t nt, int mode, const int64_t* tbase, hipStream_t stream) {
 #define FURY_REG_M(KK, M) \
-  hipLaunchKernelGGL((encode_var_reg<KK, M>), dim3(nt), dim3(kEncRows), 0, stream, b, offs, rows, cap);
+  hipLaunchKernelGGL((encode_var_reg<KK, M>), dim3(nt), dim3(kEncRows), 0, stream, b, offs, rows, cap, tbase);
 #define FURY_REG(KK)                                                                           \
   case KK:                                                                                     \
     if (mode == kSeqBytes) { FURY_REG_M(KK, kSeqBytes) }                                       \
