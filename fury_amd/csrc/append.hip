@@ -123,8 +123,8 @@ extern "C" int fury_arrow_append(const fury_schema* s, fury_column* dst, int64_t
     return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_arrow_append: negative row count");
   if (src_rows == 0) return FURY_OK;
   if (!dst || !src) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_arrow_append: columns is null");
-  if (int e = take_device_error()) return e;
   hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (int e = take_device_error(hs)) return e;
   const int nn = static_cast<int>(s->nodes.size());
   std::vector<const fury_column*> dc(nn, nullptr), sc(nn, nullptr);
   std::vector<int64_t> dm(nn, 0), sm(nn, 0);      // entries per node: destination, source

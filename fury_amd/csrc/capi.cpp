@@ -22,33 +22,70 @@ int check_hip(int hip_status, const char* what) {
                                         hipGetErrorString(static_cast<hipError_t>(hip_status)));
 }
 
+// Device error words (kernels.h): one slot of kErrWords words per stream, in host-pinned mapped
+// memory.  A kernel raises into the slot of the stream it was launched on, and a call takes (reads
+// and clears) only the slot of its own stream, so a malformed decode on one stream is never
+// reported by -- or swallowed into -- an unrelated call on another stream / thread.
+// The legacy null stream is keyed per host thread.  Slots are assigned on first use; past
+// kErrSlots distinct streams the overflow streams share slot 0.
 namespace {
-uint32_t* g_err_host = nullptr;     // host view of the device error word
-uint32_t* g_err_dev = nullptr;      // the same word as kernels address it
+constexpr int kErrSlots = 1024;
+uint32_t* g_err_host = nullptr;     // host view of the slots
+uint32_t* g_err_dev = nullptr;      // the same memory as kernels address it
 std::once_flag g_err_once;
-}  // namespace
+std::mutex g_slot_mu;
+std::unordered_map<uintptr_t, int> g_slot_of;
+int g_slot_next = 1;
 
-uint32_t* device_error_word() {
+uintptr_t stream_key(hipStream_t s) {
+  if (s) return reinterpret_cast<uintptr_t>(s);
+  thread_local char key;              // odd keys: never a stream handle (handles are aligned)
+  return reinterpret_cast<uintptr_t>(&key) | 1;
+}
+
+void init_err() {
   std::call_once(g_err_once, [] {
     void* p = nullptr;
-    if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return;
+    const size_t bytes = size_t(kErrSlots) * kErrWords * 4;
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return;
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
       (void)hipHostFree(p);
       return;
     }
-    std::memset(p, 0, 64);
+    std::memset(p, 0, bytes);
     g_err_host = static_cast<uint32_t*>(p);
     g_err_dev = static_cast<uint32_t*>(d);
   });
-  return g_err_dev;
+}
+
+int error_slot(hipStream_t s) {
+  const uintptr_t k = stream_key(s);
+  std::lock_guard<std::mutex> lock(g_slot_mu);
+  auto it = g_slot_of.find(k);
+  if (it != g_slot_of.end()) return it->second;
+  const int slot = g_slot_next < kErrSlots ? g_slot_next++ : 0;
+  g_slot_of.emplace(k, slot);
+  return slot;
+}
+}  // namespace
+
+uint32_t* device_error_word(hipStream_t stream) {
+  init_err();
+  if (!g_err_dev) return nullptr;
+  return g_err_dev + size_t(kErrWords) * error_slot(stream);
 }
 
 std::atomic<int64_t> g_err_taken{0};
 
 int64_t device_error_count() {
-  const volatile uint32_t* w = g_err_host;
-  return g_err_taken.load() + (w && w[kErrLookBack] ? 1 : 0);
+  int64_t pending = 0;
+  if (g_err_host) {
+    std::lock_guard<std::mutex> lock(g_slot_mu);
+    for (int i = 0; i < g_slot_next; i++)
+      pending += __atomic_load_n(g_err_host + size_t(kErrWords) * i + kErrLookBack, __ATOMIC_ACQUIRE) ? 1 : 0;
+  }
+  return g_err_taken.load() + pending;
 }
 
 // Where a kernel found the problem: a row index, or (bit 63 set) a nested schema node and Arrow
@@ -59,16 +96,22 @@ static std::string where_text(uint64_t w) {
          std::to_string(w & ((1ull << 40) - 1));
 }
 
-int take_device_error() {
+// Takes one flag of the slot: the flag is exchanged for 0 first, then its location word is read
+// and cleared (raise_at stores the location before it releases the flag).
+static bool take_flag(uint32_t* w, int flag, uint64_t* where) {
+  if (!__atomic_exchange_n(w + flag, 0u, __ATOMIC_ACQ_REL)) return false;
+  if (where) *where = __atomic_exchange_n(reinterpret_cast<uint64_t*>(w + flag + 2), 0ull, __ATOMIC_ACQ_REL);
+  return true;
+}
+
+int take_device_error(hipStream_t stream) {
   if (!g_err_host) return FURY_OK;
-  volatile uint32_t* w = g_err_host;
-  const uint32_t lb = w[kErrLookBack], oob = w[kErrBounds], map = w[kErrMapCount];
+  uint32_t* w = g_err_host + size_t(kErrWords) * error_slot(stream);
+  uint64_t oob_at = 0, map_at = 0;
+  const bool lb = take_flag(w, kErrLookBack, nullptr);
+  const bool oob = take_flag(w, kErrBounds, &oob_at);
+  const bool map = take_flag(w, kErrMapCount, &map_at);
   if (!lb && !oob && !map) return FURY_OK;
-  const uint64_t oob_at = static_cast<uint64_t>(w[kErrBounds + 1]) |
-                          (static_cast<uint64_t>(w[kErrBounds + 2]) << 32);
-  const uint64_t map_at = static_cast<uint64_t>(w[kErrMapCount + 1]) |
-                          (static_cast<uint64_t>(w[kErrMapCount + 2]) << 32);
-  for (int i = 0; i < 16; i++) w[i] = 0;
   if (lb) {
     g_err_taken.fetch_add(1);
     return set_error(FURY_ERR_DEVICE,
@@ -269,7 +312,8 @@ namespace {
 
 bool misaligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; }
 
-int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const char* fn) {
+int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const char* fn,
+                  hipStream_t hs) {
   if (!s) return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(fn) + ": schema is null");
   if (nrows < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(fn) + ": nrows < 0");
   if (nrows > 0 && s->num_fields > 0 && !cols)
@@ -277,7 +321,7 @@ int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const c
   if (!s->device_ok)
     return set_error(FURY_ERR_UNSUPPORTED,
                      std::string(fn) + ": no device kernel for " + s->device_reason);
-  return take_device_error();
+  return take_device_error(hs);
 }
 
 int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
@@ -415,7 +459,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   } else {
     a->tile_rows = encode_tile_rows(*a);
   }
-  a->err = device_error_word();
+  a->err = device_error_word(hs);
   a->help_now = lookback_help_mode();
   return FURY_OK;
 }
@@ -510,7 +554,7 @@ extern "C" {
 
 int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrows,
                      int64_t* row_offsets, void* stream) {
-  int st = common_checks(s, cols, nrows, "fury_row_measure");
+  int st = common_checks(s, cols, nrows, "fury_row_measure", static_cast<hipStream_t>(stream));
   if (st) return st;
   if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
   if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
@@ -524,7 +568,7 @@ int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrow
 
 int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows,
                     const int64_t* row_offsets, void* rows, void* stream) {
-  int st = common_checks(s, cols, nrows, "fury_row_encode");
+  int st = common_checks(s, cols, nrows, "fury_row_encode", static_cast<hipStream_t>(stream));
   if (st) return st;
   if (nrows == 0) return FURY_OK;
   if (!rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
@@ -558,7 +602,7 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
 
 int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int64_t nrows,
                              int64_t* row_offsets, void* rows, int64_t capacity, void* stream) {
-  int st = common_checks(s, cols, nrows, "fury_row_encode_measured");
+  int st = common_checks(s, cols, nrows, "fury_row_encode_measured", static_cast<hipStream_t>(stream));
   if (st) return st;
   hipStream_t hs = static_cast<hipStream_t>(stream);
   if (capacity < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "capacity < 0");
@@ -610,7 +654,7 @@ static int zero_empty_offsets(const fury_schema* s, fury_column* cols, hipStream
 
 int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                             int64_t nrows, fury_column* cols, void* stream) {
-  int st = common_checks(s, cols, nrows, "fury_row_decode_measure");
+  int st = common_checks(s, cols, nrows, "fury_row_decode_measure", static_cast<hipStream_t>(stream));
   if (st) return st;
   if (nrows == 0) return zero_empty_offsets(s, cols, static_cast<hipStream_t>(stream));
   if (s->is_fixed) return FURY_OK;   // nothing variable to size
@@ -629,7 +673,7 @@ int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_
 static int decode_impl(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                        int64_t nrows, fury_column* cols, void* stream, bool arrow,
                        const char* fn) {
-  int st = common_checks(s, cols, nrows, fn);
+  int st = common_checks(s, cols, nrows, fn, static_cast<hipStream_t>(stream));
   if (st) return st;
   if (nrows == 0) return zero_empty_offsets(s, cols, static_cast<hipStream_t>(stream));
   if (!rows) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows is null");
@@ -675,8 +719,8 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   if (!s->device_ok) return set_error(FURY_ERR_UNSUPPORTED, "no device kernel for " + s->device_reason);
   if (nrows > 0 && (!rows || !row_offsets))
     return set_error(FURY_ERR_INVALID_ARGUMENT, "rows / row_offsets is null");
-  if (const int e = take_device_error()) return e;
   hipStream_t hs = static_cast<hipStream_t>(stream);
+  if (const int e = take_device_error(hs)) return e;
   const int nn = static_cast<int>(s->nodes.size());
   fury_decode_plan* p = new fury_decode_plan();
   p->schema = s;
@@ -687,7 +731,7 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   if (nrows > 0) {
     // lv_prepare synchronises `stream`: rows whose values leave the batch are reported here
     int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
-    if (!st) st = take_device_error();
+    if (!st) st = take_device_error(hs);
     if (st) {
       if (p->lv) lv_free(p->lv);
       delete p;
@@ -745,7 +789,7 @@ int fury_device_status(void* stream) {
   const int st = check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream)),
                            "hipStreamSynchronize");
   if (st) return st;
-  return take_device_error();
+  return take_device_error(static_cast<hipStream_t>(stream));
 }
 
 int fury_set_tuning(const char* key, int32_t value) {

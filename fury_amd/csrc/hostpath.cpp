@@ -87,7 +87,11 @@ struct Streams {
       const int e = check_hip(hipStreamSynchronize(x), "hipStreamSynchronize");
       if (!st) st = e;
     }
-    return st ? st : take_device_error();
+    for (auto& x : s) {                    // every stage stream's error slot (all are taken)
+      const int e = take_device_error(x);
+      if (!st) st = e;
+    }
+    return st;
   }
 };
 
@@ -894,7 +898,7 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     if (d.values && vb > 0) (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
   }
   st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
-  return st ? st : take_device_error();
+  return st ? st : take_device_error(hs);
 }
 
 int fury_host_alloc(int64_t bytes, void** out) {

@@ -101,7 +101,8 @@ JNIEXPORT jlong JNICALL Java_org_apache_fury_format_encoder_GpuRowEncoder_native
   if (raise(env, fury_jni_decode_host_prepare(reinterpret_cast<const fury_schema*>(schema),
                                               reinterpret_cast<const void*>(rows),
                                               reinterpret_cast<const int64_t*>(row_offsets),
-                                              nrows, c.data(), &plan, device)))
+                                              nrows, c.data(), static_cast<int64_t>(c.size()),
+                                              &plan, device)))
     return 0;
   env->SetLongArrayRegion(counts, 0, static_cast<jsize>(c.size()),
                           reinterpret_cast<const jlong*>(c.data()));

@@ -144,9 +144,13 @@ int fury_jni_decode_host(const fury_schema* s, const void* rows, const int64_t* 
 
 int fury_jni_decode_host_prepare(const fury_schema* s, const void* rows,
                                  const int64_t* row_offsets, int64_t nrows, int64_t* counts,
-                                 fury_decode_plan** plan, int32_t device) {
+                                 int64_t counts_len, fury_decode_plan** plan, int32_t device) {
   if (!s || !counts) return set_error(FURY_ERR_INVALID_ARGUMENT, "fury_jni_decode_host_prepare: null");
   const size_t nn = s->nodes.size();
+  if (counts_len < 0 || static_cast<uint64_t>(counts_len) < 2 * nn)
+    return set_error(FURY_ERR_INVALID_ARGUMENT,
+                     "fury_jni_decode_host_prepare: counts has " + std::to_string(counts_len) +
+                         " entries, the schema needs " + std::to_string(2 * nn));
   std::vector<int64_t> e(nn + 1), b(nn + 1);
   const int st = fury_decode_host_prepare(s, rows, row_offsets, nrows, e.data(), b.data(), plan,
                                           device);

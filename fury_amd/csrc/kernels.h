@@ -94,20 +94,23 @@ struct VarArgs {
   int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
   int32_t help_now;          // look-backs help a silent predecessor at once (test hook, tuning
                              // "lookback_help"); 0 in production
-  uint32_t* err;             // host-visible device error word (device_error_word()) or NULL
+  uint32_t* err;             // the launch stream's device error slot (device_error_word) or NULL
 };
 
-// Host-visible device error words: host-pinned, mapped memory (16 x 32 bit) that kernels set with
-// system-scope STORES (no read-modify-write over PCIe) when they cannot produce a valid result:
+// Host-visible device error words: host-pinned, mapped memory, one slot of kErrWords 32-bit words
+// PER STREAM (capi.cpp), that kernels set with system-scope STORES (no read-modify-write over
+// PCIe) when they cannot produce a valid result:
 //   [kErrLookBack]            a look-back that gave up (FURY_ERR_DEVICE)
-//   [kErrBounds], [+1, +2]    a decode read that would leave the batch, and where (64-bit: a row,
-//                             or bit 63 | node << 40 | entry) (FURY_ERR_OUT_OF_BOUNDS)
-//   [kErrMapCount], [+1, +2]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
-// Allocated once per process; NULL if the runtime cannot map host memory.  take_device_error()
-// reads and clears them and sets the thread's last error when one was raised.
+//   [kErrBounds], [+2, +3]    a decode read that would leave the batch, and where (one 64-bit
+//                             word: a row, or bit 63 | node << 40 | entry) (FURY_ERR_OUT_OF_BOUNDS)
+//   [kErrMapCount], [+2, +3]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
+// device_error_word(stream) is the slot kernels launched on `stream` raise into (NULL if the runtime
+// cannot map host memory); take_device_error(stream) takes that slot only (flag exchanged first,
+// then its location) and sets the thread's last error when one was raised.
+constexpr int kErrWords = 16;
 constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8;
-uint32_t* device_error_word();
-int take_device_error();
+uint32_t* device_error_word(hipStream_t stream);
+int take_device_error(hipStream_t stream);
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
 
 // Cached device workspace (capi.cpp): stream-ordered like hipMallocAsync / hipFreeAsync, without
@@ -126,13 +129,13 @@ void dev_free(void* p, hipStream_t stream);
 __device__ __forceinline__ bool span_ok(int64_t p, int64_t len, int64_t total) {
   return p >= 0 && len >= 0 && len <= total - p;
 }
+// The location is one 64-bit store (concurrent raisers never mix halves), made visible before the
+// flag by a release store of the flag; stores only -- no atomics over PCIe.
 __device__ __forceinline__ void raise_at(uint32_t* err, int slot, uint64_t where) {
   if (!err) return;
-  __hip_atomic_store(err + slot + 1, static_cast<uint32_t>(where), __ATOMIC_RELAXED,
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(err + slot + 2), where, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(err + slot + 2, static_cast<uint32_t>(where >> 32), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(err + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(err + slot, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ void raise_oob(uint32_t* err, int64_t row) {
   raise_at(err, kErrBounds, static_cast<uint64_t>(row));

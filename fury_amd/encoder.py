@@ -385,13 +385,16 @@ class RowEncoder:
         return RowBatch(rows[:total] if total else rows[:0], offs, nrows, self.schema_hash)
 
     def alloc_columns(self, nrows: int, validity: bool = True) -> List[Column]:
-        """Output columns for fixed-width fields (variable ones are sized by decode_measure)."""
+        """Output columns for fixed-width fields (variable ones are sized by decode_measure).
+        Validity and BOOL bitmaps are whole 32-bit words (the kernels store / OR them as words,
+        include/fury_row.h: 4-byte aligned, padded to a multiple of 4 bytes)."""
         out = []
+        words = ((nrows + 31) // 32) * 4
         for f in self._schema.fields:
-            vb = (torch.empty((nrows + 7) // 8, dtype=torch.uint8, device=self.device)
+            vb = (torch.empty(words, dtype=torch.uint8, device=self.device)
                   if validity else None)
             if f.type_id == BOOL:
-                out.append(Column(values=torch.empty((nrows + 7) // 8, dtype=torch.uint8,
+                out.append(Column(values=torch.empty(words, dtype=torch.uint8,
                                                      device=self.device), validity=vb))
             elif type_width(f.type_id) > 0:
                 out.append(Column(values=torch.empty(nrows * type_width(f.type_id),

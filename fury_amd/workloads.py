@@ -15,8 +15,8 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from .types import (BINARY, BOOL, DATE32, DECIMAL, FLOAT32, FLOAT64, INT8, INT16, INT32, INT64,
-                    LIST, MAP, STRING, STRUCT, TIMESTAMP, Field, array_field, field, map_field,
-                    not_null_field, struct_field, type_width)
+                    LIST, MAP, STRING, STRUCT, TIMESTAMP, Field, array_field, field,
+                    infer_bean_schema, map_field, not_null_field, struct_field, type_width)
 
 
 @dataclass
@@ -91,9 +91,49 @@ def foo() -> List[Field]:
             struct_field("f5", bar())]
 
 
+def beana() -> List[Field]:
+    """fury-test-core BeanA (test/bean/BeanA.java:33-54) as TypeInference.inferSchema builds it
+    (TypeInference.java:136-238): fields sorted by Java name with String.compareTo
+    (Descriptor.java:324-332), renamed lower_underscore (:228), the transient ``f13`` skipped
+    (Descriptor.java:391).  ``byte[]`` / ``int[]`` are primitive arrays (list of non-null items,
+    :192-198), ``Iterable<BeanB>`` / ``List<BeanB>`` lists of nullable BeanB structs, ``int[][]``
+    a list of nullable ``int[]`` lists, ``Map<String, BeanB>`` a map with a non-null String key
+    (:204-213), BigDecimal a decimal(38, 18) (:173-177)."""
+    def bean_b(name: str) -> Field:
+        return struct_field(name, beanb())
+
+    def lst(item: Field) -> Field:
+        return Field("", LIST, True, (item,))
+
+    java = [
+        ("f1", not_null_field("", INT16)), ("f2", field("", INT32)),
+        ("f3", not_null_field("", INT64)), ("f4", field("", FLOAT32)),
+        ("f5", not_null_field("", FLOAT64)), ("beanB", bean_b("")),
+        ("intArray", array_field("", INT32, elem_nullable=False)),
+        ("bytes", array_field("", INT8, elem_nullable=False)),
+        ("f12", not_null_field("", BOOL)), ("f15", field("", INT32)),
+        ("f16", field("", DECIMAL)), ("f17", field("", STRING)),
+        ("longStringField", field("", STRING)), ("doubleList", array_field("", FLOAT64)),
+        ("beanBIterable", lst(bean_b("item"))), ("beanBList", lst(bean_b("item"))),
+        ("stringBeanBMap", map_field("", field("key", STRING), bean_b("value"))),
+        ("int2DArray", lst(array_field("item", INT32, elem_nullable=False))),
+        ("double2DList", lst(array_field("item", FLOAT64))),
+    ]
+    return infer_bean_schema(java)
+
+
+def row_test_fields() -> List[Field]:
+    """The schema of cpp/fury/row/row_test.cc:31-44 (RowTest.Write): f1 utf8, f2 int32,
+    f3 list<int32>, f4 map<utf8, float32>, f5 struct<n1 utf8, n2 int32>."""
+    return [field("f1", STRING), field("f2", INT32), array_field("f3", INT32),
+            map_field("f4", field("key", STRING), field("value", FLOAT32)),
+            struct_field("f5", [field("n1", STRING), field("n2", INT32)])]
+
+
 SCHEMAS: Dict[str, List[Field]] = {
     "struct100": struct100(), "docs_struct": docs_struct(), "mixed": mixed(),
     "nested": nested(), "narrow": narrow(), "bar": bar(), "beanb": beanb(), "foo": foo(),
+    "beana": beana(), "row_test": row_test_fields(),
 }
 
 # ---------------------------------------------------------------------------------------------
@@ -430,6 +470,116 @@ class JavaRandom:
 
     def next_double(self) -> float:
         return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
+
+    def next_int_bound(self, bound: int) -> int:
+        """Random.nextInt(int bound)."""
+        if bound & -bound == bound:
+            return (bound * self._next31()) >> 31
+        while True:
+            bits = self._next31()
+            val = bits % bound
+            if bits - val + (bound - 1) < 1 << 31:
+                return val
+
+    def _next31(self) -> int:
+        self.seed = (self.seed * self._MUL + 0xB) & self._MASK
+        return self.seed >> 17
+
+    def next_bytes(self, n: int) -> bytes:
+        """Random.nextBytes: little-endian bytes of successive nextInt() words."""
+        out = bytearray()
+        while len(out) < n:
+            r = self.next_int() & 0xFFFFFFFF
+            for _ in range(min(n - len(out), 4)):
+                out.append(r & 0xFF)
+                r >>= 8
+        return bytes(out)
+
+
+def _java_string_hash(s: str) -> int:
+    h = 0
+    for u in s.encode("utf-16-be").hex(" ", 2).split():
+        h = (31 * h + int(u, 16)) & 0xFFFFFFFF
+    return h
+
+
+def java_hash_map_order(keys: Sequence[str]) -> List[str]:
+    """Iteration order of a java.util.HashMap<String, ?> filled by put() in ``keys`` order
+    (distinct keys, no treeified bins): table size 16 doubled while size > 0.75 * table; bucket
+    = (h ^ (h >>> 16)) & (table - 1); buckets in index order, each in insertion order (resize
+    splits keep it)."""
+    cap = 16
+    while len(keys) > cap * 3 // 4:
+        cap *= 2
+    def bucket(k):
+        h = _java_string_hash(k)
+        return (h ^ (h >> 16)) & (cap - 1)
+    return [k for _, _, k in sorted((bucket(k), i, k) for i, k in enumerate(keys))]
+
+
+def _java_random_string(size: int, rnd: "JavaRandom") -> str:
+    """TestUtils.random(size, Random) (fury-test-core TestUtils.java:34-43): chars ' '..'z'."""
+    return "".join(chr(32 + rnd.next_int_bound(ord("z") + 1 - 32)) for _ in range(size))
+
+
+def create_beanb(arr_size: int) -> dict:
+    """BeanB.createBeanB(arrSize) (fury-test-core test/bean/BeanB.java:39-65), new Random(37),
+    as a bean dict keyed by the schema's field names."""
+    rnd = JavaRandom(37)
+    b = {"f1": ((rnd.next_int() + 2**15) & 0xFFFF) - 2**15, "f2": rnd.next_int(),
+         "f3": rnd.next_long(), "f4": rnd.next_float(), "f5": rnd.next_double(),
+         "int_arr": None, "int_list": None}
+    if arr_size > 0:
+        b["int_arr"] = [rnd.next_int() for _ in range(arr_size)]
+        b["int_list"] = [rnd.next_int() for _ in range(arr_size)]
+    return b
+
+
+# BeanA.createBeanA's BigDecimal: unscaled 122222222222222225454657712222222222, scale 18
+# (BeanA.java:67-68), as the 16-byte little-endian two's complement Arrow writes
+# (DecimalUtility.writeBigDecimalToArrowBuf, BinaryWriter.writeDecimal :214-226).
+BEANA_DECIMAL_UNSCALED = 122222222222222225454657712222222222
+
+
+def decimal_bytes(unscaled: int) -> bytes:
+    return unscaled.to_bytes(16, "little", signed=True)
+
+
+def create_beana(arr_size: int) -> dict:
+    """BeanA.createBeanA(arrSize) (fury-test-core test/bean/BeanA.java:56-137), value for value:
+    new Random(37) drawn in the same order, f17 / long_string_field from TestUtils.random(n, 1),
+    ``arr[i] = rnd.nextInt()`` in the int2DArray loop exactly as written (only the diagonal is
+    set), map entries in java.util.HashMap iteration order, the transient f13 absent."""
+    rnd = JavaRandom(37)
+    a = {"f1": ((rnd.next_int() + 2**15) & 0xFFFF) - 2**15, "f2": rnd.next_int(),
+         "f3": rnd.next_long(), "f4": rnd.next_float(), "f5": rnd.next_double()}
+    a["f15"] = rnd.next_int()
+    a["f12"] = True
+    a["bean_b"] = create_beanb(arr_size)
+    a["f16"] = decimal_bytes(BEANA_DECIMAL_UNSCALED)
+    a["f17"] = _java_random_string(40, JavaRandom(1))
+    a["long_string_field"] = _java_random_string(20, JavaRandom(1))
+    for k in ("bytes", "double_list", "double2_d_list", "int_array", "int2_d_array",
+              "bean_b_list", "string_bean_b_map", "bean_b_iterable"):
+        a[k] = None
+    if arr_size > 0:
+        a["bytes"] = [b - 256 if b >= 128 else b for b in rnd.next_bytes(arr_size)]
+        dl = [rnd.next_double() for _ in range(arr_size)]
+        dl[0] = None
+        a["double_list"] = dl
+        a["double2_d_list"] = [[rnd.next_double() for _ in range(arr_size)]
+                               for _ in range(arr_size)]
+        a["int_array"] = [rnd.next_int() for _ in range(arr_size)]
+        i2 = [[0] * arr_size for _ in range(arr_size)]
+        for i in range(arr_size):
+            for _ in range(arr_size):
+                i2[i][i] = rnd.next_int()
+        a["int2_d_array"] = i2
+        a["bean_b_list"] = [create_beanb(arr_size) for _ in range(arr_size)]
+        keys = [f"key{i}" for i in range(arr_size)]
+        a["string_bean_b_map"] = [(k, create_beanb(arr_size)) for k in java_hash_map_order(keys)]
+        a["bean_b_iterable"] = [create_beanb(arr_size) for _ in range(arr_size)]
+    return a
 
 
 def docs_struct_values(fields: Sequence[Field]) -> List[Column]:

@@ -185,7 +185,8 @@ int fury_row_decode_measure(const fury_schema* schema, const void* rows,
  * when validity != NULL, a cleared validity bit).  One device pass: the STRING/BINARY/LIST
  * offsets are computed here (fury_row_decode_measure is only needed to size the buffers); when
  * offsets[nrows] exceeds a column's capacity the payload past the capacity is not written —
- * grow the buffer and decode again. */
+ * grow the buffer and decode again.  Malformed rows are reported asynchronously, on `stream`
+ * (fury_device_status below). */
 int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, fury_column* columns, void* stream);
 /* ArrowWriter.write(row) for every row + finishAsRecordBatch: as fury_row_decode but every
@@ -242,12 +243,22 @@ int fury_decode_execute(fury_decode_plan* plan, fury_column* columns, int32_t ar
 void fury_decode_plan_destroy(fury_decode_plan* plan);
 
 /* ---- asynchronous device errors (no reference equivalent) ------------------------------- */
-/* Synchronises `stream` and returns FURY_ERR_DEVICE if a kernel of an earlier asynchronous call
- * (on any stream of this process) could not produce a valid result -- a decoupled look-back of
- * the variable-length decode that gave up waiting -- and clears that state; FURY_OK otherwise.
- * Every entry point also reports such a failure (without synchronising) the next time it is
- * called.  By construction (a look-back computes a silent predecessor's aggregate itself) it is
- * never raised on working hardware. */
+/* Decode kernels report what they find in the rows ASYNCHRONOUSLY: fury_row_decode,
+ * fury_rows_to_arrow and fury_decode_execute return before their kernels run, so a malformed
+ * batch is reported later --
+ *   FURY_ERR_OUT_OF_BOUNDS  a variable-length value, array or map header outside the batch's row
+ *                           bytes (MemoryBuffer's IndexOutOfBoundsException);
+ *   FURY_ERR_UNSUPPORTED    map key / value arrays of different lengths (BinaryMap.pointTo);
+ *   FURY_ERR_DEVICE         a decoupled look-back that gave up waiting (by construction -- a
+ *                           look-back computes a silent predecessor's aggregate itself -- never
+ *                           raised on working hardware).
+ * The report goes to the STREAM the call was launched on (the legacy null stream: per host
+ * thread): fury_device_status(stream) synchronises that stream and returns it, and the next entry
+ * point called on the same stream returns it before doing anything (without synchronising: it sees
+ * the kernels that have finished).  Either clears it.  Calls on other streams never see it.  When
+ * one is reported, every output of the failing call is invalid (the values that failed decode as
+ * null; the rest may be incomplete).  fury_decode_prepare and the host-memory entry points
+ * synchronise and report their own batch's errors directly. */
 int fury_device_status(void* stream);
 
 /* ---- workspace (no reference equivalent) ------------------------------------------------- */
@@ -342,7 +353,9 @@ int fury_decode_host_execute(fury_decode_plan* plan, fury_column* columns);
  *   desc: describe() in pre-order -- 5 int64 per schema node {values address, validity address,
  *     offsets address, values capacity, numChildren} (host addresses); its child counts must
  *     match the schema's (FURY_ERR_INVALID_ARGUMENT otherwise);
- *   counts: 2 int64 per node (breadth-first, fury_decode_prepare order): entries, payload bytes. */
+ *   counts: 2 int64 per node (breadth-first, fury_decode_prepare order): entries, payload bytes;
+ *   counts_len (the Java array's length) below 2 * fury_schema_num_nodes is
+ *   FURY_ERR_INVALID_ARGUMENT, nothing written. */
 const char* fury_jni_exception_class(int status);   /* Java class name of a status, NULL for OK */
 int fury_jni_schema_create(const char* const* names, const int32_t* meta, int32_t nodes,
                            int32_t top, fury_schema** out);
@@ -353,7 +366,7 @@ int fury_jni_decode_host(const fury_schema* schema, const void* rows, const int6
                          int64_t nrows, const int64_t* desc, int64_t desc_len, int32_t device);
 int fury_jni_decode_host_prepare(const fury_schema* schema, const void* rows,
                                  const int64_t* row_offsets, int64_t nrows, int64_t* counts,
-                                 fury_decode_plan** plan, int32_t device);
+                                 int64_t counts_len, fury_decode_plan** plan, int32_t device);
 int fury_jni_decode_host_execute(const fury_schema* schema, fury_decode_plan* plan,
                                  const int64_t* desc, int64_t desc_len);
 

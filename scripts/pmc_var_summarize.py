@@ -4,7 +4,7 @@ encode / decode pipelines (C3 mixed, C4 nested bench workloads).
 Per kernel: median FETCH_SIZE / WRITE_SIZE (KB per dispatch) over the bench's dispatches, with the
 gfx950 corrections of MI355X_MICROARCH.md §HBM as calibrated on tools/hbm_probe in
 profiles/pmc_struct100.json (FETCH_SIZE counts half of the bytes of 8- and 16-B-per-lane reads:
-x2; WRITE_SIZE exact: x1).  Encode = measure_kernel + encode_var_reg (+ the small scan kernels);
+x2; WRITE_SIZE exact: x1).  Encode = measure_tiles (or measure_kernel + add_group_prefix) + encode_var_reg + the scan kernels;
 decode = decode_var_reg (decode_measure_* run only in the untimed sizing path).  Algorithmic bytes per launch come from the bench line in the same
 pass's log (encode and decode both move column bytes + row bytes: half of a step).
 
@@ -59,7 +59,8 @@ def main():
                              "fetch_bytes_corrected": round(fb), "write_bytes_corrected": round(wb),
                              "hbm_bytes_per_launch": round(fb + wb)}
     enc = sum(v["hbm_bytes_per_launch"] for n, v in kernels.items()
-              if n.startswith(("encode_var", "measure_kernel", "add_group_prefix")))
+              if n.startswith(("encode_var", "measure_kernel", "measure_tiles", "add_group_prefix",
+                                   "scan_", "add_groups")))
     dec = sum(v["hbm_bytes_per_launch"] for n, v in kernels.items()
               if n.startswith("decode_var"))
     res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "

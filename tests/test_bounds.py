@@ -290,3 +290,46 @@ def test_host_decode_out_of_bounds(oracle, dev):
     with pytest.raises(IndexOutOfBoundsException, match=f"row {i} "):
         enc.decode_host(bad, offs, n)
     enc.decode_host(rows, offs, n)
+
+
+def test_device_errors_stay_on_their_stream(oracle, dev):
+    """A malformed decode on stream A (error left pending: not yet taken) does not leak into an
+    unrelated encode + decode on stream B run from another thread meanwhile -- those succeed,
+    bit-exact -- and A's own status call still reports A's error (row and all), once.  (The
+    error words are per stream: include/fury_row.h, asynchronous device errors.)"""
+    import threading
+    from fury_amd.encoder import IndexOutOfBoundsException, column_to_device, column_to_host
+    fields = SCHEMAS["mixed"]
+    n = 3001
+    enc, host, rows, offs = _encode(oracle, fields, n, 11, dev, null_pct=10, str_max=30)
+    i, k = _victim(fields, rows, offs, n, {T.STRING})
+    bad = _batch(enc, _corrupt(fields, rows, offs, n, i, k, "offset_past_end"), offs, n, dev)
+    good = _batch(enc, rows, offs, n, dev)
+    dcols = [column_to_device(c, dev) for c in host]
+    torch.cuda.synchronize()
+    sa = torch.cuda.Stream(dev)
+    enc._decode(bad, True, False, sa, None, "bound")      # raises on the device, not taken yet
+    sa.synchronize()
+    out = {}
+
+    def other():
+        try:
+            sb = torch.cuda.Stream(dev)
+            b2 = enc.encode_batch(dcols, n, stream=sb)
+            cols = enc.decode_batch(good, stream=sb)
+            sb.synchronize()
+            out["rows"] = b2.rows.cpu().numpy()
+            out["cols"] = [column_to_host(c) for c in cols]
+        except Exception as e:          # noqa: BLE001 -- reported below
+            out["err"] = e
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert "err" not in out, out.get("err")
+    assert np.array_equal(out["rows"], rows)
+    assert_columns_equal(fields, out["cols"], oracle.decode(fields, rows, offs, n), n)
+    enc.device_status()                 # this thread's default stream: nothing pending
+    with pytest.raises(IndexOutOfBoundsException, match=f"row {i} "):
+        enc.device_status(sa)
+    enc.device_status(sa)               # taken once

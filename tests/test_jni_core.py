@@ -246,8 +246,13 @@ def test_jni_core_nested_foo(oracle):
     nn = L.fury_schema_num_nodes(h)
     counts = np.zeros(2 * nn, np.int64)
     plan = ctypes.c_void_p()
+    short = np.zeros(2 * nn - 1, np.int64)
     assert L.fury_jni_decode_host_prepare(h, rows.ctypes.data, offs.ctypes.data, n,
-                                          _i64p(counts), ctypes.byref(plan), 0) == 0
+                                          _i64p(short), len(short), ctypes.byref(plan),
+                                          0) == 1          # FURY_ERR_INVALID_ARGUMENT
+    assert not short.any() and not plan.value
+    assert L.fury_jni_decode_host_prepare(h, rows.ctypes.data, offs.ctypes.data, n,
+                                          _i64p(counts), len(counts), ctypes.byref(plan), 0) == 0
     order = _bfs(fields)
     cols = [_alloc_host_node(f, int(counts[2 * i]), int(counts[2 * i + 1]))
             for i, (f, _) in enumerate(order)]

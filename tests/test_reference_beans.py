@@ -1,0 +1,236 @@
+"""The reference's own test beans through the oracle and the device path.
+
+* ``BeanA`` / ``BeanB`` (java/fury-test-core/src/main/java/org/apache/fury/test/bean/BeanA.java:
+  33-137, BeanB.java:28-65) as ``RowEncoderTest.testEncoder`` uses them
+  (java/fury-format/src/test/java/org/apache/fury/format/encoder/RowEncoderTest.java:41-64):
+  toRow -> fromRow three times, equal beans; then ``testStreamingEncode`` (CodecBuilderTest.java:
+  51-67): two ``encode(buffer, obj)`` frames after one byte, two ``decode(buffer)``.
+* The C++ sibling's ``RowTest.Write`` row (cpp/fury/row/row_test.cc:31-99): encoded on the
+  device, its ``ToString`` read from the device bytes equals the known answer at :96-98.
+
+The BeanA schema hash is checked against the reference's ``infer.py`` output in
+tests/golden/schema_hashes.json by tests/test_oracle.py (every SCHEMAS entry).
+"""
+from __future__ import annotations
+
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from fury_amd import types as T
+from fury_amd.beans import beans_to_columns, columns_to_beans
+from fury_amd.workloads import (SCHEMAS, JavaRandom, create_beana, create_beanb, decimal_bytes,
+                                java_hash_map_order)
+from oracle import bean_oracle as B
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _known():
+    return json.load(open(os.path.join(GOLDEN, "known_answers.json")))
+
+
+# ---- value generators ------------------------------------------------------------------------
+def random_bean(fields, rnd: JavaRandom, depth: int = 0) -> dict:
+    """A random bean of ``fields`` (any nesting) drawn from java.util.Random: nulls where the
+    field is nullable, strings of 0..70 chars (UTF-8 multibyte among them), lists / maps of 0..6
+    entries (0..3 below depth 1)."""
+    return {f.name: _random_value(f, rnd, depth) for f in fields}
+
+
+def _random_value(f, rnd, depth):
+    if f.nullable and rnd.next_int_bound(100) < 12:
+        return None
+    t = f.type_id
+    if t == T.BOOL:
+        return rnd.next_int_bound(2) == 1
+    if t in (T.INT8, T.INT16, T.INT32, T.DATE32):
+        bits = {T.INT8: 8, T.INT16: 16}.get(t, 32)
+        v = rnd.next_int() & ((1 << bits) - 1)
+        return v - (1 << bits) if v >= 1 << (bits - 1) else v
+    if t in (T.INT64, T.TIMESTAMP):
+        return rnd.next_long()
+    if t == T.FLOAT32:
+        return rnd.next_float()
+    if t == T.FLOAT64:
+        return rnd.next_double()
+    if t == T.STRING:
+        n = rnd.next_int_bound(71)
+        return "".join(chr(0x3b1 + rnd.next_int_bound(20)) if rnd.next_int_bound(9) == 0
+                       else chr(32 + rnd.next_int_bound(91)) for _ in range(n))
+    if t == T.BINARY:
+        return rnd.next_bytes(rnd.next_int_bound(40))
+    if t == T.DECIMAL:
+        return decimal_bytes((rnd.next_long() << 40) // 3)
+    if t == T.STRUCT:
+        return random_bean(f.children, rnd, depth + 1)
+    k = rnd.next_int_bound(7 if depth < 1 else 4)
+    if t == T.LIST:
+        return [_random_value(f.children[0], rnd, depth + 1) for _ in range(k)]
+    if t == T.MAP:
+        keys = [f"k{rnd.next_int_bound(1000)}" for _ in range(k)]
+        keys = list(dict.fromkeys(keys))
+        if f.children[0].type_id == T.STRING:
+            return [(kk, _random_value(f.children[1], rnd, depth + 1))
+                    for kk in java_hash_map_order(keys)]
+        return [(_random_value(f.children[0], rnd, depth + 1),
+                 _random_value(f.children[1], rnd, depth + 1)) for _ in range(k)]
+    raise ValueError(t)
+
+
+def beana_batch(n: int, seed: int = 37):
+    """n BeanA beans: createBeanA(0..6) first (arrSize 0 = every array / list / map null), then
+    random BeanA beans."""
+    fields = SCHEMAS["beana"]
+    beans = [create_beana(k) for k in range(7)]
+    rnd = JavaRandom(seed)
+    while len(beans) < n:
+        beans.append(random_bean(fields, rnd))
+    return fields, beans[:n]
+
+
+# ---- CPU: schema, values, oracles ------------------------------------------------------------
+def test_beana_schema_follows_type_inference():
+    """TypeInference order / names (TypeInferenceTest.java:34-46 pins the rule): Java names sorted
+    with String.compareTo, lower_underscore, transient f13 absent."""
+    names = [f.name for f in SCHEMAS["beana"]]
+    assert names == ["bean_b", "bean_b_iterable", "bean_b_list", "bytes", "double2_d_list",
+                     "double_list", "f1", "f12", "f15", "f16", "f17", "f2", "f3", "f4", "f5",
+                     "int2_d_array", "int_array", "long_string_field", "string_bean_b_map"]
+    f = {x.name: x for x in SCHEMAS["beana"]}
+    assert not f["f1"].nullable and f["f2"].nullable and not f["f12"].nullable
+    assert f["bytes"].children[0].type_id == T.INT8 and not f["bytes"].children[0].nullable
+    assert f["int2_d_array"].children[0].type_id == T.LIST
+    assert f["int2_d_array"].children[0].nullable
+    assert not f["int2_d_array"].children[0].children[0].nullable
+    assert f["double2_d_list"].children[0].children[0].nullable
+    assert [c.name for c in f["string_bean_b_map"].children] == ["key", "value"]
+    assert not f["string_bean_b_map"].children[0].nullable
+
+
+def test_beana_schema_hash_is_reference_value(oracle):
+    d = json.load(open(os.path.join(GOLDEN, "schema_hashes.json")))["schemas"]["beana"]
+    assert oracle.schema_hash(SCHEMAS["beana"]) == d["hash"]
+    from fury_amd.encoder import Schema
+    try:
+        s = Schema(SCHEMAS["beana"])
+    except OSError:
+        pytest.skip("native library not built")
+    assert s.schema_hash == d["hash"]
+
+
+def test_create_beana_shape():
+    """createBeanA(2): the int2DArray loop writes arr[i] (BeanA.java:104-111), so only the
+    diagonal is set; the HashMap iterates key1 before key0; doubleList[0] is null."""
+    a = create_beana(2)
+    assert a["int2_d_array"][0][1] == 0 and a["int2_d_array"][1][0] == 0
+    assert a["int2_d_array"][0][0] != 0 and a["int2_d_array"][1][1] != 0
+    assert [k for k, _ in a["string_bean_b_map"]] == ["key1", "key0"]
+    assert a["double_list"][0] is None
+    assert a["bean_b"] == create_beanb(2) == a["bean_b_list"][1]
+    assert create_beana(0)["bytes"] is None and create_beana(0)["bean_b"]["int_arr"] is None
+
+
+def test_beana_columnar_oracle_equals_bean_oracle(oracle):
+    """The two restatements agree on BeanA rows (createBeanA(0..6) + random beans)."""
+    fields, beans = beana_batch(300)
+    cols = beans_to_columns(fields, beans)
+    rows, offs = oracle.encode(fields, cols, len(beans))
+    for i, bean in enumerate(beans):
+        assert rows[offs[i]:offs[i + 1]].tobytes() == B.encode_row(fields, bean), f"row {i}"
+    dec = oracle.decode(fields, rows, offs, len(beans))
+    assert columns_to_beans(fields, dec, len(beans)) == beans
+
+
+# ---- GPU: the device path --------------------------------------------------------------------
+def _gpu():
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch, torch.device("cuda:0")
+
+
+@pytest.mark.gpu
+def test_beana_device_batch_bit_exact(oracle):
+    """12,007 BeanA rows (createBeanA(0..6) + random) encoded on the device: rows and offsets
+    byte-equal to the C restatement, decode equal to its decode and to the input beans
+    (RowEncoderTest's assertEquals), the measured single-pass encode equal too."""
+    torch, dev = _gpu()
+    from fury_amd.encoder import Encoders, column_to_device, column_to_host
+    from tests.helpers import assert_columns_equal
+    fields, beans = beana_batch(12_007)
+    n = len(beans)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    assert enc.nested
+    dcols = [column_to_device(c, dev) for c in host]
+    batch = enc.encode_batch(dcols, n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.row_offsets.cpu().numpy(), want_offs)
+    got = batch.rows.cpu().numpy()
+    assert got.shape == want.shape
+    assert np.array_equal(got, want), f"first differing byte {np.nonzero(got != want)[0][:4]}"
+    for i in range(7):
+        assert got[want_offs[i]:want_offs[i + 1]].tobytes() == B.encode_row(fields, beans[i])
+    dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    assert_columns_equal(fields, dec, oracle.decode(fields, want, want_offs, n), n)
+    assert columns_to_beans(fields, dec, n) == beans
+    total = int(want_offs[-1])
+    rows = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    enc.encode_measured_into(dcols, n, rows, offs)
+    torch.cuda.synchronize()
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["beana", "beanb"])
+def test_row_encoder_test_encoder_on_device(name):
+    """RowEncoderTest.testEncoder (RowEncoderTest.java:41-64) through the device encoder:
+    toRow/fromRow of createBeanA(2) / createBeanB(2) three times equal to the bean, the row bytes
+    equal to the bean restatement's; then testStreamingEncode (CodecBuilderTest.java:51-67): one
+    byte, two encode(buffer, obj) frames, two decode(buffer) equal to the bean."""
+    torch, dev = _gpu()
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = SCHEMAS[name]
+    bean = create_beana(2) if name == "beana" else create_beanb(2)
+    enc = Encoders.bean(fields, device=dev)
+    for _ in range(3):
+        row = enc.to_row(bean)
+        assert row == B.encode_row(fields, bean)
+        assert enc.from_row(row) == bean
+    assert enc.decode(enc.encode(bean)) == bean
+    cols = [column_to_device(c, dev) for c in beans_to_columns(fields, [bean, bean])]
+    framed = enc.encode_stream(cols, 2)
+    buf = torch.empty(1 + framed.numel(), dtype=torch.uint8, device=dev)
+    buf[0] = 0xFF
+    buf[1:] = framed
+    hb = buf.cpu().numpy().tobytes()
+    assert struct.unpack_from("<i", hb, 1)[0] == 8 + len(row)
+    assert struct.unpack_from("<q", hb, 5)[0] == enc.schema_hash
+    from fury_amd.encoder import column_to_host
+    out = [column_to_host(c) for c in enc.decode_stream(buf[1:], 2)]
+    assert columns_to_beans(fields, out, 2) == [bean, bean]
+
+
+@pytest.mark.gpu
+def test_cpp_row_test_to_string_from_device_bytes():
+    """cpp/fury/row/row_test.cc:31-99: the RowTest.Write row (f1="str", f2=1, f3=[2, 2],
+    f4={key1: 1.0, key2: 1.0}, f5={n1="str", n2=1}) encoded on the device; Row::ToString of the
+    DEVICE bytes and of the device-decoded bean is the known answer of :96-98."""
+    torch, dev = _gpu()
+    from fury_amd.encoder import Encoders
+    fields = SCHEMAS["row_test"]
+    bean = {"f1": "str", "f2": 1, "f3": [2, 2], "f4": [("key1", 1.0), ("key2", 1.0)],
+            "f5": {"n1": "str", "n2": 1}}
+    enc = Encoders.bean(fields, device=dev)
+    row = enc.to_row(bean)
+    want = _known()["cpp_row_to_string"]["value"]
+    assert B.row_to_string(fields, row) == want
+    assert row == B.encode_row(fields, bean)
+    back = enc.from_row(row)
+    assert back == bean
+    assert B.row_to_string(fields, B.encode_row(fields, back)) == want
