@@ -523,6 +523,7 @@ int gen_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
     const int st = upload_table(tab.data(), tab.size() * sizeof(GenNode), hs, dt);
     if (st) return st;
     g->tab = static_cast<const GenNode*>(dt->dev);
+    g->htab = reinterpret_cast<const GenNode*>(dt->host.data());
   }
   return FURY_OK;
 }
@@ -729,11 +730,21 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   p->nrows = nrows;
   std::vector<int64_t> totals(2 * nn, 0);
   if (nrows > 0) {
-    // lv_prepare synchronises `stream`: rows whose values leave the batch are reported here
-    int st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
+    // both engines synchronise `stream`: rows whose values leave the batch are reported here.
+    // The tile-staged engine first; the level engine when it declines the batch.
+    int st = tree_prepare(s, p->rows, row_offsets, nrows, hs, &p->tree, &totals);
+    if (!st && !p->tree) {
+      if (const int e = take_device_error(hs)) {
+        st = e;
+      } else {
+        totals.assign(2 * nn, 0);
+        st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
+      }
+    }
     if (!st) st = take_device_error(hs);
     if (st) {
       if (p->lv) lv_free(p->lv);
+      if (p->tree) tree_free(p->tree);
       delete p;
       return st;
     }
@@ -762,12 +773,14 @@ int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, v
     return st;
   }
   const GenNode* outs = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
+  if (p->tree) return tree_execute(p->tree, outs, p->rows, p->offs, p->totals, hs);
   return lv_execute(p->lv, outs, p->rows, p->offs, hs);
 }
 
 void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
   if (p->lv) lv_free(p->lv);
+  if (p->tree) tree_free(p->tree);
   if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
   if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
   delete p;
@@ -804,12 +817,41 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_unframe_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "nested_decode") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 0..1");
+    set_tree_mode(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "nested_encode") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..1");
+    set_tree_encode_mode(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "tree_enc_lds" || std::string(key) == "tree_measure_lds") {
+    if (value < 1024 || value > 96 * 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1024..98304 bytes");
+    set_tree_encode_lds(std::string(key) == "tree_enc_lds" ? 1 : 0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "tree_stage" || std::string(key) == "tree_arena") {
+    if (value < 1024 || value > 96 * 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1024..98304 bytes");
+    if (std::string(key) == "tree_stage") set_tree_lds(static_cast<uint32_t>(value), 0);
+    else set_tree_lds(0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
   return set_error(FURY_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
 int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "lookback_help") return lookback_help_mode();
   if (key && std::string(key) == "unframe") return unframe_mode();
+  if (key && std::string(key) == "nested_decode") return tree_mode();
+  if (key && std::string(key) == "nested_encode") return tree_encode_mode();
+  if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
+  if (key && std::string(key) == "tree_measure_lds") return static_cast<int32_t>(tree_encode_lds(0));
+  if (key && std::string(key) == "tree_stage") return static_cast<int32_t>(tree_lds(0));
+  if (key && std::string(key) == "tree_arena") return static_cast<int32_t>(tree_lds(1));
   if (key && std::string(key) == "lookback_timeouts")
     return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")

@@ -332,6 +332,569 @@ __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
   if (r < g.nrows && offs[r + 1] <= cap) put_row<true, kRoot>(nodes, g.ntop, r, rows + offs[r]);
 }
 
+// ---- tree tiles: the encode walked level by level on chip ------------------------------------
+// A workgroup owns a tile of consecutive rows.  Phase R: every node's Arrow entry range for the
+// tile, top-down (a struct child's = its parent's, a list / map child's = the parent's element
+// range from its offsets).  The tile's inputs -- each node's validity bits, offsets, values,
+// string payload -- are then contiguous ranges, staged into LDS by LDS-DMA in ONE round trip.
+// Phase S (bottom-up): the encoded size of every non-scalar entry (a struct's = its fixed part +
+// its children's; a list's = header + element slots + its elements' var parts, read as a
+// difference of the element node's in-tile prefix: one block scan per node under a list / map).
+// The measure pass stops here (row sizes).  The encode pass then places every value top-down in
+// a zeroed LDS image of the tile's output bytes: a row / struct thread writes its null bits and
+// slots and gives each var child its position; an element finds its list by binary search over
+// the staged offsets and writes its own slot and null bit; a string copies its staged payload.
+// The image leaves as one contiguous range.  Tiles whose inputs + arrays + image do not fit the
+// LDS budget are walked in halves; a single row that does not fit is encoded by the row
+// interpreter above, straight to HBM.
+struct TENode {
+  const uint8_t* values;
+  const uint8_t* validity;
+  const int32_t* offsets;
+  int32_t type;
+  int32_t first_child;
+  int32_t num_children;
+  int32_t parent;           // -1: top-level field
+  int32_t ord;              // index among the parent's children
+  int32_t width;            // scalar bytes (BOOL: 1), -1 otherwise
+  int32_t esize;            // slot bytes as an array element
+  int32_t pad_;
+};
+
+constexpr int kTEMaxLevels = 64;
+constexpr int kTEThreads = 256;
+
+struct TEArgs {
+  const TENode* nodes;
+  const GenNode* gtab;      // the same schema for the row interpreter (single-row fallback)
+  const int64_t* offs;      // encode: row offsets (input)
+  int64_t* sizes;           // measure: row sizes (output)
+  uint8_t* rows;
+  int64_t nrows;
+  int64_t cap;
+  int32_t nn, ntop, root, nlevels;
+  int32_t tile_rows;
+  uint32_t lds_cap;
+  uint32_t* fallback;       // bit r: row r is left to te_fixup_kernel (zeroed by the launcher)
+  int32_t level_start[kTEMaxLevels + 1];
+};
+
+struct EMeta {
+  int64_t lo;               // first Arrow entry of the node in the (sub-)tile
+  int64_t plo;              // STRING / BINARY: first payload byte (offsets[lo])
+  uint32_t cnt;             // entries in the (sub-)tile
+  uint32_t vst, ost, pst;   // LDS: validity byte lo / 8, offsets[lo], values / payload start
+  uint32_t S;               // LDS: sizes -> prefixes -> positions (non-scalar nodes), cnt + 1
+  uint32_t X;               // LDS: LIST: element var base; MAP: + value array pos, value var base
+  int64_t phi;              // STRING / BINARY: payload end (offsets[lo + cnt])
+};
+
+constexpr uint32_t kTNone = 0xffffffffu;
+constexpr uint32_t kTDead = 0xffffffffu;
+
+using CTENode = __attribute__((address_space(4))) const TENode;
+__device__ __forceinline__ CTENode& te(const TEArgs& a, int n) { return ((CTENode*)(a.nodes))[n]; }
+
+__device__ __forceinline__ bool te_scalar(int t) { return gwidth(t) > 0; }
+__device__ __forceinline__ uint32_t r8u(uint32_t n) { return (n + 7) & ~7u; }
+__device__ __forceinline__ uint32_t bmu(uint32_t n) { return ((n + 63) >> 6) << 3; }
+
+// LDS-DMA of the 16-B pieces covering [gb, ge) at pool + at (at 16-aligned, advanced); returns the
+// LDS offset of byte gb, or kTNone when the pieces do not fit below cap (nothing issued).
+__device__ __forceinline__ uint32_t te_stage(uint8_t* pool, uint32_t& at, uint32_t cap,
+                                             const uint8_t* gb, const uint8_t* ge) {
+  if (ge <= gb) return at;
+  const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
+  const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
+  const uint64_t bytes = hi - lo;
+  if (at + bytes > cap) return kTNone;
+  const uint32_t nch = static_cast<uint32_t>(bytes >> 4);
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint32_t i0 = wave * 64; i0 < nch; i0 += kTEThreads)
+    if (i0 + lane < nch)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * (i0 + lane)),
+                                       pool + at + 16 * i0, 16, 0, 0);
+  const uint32_t r = at + static_cast<uint32_t>(reinterpret_cast<uint64_t>(gb) - lo);
+  at += static_cast<uint32_t>(bytes);
+  return r;
+}
+
+__device__ __forceinline__ uint64_t te_wscan(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan of uint32 a[0, m) (LDS) by the block; a[m - 1] is the node's trailing 0 slot, so
+// afterwards a[m - 1] = the total.
+__device__ void te_block_scan(uint32_t* a, uint32_t m, uint64_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t per = (m + kTEThreads - 1) / kTEThreads;
+  const uint32_t b = min<uint32_t>(tid * per, m), e = min<uint32_t>(b + per, m);
+  uint64_t s = 0;
+  for (uint32_t i = b; i < e; i++) s += a[i];
+  const uint64_t inc = te_wscan(s);
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint64_t pre = 0;
+#pragma unroll
+  for (int w = 0; w < kTEThreads / 64; w++) pre += w < wave ? wsum[w] : 0;
+  uint64_t run = pre + inc - s;
+  for (uint32_t i = b; i < e; i++) {
+    const uint32_t v = a[i];
+    a[i] = static_cast<uint32_t>(run);
+    run += v;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool te_valid(const uint8_t* pool, const EMeta& m, int64_t q,
+                                         const uint8_t* gvalid) {
+  if (!gvalid) return true;
+  const int64_t i = (m.lo & 7) + q;
+  return (pool[m.vst + (i >> 3)] >> (i & 7)) & 1;
+}
+__device__ __forceinline__ int32_t te_off(const uint8_t* pool, const EMeta& m, int64_t q) {
+  return reinterpret_cast<const int32_t*>(pool + m.ost)[q];
+}
+// Scalar value q of a node from its staged values (BOOL: bit-packed, as 0 / 1).
+__device__ __forceinline__ uint64_t te_value(const uint8_t* pool, const EMeta& m, int t, int w, int64_t q) {
+  if (t == FURY_TYPE_BOOL) {
+    const int64_t i = (m.lo & 7) + q;
+    return (pool[m.pst + (i >> 3)] >> (i & 7)) & 1;
+  }
+  const uint8_t* p = pool + m.pst + q * w;
+  switch (w) {
+    case 8: return *reinterpret_cast<const uint64_t*>(p);
+    case 4: return *reinterpret_cast<const uint32_t*>(p);
+    case 2: return *reinterpret_cast<const uint16_t*>(p);
+    default: return *p;
+  }
+}
+
+// Encoded size of entry q of non-scalar node n (children's sizes / prefixes already in place).
+__device__ uint32_t te_size(const TEArgs& a, const uint8_t* pool, const EMeta* meta, int n, int64_t q) {
+  CTENode& N = te(a, n);
+  const EMeta& M = meta[n];
+  if (!te_valid(pool, M, q, N.validity)) return 0;
+  switch (N.type) {
+    case FURY_TYPE_STRING:
+    case FURY_TYPE_BINARY:
+      return r8u(static_cast<uint32_t>(te_off(pool, M, q + 1) - te_off(pool, M, q)));
+    case FURY_TYPE_DECIMAL:
+      return 16;
+    case FURY_TYPE_STRUCT: {
+      const int nc = N.num_children;
+      uint32_t sz = bmu(nc) + 8 * nc;
+      for (int k = 0; k < nc; k++) {
+        const int c = N.first_child + k;
+        if (te_scalar(te(a, c).type)) continue;
+        sz += reinterpret_cast<const uint32_t*>(pool + meta[c].S)[q];
+      }
+      return sz;
+    }
+    case FURY_TYPE_LIST:
+    case FURY_TYPE_MAP: {
+      const int32_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
+      const uint32_t m = static_cast<uint32_t>(o1 - o0);
+      uint32_t sz = N.type == FURY_TYPE_MAP ? 8 : 0;
+      for (int k = 0; k < (N.type == FURY_TYPE_MAP ? 2 : 1); k++) {
+        const int c = N.first_child + k;
+        CTENode& C = te(a, c);
+        sz += 8 + bmu(m) + r8u(m * C.esize);
+        if (!te_scalar(C.type)) {
+          const uint32_t* P = reinterpret_cast<const uint32_t*>(pool + meta[c].S);
+          const int64_t b = o0 - meta[c].lo;
+          sz += P[b + m] - P[b];
+        }
+      }
+      return sz;
+    }
+    default:
+      return 0;
+  }
+}
+
+// The unpadded size a slot records for a non-null value at entry q of node n with encoded size sz.
+__device__ __forceinline__ uint32_t te_raw(const TEArgs& a, const uint8_t* pool, const EMeta* meta,
+                                           int n, int64_t q, uint32_t sz) {
+  const int t = te(a, n).type;
+  if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY)
+    return static_cast<uint32_t>(te_off(pool, meta[n], q + 1) - te_off(pool, meta[n], q));
+  return sz;
+}
+
+// A struct-like container (a row: n = -1, or entry q of STRUCT node n) at image position pos:
+// null bits and slots of its children; non-scalar children get their positions (in place of
+// their sizes, kTDead when null).  lim = image bytes (writes past it are dropped).
+__device__ void te_put_struct(const TEArgs& a, uint8_t* pool, const EMeta* meta, uint8_t* img,
+                              uint32_t lim, int fc, int nc, int64_t q, uint32_t pos, bool dead) {
+  const uint32_t fixed = bmu(nc) + 8 * nc;
+  uint32_t run = pos + fixed;
+  if (!dead && pos + fixed > lim) dead = true;
+  for (int w = 0; w < (nc + 63) / 64; w++) {
+    uint64_t nulls = 0;
+    for (int k = 64 * w; k < min(nc, 64 * w + 64); k++) {
+      const int c = fc + k;
+      CTENode& C = te(a, c);
+      const bool valid = !dead && te_valid(pool, meta[c], q, C.validity);
+      if (!valid) nulls |= 1ull << (k - 64 * w);
+      uint64_t slot = 0;
+      if (te_scalar(C.type)) {
+        if (valid) slot = te_value(pool, meta[c], C.type, C.width, q);
+      } else {
+        uint32_t* S = reinterpret_cast<uint32_t*>(pool + meta[c].S);
+        const uint32_t sz = S[q];
+        if (valid) {
+          slot = (static_cast<uint64_t>(run - pos) << 32) | te_raw(a, pool, meta, c, q, sz);
+          S[q] = run;
+          run += sz;
+        } else {
+          S[q] = kTDead;
+        }
+      }
+      if (!dead) *reinterpret_cast<uint64_t*>(img + pos + bmu(nc) + 8 * k) = slot;
+    }
+    if (!dead) *reinterpret_cast<uint64_t*>(img + pos + 8 * w) = nulls;
+  }
+}
+
+// Owner of child entry g (global Arrow index) among the nc entries of a LIST / MAP node whose
+// staged offsets are O[0, nc]: the last e with O[e] <= g.
+__device__ __forceinline__ uint32_t te_owner(const int32_t* O, uint32_t nc, int64_t g) {
+  uint32_t lo = 0, hi = nc;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (O[mid] <= g) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void te_store_w(uint8_t* p, int w, uint64_t v) {
+  switch (w) {
+    case 8: *reinterpret_cast<uint64_t*>(p) = v; break;
+    case 4: *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(v); break;
+    case 2: *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(v); break;
+    default: *p = static_cast<uint8_t>(v); break;
+  }
+}
+
+// Walks rows [s0, s1).  Returns false when the LDS budget does not hold it.
+template <bool kWrite>
+__device__ bool te_walk(const TEArgs& a, EMeta* meta, uint64_t* wsum, uint8_t* pool, int64_t s0,
+                        int64_t s1) {
+  const int tid = threadIdx.x;
+  const uint32_t nr = static_cast<uint32_t>(s1 - s0);
+  // ---- R: entry ranges, top-down (a thread per node of the level)
+  for (int L = 0; L < a.nlevels; L++) {
+    const int nb = a.level_start[L], ne = a.level_start[L + 1];
+    for (int n = nb + tid; n < ne; n += kTEThreads) {
+      const TENode N = a.nodes[n];
+      int64_t lo, cnt;
+      if (L == 0) {
+        lo = s0;
+        cnt = nr;
+      } else {
+        const EMeta& P = meta[N.parent];
+        const TENode& PN = a.nodes[N.parent];
+        if (PN.type == FURY_TYPE_STRUCT) {
+          lo = P.lo;
+          cnt = P.cnt;
+        } else {
+          lo = gl(PN.offsets)[P.lo];
+          cnt = gl(PN.offsets)[P.lo + P.cnt] - lo;
+        }
+      }
+      meta[n].lo = lo;
+      meta[n].cnt = static_cast<uint32_t>(cnt);
+      if (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY) {
+        meta[n].plo = cnt ? gl(N.offsets)[lo] : 0;
+        meta[n].phi = cnt ? gl(N.offsets)[lo + cnt] : 0;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- stage the inputs (uniform allocation, every thread issues its share of every copy)
+  uint32_t at = 0;
+  const uint32_t cap = a.lds_cap;
+  for (int n = 0; n < a.nn; n++) {
+    CTENode& N = te(a, n);
+    EMeta& M = meta[n];
+    const int64_t lo = M.lo, cnt = M.cnt;
+    uint32_t vst = kTNone, ost = kTNone, pst = kTNone;
+    const int t = N.type;
+    if (cnt > 0) {
+      if (N.validity) {
+        vst = te_stage(pool, at, cap, N.validity + (lo >> 3), N.validity + ((lo + cnt + 7) >> 3));
+        if (vst == kTNone) return false;
+      }
+      if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST || t == FURY_TYPE_MAP) {
+        ost = te_stage(pool, at, cap, reinterpret_cast<const uint8_t*>(N.offsets + lo),
+                       reinterpret_cast<const uint8_t*>(N.offsets + lo + cnt + 1));
+        if (ost == kTNone) return false;
+      }
+      if (kWrite) {
+        if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY)
+          pst = te_stage(pool, at, cap, N.values + M.plo, N.values + M.phi);
+        else if (t == FURY_TYPE_BOOL)
+          pst = te_stage(pool, at, cap, N.values + (lo >> 3), N.values + ((lo + cnt + 7) >> 3));
+        else if (t == FURY_TYPE_DECIMAL)
+          pst = te_stage(pool, at, cap, N.values + 16 * lo, N.values + 16 * (lo + cnt));
+        else if (N.width > 0)
+          pst = te_stage(pool, at, cap, N.values + N.width * lo, N.values + N.width * (lo + cnt));
+        if (pst == kTNone && t != FURY_TYPE_STRUCT && t != FURY_TYPE_LIST && t != FURY_TYPE_MAP)
+          return false;
+      }
+    }
+    if (tid == 0) {
+      M.vst = vst;
+      M.ost = ost;
+      M.pst = pst;
+    }
+  }
+  // ---- arrays: sizes (+1 slot), LIST / MAP extras
+  for (int n = 0; n < a.nn; n++) {
+    CTENode& N = te(a, n);
+    const uint32_t cnt = meta[n].cnt;
+    uint32_t S = kTNone, X = kTNone;
+    if (!te_scalar(N.type)) {
+      if (at + 4 * (cnt + 1) > cap) return false;
+      S = at;
+      at += (4 * (cnt + 1) + 15) & ~15u;
+    }
+    if (kWrite && (N.type == FURY_TYPE_LIST || N.type == FURY_TYPE_MAP)) {
+      const uint32_t need = 4 * cnt * (N.type == FURY_TYPE_MAP ? 3 : 1);
+      if (at + need > cap) return false;
+      X = at;
+      at += (need + 15) & ~15u;
+    }
+    if (tid == 0) {
+      meta[n].S = S;
+      meta[n].X = X;
+    }
+  }
+  // ---- the image of the tile's output bytes (encode)
+  uint32_t img_at = 0, lim = 0;
+  if (kWrite) {
+    const int64_t b0 = gl(a.offs)[s0], b1 = gl(a.offs)[s1];
+    const int64_t bytes = b1 - b0;
+    if (bytes < 0 || at + bytes + 16 > cap) return false;
+    img_at = at;
+    lim = static_cast<uint32_t>(bytes);
+    using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+    for (uint32_t i = 16 * tid; i < ((lim + 15) & ~15u); i += 16 * kTEThreads)
+      *reinterpret_cast<v4*>(pool + img_at + i) = v4{0, 0, 0, 0};
+  }
+  __syncthreads();                               // staged inputs landed, meta visible
+  uint8_t* img = pool + img_at;
+  // ---- S: sizes bottom-up; prefixes of the nodes below a LIST / MAP
+  for (int L = a.nlevels - 1; L >= 0; L--) {
+    const int nb = a.level_start[L], ne = a.level_start[L + 1];
+    for (int n = nb; n < ne; n++) {
+      if (te_scalar(te(a, n).type)) continue;
+      const EMeta M = meta[n];
+      uint32_t* S = reinterpret_cast<uint32_t*>(pool + M.S);
+      for (uint32_t q = tid; q < M.cnt; q += kTEThreads) S[q] = te_size(a, pool, meta, n, q);
+      if (tid == 0) S[M.cnt] = 0;
+    }
+    __syncthreads();
+    if (L == 0) break;
+    for (int n = nb; n < ne; n++) {
+      CTENode& N = te(a, n);
+      if (te_scalar(N.type)) continue;
+      const int pt = te(a, N.parent).type;
+      if (pt != FURY_TYPE_LIST && pt != FURY_TYPE_MAP) continue;
+      te_block_scan(reinterpret_cast<uint32_t*>(pool + meta[n].S), meta[n].cnt + 1, wsum);
+    }
+  }
+  // ---- row sizes (measure) / row containers (encode)
+  for (uint32_t r = tid; r < nr; r += kTEThreads) {
+    if (!kWrite) {
+      uint64_t sz;
+      if (a.root) {
+        sz = reinterpret_cast<const uint32_t*>(pool + meta[0].S)[r];
+      } else {
+        sz = bmu(a.ntop) + 8ull * a.ntop;
+        for (int k = 0; k < a.ntop; k++)
+          if (!te_scalar(te(a, k).type)) sz += reinterpret_cast<const uint32_t*>(pool + meta[k].S)[r];
+      }
+      a.sizes[s0 + r] = static_cast<int64_t>(sz);
+    } else {
+      const int64_t b0 = gl(a.offs)[s0];
+      const uint32_t pos = static_cast<uint32_t>(gl(a.offs)[s0 + r] - b0);
+      if (a.root) reinterpret_cast<uint32_t*>(pool + meta[0].S)[r] = pos;
+      else te_put_struct(a, pool, meta, img, lim, 0, a.ntop, r, pos, false);
+    }
+  }
+  if (!kWrite) return true;
+  __syncthreads();
+  // ---- positions + contents, top-down
+  for (int L = 0; L < a.nlevels; L++) {
+    const int nb = a.level_start[L], ne = a.level_start[L + 1];
+    for (int n = nb; n < ne; n++) {
+      CTENode& N = te(a, n);
+      const EMeta M = meta[n];
+      const bool scalar = te_scalar(N.type);
+      const int pt = L == 0 ? -1 : te(a, N.parent).type;
+      const bool elem = pt == FURY_TYPE_LIST || pt == FURY_TYPE_MAP;
+      if (scalar && !elem) continue;              // written by the row / struct thread
+      uint32_t* S = scalar ? nullptr : reinterpret_cast<uint32_t*>(pool + M.S);
+      const EMeta PM = L == 0 ? M : meta[N.parent];
+      for (uint32_t q = tid; q < M.cnt; q += kTEThreads) {
+        uint32_t pos = scalar ? kTDead : S[q];
+        if (elem) {                                // an element: its own slot in the parent array
+          const int32_t* O = reinterpret_cast<const int32_t*>(pool + PM.ost);
+          const int64_t g = M.lo + q;
+          const uint32_t e = te_owner(O, PM.cnt, g);
+          const uint32_t j = static_cast<uint32_t>(g - O[e]);
+          const uint32_t m = static_cast<uint32_t>(O[e + 1] - O[e]);
+          const uint32_t ppos = reinterpret_cast<const uint32_t*>(pool + PM.S)[e];
+          const uint32_t* PX = reinterpret_cast<const uint32_t*>(pool + PM.X);
+          pos = kTDead;
+          if (ppos != kTDead) {
+            const uint32_t arr = pt == FURY_TYPE_LIST ? ppos : (N.ord == 0 ? ppos + 8 : PX[PM.cnt + e]);
+            const bool valid = te_valid(pool, M, q, N.validity);
+            const uint32_t sl = arr + 8 + bmu(m) + static_cast<uint32_t>(N.esize) * j;
+            if (!valid) {
+              if (arr + 8 + (j >> 3) < lim)
+                atomicOr(reinterpret_cast<uint32_t*>(img + arr + 8) + (j >> 5), 1u << (j & 31));
+            } else if (scalar) {
+              if (sl + N.esize <= lim) te_store_w(img + sl, N.esize, te_value(pool, M, N.type, N.width, q));
+            } else {
+              const uint32_t base = N.ord == 0 ? PX[e] : PX[2 * PM.cnt + e];
+              const uint32_t sz = te_size(a, pool, meta, n, q);
+              pos = base + S[q];
+              const uint64_t slot = (static_cast<uint64_t>(pos - arr) << 32) | te_raw(a, pool, meta, n, q, sz);
+              if (sl + 8 <= lim) *reinterpret_cast<uint64_t*>(img + sl) = slot;
+            }
+          }
+          if (scalar) continue;
+          S[q] = pos;                              // (only this thread reads S[q] at this level)
+        }
+        if (pos == kTDead) {                       // a null / dead struct: its children are dead
+          if (N.type == FURY_TYPE_STRUCT)
+            te_put_struct(a, pool, meta, img, lim, N.first_child, N.num_children, q, 0, true);
+          continue;
+        }
+        switch (N.type) {
+          case FURY_TYPE_STRING:
+          case FURY_TYPE_BINARY: {
+            const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
+            const uint8_t* src = pool + M.pst + (o0 - M.plo);
+            const uint32_t len = static_cast<uint32_t>(o1 - o0);
+            if (pos + len <= lim)
+              for (uint32_t i = 0; i < len; i++) img[pos + i] = src[i];
+            break;
+          }
+          case FURY_TYPE_DECIMAL: {
+            const uint8_t* src = pool + M.pst + 16 * q;
+            if (pos + 16 <= lim)
+              for (int i = 0; i < 16; i++) img[pos + i] = src[i];
+            break;
+          }
+          case FURY_TYPE_STRUCT:
+            te_put_struct(a, pool, meta, img, lim, N.first_child, N.num_children, q, pos, false);
+            break;
+          case FURY_TYPE_LIST:
+          case FURY_TYPE_MAP: {
+            const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
+            const uint32_t m = static_cast<uint32_t>(o1 - o0);
+            uint32_t* X = reinterpret_cast<uint32_t*>(pool + M.X);
+            uint32_t arr = pos;
+            if (N.type == FURY_TYPE_MAP) arr = pos + 8;
+            uint32_t kbytes = 0;
+            for (int k = 0; k < (N.type == FURY_TYPE_MAP ? 2 : 1); k++) {
+              const int c = N.first_child + k;
+              CTENode& C = te(a, c);
+              const uint32_t hdr = 8 + bmu(m) + r8u(m * C.esize);
+              if (arr + 8 <= lim) *reinterpret_cast<uint64_t*>(img + arr) = m;
+              uint32_t var = 0;
+              if (!te_scalar(C.type)) {
+                const uint32_t* P = reinterpret_cast<const uint32_t*>(pool + meta[c].S);
+                const int64_t b = o0 - meta[c].lo;
+                X[k == 0 ? q : 2 * M.cnt + q] = arr + hdr - P[b];
+                var = P[b + m] - P[b];
+              }
+              if (k == 0) {
+                kbytes = hdr + var;
+                if (N.type == FURY_TYPE_MAP) {
+                  if (pos + 8 <= lim) *reinterpret_cast<uint64_t*>(img + pos) = kbytes;
+                  arr = pos + 8 + kbytes;
+                  X[M.cnt + q] = arr;
+                }
+              }
+            }
+            break;
+          }
+          default:
+            break;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ---- the image leaves as one contiguous range (bytes at or past cap are not written)
+  const int64_t b0 = gl(a.offs)[s0];
+  const int64_t end = min<int64_t>(static_cast<int64_t>(lim), a.cap - b0);
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(img);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(a.rows + b0);
+  for (int64_t i = tid; i < (end >> 3); i += kTEThreads) __builtin_nontemporal_store(src[i], gl(dst) + i);
+  return true;
+}
+
+// Rows the tree walk could not hold in LDS (one row beyond the budget): the row interpreter, in a
+// kernel of its own (inlined into te_kernel it took 256 VGPRs and scratch from the whole walk).
+template <bool kWrite, int kRoot>
+__global__ __launch_bounds__(kTEThreads) void te_fixup_kernel(TEArgs a) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kTEThreads + threadIdx.x;
+  if (r >= a.nrows || !((gl(a.fallback)[r >> 5] >> (r & 31)) & 1)) return;
+  const GNodes gn = (GNodes)(a.gtab);
+  if (!kWrite) a.sizes[r] = put_row<false, kRoot>(gn, a.ntop, r, static_cast<uint8_t*>(nullptr));
+  else if (gl(a.offs)[r + 1] <= a.cap) put_row<true, kRoot>(gn, a.ntop, r, a.rows + gl(a.offs)[r]);
+}
+
+template <bool kWrite, int kRoot>
+__global__ __launch_bounds__(kTEThreads) void te_kernel(TEArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tes[];
+  EMeta* meta = reinterpret_cast<EMeta*>(tes);
+  uint64_t* wsum = reinterpret_cast<uint64_t*>(tes + sizeof(EMeta) * a.nn);
+  uint8_t* pool = tes + ((sizeof(EMeta) * a.nn + 64 + 15) & ~size_t(15));
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile_rows;
+  const int64_t r1 = min<int64_t>(r0 + a.tile_rows, a.nrows);
+  // encode: sub-tiles whose OUTPUT bytes take at most ~40 % of the budget (inputs and arrays are
+  // of the same order); the walk halves a sub-tile that still does not fit
+  const int64_t img_budget = kWrite ? static_cast<int64_t>(a.lds_cap) * 2 / 5 : 0;
+  int64_t s0 = r0;
+  while (s0 < r1) {
+    int64_t s1 = r1;
+    if (kWrite) {                               // largest s1 with offs[s1] - offs[s0] <= budget
+      const int64_t b0 = gl(a.offs)[s0];
+      if (gl(a.offs)[s1] - b0 > img_budget) {
+        int64_t lo = s0 + 1, hi = s1;            // offs[lo] may exceed it: at least one row
+        while (hi - lo > 0) {
+          const int64_t mid = (lo + hi + 1) >> 1;
+          if (gl(a.offs)[mid] - b0 <= img_budget) lo = mid; else hi = mid - 1;
+        }
+        s1 = lo;
+      }
+    }
+    bool ok = false;
+    for (;;) {
+      ok = te_walk<kWrite>(a, meta, wsum, pool, s0, s1);
+      __syncthreads();
+      if (ok || s1 - s0 == 1) break;
+      s1 = s0 + (s1 - s0 + 1) / 2;
+    }
+    if (!ok && threadIdx.x == 0)                 // one row beyond the budget: te_fixup_kernel
+      atomicOr(a.fallback + (s0 >> 5), 1u << (s0 & 31));
+    s0 = s1;
+  }
+}
+
 }  // namespace
 
 template <bool kWide, int kRoot>
@@ -361,7 +924,119 @@ void gen_encode_root(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint
   }
 }
 
+namespace {
+int g_tree_encode = 1;           // tuning "nested_encode": 0 tree tiles, 1 the row interpreter
+uint32_t g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
+
+int host_gwidth(int t) {
+  switch (t) {
+    case FURY_TYPE_BOOL: case FURY_TYPE_INT8: return 1;
+    case FURY_TYPE_INT16: return 2;
+    case FURY_TYPE_INT32: case FURY_TYPE_FLOAT32: case FURY_TYPE_DATE32: return 4;
+    case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
+    default: return -1;
+  }
+}
+
+// The tree-tile measure (sizes != NULL) or encode; returns 1 when the schema is left to the row
+// interpreter (tables beyond the tree limits), else a status.
+int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
+                       int64_t cap, hipStream_t stream) {
+  const int nn = g.nnodes;
+  if (g_tree_encode != 0 || nn > 512 || nn <= 0) return 1;
+  const GenNode* hn = g.htab ? g.htab : g.node;
+  std::vector<TENode> tab(nn);
+  std::vector<int32_t> level(nn, 0);
+  for (int i = 0; i < nn; i++) {
+    TENode& t = tab[i];
+    t.values = hn[i].values;
+    t.validity = hn[i].validity;
+    t.offsets = hn[i].offsets;
+    t.type = hn[i].type;
+    t.first_child = hn[i].first_child;
+    t.num_children = hn[i].num_children;
+    if (i < g.ntop) {
+      t.parent = -1;
+      t.ord = i;
+    }
+    t.width = host_gwidth(t.type);
+    t.esize = t.width > 0 ? t.width : 8;
+    for (int j = 0; j < t.num_children; j++) {
+      tab[t.first_child + j].parent = i;
+      tab[t.first_child + j].ord = j;
+      level[t.first_child + j] = level[i] + 1;
+    }
+  }
+  const int nlev = level[nn - 1] + 1;
+  if (nlev > kTEMaxLevels) return 1;
+  TEArgs a{};
+  a.level_start[0] = 0;
+  for (int L = 1; L <= nlev; L++) {
+    int i = a.level_start[L - 1];
+    while (i < nn && level[i] < L) i++;
+    a.level_start[L] = i;
+  }
+  DeviceTable dt, dg;
+  int st = upload_table(tab.data(), tab.size() * sizeof(TENode), stream, &dt);
+  if (st) return st;
+  const GenNode* gtab = g.tab;
+  if (!gtab) {
+    st = upload_table(g.node, nn * sizeof(GenNode), stream, &dg);
+    if (st) return st;
+    gtab = static_cast<const GenNode*>(dg.dev);
+  }
+  const bool write = sizes == nullptr;
+  a.nodes = static_cast<const TENode*>(dt.dev);
+  a.gtab = gtab;
+  a.offs = offs;
+  a.sizes = sizes;
+  a.rows = rows;
+  a.nrows = g.nrows;
+  a.cap = cap;
+  a.nn = nn;
+  a.ntop = g.ntop;
+  a.root = g.root;
+  a.nlevels = nlev;
+  a.tile_rows = kTEThreads;
+  a.lds_cap = g_te_lds[write ? 1 : 0];
+  const size_t lds = ((sizeof(EMeta) * nn + 64 + 15) & ~size_t(15)) + a.lds_cap;
+  const dim3 grid(static_cast<unsigned>((g.nrows + a.tile_rows - 1) / a.tile_rows));
+  const int64_t fb_bytes = ((g.nrows + 31) / 32) * 4;
+  void* fb = nullptr;
+  if ((st = dev_alloc(fb_bytes, stream, &fb))) return st;
+  if ((st = check_hip(hipMemsetAsync(fb, 0, fb_bytes, stream), "hipMemsetAsync"))) return st;
+  a.fallback = static_cast<uint32_t*>(fb);
+  auto go = [&](auto kern, auto fix) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(kern, grid, dim3(kTEThreads), lds, stream, a);
+    hipLaunchKernelGGL(fix, dim3(static_cast<unsigned>((g.nrows + kTEThreads - 1) / kTEThreads)),
+                       dim3(kTEThreads), 0, stream, a);
+  };
+  switch ((write ? 3 : 0) + g.root) {
+    case 0: go(te_kernel<false, 0>, te_fixup_kernel<false, 0>); break;
+    case 1: go(te_kernel<false, 1>, te_fixup_kernel<false, 1>); break;
+    case 2: go(te_kernel<false, 2>, te_fixup_kernel<false, 2>); break;
+    case 3: go(te_kernel<true, 0>, te_fixup_kernel<true, 0>); break;
+    case 4: go(te_kernel<true, 1>, te_fixup_kernel<true, 1>); break;
+    default: go(te_kernel<true, 2>, te_fixup_kernel<true, 2>); break;
+  }
+  st = check_hip(hipGetLastError(), "tree encode launch");
+  dev_free(fb, stream);
+  return st;
+}
+}  // namespace
+
+void set_tree_encode_mode(int v) { g_tree_encode = v; }
+int tree_encode_mode() { return g_tree_encode; }
+void set_tree_encode_lds(int which, uint32_t bytes) { g_te_lds[which ? 1 : 0] = (bytes + 15) & ~15u; }
+uint32_t tree_encode_lds(int which) { return g_te_lds[which ? 1 : 0]; }
+
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
+  if (g.nrows > 0) {
+    const int t = launch_tree_encode(g, nullptr, sizes, nullptr, 0, stream);
+    if (t != 1) return t;
+  }
   if (g.tab) gen_encode_root<true>(g, nullptr, sizes, nullptr, 0, stream);
   else gen_encode_root<false>(g, nullptr, sizes, nullptr, 0, stream);
   return check_hip(hipGetLastError(), "gen_measure launch");
@@ -369,6 +1044,10 @@ int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
 
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
+  if (g.nrows > 0) {
+    const int t = launch_tree_encode(g, offs, nullptr, rows, cap, stream);
+    if (t != 1) return t;
+  }
   if (g.tab) gen_encode_root<true>(g, offs, nullptr, rows, cap, stream);
   else gen_encode_root<false>(g, offs, nullptr, rows, cap, stream);
   return check_hip(hipGetLastError(), "gen_encode launch");

@@ -66,7 +66,7 @@ struct fury_schema {
 };
 
 // Decode plan of the two-step (nested) decode, device and host-memory flavours.
-namespace fury { struct LvPlan; }
+namespace fury { struct LvPlan; struct TreePlan; }
 
 struct fury_decode_plan {
   const fury_schema* schema = nullptr;
@@ -74,6 +74,7 @@ struct fury_decode_plan {
   const int64_t* offs = nullptr;
   int64_t nrows = 0;
   fury::LvPlan* lv = nullptr;      // level-by-level engine state (levels.hip); NULL when nrows = 0
+  fury::TreePlan* tree = nullptr;  // tile-staged engine state (tree.hip): used when set
   bool arrow = false;
   std::vector<int64_t> totals;     // per node: Arrow entries, payload bytes
   void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)

@@ -205,11 +205,18 @@ struct GenArgs {
   int32_t root;            // fury_schema.root: 0 rows, 1 top-level arrays, 2 top-level maps
   int32_t pad_;
   const GenNode* tab;      // device node table for > kGenMaxNodes nodes, else NULL
+  const GenNode* htab;     // its host copy (launchers only; never read on the device)
 };
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
+// Nested encode engine (generic.hip): tuning "nested_encode" 0 = tree tiles (default), 1 = the
+// thread-per-row interpreter; "tree_enc_lds" / "tree_measure_lds" = their LDS budgets (bytes).
+void set_tree_encode_mode(int v);
+int tree_encode_mode();
+void set_tree_encode_lds(int which, uint32_t bytes);   // which: 0 measure, 1 encode
+uint32_t tree_encode_lds(int which);
 // Level-by-level nested decode (levels.hip): prepare = per-level count / scan / expand passes
 // (totals[2 i] entries, totals[2 i + 1] payload bytes of node i), execute = one write pass into
 // the outputs of gen_args' node table.
@@ -219,6 +226,18 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
 int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                hipStream_t hs);
 void lv_free(LvPlan* p);
+// Tile-staged nested decode (tree.hip): prepare = pass 1 + tile scan + one host sync (*out NULL:
+// the batch needs the level engine above), execute = pass 2 into gen_args' node table.
+struct TreePlan;
+int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, int64_t nrows,
+                 hipStream_t hs, TreePlan** out, std::vector<int64_t>* totals);
+int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
+                 const std::vector<int64_t>& totals, hipStream_t hs);
+void tree_free(TreePlan* p);
+void set_tree_mode(int v);           // tuning "nested_decode": 0 tree tiles (default), 1 levels
+int tree_mode();
+void set_tree_lds(uint32_t stage, uint32_t arena);   // tuning "tree_stage" / "tree_arena" (bytes)
+uint32_t tree_lds(int which);
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);

@@ -29,6 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=400_000)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--legs", default="0",
+                    help="engines: 0 tree tiles, 1 interpreter encode + level decode (tunings "
+                         "nested_encode / nested_decode)")
     args = ap.parse_args()
     import torch
     from fury_amd.beans import beans_to_columns
@@ -58,13 +61,23 @@ def main():
             torch.cuda.synchronize()
             xs.append(a.elapsed_time(b) / args.iters)
         return statistics.median(xs)
+    import ctypes
+    from fury_amd import _native as N
+    for leg in [int(x) for x in args.legs.split(",")]:
+        for k in (b"nested_encode", b"nested_decode"):
+            assert N.lib().fury_set_tuning(k, leg) == 0
+        leg_run(args, t, enc, cols, n, batch, out, leg)
+
+
+def leg_run(args, t, enc, cols, n, batch, out, leg):
+    import ctypes
+    import torch
+    from fury_amd import _native as N
     enc_ms = t(lambda: enc.encode_batch(cols, n))
     dec_ms = t(lambda: enc.decode_batch(batch))
     # the pieces: measure (row sizes + scan), encode into sized rows, decode count pass
     # (fury_decode_prepare incl. its host read of the node totals), decode execute alone
-    import ctypes
-    from fury_amd import _native as N
-    from fury_amd.encoder import _bfs, _c_columns, _ptr
+    from fury_amd.encoder import _c_columns, _ptr
     L = N.lib()
     h = enc._schema.handle
     sh = torch.cuda.current_stream().cuda_stream
@@ -92,7 +105,7 @@ def main():
     L.fury_decode_plan_destroy(plan)
     cb = _bytes(cols)
     rb = batch.rows.numel() + 8 * (n + 1)
-    print(json.dumps({"pieces_ms": {"measure": round(meas_ms, 3), "encode": round(enc_only_ms, 3),
+    print(json.dumps({"leg": leg, "pieces_ms": {"measure": round(meas_ms, 3), "encode": round(enc_only_ms, 3),
                                     "decode_prepare": round(prep_ms, 3),
                                     "decode_execute": round(exec_ms, 3)},
                       "execute_GBps": round((cb + rb) / exec_ms / 1e6, 1),"schema": "tests _nested_fields (7 fields, depth 3)", "rows": n,

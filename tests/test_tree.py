@@ -1,0 +1,214 @@
+"""The tile-staged nested decode (tree.hip) against the oracle and against the level engine
+(levels.hip, tuning "nested_decode" = 1) on the same rows: every nested schema shape the tests
+know, the reference's BeanA, collections (ArrayEncoder / MapEncoder batches), and LDS budgets
+small enough to force the walk in halves and rows read from HBM past the stage.  Marked gpu."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+from fury_amd import types as T  # noqa: E402
+from fury_amd.workloads import SCHEMAS  # noqa: E402
+from tests.helpers import assert_columns_equal  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch.device("cuda:0")
+
+
+def _tune(key, v):
+    from fury_amd import _native as N
+    assert N.lib().fury_set_tuning(key.encode(), v) == 0, N.last_error()
+
+
+@pytest.fixture
+def engines():
+    """Restores the default engine and LDS budgets after the test."""
+    from fury_amd import _native as N
+    L = N.lib()
+    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena")}
+    yield
+    for k, v in old.items():
+        _tune(k, v)
+
+
+def _schemas():
+    from tests.test_device import _engine_schemas, _nested_fields
+    out = dict(_engine_schemas())
+    out["beana"] = SCHEMAS["beana"]
+    out["nested7"] = _nested_fields()
+    out["flat_mixed"] = SCHEMAS["mixed"]
+    return out
+
+
+def _beans(fields, n, seed):
+    from tests.test_device import _random_value
+    rng = np.random.default_rng(seed)
+    return [{f.name: _random_value(f, rng) for f in fields} for _ in range(n)]
+
+
+def _decode_plan(enc, batch):
+    from fury_amd.encoder import column_to_host
+    return [column_to_host(c) for c in enc._decode_nested(batch, True, False, None)]
+
+
+@pytest.mark.parametrize("name", ["nested7", "foo", "deep_lists", "struct_chain", "maps", "beana",
+                                  "flat_mixed"])
+@pytest.mark.parametrize("budget", ["default", "tiny"])
+def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, budget):
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _schemas()[name]
+    n = 2999
+    beans = _beans(fields, n, len(name) * 31)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    if budget == "tiny":              # 2 KB stage, 2 KB arena: walks in halves, HBM reads
+        _tune("tree_stage", 2048)
+        _tune("tree_arena", 2048)
+    ref = oracle.decode(fields, want, want_offs, n)
+    _tune("nested_decode", 0)
+    tree = _decode_plan(enc, batch)
+    assert_columns_equal(fields, tree, ref, n)
+    assert columns_to_beans(fields, tree, n) == beans
+    _tune("nested_decode", 1)
+    lv = _decode_plan(enc, batch)
+    assert_columns_equal(fields, lv, tree, n)
+
+
+def test_tree_decode_large_batch(oracle, dev, engines):
+    """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    from tests.test_device import _nested_beans, _nested_fields
+    fields = _nested_fields()
+    base = _nested_beans(20_000, seed=5)
+    n = 400_000
+    host = beans_to_columns(fields, (base * (n // len(base) + 1))[:n])
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    _tune("nested_decode", 0)
+    got = _decode_plan(enc, batch)
+    assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
+def test_collections_both_engines(oracle, dev, engines, mode, kind):
+    """ArrayEncoder / MapEncoder batches (root 1 / 2: each entry a top-level BinaryArray /
+    BinaryMap) through the tile engine (mode 0) and the level engine (mode 1)."""
+    from tests.test_device import test_array_encoder_batch_vs_oracle, test_map_encoder_batch_vs_oracle
+    _tune("nested_decode", mode)
+    if kind == "map":
+        test_map_encoder_batch_vs_oracle(oracle, dev)
+    else:
+        test_array_encoder_batch_vs_oracle(oracle, dev, kind)
+
+
+def test_tree_decode_skewed_rows(oracle, dev, engines):
+    """Tiles whose bytes exceed the stage (rows of very different sizes): the rows past the stage
+    are read from HBM, the result is the oracle's."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = [T.field("a", T.INT32), T.array_field("l", T.STRING),
+              T.struct_field("s", [T.field("x", T.INT64), T.array_field("y", T.INT16)])]
+    rng = np.random.default_rng(9)
+    beans = []
+    for i in range(5000):
+        big = i % 97 == 3
+        k = int(rng.integers(200, 400)) if big else int(rng.integers(0, 3))
+        beans.append({"a": i, "l": ["x" * int(rng.integers(0, 40)) for _ in range(k)],
+                      "s": None if i % 11 == 5 else {"x": i * 3, "y": list(range(k % 50))}})
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    n = len(beans)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    _tune("nested_decode", 0)
+    got = _decode_plan(enc, batch)
+    assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
+
+
+@pytest.fixture
+def enc_engines():
+    from fury_amd import _native as N
+    L = N.lib()
+    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_encode", "tree_enc_lds",
+                                                       "tree_measure_lds")}
+    yield
+    for k, v in old.items():
+        _tune(k, v)
+
+
+@pytest.mark.parametrize("name", ["nested7", "foo", "deep_lists", "struct_chain", "maps", "beana"])
+@pytest.mark.parametrize("budget", ["default", "small", "tiny"])
+def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, name, budget):
+    """The tile-staged nested encode (measure + encode) == the C restatement's bytes and offsets
+    == the row interpreter's (tuning nested_encode = 1); "small" budgets walk tiles in halves,
+    "tiny" ones leave single rows to the interpreter's fixup kernel."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _schemas()[name]
+    n = 3001
+    beans = _beans(fields, n, len(name) * 17 + 5)
+    host = beans_to_columns(fields, beans)
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    want, want_offs = oracle.encode(fields, host, n)
+    if budget == "small":
+        _tune("tree_enc_lds", 8192)
+        _tune("tree_measure_lds", 4096)
+    elif budget == "tiny":
+        _tune("tree_enc_lds", 1024)
+        _tune("tree_measure_lds", 1024)
+    _tune("nested_encode", 0)
+    b = enc.encode_batch(dcols, n)
+    assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
+    assert np.array_equal(b.rows.cpu().numpy(), want)
+    total = int(want_offs[-1])
+    rows = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    enc.encode_measured_into(dcols, n, rows, offs)
+    torch.cuda.synchronize()
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    _tune("nested_encode", 1)
+    b1 = enc.encode_batch(dcols, n)
+    assert np.array_equal(b1.rows.cpu().numpy(), want)
+
+
+def test_tree_encode_capacity(oracle, dev, enc_engines):
+    """encode_measured with a short buffer: offsets complete, no byte at or past the capacity
+    written (guard bytes intact), the bytes before it equal to the oracle's."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _schemas()["nested7"]
+    n = 2000
+    host = beans_to_columns(fields, _beans(fields, n, 77))
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    want, want_offs = oracle.encode(fields, host, n)
+    cap = (int(want_offs[n // 2]) + 13) & ~7
+    rows = torch.full((cap + 4096,), 0xAB, dtype=torch.uint8, device=dev)
+    offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    from fury_amd import _native as N
+    from fury_amd.encoder import _c_columns, _ptr, _stream_handle
+    keep: list = []
+    st = N.lib().fury_row_encode_measured(enc.schema().handle, _c_columns(dcols, keep), n,
+                                          _ptr(offs), _ptr(rows), cap, _stream_handle(None))
+    assert st == 0, N.last_error()
+    torch.cuda.synchronize()
+    got = rows.cpu().numpy()
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert (got[cap:] == 0xAB).all()
+    full = int(np.searchsorted(want_offs, cap, side="right")) - 1
+    assert np.array_equal(got[:want_offs[full]], want[:want_offs[full]])
