@@ -111,7 +111,9 @@ int take_device_error(hipStream_t stream) {
   const bool lb = take_flag(w, kErrLookBack, nullptr);
   const bool oob = take_flag(w, kErrBounds, &oob_at);
   const bool map = take_flag(w, kErrMapCount, &map_at);
-  if (!lb && !oob && !map) return FURY_OK;
+  uint64_t deep_at = 0;
+  const bool deep = take_flag(w, kErrTooDeep, &deep_at);
+  if (!lb && !oob && !map && !deep) return FURY_OK;
   if (lb) {
     g_err_taken.fetch_add(1);
     return set_error(FURY_ERR_DEVICE,
@@ -124,6 +126,11 @@ int take_device_error(hipStream_t stream) {
                          " has a variable-length value, array or map header outside the batch's "
                          "row bytes (MemoryBuffer bounds check); the outputs of that call are "
                          "invalid");
+  if (deep)
+    return set_error(FURY_ERR_UNSUPPORTED,
+                     "encode: " + where_text(deep_at) +
+                         " is too large to assemble on chip and the schema is nested deeper than "
+                         "the row interpreter reaches; the rows of that call are invalid");
   return set_error(FURY_ERR_UNSUPPORTED,
                    "decode: " + where_text(map_at) +
                        ": map key and value arrays have different element counts "
@@ -822,8 +829,18 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_tree_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "tree_threads") {
+    if (value != 256 && value != 512 && value != 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "tree_threads: 256, 512 or 1024");
+    set_tree_threads(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "tree_debug") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "tree_debug: 0..1");
+    return set_tree_debug(value) ? set_error(FURY_ERR_DEVICE, "tree_debug buffer") : FURY_OK;
+  }
   if (std::string(key) == "nested_encode") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..1");
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..2");
     set_tree_encode_mode(value);
     return FURY_OK;
   }
@@ -831,6 +848,12 @@ int fury_set_tuning(const char* key, int32_t value) {
     if (value < 1024 || value > 96 * 1024)
       return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1024..98304 bytes");
     set_tree_encode_lds(std::string(key) == "tree_enc_lds" ? 1 : 0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "tree_enc_rows" || std::string(key) == "tree_measure_rows") {
+    if (value < 1 || value > 4096)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1..4096 rows");
+    set_tree_encode_rows(std::string(key) == "tree_enc_rows" ? 1 : 0, value);
     return FURY_OK;
   }
   if (std::string(key) == "tree_stage" || std::string(key) == "tree_arena") {
@@ -848,7 +871,10 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "nested_decode") return tree_mode();
   if (key && std::string(key) == "nested_encode") return tree_encode_mode();
+  if (key && std::string(key) == "tree_threads") return tree_threads();
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
+  if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);
+  if (key && std::string(key) == "tree_measure_rows") return tree_encode_rows(0);
   if (key && std::string(key) == "tree_measure_lds") return static_cast<int32_t>(tree_encode_lds(0));
   if (key && std::string(key) == "tree_stage") return static_cast<int32_t>(tree_lds(0));
   if (key && std::string(key) == "tree_arena") return static_cast<int32_t>(tree_lds(1));

@@ -339,14 +339,15 @@ __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
 // string payload -- are then contiguous ranges, staged into LDS by LDS-DMA in ONE round trip.
 // Phase S (bottom-up): the encoded size of every non-scalar entry (a struct's = its fixed part +
 // its children's; a list's = header + element slots + its elements' var parts, read as a
-// difference of the element node's in-tile prefix: one block scan per node under a list / map).
-// The measure pass stops here (row sizes).  The encode pass then places every value top-down in
-// a zeroed LDS image of the tile's output bytes: a row / struct thread writes its null bits and
-// slots and gives each var child its position; an element finds its list by binary search over
-// the staged offsets and writes its own slot and null bit; a string copies its staged payload.
+// difference of the element node's in-tile prefix: one block scan per level over the nodes below a
+// list / map).  The measure pass stops here (row sizes).  The encode pass then places every value
+// top-down in a zeroed LDS image of the tile's output bytes: a row / struct thread writes its null
+// bits and slots and gives each var child its position; an element finds its list by binary search
+// over the staged offsets and writes its own slot and null bit; a string copies its staged payload.
+// Every phase spreads ALL (node, entry) pairs of a level over the workgroup (node records in LDS).
 // The image leaves as one contiguous range.  Tiles whose inputs + arrays + image do not fit the
 // LDS budget are walked in halves; a single row that does not fit is encoded by the row
-// interpreter above, straight to HBM.
+// interpreter above (te_fixup_kernel), straight to HBM.
 struct TENode {
   const uint8_t* values;
   const uint8_t* validity;
@@ -358,7 +359,7 @@ struct TENode {
   int32_t ord;              // index among the parent's children
   int32_t width;            // scalar bytes (BOOL: 1), -1 otherwise
   int32_t esize;            // slot bytes as an array element
-  int32_t pad_;
+  int32_t level;
 };
 
 constexpr int kTEMaxLevels = 64;
@@ -376,24 +377,35 @@ struct TEArgs {
   int32_t tile_rows;
   uint32_t lds_cap;
   uint32_t* fallback;       // bit r: row r is left to te_fixup_kernel (zeroed by the launcher)
+  uint64_t* dbg;            // diagnostics (tuning "tree_debug"): phase times, or NULL
+  uint32_t* err;            // the stream's device error slot
+  int32_t deep;             // nested deeper than the row interpreter unrolls
+  int32_t pad_;
   int32_t level_start[kTEMaxLevels + 1];
+  int32_t nelem[kTEMaxLevels];   // per level: non-scalar LIST / MAP elements (first in `ord`)
 };
+
+#define TEMARK(sh, id)                                                             \
+  do {                                                                             \
+    if ((sh).tacc && threadIdx.x == 0) {                                           \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                        \
+      (sh).tacc[id] += t_ - (sh).tacc[15];                                         \
+      (sh).tacc[15] = t_;                                                          \
+    }                                                                              \
+  } while (0)
 
 struct EMeta {
   int64_t lo;               // first Arrow entry of the node in the (sub-)tile
   int64_t plo;              // STRING / BINARY: first payload byte (offsets[lo])
+  int64_t phi;              // STRING / BINARY: payload end (offsets[lo + cnt])
   uint32_t cnt;             // entries in the (sub-)tile
   uint32_t vst, ost, pst;   // LDS: validity byte lo / 8, offsets[lo], values / payload start
   uint32_t S;               // LDS: sizes -> prefixes -> positions (non-scalar nodes), cnt + 1
   uint32_t X;               // LDS: LIST: element var base; MAP: + value array pos, value var base
-  int64_t phi;              // STRING / BINARY: payload end (offsets[lo + cnt])
 };
 
 constexpr uint32_t kTNone = 0xffffffffu;
 constexpr uint32_t kTDead = 0xffffffffu;
-
-using CTENode = __attribute__((address_space(4))) const TENode;
-__device__ __forceinline__ CTENode& te(const TEArgs& a, int n) { return ((CTENode*)(a.nodes))[n]; }
 
 __device__ __forceinline__ bool te_scalar(int t) { return gwidth(t) > 0; }
 __device__ __forceinline__ uint32_t r8u(uint32_t n) { return (n + 7) & ~7u; }
@@ -429,8 +441,7 @@ __device__ __forceinline__ uint64_t te_wscan(uint64_t x) {
   return x;
 }
 
-// Exclusive scan of uint32 a[0, m) (LDS) by the block; a[m - 1] is the node's trailing 0 slot, so
-// afterwards a[m - 1] = the total.
+// Exclusive scan of uint32 a[0, m) (LDS) by the block (thread t owns a contiguous chunk).
 __device__ void te_block_scan(uint32_t* a, uint32_t m, uint64_t* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t per = (m + kTEThreads - 1) / kTEThreads;
@@ -477,8 +488,8 @@ __device__ __forceinline__ uint64_t te_value(const uint8_t* pool, const EMeta& m
 }
 
 // Encoded size of entry q of non-scalar node n (children's sizes / prefixes already in place).
-__device__ uint32_t te_size(const TEArgs& a, const uint8_t* pool, const EMeta* meta, int n, int64_t q) {
-  CTENode& N = te(a, n);
+__device__ uint32_t te_size(const TENode* D, const uint8_t* pool, const EMeta* meta, int n, int64_t q) {
+  const TENode& N = D[n];
   const EMeta& M = meta[n];
   if (!te_valid(pool, M, q, N.validity)) return 0;
   switch (N.type) {
@@ -492,7 +503,7 @@ __device__ uint32_t te_size(const TEArgs& a, const uint8_t* pool, const EMeta* m
       uint32_t sz = bmu(nc) + 8 * nc;
       for (int k = 0; k < nc; k++) {
         const int c = N.first_child + k;
-        if (te_scalar(te(a, c).type)) continue;
+        if (te_scalar(D[c].type)) continue;
         sz += reinterpret_cast<const uint32_t*>(pool + meta[c].S)[q];
       }
       return sz;
@@ -504,7 +515,7 @@ __device__ uint32_t te_size(const TEArgs& a, const uint8_t* pool, const EMeta* m
       uint32_t sz = N.type == FURY_TYPE_MAP ? 8 : 0;
       for (int k = 0; k < (N.type == FURY_TYPE_MAP ? 2 : 1); k++) {
         const int c = N.first_child + k;
-        CTENode& C = te(a, c);
+        const TENode& C = D[c];
         sz += 8 + bmu(m) + r8u(m * C.esize);
         if (!te_scalar(C.type)) {
           const uint32_t* P = reinterpret_cast<const uint32_t*>(pool + meta[c].S);
@@ -520,18 +531,19 @@ __device__ uint32_t te_size(const TEArgs& a, const uint8_t* pool, const EMeta* m
 }
 
 // The unpadded size a slot records for a non-null value at entry q of node n with encoded size sz.
-__device__ __forceinline__ uint32_t te_raw(const TEArgs& a, const uint8_t* pool, const EMeta* meta,
+__device__ __forceinline__ uint32_t te_raw(const TENode* D, const uint8_t* pool, const EMeta* meta,
                                            int n, int64_t q, uint32_t sz) {
-  const int t = te(a, n).type;
+  const int t = D[n].type;
   if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY)
     return static_cast<uint32_t>(te_off(pool, meta[n], q + 1) - te_off(pool, meta[n], q));
   return sz;
 }
 
-// A struct-like container (a row: n = -1, or entry q of STRUCT node n) at image position pos:
-// null bits and slots of its children; non-scalar children get their positions (in place of
-// their sizes, kTDead when null).  lim = image bytes (writes past it are dropped).
-__device__ void te_put_struct(const TEArgs& a, uint8_t* pool, const EMeta* meta, uint8_t* img,
+// A struct-like container (a row: children = the top-level fields, or entry q of a STRUCT node)
+// at image position pos: null bits and slots of its children; non-scalar children get their
+// positions (in place of their sizes; kTDead when null / dead).  lim = image bytes (writes past it
+// are dropped).
+__device__ void te_put_struct(const TENode* D, uint8_t* pool, const EMeta* meta, uint8_t* img,
                               uint32_t lim, int fc, int nc, int64_t q, uint32_t pos, bool dead) {
   const uint32_t fixed = bmu(nc) + 8 * nc;
   uint32_t run = pos + fixed;
@@ -540,7 +552,7 @@ __device__ void te_put_struct(const TEArgs& a, uint8_t* pool, const EMeta* meta,
     uint64_t nulls = 0;
     for (int k = 64 * w; k < min(nc, 64 * w + 64); k++) {
       const int c = fc + k;
-      CTENode& C = te(a, c);
+      const TENode& C = D[c];
       const bool valid = !dead && te_valid(pool, meta[c], q, C.validity);
       if (!valid) nulls |= 1ull << (k - 64 * w);
       uint64_t slot = 0;
@@ -550,7 +562,7 @@ __device__ void te_put_struct(const TEArgs& a, uint8_t* pool, const EMeta* meta,
         uint32_t* S = reinterpret_cast<uint32_t*>(pool + meta[c].S);
         const uint32_t sz = S[q];
         if (valid) {
-          slot = (static_cast<uint64_t>(run - pos) << 32) | te_raw(a, pool, meta, c, q, sz);
+          slot = (static_cast<uint64_t>(run - pos) << 32) | te_raw(D, pool, meta, c, q, sz);
           S[q] = run;
           run += sz;
         } else {
@@ -583,24 +595,64 @@ __device__ __forceinline__ void te_store_w(uint8_t* p, int w, uint64_t v) {
   }
 }
 
-// Walks rows [s0, s1).  Returns false when the LDS budget does not hold it.
+// Slot k of a level's flattened (node, entry) list: cum[k] - cum[0] <= i < cum[k + 1] - cum[0].
+__device__ __forceinline__ int te_item(const uint32_t* cum, int nk, uint32_t i) {
+  const uint32_t x = i + cum[0];
+  int lo = 0, hi = nk;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cum[mid] <= x) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// LDS working set of te_kernel: [node records][layout order][meta][wsum, wtot][ex][diag][pool].
+constexpr int kTEScans = 7;
+struct TEShared {
+  TENode* D;
+  int32_t* ord;             // layout order: level by level, each level's non-scalar elements of a
+                            // LIST / MAP first (their size arrays are one scanned block), then its
+                            // other non-scalar nodes, then its scalars
+  EMeta* meta;
+  uint64_t* wsum;
+  uint32_t* wtot;
+  uint32_t* ex;             // [kTEScans][nn + 1] layout scans over `ord`
+  uint8_t* pool;
+  uint64_t* tacc;           // diagnostics: 16 phase accumulators (NULL when off)
+};
+
+__host__ __device__ inline size_t te_lds_head(int nn) {
+  size_t b = (sizeof(TENode) + 4 + sizeof(EMeta)) * static_cast<size_t>(nn);
+  b = (b + 7) & ~size_t(7);
+  b += 64 + 4 * kTEScans * (kTEThreads / 64);            // wsum, wtot
+  b += 4 * kTEScans * static_cast<size_t>(nn + 1);        // ex
+  b = (b + 7) & ~size_t(7);
+  b += 128;                                               // diagnostics
+  return (b + 15) & ~size_t(15);
+}
+
+// Walks rows [s0, s1).  Returns false when the LDS budget does not hold it (uniform).
 template <bool kWrite>
-__device__ bool te_walk(const TEArgs& a, EMeta* meta, uint64_t* wsum, uint8_t* pool, int64_t s0,
-                        int64_t s1) {
+__device__ bool te_walk(const TEArgs& a, const TEShared& sh, int64_t s0, int64_t s1) {
   const int tid = threadIdx.x;
   const uint32_t nr = static_cast<uint32_t>(s1 - s0);
+  const TENode* D = sh.D;
+  EMeta* meta = sh.meta;
+  uint8_t* pool = sh.pool;
+  const int nn = a.nn;
+  TEMARK(sh, 7);
   // ---- R: entry ranges, top-down (a thread per node of the level)
   for (int L = 0; L < a.nlevels; L++) {
     const int nb = a.level_start[L], ne = a.level_start[L + 1];
     for (int n = nb + tid; n < ne; n += kTEThreads) {
-      const TENode N = a.nodes[n];
+      const TENode& N = D[n];
       int64_t lo, cnt;
       if (L == 0) {
         lo = s0;
         cnt = nr;
       } else {
         const EMeta& P = meta[N.parent];
-        const TENode& PN = a.nodes[N.parent];
+        const TENode& PN = D[N.parent];
         if (PN.type == FURY_TYPE_STRUCT) {
           lo = P.lo;
           cnt = P.cnt;
@@ -618,99 +670,166 @@ __device__ bool te_walk(const TEArgs& a, EMeta* meta, uint64_t* wsum, uint8_t* p
     }
     __syncthreads();
   }
-  // ---- stage the inputs (uniform allocation, every thread issues its share of every copy)
-  uint32_t at = 0;
+  TEMARK(sh, 0);
+  // ---- layout of everything the walk keeps in LDS: block scans over the nodes (in `ord`) of the
+  // staged validity / offsets / values pieces, the size and LIST / MAP extra arrays, and each
+  // level's size-phase (S) and position-phase (P) entries
   const uint32_t cap = a.lds_cap;
-  for (int n = 0; n < a.nn; n++) {
-    CTENode& N = te(a, n);
-    EMeta& M = meta[n];
-    const int64_t lo = M.lo, cnt = M.cnt;
-    uint32_t vst = kTNone, ost = kTNone, pst = kTNone;
+  const int32_t* ord = sh.ord;
+  auto stage_span = [&](const uint8_t* gb, const uint8_t* ge) -> uint32_t {
+    if (ge <= gb) return 0u;
+    const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
+    const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
+    return static_cast<uint32_t>(hi - lo);
+  };
+  auto value_span = [&](const TENode& N, const EMeta& M, const uint8_t** gb, const uint8_t** ge) {
     const int t = N.type;
-    if (cnt > 0) {
-      if (N.validity) {
-        vst = te_stage(pool, at, cap, N.validity + (lo >> 3), N.validity + ((lo + cnt + 7) >> 3));
-        if (vst == kTNone) return false;
+    const int64_t lo = M.lo, cnt = M.cnt;
+    *gb = *ge = nullptr;
+    if (cnt == 0) return;
+    if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY) {
+      *gb = N.values + M.plo;
+      *ge = N.values + M.phi;
+    } else if (t == FURY_TYPE_BOOL) {
+      *gb = N.values + (lo >> 3);
+      *ge = N.values + ((lo + cnt + 7) >> 3);
+    } else if (t == FURY_TYPE_DECIMAL) {
+      *gb = N.values + 16 * lo;
+      *ge = N.values + 16 * (lo + cnt);
+    } else if (N.width > 0) {
+      *gb = N.values + N.width * lo;
+      *ge = N.values + N.width * (lo + cnt);
+    }
+  };
+  uint32_t* ex = sh.ex;
+  const int M1 = nn + 1;
+  block_scan_k<kTEThreads, kTEScans>(nn, [&](int j, int k) -> uint32_t {
+    const int n = ord[j];
+    const TENode& N = D[n];
+    const EMeta& M = meta[n];
+    const int t = N.type;
+    const uint32_t cnt = M.cnt;
+    const bool sc = te_scalar(t);
+    switch (k) {
+      case 0:
+        return cnt && N.validity ? stage_span(N.validity + (M.lo >> 3), N.validity + ((M.lo + cnt + 7) >> 3)) : 0u;
+      case 1:
+        return cnt && (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST ||
+                       t == FURY_TYPE_MAP)
+                   ? stage_span(reinterpret_cast<const uint8_t*>(N.offsets + M.lo),
+                                reinterpret_cast<const uint8_t*>(N.offsets + M.lo + cnt + 1))
+                   : 0u;
+      case 2: {
+        if (!kWrite) return 0u;
+        const uint8_t *gb, *ge;
+        value_span(N, M, &gb, &ge);
+        return stage_span(gb, ge);
       }
-      if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY || t == FURY_TYPE_LIST || t == FURY_TYPE_MAP) {
-        ost = te_stage(pool, at, cap, reinterpret_cast<const uint8_t*>(N.offsets + lo),
-                       reinterpret_cast<const uint8_t*>(N.offsets + lo + cnt + 1));
-        if (ost == kTNone) return false;
-      }
-      if (kWrite) {
-        if (t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY)
-          pst = te_stage(pool, at, cap, N.values + M.plo, N.values + M.phi);
-        else if (t == FURY_TYPE_BOOL)
-          pst = te_stage(pool, at, cap, N.values + (lo >> 3), N.values + ((lo + cnt + 7) >> 3));
-        else if (t == FURY_TYPE_DECIMAL)
-          pst = te_stage(pool, at, cap, N.values + 16 * lo, N.values + 16 * (lo + cnt));
-        else if (N.width > 0)
-          pst = te_stage(pool, at, cap, N.values + N.width * lo, N.values + N.width * (lo + cnt));
-        if (pst == kTNone && t != FURY_TYPE_STRUCT && t != FURY_TYPE_LIST && t != FURY_TYPE_MAP)
-          return false;
+      case 3:
+        return sc ? 0u : 4 * (cnt + 1);
+      case 4:
+        return kWrite && (t == FURY_TYPE_LIST || t == FURY_TYPE_MAP) ? 4 * cnt * (t == FURY_TYPE_MAP ? 3 : 1) : 0u;
+      case 5:
+        return sc ? 0u : cnt;
+      default: {
+        const bool elem = N.parent >= 0 && (D[N.parent].type == FURY_TYPE_LIST || D[N.parent].type == FURY_TYPE_MAP);
+        return (!sc || elem) ? cnt : 0u;
       }
     }
-    if (tid == 0) {
-      M.vst = vst;
-      M.ost = ost;
-      M.pst = pst;
-    }
-  }
-  // ---- arrays: sizes (+1 slot), LIST / MAP extras
-  for (int n = 0; n < a.nn; n++) {
-    CTENode& N = te(a, n);
-    const uint32_t cnt = meta[n].cnt;
-    uint32_t S = kTNone, X = kTNone;
-    if (!te_scalar(N.type)) {
-      if (at + 4 * (cnt + 1) > cap) return false;
-      S = at;
-      at += (4 * (cnt + 1) + 15) & ~15u;
-    }
-    if (kWrite && (N.type == FURY_TYPE_LIST || N.type == FURY_TYPE_MAP)) {
-      const uint32_t need = 4 * cnt * (N.type == FURY_TYPE_MAP ? 3 : 1);
-      if (at + need > cap) return false;
-      X = at;
-      at += (need + 15) & ~15u;
-    }
-    if (tid == 0) {
-      meta[n].S = S;
-      meta[n].X = X;
-    }
-  }
-  // ---- the image of the tile's output bytes (encode)
-  uint32_t img_at = 0, lim = 0;
+  }, ex, sh.wtot);
+  const uint32_t vbase = 0, obase = ex[0 * M1 + nn], pbase = obase + ex[1 * M1 + nn];
+  const uint32_t sbase = (pbase + ex[2 * M1 + nn] + 15) & ~15u;
+  const uint32_t xbase = (sbase + ex[3 * M1 + nn] + 15) & ~15u;
+  const uint32_t img_at = (xbase + ex[4 * M1 + nn] + 15) & ~15u;
+  uint32_t lim = 0;
   if (kWrite) {
-    const int64_t b0 = gl(a.offs)[s0], b1 = gl(a.offs)[s1];
-    const int64_t bytes = b1 - b0;
-    if (bytes < 0 || at + bytes + 16 > cap) return false;
-    img_at = at;
+    const int64_t bytes = gl(a.offs)[s1] - gl(a.offs)[s0];
+    if (bytes < 0 || img_at + bytes + 16 > cap) return false;
     lim = static_cast<uint32_t>(bytes);
+  } else if (img_at > cap) {
+    return false;
+  }
+  // meta of every node; its staged pieces issued by one wave
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int j = tid; j < nn; j += kTEThreads) {
+    const int n = ord[j];
+    EMeta& M = meta[n];
+    M.S = sbase + ex[3 * M1 + j];
+    M.X = xbase + ex[4 * M1 + j];
+  }
+  for (int j = wave; j < nn; j += kTEThreads / 64) {
+    const int n = ord[j];
+    const TENode& N = D[n];
+    EMeta& M = meta[n];
+    const uint32_t off[3] = {vbase + ex[0 * M1 + j], obase + ex[1 * M1 + j], pbase + ex[2 * M1 + j]};
+    const uint8_t* gb[3] = {nullptr, nullptr, nullptr};
+    const uint8_t* ge[3] = {nullptr, nullptr, nullptr};
+    if (M.cnt && N.validity) {
+      gb[0] = N.validity + (M.lo >> 3);
+      ge[0] = N.validity + ((M.lo + M.cnt + 7) >> 3);
+    }
+    if (M.cnt && (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY || N.type == FURY_TYPE_LIST ||
+                  N.type == FURY_TYPE_MAP)) {
+      gb[1] = reinterpret_cast<const uint8_t*>(N.offsets + M.lo);
+      ge[1] = reinterpret_cast<const uint8_t*>(N.offsets + M.lo + M.cnt + 1);
+    }
+    if (kWrite) value_span(N, M, &gb[2], &ge[2]);
+    uint32_t at3[3];
+#pragma unroll
+    for (int g = 0; g < 3; g++) {
+      at3[g] = kTNone;
+      if (!gb[g] || ge[g] <= gb[g]) {
+        if (gb[g]) at3[g] = off[g];             // empty range: never read
+        continue;
+      }
+      const uint64_t lo = reinterpret_cast<uint64_t>(gb[g]) & ~uint64_t(15);
+      const uint32_t nch = stage_span(gb[g], ge[g]) >> 4;
+      for (uint32_t i = lane; i < nch; i += 64)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * i),
+                                         pool + off[g] + 16 * i, 16, 0, 0);
+      at3[g] = off[g] + static_cast<uint32_t>(reinterpret_cast<uint64_t>(gb[g]) - lo);
+    }
+    if (lane == 0) {
+      M.vst = at3[0];
+      M.ost = at3[1];
+      M.pst = at3[2];
+    }
+  }
+  if (kWrite) {
     using v4 = __attribute__((ext_vector_type(4))) uint32_t;
     for (uint32_t i = 16 * tid; i < ((lim + 15) & ~15u); i += 16 * kTEThreads)
       *reinterpret_cast<v4*>(pool + img_at + i) = v4{0, 0, 0, 0};
   }
-  __syncthreads();                               // staged inputs landed, meta visible
+  TEMARK(sh, 1);
+  __syncthreads();                               // staged inputs landed, meta and lists visible
+  TEMARK(sh, 2);
   uint8_t* img = pool + img_at;
-  // ---- S: sizes bottom-up; prefixes of the nodes below a LIST / MAP
+  // ---- S: sizes bottom-up (all non-scalar entries of a level at once); prefixes of the nodes
+  // below a LIST / MAP (one scan per level)
   for (int L = a.nlevels - 1; L >= 0; L--) {
-    const int nb = a.level_start[L], ne = a.level_start[L + 1];
-    for (int n = nb; n < ne; n++) {
-      if (te_scalar(te(a, n).type)) continue;
-      const EMeta M = meta[n];
-      uint32_t* S = reinterpret_cast<uint32_t*>(pool + M.S);
-      for (uint32_t q = tid; q < M.cnt; q += kTEThreads) S[q] = te_size(a, pool, meta, n, q);
-      if (tid == 0) S[M.cnt] = 0;
+    const int j0 = a.level_start[L], j1 = a.level_start[L + 1];
+    const uint32_t* cum = ex + 5 * M1;
+    const uint32_t c0 = cum[j0], W = cum[j1] - c0;
+    for (uint32_t i = tid; i < W; i += kTEThreads) {
+      const int j = j0 + te_item(cum + j0, j1 - j0, i);
+      const int n = ord[j];
+      const uint32_t q = i + c0 - cum[j];
+      uint32_t* S = reinterpret_cast<uint32_t*>(pool + meta[n].S);
+      S[q] = te_size(D, pool, meta, n, q);
+      if (q + 1 == meta[n].cnt) S[q + 1] = 0;
+    }
+    for (int j = j0 + tid; j < j1; j += kTEThreads) {
+      const int n = ord[j];
+      if (!te_scalar(D[n].type) && meta[n].cnt == 0) reinterpret_cast<uint32_t*>(pool + meta[n].S)[0] = 0;
     }
     __syncthreads();
-    if (L == 0) break;
-    for (int n = nb; n < ne; n++) {
-      CTENode& N = te(a, n);
-      if (te_scalar(N.type)) continue;
-      const int pt = te(a, N.parent).type;
-      if (pt != FURY_TYPE_LIST && pt != FURY_TYPE_MAP) continue;
-      te_block_scan(reinterpret_cast<uint32_t*>(pool + meta[n].S), meta[n].cnt + 1, wsum);
+    const int ne = a.nelem[L];                  // the level's first ne slots: elements, one block
+    if (L > 0 && ne > 0) {
+      const uint32_t b0 = ex[3 * M1 + j0], b1 = ex[3 * M1 + j0 + ne];
+      if (b1 > b0) te_block_scan(reinterpret_cast<uint32_t*>(pool + sbase + b0), (b1 - b0) / 4, sh.wsum);
     }
   }
+  TEMARK(sh, 3);
   // ---- row sizes (measure) / row containers (encode)
   for (uint32_t r = tid; r < nr; r += kTEThreads) {
     if (!kWrite) {
@@ -720,129 +839,130 @@ __device__ bool te_walk(const TEArgs& a, EMeta* meta, uint64_t* wsum, uint8_t* p
       } else {
         sz = bmu(a.ntop) + 8ull * a.ntop;
         for (int k = 0; k < a.ntop; k++)
-          if (!te_scalar(te(a, k).type)) sz += reinterpret_cast<const uint32_t*>(pool + meta[k].S)[r];
+          if (!te_scalar(D[k].type)) sz += reinterpret_cast<const uint32_t*>(pool + meta[k].S)[r];
       }
       a.sizes[s0 + r] = static_cast<int64_t>(sz);
     } else {
       const int64_t b0 = gl(a.offs)[s0];
       const uint32_t pos = static_cast<uint32_t>(gl(a.offs)[s0 + r] - b0);
       if (a.root) reinterpret_cast<uint32_t*>(pool + meta[0].S)[r] = pos;
-      else te_put_struct(a, pool, meta, img, lim, 0, a.ntop, r, pos, false);
+      else te_put_struct(D, pool, meta, img, lim, 0, a.ntop, r, pos, false);
     }
   }
+  TEMARK(sh, 4);
   if (!kWrite) return true;
   __syncthreads();
-  // ---- positions + contents, top-down
+  // ---- positions + contents, top-down (all element / non-scalar entries of a level at once)
   for (int L = 0; L < a.nlevels; L++) {
-    const int nb = a.level_start[L], ne = a.level_start[L + 1];
-    for (int n = nb; n < ne; n++) {
-      CTENode& N = te(a, n);
-      const EMeta M = meta[n];
+    const int j0 = a.level_start[L], j1 = a.level_start[L + 1];
+    const uint32_t* cum = ex + 6 * M1;
+    const uint32_t c0 = cum[j0], W = cum[j1] - c0;
+    for (uint32_t i = tid; i < W; i += kTEThreads) {
+      const int j = j0 + te_item(cum + j0, j1 - j0, i);
+      const int n = ord[j];
+      const uint32_t q = i + c0 - cum[j];
+      const TENode& N = D[n];
+      const EMeta& M = meta[n];
       const bool scalar = te_scalar(N.type);
-      const int pt = L == 0 ? -1 : te(a, N.parent).type;
+      const int pt = L == 0 ? -1 : D[N.parent].type;
       const bool elem = pt == FURY_TYPE_LIST || pt == FURY_TYPE_MAP;
-      if (scalar && !elem) continue;              // written by the row / struct thread
       uint32_t* S = scalar ? nullptr : reinterpret_cast<uint32_t*>(pool + M.S);
-      const EMeta PM = L == 0 ? M : meta[N.parent];
-      for (uint32_t q = tid; q < M.cnt; q += kTEThreads) {
-        uint32_t pos = scalar ? kTDead : S[q];
-        if (elem) {                                // an element: its own slot in the parent array
-          const int32_t* O = reinterpret_cast<const int32_t*>(pool + PM.ost);
-          const int64_t g = M.lo + q;
-          const uint32_t e = te_owner(O, PM.cnt, g);
-          const uint32_t j = static_cast<uint32_t>(g - O[e]);
-          const uint32_t m = static_cast<uint32_t>(O[e + 1] - O[e]);
-          const uint32_t ppos = reinterpret_cast<const uint32_t*>(pool + PM.S)[e];
-          const uint32_t* PX = reinterpret_cast<const uint32_t*>(pool + PM.X);
-          pos = kTDead;
-          if (ppos != kTDead) {
-            const uint32_t arr = pt == FURY_TYPE_LIST ? ppos : (N.ord == 0 ? ppos + 8 : PX[PM.cnt + e]);
-            const bool valid = te_valid(pool, M, q, N.validity);
-            const uint32_t sl = arr + 8 + bmu(m) + static_cast<uint32_t>(N.esize) * j;
-            if (!valid) {
-              if (arr + 8 + (j >> 3) < lim)
-                atomicOr(reinterpret_cast<uint32_t*>(img + arr + 8) + (j >> 5), 1u << (j & 31));
-            } else if (scalar) {
-              if (sl + N.esize <= lim) te_store_w(img + sl, N.esize, te_value(pool, M, N.type, N.width, q));
-            } else {
-              const uint32_t base = N.ord == 0 ? PX[e] : PX[2 * PM.cnt + e];
-              const uint32_t sz = te_size(a, pool, meta, n, q);
-              pos = base + S[q];
-              const uint64_t slot = (static_cast<uint64_t>(pos - arr) << 32) | te_raw(a, pool, meta, n, q, sz);
-              if (sl + 8 <= lim) *reinterpret_cast<uint64_t*>(img + sl) = slot;
+      uint32_t pos = scalar ? kTDead : S[q];
+      if (elem) {                                // an element: its own slot in the parent array
+        const EMeta& PM = meta[N.parent];
+        const int32_t* O = reinterpret_cast<const int32_t*>(pool + PM.ost);
+        const int64_t g = M.lo + q;
+        const uint32_t e = te_owner(O, PM.cnt, g);
+        const uint32_t j = static_cast<uint32_t>(g - O[e]);
+        const uint32_t m = static_cast<uint32_t>(O[e + 1] - O[e]);
+        const uint32_t ppos = reinterpret_cast<const uint32_t*>(pool + PM.S)[e];
+        const uint32_t* PX = reinterpret_cast<const uint32_t*>(pool + PM.X);
+        pos = kTDead;
+        if (ppos != kTDead) {
+          const uint32_t arr = pt == FURY_TYPE_LIST ? ppos : (N.ord == 0 ? ppos + 8 : PX[PM.cnt + e]);
+          const bool valid = te_valid(pool, M, q, N.validity);
+          const uint32_t sl = arr + 8 + bmu(m) + static_cast<uint32_t>(N.esize) * j;
+          if (!valid) {
+            if (arr + 8 + (j >> 3) < lim)
+              atomicOr(reinterpret_cast<uint32_t*>(img + arr + 8) + (j >> 5), 1u << (j & 31));
+          } else if (scalar) {
+            if (sl + N.esize <= lim) te_store_w(img + sl, N.esize, te_value(pool, M, N.type, N.width, q));
+          } else {
+            const uint32_t base = N.ord == 0 ? PX[e] : PX[2 * PM.cnt + e];
+            const uint32_t sz = te_size(D, pool, meta, n, q);
+            pos = base + S[q];
+            const uint64_t slot = (static_cast<uint64_t>(pos - arr) << 32) | te_raw(D, pool, meta, n, q, sz);
+            if (sl + 8 <= lim) *reinterpret_cast<uint64_t*>(img + sl) = slot;
+          }
+        }
+        if (scalar) continue;
+        S[q] = pos;                              // (only this thread reads S[q] at this level)
+      }
+      if (pos == kTDead) {                       // a null / dead struct: its children are dead
+        if (N.type == FURY_TYPE_STRUCT)
+          te_put_struct(D, pool, meta, img, lim, N.first_child, N.num_children, q, 0, true);
+        continue;
+      }
+      switch (N.type) {
+        case FURY_TYPE_STRING:
+        case FURY_TYPE_BINARY: {
+          const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
+          const uint8_t* src = pool + M.pst + (o0 - M.plo);
+          const uint32_t len = static_cast<uint32_t>(o1 - o0);
+          if (pos + len <= lim)
+            for (uint32_t b = 0; b < len; b++) img[pos + b] = src[b];
+          break;
+        }
+        case FURY_TYPE_DECIMAL: {
+          const uint8_t* src = pool + M.pst + 16 * q;
+          if (pos + 16 <= lim)
+            for (int b = 0; b < 16; b++) img[pos + b] = src[b];
+          break;
+        }
+        case FURY_TYPE_STRUCT:
+          te_put_struct(D, pool, meta, img, lim, N.first_child, N.num_children, q, pos, false);
+          break;
+        case FURY_TYPE_LIST:
+        case FURY_TYPE_MAP: {
+          const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
+          const uint32_t m = static_cast<uint32_t>(o1 - o0);
+          uint32_t* X = reinterpret_cast<uint32_t*>(pool + M.X);
+          uint32_t arr = N.type == FURY_TYPE_MAP ? pos + 8 : pos;
+          for (int kk = 0; kk < (N.type == FURY_TYPE_MAP ? 2 : 1); kk++) {
+            const int c = N.first_child + kk;
+            const TENode& C = D[c];
+            const uint32_t hdr = 8 + bmu(m) + r8u(m * C.esize);
+            if (arr + 8 <= lim) *reinterpret_cast<uint64_t*>(img + arr) = m;
+            uint32_t var = 0;
+            if (!te_scalar(C.type)) {
+              const uint32_t* P = reinterpret_cast<const uint32_t*>(pool + meta[c].S);
+              const int64_t b = o0 - meta[c].lo;
+              X[kk == 0 ? q : 2 * M.cnt + q] = arr + hdr - P[b];
+              var = P[b + m] - P[b];
+            }
+            if (kk == 0 && N.type == FURY_TYPE_MAP) {
+              const uint32_t kbytes = hdr + var;
+              if (pos + 8 <= lim) *reinterpret_cast<uint64_t*>(img + pos) = kbytes;
+              arr = pos + 8 + kbytes;
+              X[M.cnt + q] = arr;
             }
           }
-          if (scalar) continue;
-          S[q] = pos;                              // (only this thread reads S[q] at this level)
+          break;
         }
-        if (pos == kTDead) {                       // a null / dead struct: its children are dead
-          if (N.type == FURY_TYPE_STRUCT)
-            te_put_struct(a, pool, meta, img, lim, N.first_child, N.num_children, q, 0, true);
-          continue;
-        }
-        switch (N.type) {
-          case FURY_TYPE_STRING:
-          case FURY_TYPE_BINARY: {
-            const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
-            const uint8_t* src = pool + M.pst + (o0 - M.plo);
-            const uint32_t len = static_cast<uint32_t>(o1 - o0);
-            if (pos + len <= lim)
-              for (uint32_t i = 0; i < len; i++) img[pos + i] = src[i];
-            break;
-          }
-          case FURY_TYPE_DECIMAL: {
-            const uint8_t* src = pool + M.pst + 16 * q;
-            if (pos + 16 <= lim)
-              for (int i = 0; i < 16; i++) img[pos + i] = src[i];
-            break;
-          }
-          case FURY_TYPE_STRUCT:
-            te_put_struct(a, pool, meta, img, lim, N.first_child, N.num_children, q, pos, false);
-            break;
-          case FURY_TYPE_LIST:
-          case FURY_TYPE_MAP: {
-            const int64_t o0 = te_off(pool, M, q), o1 = te_off(pool, M, q + 1);
-            const uint32_t m = static_cast<uint32_t>(o1 - o0);
-            uint32_t* X = reinterpret_cast<uint32_t*>(pool + M.X);
-            uint32_t arr = pos;
-            if (N.type == FURY_TYPE_MAP) arr = pos + 8;
-            uint32_t kbytes = 0;
-            for (int k = 0; k < (N.type == FURY_TYPE_MAP ? 2 : 1); k++) {
-              const int c = N.first_child + k;
-              CTENode& C = te(a, c);
-              const uint32_t hdr = 8 + bmu(m) + r8u(m * C.esize);
-              if (arr + 8 <= lim) *reinterpret_cast<uint64_t*>(img + arr) = m;
-              uint32_t var = 0;
-              if (!te_scalar(C.type)) {
-                const uint32_t* P = reinterpret_cast<const uint32_t*>(pool + meta[c].S);
-                const int64_t b = o0 - meta[c].lo;
-                X[k == 0 ? q : 2 * M.cnt + q] = arr + hdr - P[b];
-                var = P[b + m] - P[b];
-              }
-              if (k == 0) {
-                kbytes = hdr + var;
-                if (N.type == FURY_TYPE_MAP) {
-                  if (pos + 8 <= lim) *reinterpret_cast<uint64_t*>(img + pos) = kbytes;
-                  arr = pos + 8 + kbytes;
-                  X[M.cnt + q] = arr;
-                }
-              }
-            }
-            break;
-          }
-          default:
-            break;
-        }
+        default:
+          break;
       }
     }
     __syncthreads();
   }
+  TEMARK(sh, 5);
   // ---- the image leaves as one contiguous range (bytes at or past cap are not written)
   const int64_t b0 = gl(a.offs)[s0];
   const int64_t end = min<int64_t>(static_cast<int64_t>(lim), a.cap - b0);
   const uint64_t* src = reinterpret_cast<const uint64_t*>(img);
   uint64_t* dst = reinterpret_cast<uint64_t*>(a.rows + b0);
   for (int64_t i = tid; i < (end >> 3); i += kTEThreads) __builtin_nontemporal_store(src[i], gl(dst) + i);
+  TEMARK(sh, 6);
   return true;
 }
 
@@ -852,6 +972,11 @@ template <bool kWrite, int kRoot>
 __global__ __launch_bounds__(kTEThreads) void te_fixup_kernel(TEArgs a) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kTEThreads + threadIdx.x;
   if (r >= a.nrows || !((gl(a.fallback)[r >> 5] >> (r & 31)) & 1)) return;
+  if (a.deep) {                                 // the interpreter cannot reach these levels
+    raise_at(a.err, kErrTooDeep, static_cast<uint64_t>(r));
+    if (!kWrite) a.sizes[r] = 0;
+    return;
+  }
   const GNodes gn = (GNodes)(a.gtab);
   if (!kWrite) a.sizes[r] = put_row<false, kRoot>(gn, a.ntop, r, static_cast<uint8_t*>(nullptr));
   else if (gl(a.offs)[r + 1] <= a.cap) put_row<true, kRoot>(gn, a.ntop, r, a.rows + gl(a.offs)[r]);
@@ -860,9 +985,36 @@ __global__ __launch_bounds__(kTEThreads) void te_fixup_kernel(TEArgs a) {
 template <bool kWrite, int kRoot>
 __global__ __launch_bounds__(kTEThreads) void te_kernel(TEArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tes[];
-  EMeta* meta = reinterpret_cast<EMeta*>(tes);
-  uint64_t* wsum = reinterpret_cast<uint64_t*>(tes + sizeof(EMeta) * a.nn);
-  uint8_t* pool = tes + ((sizeof(EMeta) * a.nn + 64 + 15) & ~size_t(15));
+  TEShared sh;
+  {
+    const int nn = a.nn;
+    uint8_t* p = tes;
+    sh.D = reinterpret_cast<TENode*>(p);
+    p += sizeof(TENode) * nn;
+    sh.ord = reinterpret_cast<int32_t*>(p);
+    p += 4 * nn;
+    p = tes + ((p - tes + 7) & ~size_t(7));
+    sh.meta = reinterpret_cast<EMeta*>(p);
+    p += sizeof(EMeta) * nn;
+    p = tes + ((p - tes + 7) & ~size_t(7));
+    sh.wsum = reinterpret_cast<uint64_t*>(p);
+    p += 64;
+    sh.wtot = reinterpret_cast<uint32_t*>(p);
+    p += 4 * kTEScans * (kTEThreads / 64);
+    sh.ex = reinterpret_cast<uint32_t*>(p);
+    p += 4 * kTEScans * (nn + 1);
+    p = tes + ((p - tes + 7) & ~size_t(7));
+    sh.tacc = a.dbg ? reinterpret_cast<uint64_t*>(p) : nullptr;
+    sh.pool = tes + te_lds_head(nn);
+  }
+  if (sh.tacc && threadIdx.x < 16)
+    sh.tacc[threadIdx.x] = threadIdx.x == 15 ? __builtin_amdgcn_s_memrealtime() : 0;
+  {
+    const int32_t* gord = reinterpret_cast<const int32_t*>(a.nodes + a.nn);
+    for (int n = threadIdx.x; n < a.nn; n += kTEThreads) sh.ord[n] = gord[n];
+  }
+  for (int n = threadIdx.x; n < a.nn; n += kTEThreads) sh.D[n] = a.nodes[n];
+  __syncthreads();
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile_rows;
   const int64_t r1 = min<int64_t>(r0 + a.tile_rows, a.nrows);
   // encode: sub-tiles whose OUTPUT bytes take at most ~40 % of the budget (inputs and arrays are
@@ -884,7 +1036,8 @@ __global__ __launch_bounds__(kTEThreads) void te_kernel(TEArgs a) {
     }
     bool ok = false;
     for (;;) {
-      ok = te_walk<kWrite>(a, meta, wsum, pool, s0, s1);
+      ok = te_walk<kWrite>(a, sh, s0, s1);
+      if (!ok) TEMARK(sh, 9);
       __syncthreads();
       if (ok || s1 - s0 == 1) break;
       s1 = s0 + (s1 - s0 + 1) / 2;
@@ -893,6 +1046,12 @@ __global__ __launch_bounds__(kTEThreads) void te_kernel(TEArgs a) {
       atomicOr(a.fallback + (s0 >> 5), 1u << (s0 & 31));
     s0 = s1;
   }
+  TEMARK(sh, 8);
+  if (sh.tacc && threadIdx.x < 15)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg) + (kWrite ? 48 : 32) + threadIdx.x,
+              static_cast<unsigned long long>(sh.tacc[threadIdx.x]));
+  if (sh.tacc && threadIdx.x == 15)
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg) + 66 + (kWrite ? 1 : 0), 1ull);
 }
 
 }  // namespace
@@ -925,8 +1084,12 @@ void gen_encode_root(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint
 }
 
 namespace {
-int g_tree_encode = 1;           // tuning "nested_encode": 0 tree tiles, 1 the row interpreter
+// tuning "nested_encode": 0 tree tiles (measure + encode), 1 the row interpreter (both), 2 tree
+// measure + interpreter encode (default: the fastest pair measured, scripts/ab_generic.py).
+// Schemas nested deeper than the interpreter unrolls (kGenMaxDepth) always take the tree tiles.
+int g_tree_encode = 2;
 uint32_t g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
+int g_te_rows[2] = {256, 256};                   // rows per workgroup tile: measure, encode
 
 int host_gwidth(int t) {
   switch (t) {
@@ -943,7 +1106,7 @@ int host_gwidth(int t) {
 int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
                        int64_t cap, hipStream_t stream) {
   const int nn = g.nnodes;
-  if (g_tree_encode != 0 || nn > 512 || nn <= 0) return 1;
+  if (nn > 256 || nn <= 0) return 1;
   const GenNode* hn = g.htab ? g.htab : g.node;
   std::vector<TENode> tab(nn);
   std::vector<int32_t> level(nn, 0);
@@ -959,6 +1122,7 @@ int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, ui
       t.parent = -1;
       t.ord = i;
     }
+    t.level = level[i];
     t.width = host_gwidth(t.type);
     t.esize = t.width > 0 ? t.width : 8;
     for (int j = 0; j < t.num_children; j++) {
@@ -969,15 +1133,43 @@ int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, ui
   }
   const int nlev = level[nn - 1] + 1;
   if (nlev > kTEMaxLevels) return 1;
+  const bool deep = nlev >= kGenMaxDepth;       // beyond the row interpreter
+  if (!deep && (g_tree_encode == 1 || (g_tree_encode == 2 && sizes == nullptr))) return 1;
   TEArgs a{};
+  a.deep = deep ? 1 : 0;
+  a.err = device_error_word(stream);
   a.level_start[0] = 0;
   for (int L = 1; L <= nlev; L++) {
     int i = a.level_start[L - 1];
     while (i < nn && level[i] < L) i++;
     a.level_start[L] = i;
   }
+  // layout order (TEShared.ord): per level, the non-scalar LIST / MAP elements first, then the
+  // other non-scalar nodes, then the scalars (BFS: a level's nodes are contiguous)
+  std::vector<int32_t> ord;
+  for (int L = 0; L < nlev; L++) {
+    const int b = a.level_start[L], e = a.level_start[L + 1];
+    auto elem = [&](int i) {
+      const int p = tab[i].parent;
+      return p >= 0 && (tab[p].type == FURY_TYPE_LIST || tab[p].type == FURY_TYPE_MAP);
+    };
+    int ne = 0;
+    for (int i = b; i < e; i++)
+      if (tab[i].width < 0 && elem(i)) {
+        ord.push_back(i);
+        ne++;
+      }
+    for (int i = b; i < e; i++)
+      if (tab[i].width < 0 && !elem(i)) ord.push_back(i);
+    for (int i = b; i < e; i++)
+      if (tab[i].width > 0) ord.push_back(i);
+    a.nelem[L] = ne;
+  }
+  std::vector<uint8_t> blob(tab.size() * sizeof(TENode) + 4 * ord.size());
+  memcpy(blob.data(), tab.data(), tab.size() * sizeof(TENode));
+  memcpy(blob.data() + tab.size() * sizeof(TENode), ord.data(), 4 * ord.size());
   DeviceTable dt, dg;
-  int st = upload_table(tab.data(), tab.size() * sizeof(TENode), stream, &dt);
+  int st = upload_table(blob.data(), blob.size(), stream, &dt);
   if (st) return st;
   const GenNode* gtab = g.tab;
   if (!gtab) {
@@ -997,9 +1189,10 @@ int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, ui
   a.ntop = g.ntop;
   a.root = g.root;
   a.nlevels = nlev;
-  a.tile_rows = kTEThreads;
+  a.tile_rows = g_te_rows[write ? 1 : 0];
+  a.dbg = tree_debug_buffer();
   a.lds_cap = g_te_lds[write ? 1 : 0];
-  const size_t lds = ((sizeof(EMeta) * nn + 64 + 15) & ~size_t(15)) + a.lds_cap;
+  const size_t lds = te_lds_head(nn) + a.lds_cap;
   const dim3 grid(static_cast<unsigned>((g.nrows + a.tile_rows - 1) / a.tile_rows));
   const int64_t fb_bytes = ((g.nrows + 31) / 32) * 4;
   void* fb = nullptr;
@@ -1031,6 +1224,8 @@ void set_tree_encode_mode(int v) { g_tree_encode = v; }
 int tree_encode_mode() { return g_tree_encode; }
 void set_tree_encode_lds(int which, uint32_t bytes) { g_te_lds[which ? 1 : 0] = (bytes + 15) & ~15u; }
 uint32_t tree_encode_lds(int which) { return g_te_lds[which ? 1 : 0]; }
+void set_tree_encode_rows(int which, int rows) { g_te_rows[which ? 1 : 0] = rows; }
+int tree_encode_rows(int which) { return g_te_rows[which ? 1 : 0]; }
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
   if (g.nrows > 0) {

@@ -104,11 +104,13 @@ struct VarArgs {
 //   [kErrBounds], [+2, +3]    a decode read that would leave the batch, and where (one 64-bit
 //                             word: a row, or bit 63 | node << 40 | entry) (FURY_ERR_OUT_OF_BOUNDS)
 //   [kErrMapCount], [+2, +3]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
+//   [kErrTooDeep], [+2, +3]   encode: a row too large for on-chip assembly in a schema nested
+//                             deeper than the row interpreter reaches (FURY_ERR_UNSUPPORTED)
 // device_error_word(stream) is the slot kernels launched on `stream` raise into (NULL if the runtime
 // cannot map host memory); take_device_error(stream) takes that slot only (flag exchanged first,
 // then its location) and sets the thread's last error when one was raised.
 constexpr int kErrWords = 16;
-constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8;
+constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12;
 uint32_t* device_error_word(hipStream_t stream);
 int take_device_error(hipStream_t stream);
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
@@ -142,6 +144,52 @@ __device__ __forceinline__ void raise_oob(uint32_t* err, int64_t row) {
 }
 __device__ __forceinline__ uint64_t err_where_entry(int node, int64_t entry) {
   return (1ull << 63) | (static_cast<uint64_t>(node) << 40) | static_cast<uint64_t>(entry);
+}
+
+// Exclusive block scans of K parallel sequences over the slots [0, m) by an NT-thread workgroup
+// (thread t owns a contiguous run): f(j, k) is slot j's value in sequence k; ex[k * (m + 1) + j]
+// receives the exclusive prefix and ex[k * (m + 1) + m] the total.  f is evaluated twice per
+// slot; wtot holds K * NT / 64 words.  Two barriers.  (Layouts of per-node arrays in the
+// tree-tile kernels: one parallel pass instead of a serial walk over the schema's nodes.)
+template <int NT, int K, class F>
+__device__ void block_scan_k(int m, F f, uint32_t* ex, uint32_t* wtot) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (m + NT - 1) / NT;
+  const int b = min(tid * per, m), e = min(b + per, m);
+  uint32_t sum[K], inc[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    sum[k] = 0;
+    for (int j = b; j < e; j++) sum[k] += f(j, k);
+    uint32_t x = sum[k];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    inc[k] = x;
+    if (lane == 63) wtot[k * NW + wave] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      const uint32_t v = wtot[k * NW + w];
+      pre += w < wave ? v : 0;
+      tot += v;
+    }
+    uint32_t run = pre + inc[k] - sum[k];
+    uint32_t* o = ex + k * (m + 1);
+    for (int j = b; j < e; j++) {
+      o[j] = run;
+      run += f(j, k);
+    }
+    if (tid == 0) o[m] = tot;
+  }
+  __syncthreads();
 }
 
 // Copies a host column table to device memory on `stream` (stream-ordered: through a pinned
@@ -217,6 +265,8 @@ void set_tree_encode_mode(int v);
 int tree_encode_mode();
 void set_tree_encode_lds(int which, uint32_t bytes);   // which: 0 measure, 1 encode
 uint32_t tree_encode_lds(int which);
+void set_tree_encode_rows(int which, int rows);        // tuning "tree_enc_rows" / "tree_measure_rows"
+int tree_encode_rows(int which);
 // Level-by-level nested decode (levels.hip): prepare = per-level count / scan / expand passes
 // (totals[2 i] entries, totals[2 i + 1] payload bytes of node i), execute = one write pass into
 // the outputs of gen_args' node table.
@@ -238,6 +288,10 @@ void set_tree_mode(int v);           // tuning "nested_decode": 0 tree tiles (de
 int tree_mode();
 void set_tree_lds(uint32_t stage, uint32_t arena);   // tuning "tree_stage" / "tree_arena" (bytes)
 uint32_t tree_lds(int which);
+int set_tree_debug(int on);          // tuning "tree_debug": phase accumulators on / off
+void set_tree_threads(int v);        // tuning "tree_threads": 256 / 512 / 1024
+int tree_threads();
+uint64_t* tree_debug_buffer();
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);
 void device_scan(int64_t* s, int64_t n, int64_t* total, int64_t* ws, hipStream_t stream);

@@ -71,8 +71,22 @@ struct TreeArgs {
   int32_t nn, ntop, root, nlevels;
   int32_t tile_rows;
   uint32_t stage_cap, arena_cap;
+  int32_t maxw;             // widest level (nodes)
+  int32_t pad_;
+  uint64_t* dbg;            // diagnostics (tuning "tree_debug"): phase times, or NULL
   int32_t level_start[kTreeMaxLevels + 1];
 };
+
+// Diagnostics: thread 0 of a workgroup adds the time since its previous mark to tacc[id]
+// (s_memrealtime, 100 MHz); the kernel adds tacc to dbg at the end.
+#define TMARK(sh, id)                                                              \
+  do {                                                                             \
+    if ((sh).tacc && threadIdx.x == 0) {                                           \
+      const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                        \
+      (sh).tacc[id] += t_ - (sh).tacc[15];                                         \
+      (sh).tacc[15] = t_;                                                          \
+    }                                                                              \
+  } while (0)
 
 namespace {
 
@@ -84,6 +98,7 @@ struct TMeta {
   uint32_t src;             // arena byte offset of its int64 source array (non-scalar nodes)
   uint32_t cnt;             // arena byte offset of its uint32 count / prefix array (+1 slot)
   uint32_t tot;             // in-tile total of the counts (elements / payload bytes)
+  uint32_t pad_;            // scanned count block value at the node's first slot (its base)
   int64_t run_e;            // pass 2: output entry base of the current sub-tile
   int64_t run_b;            // pass 2: payload byte base of the current sub-tile
 };
@@ -161,12 +176,13 @@ __device__ __forceinline__ int64_t tarray_ok(const Rows& R, int64_t p, int es, i
 }
 
 // Issues LDS-DMA copies of the 16-B pieces covering [gb, ge) to lds (16-aligned); returns nothing.
+template <int NT>
 __device__ __forceinline__ void tstage(uint8_t* lds, const uint8_t* gb, const uint8_t* ge) {
   const uint64_t lo = reinterpret_cast<uint64_t>(gb) & ~uint64_t(15);
   const uint64_t hi = (reinterpret_cast<uint64_t>(ge) + 15) & ~uint64_t(15);
   const uint32_t nch = static_cast<uint32_t>((hi - lo) >> 4);
   const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint32_t i0 = wave * 64; i0 < nch; i0 += kTreeThreads)
+  for (uint32_t i0 = wave * 64; i0 < nch; i0 += NT)
     if (i0 + lane < nch)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(lo + 16ull * (i0 + lane)),
                                        lds + 16 * i0, 16, 0, 0);
@@ -184,9 +200,10 @@ __device__ __forceinline__ uint64_t tw_scan64(uint64_t x) {
 
 // Exclusive scan of the uint32 array a[0, m) in LDS by the whole block (thread t owns a
 // contiguous chunk).  Returns false when the sum does not fit 32 bits (every thread agrees).
+template <int NT>
 __device__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t per = (m + kTreeThreads - 1) / kTreeThreads;
+  const uint32_t per = (m + NT - 1) / NT;
   const uint32_t b = min<uint32_t>(tid * per, m), e = min<uint32_t>(b + per, m);
   uint64_t s = 0;
   for (uint32_t i = b; i < e; i++) s += a[i];
@@ -195,7 +212,7 @@ __device__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t* wsum) {
   __syncthreads();
   uint64_t pre = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kTreeThreads / 64; w++) {
+  for (int w = 0; w < NT / 64; w++) {
     const uint64_t v = wsum[w];
     pre += w < wave ? v : 0;
     tot += v;
@@ -336,16 +353,56 @@ __device__ __forceinline__ uint32_t towner(const uint32_t* P, uint32_t m, uint32
   return lo;
 }
 
-// One walk of rows [s0, s1).  Returns false when the tile's arrays do not fit the arena.
-template <bool kWrite>
-__device__ bool tree_walk(const TreeArgs& a, TMeta* meta, uint64_t* wsum, uint8_t* stg,
-                          uint8_t* arena, int64_t t, int64_t s0, int64_t s1, int64_t total) {
+// ORs bit `gi` of a bitmap for every lane with pred: one ballot (<= 3 atomics) when the wave's
+// lanes are consecutive entries of one node (gi0 = lane 0's entry), else per-lane atomics.
+__device__ __forceinline__ void tbits(uint8_t* bits, bool uni, int64_t gi0, int64_t gi, bool pred) {
+  if (uni) {
+    tballot_or(bits, gi0, pred);
+  } else if (pred) {
+    __hip_atomic_fetch_or(gl(reinterpret_cast<uint32_t*>(bits)) + (gi >> 5), 1u << (gi & 31),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Item i of a level's flattened (node, entry) list: k = the list slot with cum[k] <= i < cum[k+1].
+__device__ __forceinline__ int titem(const uint32_t* cum, int nk, uint32_t i) {
+  int lo = 0, hi = nk;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (cum[mid] <= i) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+// LDS working set of one workgroup (dynamic shared memory, laid out by tree_lds_head).
+struct TShared {
+  TNode* D;                 // node records (copied once)
+  TMeta* meta;
+  uint64_t* wsum;           // block scans of counts
+  uint32_t* wtot;           // per-wave totals of the node-layout scans
+  int64_t* roffs;           // row offsets of the (sub-)tile
+  uint32_t* ex;             // node-layout scans, two levels' worth: [2][4][maxw + 1]
+  uint8_t* stg;
+  uint8_t* arena;
+  uint64_t* tacc;           // diagnostics: 16 phase accumulators (NULL when off)
+};
+
+// One walk of rows [s0, s1), every level's (node, entry) pairs spread over the whole workgroup.
+// Returns false when the tile's arrays do not fit the arena (uniform).
+template <bool kWrite, int NT>
+__device__ bool tree_walk(const TreeArgs& a, const TShared& sh, int64_t t, int64_t s0, int64_t s1,
+                          int64_t total) {
   const int tid = threadIdx.x;
   const int64_t nr = s1 - s0;
+  const TNode* D = sh.D;
+  TMeta* meta = sh.meta;
+  uint8_t* arena = sh.arena;
+  TMARK(sh, 0);
+  for (int64_t i = tid; i < nr; i += NT) sh.roffs[i] = gl(a.offs)[s0 + i];
   // ---- stage the rows
   Rows R;
   R.g = a.rows;
-  R.stg = stg;
+  R.stg = sh.stg;
   {
     const int64_t g0 = min<int64_t>(max<int64_t>(gl(a.offs)[s0], 0), total);
     const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[s1], g0), total);
@@ -353,123 +410,121 @@ __device__ bool tree_walk(const TreeArgs& a, TMeta* meta, uint64_t* wsum, uint8_
     R.lo_al = g0 - static_cast<int64_t>((reinterpret_cast<uintptr_t>(a.rows) + g0) & 15);
     R.lo = g0;
     R.hi = min<int64_t>(g1, R.lo_al + a.stage_cap);
-    if (R.hi > R.lo) tstage(stg, a.rows + R.lo_al, a.rows + R.hi);
+    if (R.hi > R.lo) tstage<NT>(sh.stg, a.rows + R.lo_al, a.rows + R.hi);
     else R.hi = R.lo;
-    __syncthreads();
   }
   uint32_t region_lo = 0, region_hi = 0;        // arena bytes of the previous level's arrays
   for (int L = 0; L < a.nlevels; L++) {
-    const int nb = a.level_start[L], ne = a.level_start[L + 1];
-    // ---- entries of this level's nodes and their arrays (uniform: every thread computes it)
-    uint32_t need = 0;
-    for (int n = nb; n < ne; n++) {
-      CTNode& N = tn(a, n);
+    const int nb = a.level_start[L], ne = a.level_start[L + 1], m = ne - nb;
+    // ---- entries of this level's nodes (a thread per node), then their arrays and item lists
+    // by block scans over the nodes: SRC bytes, CNT bytes, expansion entries (A), write entries (B)
+    for (int j = tid; j < m; j += NT) {
+      const TNode& N = D[nb + j];
       uint32_t ec;
       if (L == 0) ec = static_cast<uint32_t>(nr);
-      else if (tn(a, N.parent).type == FURY_TYPE_STRUCT) ec = meta[N.parent].ecnt;
+      else if (D[N.parent].type == FURY_TYPE_STRUCT) ec = meta[N.parent].ecnt;
       else ec = meta[N.parent].tot;
-      if (!is_scalar(N.type)) need += 8 * ec;
-      if (is_counted(N.type)) need += 4 * (ec + 1);
-      if (tid == 0) meta[n].ecnt = ec;
+      meta[nb + j].ecnt = ec;
     }
-    need = (need + 15) & ~15u;
+    TMARK(sh, 1);
+    __syncthreads();                             // (also: the stage and row offsets landed)
+    uint32_t* ex = sh.ex + (L & 1) * 4 * (a.maxw + 1);
+    block_scan_k<NT, 4>(m, [&](int j, int k) -> uint32_t {
+      const int t = D[nb + j].type;
+      const uint32_t ec = meta[nb + j].ecnt;
+      switch (k) {
+        case 0: return is_scalar(t) ? 0u : 8 * ec;
+        case 1: return is_counted(t) ? 4 * (ec + 1) : 0u;
+        case 2: return (kWrite || !is_scalar(t)) ? ec : 0u;
+        default: return (kWrite && !is_scalar(t)) ? ec : 0u;
+      }
+    }, ex, sh.wtot);
+    TMARK(sh, 2);
+    const uint32_t* cumA = ex + 2 * (m + 1);
+    const uint32_t* cumB = ex + 3 * (m + 1);
+    const uint32_t srcb = ex[m], cntb = ex[(m + 1) + m];
+    const uint32_t need = (srcb + cntb + 15) & ~15u;
     uint32_t at;
     if (need <= region_lo) at = 0;
     else if (region_hi + need <= a.arena_cap) at = region_hi;
-    else return false;                          // (uniform)
-    __syncthreads();
-    // (second uniform pass: array offsets; the SRC arrays first, then the contiguous count block)
-    uint32_t p = at;
-    for (int n = nb; n < ne; n++) {
-      const uint32_t ec = meta[n].ecnt;
-      if (!is_scalar(tn(a, n).type)) {
-        if (tid == 0) meta[n].src = p;
-        p += 8 * ec;
-      }
+    else return false;
+    const uint32_t cblk = at + srcb, cend = cblk + cntb;
+    for (int j = tid; j < m; j += NT) {
+      meta[nb + j].src = at + ex[j];
+      meta[nb + j].cnt = cblk + ex[(m + 1) + j];
     }
-    const uint32_t cblk = p;
-    for (int n = nb; n < ne; n++) {
-      const uint32_t ec = meta[n].ecnt;
-      if (is_counted(tn(a, n).type)) {
-        if (tid == 0) meta[n].cnt = p;
-        p += 4 * (ec + 1);
-      }
-    }
-    const uint32_t cend = p;
     region_lo = at;
     region_hi = at + need;
     __syncthreads();
-    // ---- expand: the entries of this level from the parent level (or the rows)
-    for (int n = nb; n < ne; n++) {
-      CTNode& N = tn(a, n);
-      const uint32_t ec = meta[n].ecnt;
-      const bool scalar = is_scalar(N.type);
-      const bool counted = is_counted(N.type);
-      int64_t* SRC = scalar ? nullptr : reinterpret_cast<int64_t*>(arena + meta[n].src);
-      uint32_t* CNT = counted ? reinterpret_cast<uint32_t*>(arena + meta[n].cnt) : nullptr;
-      const int32_t ptype = L == 0 ? -1 : tn(a, N.parent).type;
-      const TMeta pm = L == 0 ? TMeta{} : meta[N.parent];
-      const int64_t* PSRC = L == 0 ? nullptr : reinterpret_cast<const int64_t*>(arena + pm.src);
-      const uint32_t* PP = (L == 0 || ptype == FURY_TYPE_STRUCT) ? nullptr
-                           : reinterpret_cast<const uint32_t*>(arena + pm.cnt);
-      const int es = N.esize;
-      const int64_t gbase = kWrite ? meta[n].run_e : 0;
-      for (uint32_t q0 = 0; q0 < ec; q0 += kTreeThreads) {
-        const uint32_t q = q0 + tid;
-        const bool live = q < ec;
+    TMARK(sh, 3);
+    // ---- expand: every (node, entry) of the level from the parent level (or the rows)
+    {
+      const uint32_t W = cumA[m];
+      for (uint32_t i0 = 0; i0 < W; i0 += NT) {
+        const uint32_t i = i0 + tid;
+        const bool live = i < W;
+        const int k = titem(cumA, m, live ? i : W - 1);
+        const int n = nb + k;
+        const uint32_t q = (live ? i : W - 1) - cumA[k];
+        const TNode& N = D[n];
+        const bool scalar = is_scalar(N.type);
+        // (with every lane active: whether the wave's lanes are consecutive entries of one node)
+        const bool uni = __all(n == __shfl(n, 0)) != 0;
+        const int64_t gi = (kWrite ? meta[n].run_e : 0) + q;
+        const int64_t gi0 = __shfl(gi, 0);
         bool nul = true;
         int64_t slotp = 0, cont = 0;
         int64_t vpos = kNullPos;                // collection roots: the value at the row base
-        int swid = 8;                           // bytes of the slot holding a scalar
+        int rw = N.width;                       // bytes of a scalar's value in its slot
         if (live) {
           if (L == 0) {
-            const int64_t row = s0 + q;
-            const int64_t base = gl(a.offs)[row];
+            const int64_t base = sh.roffs[q];
             if (a.root) {
               nul = false;
               vpos = base;
             } else if (!span_ok(base, tbm(a.ntop) + 8 * a.ntop, total)) {
-              if (N.ord == 0) raise_oob(a.err, row);
+              if (N.ord == 0) raise_oob(a.err, s0 + q);
             } else {
               nul = rdbit(R, base, N.ord);
               slotp = base + tbm(a.ntop) + 8 * N.ord;
               cont = base;
             }
-          } else if (ptype == FURY_TYPE_STRUCT) {
-            const int64_t pb = PSRC[q];
-            if (pb >= 0) {
-              const int pnc = tn(a, N.parent).num_children;
-              nul = rdbit(R, pb, N.ord);
-              slotp = pb + tbm(pnc) + 8 * N.ord;
-              cont = pb;
+          } else {
+            const TNode& P = D[N.parent];
+            const TMeta& pm = meta[N.parent];
+            const int64_t* PSRC = reinterpret_cast<const int64_t*>(arena + pm.src);
+            if (P.type == FURY_TYPE_STRUCT) {
+              const int64_t pb = PSRC[q];
+              if (pb >= 0) {
+                nul = rdbit(R, pb, N.ord);
+                slotp = pb + tbm(P.num_children) + 8 * N.ord;
+                cont = pb;
+              }
+            } else {                            // LIST / MAP element
+              const uint32_t* PP = reinterpret_cast<const uint32_t*>(arena + pm.cnt);
+              const uint32_t e = towner(PP, pm.ecnt, q + pm.pad_);
+              const uint32_t j = q + pm.pad_ - PP[e];
+              const int64_t m = PP[e + 1] - PP[e];
+              const int64_t pb = PSRC[e];
+              int64_t arr = pb;
+              if (P.type == FURY_TYPE_MAP)
+                arr = N.ord == 0 ? pb + 8 : pb + 8 + static_cast<int32_t>(rd8(R, pb));
+              nul = rdbit(R, arr + 8, j);
+              slotp = arr + 8 + tbm(m) + static_cast<int64_t>(N.esize) * j;
+              cont = arr;
+              rw = N.esize;
             }
-          } else {                              // LIST / MAP element
-            const uint32_t e = towner(PP, pm.ecnt, q);
-            const uint32_t j = q - PP[e];
-            const int64_t m = PP[e + 1] - PP[e];
-            const int64_t pb = PSRC[e];
-            int64_t arr = pb;
-            if (ptype == FURY_TYPE_MAP)
-              arr = N.ord == 0 ? pb + 8 : pb + 8 + static_cast<int32_t>(rd8(R, pb));
-            nul = rdbit(R, arr + 8, j);
-            slotp = arr + 8 + tbm(m) + static_cast<int64_t>(es) * j;
-            cont = arr;
-            swid = es;
           }
         }
-        if (scalar) {
-          if (kWrite) {
-            const int w = N.width;
-            uint64_t x = 0;
-            if (live && !nul) x = rdw(R, slotp, swid == 8 ? w : es);
-            const int64_t gi = gbase + q;
-            if (N.type == FURY_TYPE_BOOL) {
-              if (N.values) tballot_or(N.values, gbase + q0 + (tid & ~63), live && !nul && (x & 0xff));
-            } else if (live && N.values) {
-              tstore_w(N.values + gi * w, w, x);
-            }
-            if (N.validity) tballot_or(N.validity, gbase + q0 + (tid & ~63), live && !nul);
+        if (scalar) {                           // (pass 2 only: pass 1 lists no scalars)
+          uint64_t x = 0;
+          if (live && !nul) x = rdw(R, slotp, rw);
+          if (N.type == FURY_TYPE_BOOL) {
+            if (N.values) tbits(N.values, uni, gi0, gi, live && !nul && (x & 0xff));
+          } else if (live && N.values) {
+            tstore_w(N.values + gi * N.width, N.width, x);
           }
+          if (N.validity) tbits(N.validity, uni, gi0, gi, live && !nul);
           continue;
         }
         if (!live) continue;
@@ -484,67 +539,72 @@ __device__ bool tree_walk(const TreeArgs& a, TMeta* meta, uint64_t* wsum, uint8_
             pos = cont + static_cast<int32_t>(slot >> 32);
             size = static_cast<int32_t>(slot);
           }
-          if (!tcheck(a, R, N, pos, size, total, &c, err_where_tile(n, s0))) pos = kNullPos;
+          if (!tcheck(a, R, tn(a, n), pos, size, total, &c, err_where_tile(n, s0))) pos = kNullPos;
         }
-        SRC[q] = pos;
-        if (counted) CNT[q] = c;
+        reinterpret_cast<int64_t*>(arena + meta[n].src)[q] = pos;
+        if (is_counted(N.type)) {
+          uint32_t* CNT = reinterpret_cast<uint32_t*>(arena + meta[n].cnt);
+          CNT[q] = c;
+          if (q + 1 == meta[n].ecnt) CNT[q + 1] = 0;
+        }
       }
-      if (counted && tid == 0) CNT[ec] = 0;
+      // counted nodes without entries still need their trailing slot
+      for (int n = nb + tid; n < ne; n += NT)
+        if (is_counted(D[n].type) && meta[n].ecnt == 0)
+          reinterpret_cast<uint32_t*>(arena + meta[n].cnt)[0] = 0;
     }
+    TMARK(sh, 4);
     __syncthreads();
-    // ---- in-tile prefixes of the level's counts (one scan over the contiguous count block; a
-    // node's prefix is relative to its first slot)
+    TMARK(sh, 5);
+    // ---- in-tile prefixes of the level's counts: one scan over the contiguous count block; a
+    // node's prefix is relative to its first slot (meta.pad_ = that base, meta.tot = its total)
     if (cend > cblk) {
       uint32_t* blk = reinterpret_cast<uint32_t*>(arena + cblk);
-      if (!block_scan_u32(blk, (cend - cblk) / 4, wsum)) return false;
-      // rebase each node's segment to start at 0 and record its total
-      for (int n = nb; n < ne; n++) {
-        if (!is_counted(tn(a, n).type)) continue;
-        uint32_t* P = reinterpret_cast<uint32_t*>(arena + meta[n].cnt);
-        const uint32_t ec = meta[n].ecnt;
-        const uint32_t b0 = P[0];
-        const uint32_t tot = P[ec] - b0;
-        __syncthreads();                        // every thread has read P[0] before it changes
-        for (uint32_t i = tid; i <= ec; i += kTreeThreads) P[i] -= b0;
-        if (tid == 0) meta[n].tot = tot;
+      if (!block_scan_u32<NT>(blk, (cend - cblk) / 4, sh.wsum)) return false;
+      for (int n = nb + tid; n < ne; n += NT) {
+        if (!is_counted(D[n].type)) continue;
+        const uint32_t* P = reinterpret_cast<const uint32_t*>(arena + meta[n].cnt);
+        meta[n].pad_ = P[0];
+        meta[n].tot = P[meta[n].ecnt] - P[0];
       }
       __syncthreads();
     }
+    TMARK(sh, 6);
     // ---- pass 2: the level's non-scalar outputs (pass 1 only needed the counts)
     if (!kWrite) continue;
-    for (int n = nb; n < ne; n++) {
-      CTNode& N = tn(a, n);
-      if (is_scalar(N.type)) continue;
-      const uint32_t ec = meta[n].ecnt;
-      const int64_t* SRC = reinterpret_cast<const int64_t*>(arena + meta[n].src);
-      const uint32_t* P = is_counted(N.type) ? reinterpret_cast<const uint32_t*>(arena + meta[n].cnt) : nullptr;
-      const int64_t gbase = meta[n].run_e;
-      const int64_t bbase = meta[n].run_b;
-      const int64_t cbase = (N.type == FURY_TYPE_LIST || N.type == FURY_TYPE_MAP)
-                                ? meta[N.first_child].run_e : 0;
-      for (uint32_t e0 = 0; e0 < ec; e0 += kTreeThreads) {
-        const uint32_t e = e0 + tid;
-        const bool live = e < ec;
-        const int64_t pos = live ? SRC[e] : kNullPos;
+    {
+      const uint32_t W = cumB[m];
+      for (uint32_t i0 = 0; i0 < W; i0 += NT) {
+        const uint32_t i = i0 + tid;
+        const bool live = i < W;
+        const int k = titem(cumB, m, live ? i : W - 1);
+        const int n = nb + k;
+        const uint32_t e = (live ? i : W - 1) - cumB[k];
+        const TNode& N = D[n];
+        const TMeta& M = meta[n];
+        const int64_t pos = live ? reinterpret_cast<const int64_t*>(arena + M.src)[e] : kNullPos;
         const bool valid = pos >= 0;
-        if (N.validity) tballot_or(N.validity, gbase + e0 + (tid & ~63), valid);
+        const int64_t gi = M.run_e + e;
+        const bool uni = __all(n == __shfl(n, 0)) != 0;
+        const int64_t gi0 = __shfl(gi, 0);
+        if (N.validity) tbits(N.validity, uni, gi0, gi, live && valid);
         if (!live) continue;
-        const int64_t gi = gbase + e;
+        const uint32_t* P = is_counted(N.type) ? reinterpret_cast<const uint32_t*>(arena + M.cnt) : nullptr;
         switch (N.type) {
           case FURY_TYPE_STRING:
           case FURY_TYPE_BINARY: {
-            const uint32_t p0 = P[e], p1 = P[e + 1];
+            const uint32_t p0 = P[e] - M.pad_, p1 = P[e + 1] - M.pad_;
             if (N.offsets) {
-              gl(N.offsets)[gi + 1] = static_cast<int32_t>(bbase + p1);
+              gl(N.offsets)[gi + 1] = static_cast<int32_t>(M.run_b + p1);
               if (gi == 0) gl(N.offsets)[0] = 0;
             }
-            if (valid && N.values) tcopy_out(N.values + bbase + p0, R, pos, p1 - p0);
+            if (valid && N.values) tcopy_out(N.values + M.run_b + p0, R, pos, p1 - p0);
             break;
           }
           case FURY_TYPE_LIST:
           case FURY_TYPE_MAP:
             if (N.offsets) {
-              gl(N.offsets)[gi + 1] = static_cast<int32_t>(cbase + P[e + 1]);
+              gl(N.offsets)[gi + 1] = static_cast<int32_t>(meta[N.first_child].run_e + P[e + 1] - M.pad_);
               if (gi == 0) gl(N.offsets)[0] = 0;
             }
             break;
@@ -560,22 +620,53 @@ __device__ bool tree_walk(const TreeArgs& a, TMeta* meta, uint64_t* wsum, uint8_
         }
       }
     }
+    TMARK(sh, 7);
   }
   return true;
 }
 
-template <bool kWrite>
-__global__ __launch_bounds__(kTreeThreads) void tree_dec_kernel(TreeArgs a) {
+// Dynamic LDS of tree_dec_kernel: [node records][meta][wsum 64][row offsets][level lists][stage]
+// [arena].
+__host__ __device__ inline size_t tree_lds_head(int nn, int maxw, int nt) {
+  size_t b = sizeof(TNode) * nn;
+  b += sizeof(TMeta) * nn;
+  b += 8 * 16 + 4 * 4 * 16;                      // wsum, wtot (up to 16 waves)
+  b += 8 * static_cast<size_t>(nt);             // roffs
+  b += 4 * 2 * 4 * static_cast<size_t>(maxw + 1);  // ex
+  b += 128;                                      // diagnostics
+  return (b + 15) & ~size_t(15);
+}
+
+template <bool kWrite, int NT>
+__global__ __launch_bounds__(NT) void tree_dec_kernel(TreeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tsm[];
-  TMeta* meta = reinterpret_cast<TMeta*>(tsm);
-  uint64_t* wsum = reinterpret_cast<uint64_t*>(tsm + sizeof(TMeta) * a.nn);
-  uint8_t* stg = tsm + ((sizeof(TMeta) * a.nn + 64 + 15) & ~size_t(15));
-  uint8_t* arena = stg + a.stage_cap;
+  TShared sh;
+  {
+    uint8_t* p = tsm;
+    sh.D = reinterpret_cast<TNode*>(p);
+    p += sizeof(TNode) * a.nn;
+    sh.meta = reinterpret_cast<TMeta*>(p);
+    p += sizeof(TMeta) * a.nn;
+    sh.wsum = reinterpret_cast<uint64_t*>(p);
+    p += 8 * 16;
+    sh.wtot = reinterpret_cast<uint32_t*>(p);
+    p += 4 * 4 * 16;
+    sh.roffs = reinterpret_cast<int64_t*>(p);
+    p += 8 * NT;
+    sh.ex = reinterpret_cast<uint32_t*>(p);
+    p += 4 * 2 * 4 * (a.maxw + 1);
+    sh.tacc = a.dbg ? reinterpret_cast<uint64_t*>(p) : nullptr;
+    sh.stg = tsm + tree_lds_head(a.nn, a.maxw, NT);
+    sh.arena = sh.stg + a.stage_cap;
+  }
+  TMeta* meta = sh.meta;
   const int tid = threadIdx.x;
   const int64_t t = blockIdx.x;
   const int64_t r0 = t * a.tile_rows, r1 = min<int64_t>(r0 + a.tile_rows, a.nrows);
   const int64_t total = gl(a.offs)[a.nrows];
-  for (int n = tid; n < a.nn; n += kTreeThreads) {
+  if (sh.tacc && tid < 16) sh.tacc[tid] = tid == 15 ? __builtin_amdgcn_s_memrealtime() : 0;
+  for (int n = tid; n < a.nn; n += NT) {
+    sh.D[n] = a.nodes[n];
     meta[n].run_e = kWrite ? a.cnt[static_cast<int64_t>(n) * a.ntiles + t] : 0;
     meta[n].run_b = kWrite ? a.byt[static_cast<int64_t>(n) * a.ntiles + t] : 0;
   }
@@ -583,7 +674,8 @@ __global__ __launch_bounds__(kTreeThreads) void tree_dec_kernel(TreeArgs a) {
   int64_t s0 = r0, sub = r1 - r0;
   while (s0 < r1) {
     const int64_t s1 = min(s0 + sub, r1);
-    if (!tree_walk<kWrite>(a, meta, wsum, stg, arena, t, s0, s1, total)) {
+    if (!tree_walk<kWrite, NT>(a, sh, t, s0, s1, total)) {
+      TMARK(sh, 9);
       __syncthreads();
       if (s1 - s0 == 1) {                       // one row does not fit: the level engine decodes
         if (!kWrite && tid == 0)
@@ -594,19 +686,23 @@ __global__ __launch_bounds__(kTreeThreads) void tree_dec_kernel(TreeArgs a) {
       continue;                                 // other pass splits it the same way)
     }
     __syncthreads();
-    for (int n = tid; n < a.nn; n += kTreeThreads) {
+    for (int n = tid; n < a.nn; n += NT) {
       meta[n].run_e += meta[n].ecnt;
-      const int ty = tn(a, n).type;
+      const int ty = sh.D[n].type;
       if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) meta[n].run_b += meta[n].tot;
     }
     __syncthreads();
     s0 = s1;
   }
   if (!kWrite)
-    for (int n = tid; n < a.nn; n += kTreeThreads) {
+    for (int n = tid; n < a.nn; n += NT) {
       a.cnt[static_cast<int64_t>(n) * a.ntiles + t] = meta[n].run_e;
       a.byt[static_cast<int64_t>(n) * a.ntiles + t] = meta[n].run_b;
     }
+  TMARK(sh, 8);
+  if (sh.tacc && tid < 15) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg) + (kWrite ? 16 : 0) + tid,
+                                     static_cast<unsigned long long>(sh.tacc[tid]));
+  if (sh.tacc && tid == 15) atomicAdd(reinterpret_cast<unsigned long long*>(a.dbg) + 64 + (kWrite ? 1 : 0), 1ull);
 }
 
 // Exclusive scan over the tiles of each [node] row of cnt (rows 0..nn-1) and byt (rows nn..2nn-1);
@@ -655,17 +751,32 @@ int tree_host_width(int32_t t) {
 }
 
 int g_tree_mode = 1;             // tuning "nested_decode": 0 tree tiles, 1 level engine
+uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 uint32_t g_tree_stage = 32 * 1024, g_tree_arena = 24 * 1024;
+int g_tree_threads = 256;        // tuning "tree_threads": workgroup size of the decode (256/512/1024)
 
 }  // namespace
 
 void set_tree_mode(int v) { g_tree_mode = v; }
+uint64_t* tree_debug_buffer() { return g_tree_dbg; }
+int set_tree_debug(int on) {
+  if (on && !g_tree_dbg) {
+    if (hipMalloc(reinterpret_cast<void**>(&g_tree_dbg), 8 * 80) != hipSuccess) return FURY_ERR_DEVICE;
+    if (hipMemset(g_tree_dbg, 0, 8 * 80) != hipSuccess) return FURY_ERR_DEVICE;
+  } else if (!on && g_tree_dbg) {
+    (void)hipFree(g_tree_dbg);
+    g_tree_dbg = nullptr;
+  }
+  return FURY_OK;
+}
 int tree_mode() { return g_tree_mode; }
 void set_tree_lds(uint32_t stage, uint32_t arena) {
   if (stage) g_tree_stage = (stage + 15) & ~15u;
   if (arena) g_tree_arena = (arena + 15) & ~15u;
 }
 uint32_t tree_lds(int which) { return which ? g_tree_arena : g_tree_stage; }
+void set_tree_threads(int v) { g_tree_threads = v; }
+int tree_threads() { return g_tree_threads; }
 
 struct TreePlan {
   std::vector<TNode> nodes;
@@ -706,17 +817,21 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.tile_rows = p.tile_rows;
   a.stage_cap = p.stage_cap;
   a.arena_cap = p.arena_cap;
+  a.dbg = tree_debug_buffer();
   for (int i = 0; i <= a.nlevels; i++) a.level_start[i] = p.level_start[i];
-  const size_t lds = ((sizeof(TMeta) * a.nn + 64 + 15) & ~size_t(15)) + p.stage_cap + p.arena_cap;
-  const void* fn = write ? reinterpret_cast<const void*>(tree_dec_kernel<true>)
-                         : reinterpret_cast<const void*>(tree_dec_kernel<false>);
-  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-  if (write)
-    hipLaunchKernelGGL(tree_dec_kernel<true>, dim3(static_cast<unsigned>(p.ntiles)),
-                       dim3(kTreeThreads), lds, hs, a);
-  else
-    hipLaunchKernelGGL(tree_dec_kernel<false>, dim3(static_cast<unsigned>(p.ntiles)),
-                       dim3(kTreeThreads), lds, hs, a);
+  int maxw = 0;
+  for (int i = 0; i < a.nlevels; i++) maxw = std::max(maxw, p.level_start[i + 1] - p.level_start[i]);
+  a.maxw = maxw;
+  const int nt = g_tree_threads;
+  const size_t lds = tree_lds_head(a.nn, maxw, nt) + p.stage_cap + p.arena_cap;
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(p.ntiles)), dim3(nt), lds, hs, a);
+  };
+  if (nt == 1024) write ? go(tree_dec_kernel<true, 1024>) : go(tree_dec_kernel<false, 1024>);
+  else if (nt == 512) write ? go(tree_dec_kernel<true, 512>) : go(tree_dec_kernel<false, 512>);
+  else write ? go(tree_dec_kernel<true, 256>) : go(tree_dec_kernel<false, 256>);
   return check_hip(hipGetLastError(), "tree decode launch");
 }
 
@@ -779,7 +894,10 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   }
   const int64_t total = std::max<int64_t>(pin[0], 1);
   const double avg = std::max(8.0, static_cast<double>(total) / static_cast<double>(nrows));
-  p->tile_rows = static_cast<int32_t>(std::clamp<double>(0.9 * p->stage_cap / avg, 1.0, 256.0));
+  // rows per tile: the tile's bytes fill ~90 % of the stage, its level arrays (~1.5 x the row
+  // bytes at worst: 12 B per non-scalar entry, each behind an 8-byte slot) the arena
+  const double by_stage = 0.9 * p->stage_cap / avg, by_arena = 0.9 * p->arena_cap / (0.75 * avg);
+  p->tile_rows = static_cast<int32_t>(std::clamp<double>(std::min(by_stage, by_arena), 1.0, 256.0));
   p->ntiles = (nrows + p->tile_rows - 1) / p->tile_rows;
   int32_t* overflow = nullptr;
   int64_t* tot = nullptr;
@@ -839,3 +957,14 @@ int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, co
 }
 
 }  // namespace fury
+
+// Diagnostics, not part of include/fury_row.h: copies the tree-tile phase accumulators (80 words:
+// decode pass 1 [0, 16), pass 2 [16, 32), measure [32, 48), encode [48, 64) in 10 ns ticks, then
+// workgroup counts [64, 68)) to out and zeroes them.  Synchronises the device.
+extern "C" int fury_internal_tree_debug(int64_t* out, int32_t n) {
+  uint64_t* d = fury::tree_debug_buffer();
+  if (!d || !out || n < 1) return FURY_ERR_INVALID_ARGUMENT;
+  if (hipDeviceSynchronize() != hipSuccess) return FURY_ERR_DEVICE;
+  if (hipMemcpy(out, d, 8 * std::min(n, 80), hipMemcpyDeviceToHost) != hipSuccess) return FURY_ERR_DEVICE;
+  return hipMemset(d, 0, 8 * 80) == hipSuccess ? FURY_OK : FURY_ERR_DEVICE;
+}

@@ -63,9 +63,25 @@ def main():
         return statistics.median(xs)
     import ctypes
     from fury_amd import _native as N
-    for leg in [int(x) for x in args.legs.split(",")]:
-        for k in (b"nested_encode", b"nested_decode"):
-            assert N.lib().fury_set_tuning(k, leg) == 0
+    if args.legs.startswith("["):          # JSON list of {tuning key: value} legs
+        legs = json.loads(args.legs)
+    else:
+        legs = [{"nested_encode": int(x), "nested_decode": int(x)} for x in args.legs.split(",")]
+    ref = None
+    for leg in legs:
+        for k, v in leg.items():
+            assert N.lib().fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
+        b2 = enc.encode_batch(cols, n)
+        d2 = enc.decode_batch(b2)
+        torch.cuda.synchronize()
+        got = (b2.rows.clone(), [x for c in d2 for x in (c.values, c.validity, c.offsets)])
+        if ref is None:
+            ref = got
+        else:
+            same = torch.equal(ref[0], got[0]) and all(
+                (x is None and y is None) or (x is not None and y is not None and torch.equal(x, y))
+                for x, y in zip(ref[1], got[1]))
+            print(json.dumps({"leg": leg, "equal_to_first": same}), flush=True)
         leg_run(args, t, enc, cols, n, batch, out, leg)
 
 

@@ -1,0 +1,70 @@
+"""Phase times of the tree-tile kernels (tuning "tree_debug"): thread 0 of every workgroup adds the
+time between phase marks; printed as the mean microseconds per workgroup per phase (thread 0's
+timeline: barrier waits included).  Depth-3 nested schema of the tests, --rows rows.
+
+    python scripts/tree_phases.py --rows 4000000 [--tune key=value ...]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEC = {0: "walk start (since previous mark)", 1: "level layout (all threads)", 2: "barrier",
+       3: "thread-0 lists + barrier", 4: "expand", 5: "barrier", 6: "scan + bases", 7: "write",
+       8: "kernel tail", 9: "failed walk"}
+ENC = {7: "walk start", 0: "R ranges", 1: "stage + layout + lists", 2: "barrier (staged)",
+       3: "sizes (S)", 4: "rows: sizes / containers", 5: "positions + contents",
+       6: "image store", 8: "kernel tail", 9: "failed walk"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--tune", action="append", default=[])
+    args = ap.parse_args()
+    import torch
+    from fury_amd import _native as N
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    from tests.test_device import _nested_beans, _nested_fields
+    L = N.lib()
+    fn = L.fury_internal_tree_debug
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
+    for k in ("nested_encode", "nested_decode"):
+        assert L.fury_set_tuning(k.encode(), 0) == 0
+    for kv in args.tune:
+        k, v = kv.split("=")
+        assert L.fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
+    fields = _nested_fields()
+    base = _nested_beans(50_000, seed=1)
+    beans = (base * (args.rows // len(base) + 1))[:args.rows]
+    dev = torch.device("cuda:0")
+    cols = [column_to_device(c, dev) for c in beans_to_columns(fields, beans)]
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(cols, args.rows)
+    enc.decode_batch(batch)
+    torch.cuda.synchronize()
+    assert L.fury_set_tuning(b"tree_debug", 1) == 0
+    out = (ctypes.c_int64 * 80)()
+    fn(out, 80)                                     # zero
+    enc.encode_batch(cols, args.rows)
+    enc.decode_batch(batch)
+    assert fn(out, 80) == 0
+    res = {}
+    for name, off, cnt_i, names in (("decode_pass1", 0, 64, DEC), ("decode_pass2", 16, 65, DEC),
+                                    ("measure", 32, 66, ENC), ("encode", 48, 67, ENC)):
+        wg = max(out[cnt_i], 1)
+        res[name] = {"workgroups": out[cnt_i],
+                     "us_per_wg": {names.get(i, str(i)): round(out[off + i] / wg / 100.0, 2)
+                                   for i in range(15) if out[off + i]}}
+    print(json.dumps({"rows": args.rows, "tune": args.tune, "phases": res}, indent=1))
+    assert L.fury_set_tuning(b"tree_debug", 0) == 0
+
+
+if __name__ == "__main__":
+    main()

@@ -106,17 +106,26 @@ def test_schema_create_errors():
 def test_device_calls_reject_bad_arguments_without_touching_gpu():
     """Argument validation happens on the host before any HIP call."""
     from fury_amd import _native as N
-    from fury_amd.encoder import Schema
+    from fury_amd.encoder import Schema, UnsupportedOperationException
     L = N.lib()
     assert L.fury_row_encode(None, None, 1, None, None, None) == 1
     s = Schema(SCHEMAS["foo"])       # nested struct + map: generic engine; rows is null
     cols = (N.FuryColumn * 5)()
     assert L.fury_row_encode(s.handle, cols, 1, None, None, None) == 1
     deep = T.field("x", T.INT32)
-    for d in range(9):               # 10 levels of nesting: beyond the generic engine
+    for d in range(9):               # 10 levels of nesting: the tree tiles take it
         deep = T.struct_field(f"s{d}", [deep])
-    s3 = Schema([deep])
-    assert L.fury_row_encode(s3.handle, cols, 1, None, None, None) == 2
+    assert L.fury_row_encode(Schema([deep]).handle, cols, 1, None, None, None) == 1  # rows null
+    for d in range(9, 70):           # 71 levels: beyond the schema limit (and the tree tiles' 64)
+        deep = T.struct_field(f"s{d}", [deep])
+    with pytest.raises(UnsupportedOperationException):
+        Schema([deep])
+    wide = [T.struct_field(f"w{i}", [T.field("a", T.INT32), T.field("b", T.INT64)])
+            for i in range(100)]     # > 256 nodes and nested past the row interpreter
+    deep = T.field("x", T.INT32)
+    for d in range(9):
+        deep = T.struct_field(f"s{d}", [deep])
+    assert L.fury_row_encode(Schema(wide + [deep]).handle, cols, 1, None, None, None) == 2
     assert "nested" in N.last_error()
     assert L.fury_schema_num_nodes(s.handle) == 5 + 1 + 2 + 2
     s2 = Schema(SCHEMAS["struct100"])

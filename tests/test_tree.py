@@ -181,9 +181,11 @@ def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, nam
     enc.encode_measured_into(dcols, n, rows, offs)
     torch.cuda.synchronize()
     assert np.array_equal(rows[:total].cpu().numpy(), want)
-    _tune("nested_encode", 1)
-    b1 = enc.encode_batch(dcols, n)
-    assert np.array_equal(b1.rows.cpu().numpy(), want)
+    for mode in (1, 2):               # interpreter; tree measure + interpreter encode
+        _tune("nested_encode", mode)
+        b1 = enc.encode_batch(dcols, n)
+        assert np.array_equal(b1.row_offsets.cpu().numpy(), want_offs)
+        assert np.array_equal(b1.rows.cpu().numpy(), want)
 
 
 def test_tree_encode_capacity(oracle, dev, enc_engines):
@@ -212,3 +214,84 @@ def test_tree_encode_capacity(oracle, dev, enc_engines):
     assert (got[cap:] == 0xAB).all()
     full = int(np.searchsorted(want_offs, cap, side="right")) - 1
     assert np.array_equal(got[:want_offs[full]], want[:want_offs[full]])
+
+
+# ---- schemas nested past the row interpreter (depth-9 and beyond) -----------
+def _deep_fields(levels):
+    """`levels` levels of nesting: a struct chain with a LIST every third level and one MAP, so a
+    row stays small (at most ~3 entries per collection)."""
+    f = T.field("leaf", T.INT64)
+    depth = 1
+    d = 0
+    while depth < levels - 1:
+        if d % 3 == 1:
+            f = T.Field(f"l{d}", T.LIST, True, (f,))
+            depth += 1
+        elif d == 3 and depth + 2 <= levels - 1:
+            f = T.map_field(f"m{d}", T.field("k", T.STRING), f)
+            depth += 1
+        else:
+            f = T.struct_field(f"s{d}", [T.field(f"v{d}", T.INT32 if d % 2 else T.STRING), f])
+            depth += 1
+        d += 1
+    return [T.not_null_field("id", T.INT64), f, T.array_field("tail", T.INT16)]
+
+
+def _schema_levels(fields):
+    def lv(f):
+        return 1 + max((lv(c) for c in f.children), default=0)
+    return max(lv(f) for f in fields)
+
+
+@pytest.mark.parametrize("levels", [9, 12, 20])
+@pytest.mark.parametrize("dec_mode", [0, 1])
+def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_mode):
+    """Depth 9 / 12 / 20 schemas: the encode takes the tree tiles by itself (the row interpreter
+    stops at kGenMaxDepth levels), both decode engines read the rows back; bytes, offsets and
+    columns == the oracle's."""
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _deep_fields(levels)
+    assert _schema_levels(fields) == levels
+    n = 2500
+    beans = _beans(fields, n, levels * 7 + dec_mode)
+    host = beans_to_columns(fields, beans)
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    assert enc.nested
+    want, want_offs = oracle.encode(fields, host, n)
+    for mode in (2, 1, 0):            # deep schemas ignore "nested_encode": always the tree tiles
+        _tune("nested_encode", mode)
+        b = enc.encode_batch(dcols, n)
+        assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
+        assert np.array_equal(b.rows.cpu().numpy(), want)
+    _tune("nested_decode", dec_mode)
+    ref = oracle.decode(fields, want, want_offs, n)
+    got = _decode_plan(enc, b)
+    assert_columns_equal(fields, got, ref, n)
+    assert columns_to_beans(fields, got, n) == beans
+
+
+def test_deep_schema_row_too_large_for_chip_raises(oracle, dev, enc_engines):
+    """A depth-10 row larger than the (shrunk) on-chip budget has no interpreter fallback: the call
+    reports UnsupportedOperationException naming the row instead of writing partial bytes."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, UnsupportedOperationException, column_to_device
+    fields = _deep_fields(10)
+    n = 600
+    beans = _beans(fields, n, 3)
+    beans[123]["tail"] = list(range(400))            # ~1 KB row
+    host = beans_to_columns(fields, beans)
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    from fury_amd import _native as N
+    old = {k: N.lib().fury_get_tuning(k.encode()) for k in ("tree_enc_lds", "tree_measure_lds")}
+    _tune("tree_enc_lds", 1024)
+    _tune("tree_measure_lds", 1024)
+    with pytest.raises(UnsupportedOperationException, match="nested deeper"):
+        enc.encode_batch(dcols, n)
+    for k, v in old.items():
+        _tune(k, v)
+    b = enc.encode_batch(dcols, n)                    # the stream's error slot is clean again
+    want, _ = oracle.encode(fields, host, n)
+    assert np.array_equal(b.rows.cpu().numpy(), want)
