@@ -825,8 +825,22 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "nested_decode") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 0..1");
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 0..2");
     set_tree_mode(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "walk_threads") {
+    if (value != 128 && value != 256)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads: 128 or 256");
+    set_walk_tuning(0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "walk_stage" || std::string(key) == "walk_pool" ||
+      std::string(key) == "walk_stage_write") {
+    if (value < 0 || value > 96 * 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 0..98304 bytes");
+    set_walk_tuning(std::string(key) == "walk_stage" ? 1 : std::string(key) == "walk_pool" ? 2 : 3,
+                    static_cast<uint32_t>(value));
     return FURY_OK;
   }
   if (std::string(key) == "tree_threads") {
@@ -872,6 +886,10 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "nested_decode") return tree_mode();
   if (key && std::string(key) == "nested_encode") return tree_encode_mode();
   if (key && std::string(key) == "tree_threads") return tree_threads();
+  if (key && std::string(key) == "walk_threads") return static_cast<int32_t>(walk_tuning(0));
+  if (key && std::string(key) == "walk_stage") return static_cast<int32_t>(walk_tuning(1));
+  if (key && std::string(key) == "walk_pool") return static_cast<int32_t>(walk_tuning(2));
+  if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
   if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);
   if (key && std::string(key) == "tree_measure_rows") return tree_encode_rows(0);

@@ -291,6 +291,11 @@ uint32_t tree_lds(int which);
 int set_tree_debug(int on);          // tuning "tree_debug": phase accumulators on / off
 void set_tree_threads(int v);        // tuning "tree_threads": 256 / 512 / 1024
 int tree_threads();
+// tunings of the row-walk decode (walk.hip): 0 "walk_threads" (128 / 256 rows per tile),
+// 1 "walk_stage" (LDS stage cap of the count pass, bytes), 2 "walk_pool" (LDS bitmap-window
+// bytes), 3 "walk_stage_write" (LDS stage cap of the write pass)
+void set_walk_tuning(int which, uint32_t v);
+uint32_t walk_tuning(int which);
 uint64_t* tree_debug_buffer();
 // Exclusive scan of s[0..n) with the total stored to *total (device); ws: scan_workspace(n).
 int64_t scan_workspace(int64_t n);

@@ -1,0 +1,501 @@
+// walk.hip — nested decode with a thread per ROW ("row walk"): the default engine of
+// fury_decode_prepare / fury_decode_execute for schemas of up to kWalkMaxDepth levels and
+// kWalkMaxK counted nodes (tree.hip builds the plan and falls back to the tile-level walk or the
+// level engine beyond that).
+//
+// Reference semantics are tree.hip's (its header): the getters of BinaryRow / BinaryArray /
+// BinaryMap as the generated fromRow and ArrowWriter walk them (FMT/encoder/
+// BaseBinaryEncoderBuilder.java:459-706, FMT/vectorized/ArrowWriter.java:205-640), entries of a
+// node in (parent entry, element) order, a null struct a null entry in every child, a null list /
+// map a zero-length entry, null values zeroed, every read bounds-checked (tcheck, shared).
+//
+// MI355X design.  A workgroup owns NT consecutive rows, one per thread, whose bytes are staged in
+// LDS by LDS-DMA (rows past the stage are read from HBM).  A thread walks its row depth first:
+// inside one row, every node's entries come in (parent entry, element) order, so a row only needs
+// one CURSOR per counted slot -- each LIST / MAP node (its elements) and each STRING / BINARY node
+// (its payload bytes) -- to place everything it writes.
+//   pass 1 (prepare): the walk adds up each row's counted slots (thread-private LDS counters), one
+//     wave-scan per slot turns them into in-tile row prefixes -> rowpre[k][row] (4 B per row and
+//     slot, coalesced), and the tile totals give every node's entries / payload bytes in the tile
+//     (a node's entries are the rows, or the elements of its nearest LIST / MAP ancestor) ->
+//     [node][tile], which tree_tile_scan turns into tile bases (the one host sync reads totals).
+//   pass 2 (execute): cursors = tile base + rowpre; the walk writes values, offsets and payloads
+//     at their final positions.  Validity / BOOL bits of row-aligned nodes (one entry per row) go
+//     out by wave ballots; the other nodes' bits collect in LDS windows over the tile's entry range
+//     (ds_or), flushed as whole words at the end (edge words, shared with the neighbouring tiles,
+//     by atomic OR; a node whose window does not fit the pool ORs straight into HBM).
+// Scalar subtrees are skipped by the counting walk (TNode.walk).  The per-row work is a serial
+// chain of dependent LDS reads; occupancy, not bandwidth, bounds it.
+#include "tree_dev.h"
+
+namespace fury {
+
+namespace {
+
+// LDS working set (laid out by walk_layout).
+struct WShared {
+  uint32_t* cur;            // [K][NT]: a thread's cursor (pass 1: its row's totals)
+  int64_t* kb;              // [K]: tile base of counted slot k (pass 2)
+  int32_t* win;             // [2][nn]: LDS word of node n's validity / BOOL-value window, -1: none
+  int64_t* w0;              // [nn]: first global bitmap word of node n's windows
+  uint32_t* req;            // [2][nn + 1]: window words, scanned into window offsets
+  uint64_t* wsum;           // [K][NT / 64] (pass 1) / [16] (pass 2) scan scratch
+  uint32_t* pool;           // window words
+  uint8_t* stg;             // staged rows
+};
+
+struct WLayout {
+  size_t cur, kb, win, w0, req, wsum, pool, stg, end;
+};
+
+__host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t stage, uint32_t pool,
+                                               bool write) {
+  WLayout l{};
+  size_t b = 0;
+  l.cur = b;
+  b += 4 * static_cast<size_t>(K) * nt;
+  b = (b + 15) & ~size_t(15);
+  l.kb = b;
+  b += 8 * static_cast<size_t>(K);
+  l.w0 = b;
+  b += write ? 8 * static_cast<size_t>(nn) : 0;
+  l.win = b;
+  b += write ? 4 * 2 * static_cast<size_t>(nn) : 0;
+  l.req = b;
+  b += write ? 4 * 2 * static_cast<size_t>(nn + 1) : 0;
+  b = (b + 15) & ~size_t(15);
+  l.wsum = b;
+  b += 8 * static_cast<size_t>(write ? 16 : K * (nt / 64));
+  b = (b + 15) & ~size_t(15);
+  l.pool = b;
+  b += write ? pool : 0;
+  b = (b + 15) & ~size_t(15);
+  l.stg = b;
+  b += stage;
+  l.end = (b + 15) & ~size_t(15);
+  return l;
+}
+
+__device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, bool write) {
+  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write);
+  WShared s;
+  s.cur = reinterpret_cast<uint32_t*>(base + l.cur);
+  s.kb = reinterpret_cast<int64_t*>(base + l.kb);
+  s.win = reinterpret_cast<int32_t*>(base + l.win);
+  s.w0 = reinterpret_cast<int64_t*>(base + l.w0);
+  s.req = reinterpret_cast<uint32_t*>(base + l.req);
+  s.wsum = reinterpret_cast<uint64_t*>(base + l.wsum);
+  s.pool = reinterpret_cast<uint32_t*>(base + l.pool);
+  s.stg = base + l.stg;
+  return s;
+}
+
+// Stages the bytes of rows [r0, r0 + nr) (as much as the stage holds) and returns the reader.
+template <int NT>
+__device__ inline Rows walk_stage(const TreeArgs& a, uint8_t* stg, int64_t r0, int64_t nr,
+                                  int64_t total) {
+  Rows R;
+  R.g = a.rows;
+  R.stg = stg;
+  const int64_t g0 = min<int64_t>(max<int64_t>(gl(a.offs)[r0], 0), total);
+  const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[r0 + nr], g0), total);
+  R.lo_al = g0 - static_cast<int64_t>((reinterpret_cast<uintptr_t>(a.rows) + g0) & 15);
+  R.lo = g0;
+  R.hi = min<int64_t>(g1, R.lo_al + a.stage_cap);
+  if (R.hi > R.lo) tstage<NT>(stg, a.rows + R.lo_al, a.rows + R.hi);
+  else R.hi = R.lo;
+  return R;
+}
+
+// Walk context of one thread.
+struct WCtx {
+  const TreeArgs* a;
+  const WShared* sh;
+  const Rows* R;
+  int64_t total;
+  int64_t row;
+  int64_t wave_row;         // the row of lane 0 of this wave (ballots of row-aligned nodes)
+  int tid;
+};
+
+// Bit `e` of node n's validity (which = 0) / BOOL values (which = 1).  Row-aligned nodes (e = the
+// row) take a wave ballot: every active lane calls this at the same node, pred or not.
+__device__ __forceinline__ void wbit(const WCtx& c, CTNode& N, int n, int which, uint8_t* bits,
+                                     int64_t e, bool pred) {
+  if (N.ek < 0) {
+    tballot_or(bits, c.wave_row, pred);
+    return;
+  }
+  if (!pred) return;
+  const int w = c.sh->win[which * c.a->nn + n];
+  if (w >= 0) {
+    const int64_t rel = e - (c.sh->w0[n] << 5);
+    atomicOr(c.sh->pool + w + (rel >> 5), 1u << (rel & 31));
+  } else {
+    __hip_atomic_fetch_or(gl(reinterpret_cast<uint32_t*>(bits)) + (e >> 5), 1u << (e & 31),
+                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// A fixed-width entry (write pass): value (0 when null), BOOL bit, validity bit.
+__device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t e, bool nul,
+                                        int64_t slotp, int rw) {
+  const uint64_t x = nul ? 0 : rdw(*c.R, slotp, rw);
+  if (N.type == FURY_TYPE_BOOL) {
+    if (N.values) wbit(c, N, n, 1, N.values, e, !nul && (x & 0xff));
+  } else if (N.values) {
+    tstore_w(N.values + e * N.width, N.width, x);
+  }
+  if (N.validity) wbit(c, N, n, 0, N.validity, e, !nul);
+}
+
+// Entry e of node n (non-scalar; scalars go through wscalar): slot at slotp in a container that
+// starts at cont (vpos >= 0: the value is AT vpos -- a collection batch's top-level entry).
+// Returns whether the value is valid.  Top-level callers (D == 0) set the validity themselves.
+// Every child item -- a STRUCT's fields, a LIST's elements, a MAP's keys then values -- goes
+// through ONE loop with one call of the next level, so the levels inline into straight code (no
+// call frames: a recursive call per level would keep every register of the walk live in scratch).
+template <int D, bool W, int MD>
+__device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul, int64_t slotp,
+                                       int64_t cont, int64_t vpos) {
+  if constexpr (D >= MD) {
+    return false;
+  } else {
+    n = __builtin_amdgcn_readfirstlane(n);      // every active lane is at the same node
+    const TreeArgs& a = *c.a;
+    const Rows& R = *c.R;
+    CTNode& N = tn(a, n);
+    const int ty = N.type;
+    int64_t pos = kNullPos;
+    uint32_t cnt = 0;
+    if (!nul) {
+      int32_t size = 0;
+      if (vpos >= 0) {
+        pos = vpos;
+      } else {
+        const uint64_t slot = rd8(R, slotp);
+        pos = cont + static_cast<int32_t>(slot >> 32);
+        size = static_cast<int32_t>(slot);
+      }
+      if (!tcheck(a, R, N, pos, size, c.total, &cnt, static_cast<uint64_t>(c.row))) pos = kNullPos;
+    }
+    const bool valid = pos >= 0;
+    if (W && D > 0 && N.validity) wbit(c, N, n, 0, N.validity, e, valid);
+    if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
+      uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+      const uint32_t c0 = *cu;
+      *cu = c0 + cnt;
+      if (W) {
+        const int64_t bp = c.sh->kb[N.k] + c0;
+        if (N.offsets) {
+          gl(N.offsets)[e + 1] = static_cast<int32_t>(bp + cnt);
+          if (e == 0) gl(N.offsets)[0] = 0;
+        }
+        if (valid && N.values) tcopy_out(N.values + bp, R, pos, cnt);
+      }
+      return valid;
+    }
+    if (ty == FURY_TYPE_DECIMAL) {
+      if (W && N.values) {
+        const auto d = gl(reinterpret_cast<uint64_t*>(N.values + 16 * e));
+        d[0] = valid ? rd8(R, pos) : 0;
+        d[1] = valid ? rd8(R, pos + 8) : 0;
+      }
+      return valid;
+    }
+    const bool strc = ty == FURY_TYPE_STRUCT;
+    if (!strc && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return valid;
+    // children: STRUCT -> its fields at entry e; LIST / MAP -> m elements from entry cs
+    uint32_t m = 0;
+    int64_t cs = 0;
+    if (strc) {
+      m = (W || valid) ? static_cast<uint32_t>(N.num_children) : 0u;
+    } else {
+      uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+      const uint32_t c0 = *cu;
+      m = cnt;
+      *cu = c0 + m;
+      if (W) {
+        cs = c.sh->kb[N.k] + c0;
+        if (N.offsets) {
+          gl(N.offsets)[e + 1] = static_cast<int32_t>(cs + m);
+          if (e == 0) gl(N.offsets)[0] = 0;
+        }
+      }
+    }
+    const int64_t hb = tbm(strc ? N.num_children : static_cast<int64_t>(m));
+    const int sides = ty == FURY_TYPE_MAP ? 2 : 1;
+    for (int sd = 0; sd < sides; sd++) {
+      int64_t arr = pos;                          // LIST / MAP side: the BinaryArray
+      if (ty == FURY_TYPE_MAP && m > 0)
+        arr = sd == 0 ? pos + 8 : pos + 8 + static_cast<int32_t>(rd8(R, pos));
+      if (!strc) {
+        CTNode& C = tn(a, N.first_child + sd);
+        if (!W && !C.walk) continue;              // nothing to count below
+      }
+      for (uint32_t j = 0; j < m; j++) {
+        const int cn = strc ? N.first_child + static_cast<int>(j) : N.first_child + sd;
+        CTNode& C = tn(a, __builtin_amdgcn_readfirstlane(cn));
+        int64_t ce, cslot, ccont;
+        bool cnul;
+        int crw;
+        if (strc) {
+          ce = e;
+          cnul = !valid || rdbit(R, pos, j);
+          cslot = pos + hb + 8 * static_cast<int64_t>(j);
+          ccont = pos;
+          crw = C.width;
+        } else {
+          ce = cs + j;
+          cnul = rdbit(R, arr + 8, j);
+          cslot = arr + 8 + hb + static_cast<int64_t>(C.esize) * j;
+          ccont = arr;
+          crw = C.esize;
+        }
+        if (C.width > 0) {
+          if (W) wscalar(c, C, cn, ce, cnul, cslot, crw);
+        } else if (W || C.walk) {
+          wvalue<D + 1, W, MD>(c, cn, ce, cnul, cslot, ccont, kNullPos);
+        }
+      }
+    }
+    return valid;
+  }
+}
+
+// The top level of one row (every thread of the workgroup, live or not: ballots).
+template <bool W, int MD>
+__device__ inline void walk_row(const WCtx& c, bool live) {
+  const TreeArgs& a = *c.a;
+  const Rows& R = *c.R;
+  const int64_t base = live ? gl(a.offs)[c.row] : 0;
+  if (a.root) {                                  // collection batch: the entry IS the value
+    bool valid = false;
+    if (live) valid = wvalue<0, W, MD>(c, 0, c.row, false, 0, 0, base);
+    CTNode& N = tn(a, 0);
+    if (W && N.validity) tballot_or(N.validity, c.wave_row, live && valid);
+    return;
+  }
+  bool rowok = false;
+  if (live) {
+    rowok = span_ok(base, tbm(a.ntop) + 8 * a.ntop, c.total);
+    if (!rowok) raise_oob(a.err, c.row);
+  }
+  const int64_t hb = tbm(a.ntop);
+  for (int f = 0; f < a.ntop; f++) {
+    CTNode& N = tn(a, f);
+    const bool nul = !rowok || rdbit(R, base, f);
+    const int64_t slotp = base + hb + 8 * f;
+    if (N.width > 0) {
+      if (W) {
+        const uint64_t x = (live && !nul) ? rdw(R, slotp, N.width) : 0;
+        if (N.type == FURY_TYPE_BOOL) {
+          if (N.values) tballot_or(N.values, c.wave_row, live && !nul && (x & 0xff));
+        } else if (live && N.values) {
+          tstore_w(N.values + c.row * N.width, N.width, x);
+        }
+        if (N.validity) tballot_or(N.validity, c.wave_row, live && !nul);
+      }
+      continue;
+    }
+    if (!W && !N.walk) continue;
+    bool valid = false;
+    if (live) valid = wvalue<0, W, MD>(c, f, c.row, nul, slotp, base, kNullPos);
+    if (W && N.validity) tballot_or(N.validity, c.wave_row, live && valid);
+  }
+}
+
+// Diagnostics (tuning "tree_debug"): thread 0 adds the time between marks to acc[id]; the kernel
+// adds acc to a.dbg[base + id] at the end (count pass base 0, write pass 16; see tree.hip).
+struct WClock {
+  uint64_t* acc;            // LDS [16] or NULL
+  __device__ void mark(int id) const {
+    if (acc && threadIdx.x == 0) {
+      const uint64_t t = __builtin_amdgcn_s_memrealtime();
+      acc[id] += t - acc[15];
+      acc[15] = t;
+    }
+  }
+  __device__ void start() const {
+    if (acc && threadIdx.x < 16) acc[threadIdx.x] = threadIdx.x == 15 ? __builtin_amdgcn_s_memrealtime() : 0;
+  }
+  __device__ void flush(uint64_t* dbg, int base) const {
+    if (acc && threadIdx.x < 15)
+      atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + base + threadIdx.x,
+                static_cast<unsigned long long>(acc[threadIdx.x]));
+    if (acc && threadIdx.x == 15)
+      atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + 64 + base / 16, 1ull);
+  }
+};
+
+// Pass 1: counted-slot totals of each row -> in-tile row prefixes (rowpre) and the tile's entries
+// / payload bytes of every node (cnt / byt [node][tile]).  A tile whose slot totals do not fit 32
+// bits sets *overflow (the level engine decodes the batch).
+template <int NT, int MD>
+__global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+  const WShared sh = walk_shared(wsm, a, NT, false);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t t = blockIdx.x;
+  const int64_t r0 = t * NT;
+  const int64_t nr = min<int64_t>(NT, a.nrows - r0);
+  const int64_t total = gl(a.offs)[a.nrows];
+  const bool live = tid < nr;
+  __shared__ uint64_t tacc[16];
+  const WClock clk{a.dbg ? tacc : nullptr};
+  clk.start();
+  for (int k = 0; k < a.K; k++) sh.cur[k * NT + tid] = 0;
+  const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
+  __syncthreads();
+  clk.mark(0);
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid};
+  walk_row<false, MD>(c, live);
+  clk.mark(1);
+  // in-tile exclusive prefix of every slot over the rows (row = thread)
+  uint64_t* wsum = sh.wsum;
+  for (int k = 0; k < a.K; k++) {
+    const uint64_t v = sh.cur[k * NT + tid];
+    const uint64_t inc = tw_scan64(v);
+    if (lane == 63) wsum[k * (NT / 64) + wave] = inc;
+    sh.cur[k * NT + tid] = static_cast<uint32_t>(inc - v);   // wave-exclusive for now
+  }
+  __syncthreads();
+  bool over = false;
+  for (int k = 0; k < a.K; k++) {
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; w++) {
+      const uint64_t s = wsum[k * (NT / 64) + w];
+      pre += w < wave ? s : 0;
+      tot += s;
+    }
+    over |= tot >= (1ull << 32);
+    if (live) gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] =
+        static_cast<uint32_t>(pre + sh.cur[k * NT + tid]);
+    if (tid == 0) sh.kb[k] = static_cast<int64_t>(tot);
+  }
+  if (over && tid == 0) __hip_atomic_store(a.overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  clk.mark(2);
+  for (int n = tid; n < a.nn; n += NT) {
+    CTNode& N = tn(a, n);
+    const int64_t ent = N.ek < 0 ? nr : sh.kb[N.ek];
+    const int64_t byt = (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY) ? sh.kb[N.k] : 0;
+    a.cnt[n * a.stride + t] = ent;
+    a.byt[n * a.stride + t] = byt;
+  }
+  clk.mark(3);
+  clk.flush(a.dbg, 0);
+}
+
+// Pass 2: the walk again, writing every output at its final position.
+template <int NT, int MD>
+__global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
+  const WShared sh = walk_shared(wsm, a, NT, true);
+  const int tid = threadIdx.x;
+  const int64_t t = blockIdx.x;
+  const int64_t r0 = t * NT;
+  const int64_t nr = min<int64_t>(NT, a.nrows - r0);
+  const int64_t total = gl(a.offs)[a.nrows];
+  const bool live = tid < nr;
+  const int nn = a.nn;
+  __shared__ uint64_t tacc[16];
+  const WClock clk{a.dbg ? tacc : nullptr};
+  clk.start();
+  for (int k = 0; k < a.K; k++)
+    sh.cur[k * NT + tid] = live ? gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] : 0u;
+  for (int k = tid; k < a.K; k += NT) {
+    const int n = a.knode[k];
+    CTNode& N = tn(a, n);
+    sh.kb[k] = (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY)
+                   ? a.byt[n * a.stride + t] : a.cnt[N.first_child * a.stride + t];
+  }
+  // bitmap windows of the nodes that are not row-aligned: words covering the tile's entries
+  for (int i = tid; i < 2 * nn; i += NT) {
+    const int n = i < nn ? i : i - nn;
+    CTNode& N = tn(a, n);
+    const bool want = N.ek >= 0 && (i < nn ? N.validity != nullptr
+                                           : (N.type == FURY_TYPE_BOOL && N.values != nullptr));
+    uint32_t words = 0;
+    if (want) {
+      const int64_t e0 = a.cnt[n * a.stride + t], e1 = a.cnt[n * a.stride + t + 1];
+      if (e1 > e0) words = static_cast<uint32_t>(((e1 - 1) >> 5) - (e0 >> 5) + 1);
+      if (i < nn) sh.w0[n] = e0 >> 5;
+    }
+    sh.req[i] = words;
+  }
+  if (tid == 0) sh.req[2 * nn] = 0;
+  const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
+  __syncthreads();
+  block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
+  const uint32_t pool_words = a.pool_cap / 4;
+  for (int i = tid; i < 2 * nn; i += NT) {
+    const uint32_t off = sh.req[i], end = sh.req[i + 1];
+    sh.win[i] = (end > off && end <= pool_words) ? static_cast<int32_t>(off) : -1;
+  }
+  const uint32_t used = min(sh.req[2 * nn], pool_words);
+  for (uint32_t i = tid; i < used; i += NT) sh.pool[i] = 0;
+  __syncthreads();
+  clk.mark(0);
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid};
+  walk_row<true, MD>(c, live);
+  clk.mark(1);
+  __syncthreads();
+  clk.mark(2);
+  // flush the windows: whole words; the first and last of each (shared with the neighbouring
+  // tiles) by atomic OR
+  for (uint32_t i = tid; i < used; i += NT) {
+    int lo = 0, hi = 2 * nn;                       // window: the last i0 with req[i0] <= i
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (sh.req[mid] <= i) lo = mid; else hi = mid;
+    }
+    while (lo + 1 < 2 * nn && sh.req[lo + 1] <= i) lo++;   // skip empty windows
+    if (sh.win[lo] < 0) continue;
+    const int n = lo < nn ? lo : lo - nn;
+    CTNode& N = tn(a, n);
+    uint8_t* bits = lo < nn ? N.validity : N.values;
+    const uint32_t off = sh.req[lo], end = sh.req[lo + 1];
+    const uint32_t v = sh.pool[i];
+    auto g = gl(reinterpret_cast<uint32_t*>(bits)) + sh.w0[n] + (i - off);
+    if (i == off || i + 1 == end) {
+      if (v) __hip_atomic_fetch_or(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *g = v;
+    }
+  }
+  clk.mark(3);
+  clk.flush(a.dbg, 16);
+}
+
+}  // namespace
+
+size_t walk_lds(const TreeArgs& a, int nt, bool write) {
+  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write).end;
+}
+
+int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
+  const size_t lds = walk_lds(a, nt, write);
+  auto go = [&](auto kern) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(a.ntiles)), dim3(nt), lds, hs, a);
+  };
+  // instances per schema depth (a level of the inlined walk keeps ~30 VGPRs live)
+#define FURY_WALK(MD)                                                                        \
+  if (a.nlevels <= MD) {                                                                     \
+    if (nt == 128) write ? go(walk_write_kernel<128, MD>) : go(walk_count_kernel<128, MD>);  \
+    else write ? go(walk_write_kernel<256, MD>) : go(walk_count_kernel<256, MD>);            \
+    return check_hip(hipGetLastError(), "walk decode launch");                               \
+  }
+  FURY_WALK(2)
+  FURY_WALK(3)
+  FURY_WALK(4)
+  FURY_WALK(5)
+#undef FURY_WALK
+  return set_error(FURY_ERR_UNSUPPORTED, "walk decode: schema deeper than kWalkMaxDepth");
+  return check_hip(hipGetLastError(), "walk decode launch");
+}
+
+}  // namespace fury

@@ -32,7 +32,9 @@ def engines():
     """Restores the default engine and LDS budgets after the test."""
     from fury_amd import _native as N
     L = N.lib()
-    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena")}
+    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena",
+                                                       "walk_threads", "walk_stage", "walk_pool",
+                                                       "walk_stage_write")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -83,10 +85,20 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
     _tune("nested_decode", 1)
     lv = _decode_plan(enc, batch)
     assert_columns_equal(fields, lv, tree, n)
+    if budget == "tiny":              # row walk: 1 KB stage (rows from HBM), no bitmap windows
+        _tune("walk_stage", 1024)
+        _tune("walk_stage_write", 2048)
+        _tune("walk_pool", 0)
+        _tune("walk_threads", 128)
+    _tune("nested_decode", 2)
+    walk = _decode_plan(enc, batch)
+    assert_columns_equal(fields, walk, ref, n)
 
 
-def test_tree_decode_large_batch(oracle, dev, engines):
-    """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode."""
+@pytest.mark.parametrize("mode", [0, 2])
+def test_tree_decode_large_batch(oracle, dev, engines, mode):
+    """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode, tile
+    walk (0) and row walk (2)."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     from tests.test_device import _nested_beans, _nested_fields
@@ -97,12 +109,12 @@ def test_tree_decode_large_batch(oracle, dev, engines):
     enc = Encoders.bean(fields, device=dev)
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_decode", 0)
+    _tune("nested_decode", mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
 
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
 def test_collections_both_engines(oracle, dev, engines, mode, kind):
     """ArrayEncoder / MapEncoder batches (root 1 / 2: each entry a top-level BinaryArray /
@@ -115,7 +127,8 @@ def test_collections_both_engines(oracle, dev, engines, mode, kind):
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
 
 
-def test_tree_decode_skewed_rows(oracle, dev, engines):
+@pytest.mark.parametrize("mode", [0, 2])
+def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     """Tiles whose bytes exceed the stage (rows of very different sizes): the rows past the stage
     are read from HBM, the result is the oracle's."""
     from fury_amd.beans import beans_to_columns
@@ -134,7 +147,7 @@ def test_tree_decode_skewed_rows(oracle, dev, engines):
     n = len(beans)
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_decode", 0)
+    _tune("nested_decode", mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
@@ -223,11 +236,11 @@ def _deep_fields(levels):
     f = T.field("leaf", T.INT64)
     depth = 1
     d = 0
-    while depth < levels - 1:
+    while depth < levels:
         if d % 3 == 1:
             f = T.Field(f"l{d}", T.LIST, True, (f,))
             depth += 1
-        elif d == 3 and depth + 2 <= levels - 1:
+        elif d == 3:
             f = T.map_field(f"m{d}", T.field("k", T.STRING), f)
             depth += 1
         else:
@@ -244,7 +257,7 @@ def _schema_levels(fields):
 
 
 @pytest.mark.parametrize("levels", [9, 12, 20])
-@pytest.mark.parametrize("dec_mode", [0, 1])
+@pytest.mark.parametrize("dec_mode", [0, 1, 2])
 def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_mode):
     """Depth 9 / 12 / 20 schemas: the encode takes the tree tiles by itself (the row interpreter
     stops at kGenMaxDepth levels), both decode engines read the rows back; bytes, offsets and
@@ -290,6 +303,7 @@ def test_deep_schema_row_too_large_for_chip_raises(oracle, dev, enc_engines):
     _tune("tree_measure_lds", 1024)
     with pytest.raises(UnsupportedOperationException, match="nested deeper"):
         enc.encode_batch(dcols, n)
+        enc.device_status()                           # the encode kernel's report (asynchronous)
     for k, v in old.items():
         _tune(k, v)
     b = enc.encode_batch(dcols, n)                    # the stream's error slot is clean again
