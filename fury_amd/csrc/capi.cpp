@@ -333,10 +333,6 @@ int common_checks(const fury_schema* s, const void* cols, int64_t nrows, const c
 
 int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
                bool need_validity, FixedArgs* a, bool* fast, DeviceTable* dt, hipStream_t hs) {
-  if (s->num_fields > kMaxWideFixedCols)
-    return set_error(FURY_ERR_UNSUPPORTED, "fixed-width device path handles at most " +
-                                               std::to_string(kMaxWideFixedCols) +
-                                               " fields (a 64-row tile must fit the LDS)");
   *a = FixedArgs{};
   a->ncols = s->num_fields;
   a->bitmap_bytes = s->bitmap_bytes;
@@ -668,7 +664,8 @@ int fury_row_decode_measure(const fury_schema* s, const void* rows, const int64_
   if (s->is_fixed) return FURY_OK;   // nothing variable to size
   if (s->generic)
     return set_error(FURY_ERR_INVALID_ARGUMENT,
-                     "nested schema: size outputs with fury_decode_prepare / fury_decode_execute");
+                     "nested (or > 256-field variable-length) schema: size outputs with "
+                     "fury_decode_prepare / fury_decode_execute");
   if (!rows || !row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows/row_offsets null");
   VarArgs a;
   DeviceTable dt;
@@ -700,7 +697,8 @@ static int decode_impl(const fury_schema* s, const void* rows, const int64_t* ro
   if (misaligned(rows, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "rows must be 8-byte aligned");
   if (s->generic)
     return set_error(FURY_ERR_INVALID_ARGUMENT,
-                     "nested schema: decode with fury_decode_prepare / fury_decode_execute");
+                     "nested (or > 256-field variable-length) schema: decode with "
+                     "fury_decode_prepare / fury_decode_execute");
   VarArgs a;
   DeviceTable dt;
   st = var_args(s, cols, nrows, true, arrow, &a, &dt, hs);

@@ -349,6 +349,100 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
   }
 }
 
+// ---- schemas wider than kMaxWideFixedCols: column blocks -----------------------------------
+// A 64-row tile of a very wide row no longer fits the LDS, so the grid is (row tile, column
+// block): block b owns fields [64b, 64b + 64) of 64 rows, i.e. null-bitmap WORD b and 512 slot
+// bytes of each row (BinaryRowWriter's bitmap is whole 64-bit words, so blocks never share a
+// word).  LDS image: 64 rows x (1 + 64) words; a row's two pieces are stored as 8-byte runs.
+constexpr int kBlkCols = 64;
+constexpr int kBlkRows = 64;
+constexpr int kBlkStride = kBlkCols + 1;        // LDS words per row: bitmap word + 64 slots
+
+__global__ __launch_bounds__(kThreads) void encode_fixed_blocks(FixedArgs a, uint8_t* __restrict__ rows) {
+  __shared__ uint64_t img[kBlkRows * kBlkStride];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kBlkRows;
+  const int nr = static_cast<int>(min(static_cast<int64_t>(kBlkRows), a.nrows - r0));
+  const int b = blockIdx.y, c0 = b * kBlkCols;
+  const int nc = min(kBlkCols, a.ncols - c0);
+  for (int r = threadIdx.x; r < kBlkRows; r += kThreads) img[r * kBlkStride] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nc * kBlkRows; i += kThreads) {
+    const int c = __builtin_amdgcn_readfirstlane(i / kBlkRows);   // a wave: 64 rows of one column
+    const int r = i - c * kBlkRows;
+    if (r >= nr) continue;
+    CFixedCol& fc = fcol(a, c0 + c);
+    const int64_t row = r0 + r;
+    const uint8_t* vb = fc.validity;
+    uint64_t v = 0;
+    if (vb && !((vb[row >> 3] >> (row & 7)) & 1))
+      atomicOr(reinterpret_cast<uint32_t*>(img + r * kBlkStride) + (c >> 5), 1u << (c & 31));
+    else
+      v = load_value(fc.values, row, fc.width);
+    img[r * kBlkStride + 1 + c] = v;
+  }
+  __syncthreads();
+  const int per = 1 + nc;
+  for (int i = threadIdx.x; i < nr * per; i += kThreads) {
+    const int r = i / per, j = i - r * per;
+    uint8_t* rowp = rows + (r0 + r) * a.row_size;
+    uint8_t* dst = j == 0 ? rowp + 8 * b : rowp + a.bitmap_bytes + 8 * (c0 + j - 1);
+    *reinterpret_cast<uint64_t*>(dst) = img[r * kBlkStride + j];
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void decode_fixed_blocks(FixedArgs a,
+                                                                const uint8_t* __restrict__ rows) {
+  __shared__ uint64_t img[kBlkRows * kBlkStride];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kBlkRows;
+  const int nr = static_cast<int>(min(static_cast<int64_t>(kBlkRows), a.nrows - r0));
+  const int b = blockIdx.y, c0 = b * kBlkCols;
+  const int nc = min(kBlkCols, a.ncols - c0);
+  const int per = 1 + nc;
+  for (int i = threadIdx.x; i < nr * per; i += kThreads) {
+    const int r = i / per, j = i - r * per;
+    const uint8_t* rowp = rows + (r0 + r) * a.row_size;
+    const uint8_t* src = j == 0 ? rowp + 8 * b : rowp + a.bitmap_bytes + 8 * (c0 + j - 1);
+    img[r * kBlkStride + j] = *reinterpret_cast<const uint64_t*>(src);
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < nc * kBlkRows; i += kThreads) {
+    const int c = __builtin_amdgcn_readfirstlane(i / kBlkRows);
+    const int r = i - c * kBlkRows;                      // = lane
+    const bool live = r < nr;
+    const int64_t row = r0 + r;
+    const bool isnull = live && ((img[r * kBlkStride] >> c) & 1);
+    const uint64_t v = live && !isnull ? img[r * kBlkStride + 1 + c] : 0;
+    CFixedCol& fc = fcol(a, c0 + c);
+    const int w = fc.width;
+    uint8_t* dst = const_cast<uint8_t*>(fc.values);
+    const int64_t rbase = row - lane;                    // r0: the wave's 64 rows
+    const int64_t nvalid = a.nrows - rbase;
+    const int nbytes = nvalid >= 64 ? 8 : static_cast<int>((nvalid + 7) >> 3);
+    if (w == 0) {                                        // BOOL: byte != 0, bit-packed
+      const uint64_t bitsv = __ballot(live && (v & 0xff) != 0);
+      if (lane < nbytes) dst[(rbase >> 3) + lane] = static_cast<uint8_t>(bitsv >> (8 * lane));
+    } else if (live) {
+      store_value(dst, row, w, v);
+    }
+    uint8_t* vb = fc.validity;
+    if (vb) {
+      const uint64_t ok = __ballot(live && !isnull);
+      if (lane < nbytes) vb[(rbase >> 3) + lane] = static_cast<uint8_t>(ok >> (8 * lane));
+    }
+  }
+}
+
+int launch_blocks(bool encode, const FixedArgs& a, uint8_t* rows, hipStream_t stream) {
+  const int64_t tiles = (a.nrows + kBlkRows - 1) / kBlkRows;
+  const int blocks = (a.ncols + kBlkCols - 1) / kBlkCols;
+  if (tiles > 0x7fffffff || blocks > 65535) return set_error(FURY_ERR_INVALID_ARGUMENT, "batch too large");
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(blocks));
+  if (encode) hipLaunchKernelGGL(encode_fixed_blocks, grid, dim3(kThreads), 0, stream, a, rows);
+  else hipLaunchKernelGGL(decode_fixed_blocks, grid, dim3(kThreads), 0, stream, a, rows);
+  return check_hip(hipGetLastError(), "fixed column-block launch");
+}
+
 }  // namespace
 
 // Host-direct mode of the calling thread (hostpath.cpp): the kernels run on pinned host memory
@@ -403,6 +497,7 @@ bool pair_ok(const FixedArgs& a) {
 //   host-direct calls: plain loads / stores (see t_host_direct).
 int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
+  if (a.ncols > kMaxWideFixedCols) return launch_blocks(true, a, rows, stream);
   const int R = pick_rows_per_tile(a.row_size);
 #define FURY_ENC(RR)                                                                          \
   if (R == RR) {                                                                              \
@@ -425,6 +520,7 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
 int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t stream, bool fast) {
   if (a.nrows == 0) return FURY_OK;
   uint8_t* r = const_cast<uint8_t*>(rows);
+  if (a.ncols > kMaxWideFixedCols) return launch_blocks(false, a, r, stream);
   const int R = pick_rows_per_tile(a.row_size);
   const bool pair = fast && !t_host_direct && pair_ok(a);
 #define FURY_DEC(RR)                                                                          \

@@ -30,7 +30,7 @@ __device__ __forceinline__ T* cast_as(U* p) {
 }
 
 // Columns per fixed-tile launch: the pointer table travels in the kernel argument block
-// (scalar-loaded, no per-call device upload).  Wider schemas are rejected.
+// (scalar-loaded, no per-call device upload).  Wider schemas upload it (FixedArgs.tab).
 constexpr int kMaxFixedCols = 128;
 
 // Per-column record.  Every member is naturally aligned inside an 8-byte-aligned record: the
@@ -45,8 +45,9 @@ struct FixedCol {
 };
 
 // Schemas wider than kMaxFixedCols take their column table from device memory (uploaded per
-// call, FixedArgs.tab) and run the general tile kernel with 64-row tiles; kMaxWideFixedCols keeps
-// a 64-row tile (bitmap + 8 B per field per row) within the 160 KB of LDS.
+// call, FixedArgs.tab) and run the general tile kernel with 64-row tiles up to kMaxWideFixedCols
+// (a 64-row tile, bitmap + 8 B per field per row, within the 160 KB of LDS); wider ones run the
+// column-block kernels (64 rows x 64 fields per workgroup, no field limit).
 constexpr int kMaxWideFixedCols = 315;
 
 struct FixedArgs {

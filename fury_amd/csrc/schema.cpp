@@ -20,6 +20,7 @@ constexpr int kGenMaxNodesHost = 4096;   // = kGenMaxWideNodes (kernels.h)
 constexpr int kGenMaxDepthHost = 65;     // tree tiles (kTEMaxLevels = 64 levels)
 constexpr int kInterpDepthHost = 8;      // = kGenMaxDepth: the row interpreter's unrolled depth
 constexpr int kTreeEncNodesHost = 256;   // tree-tile encode node table (generic.hip)
+constexpr int kMaxWideVarColsHost = 256; // = kMaxWideVarCols: the flat variable-length kernels
 
 static thread_local std::string g_last_error;
 
@@ -273,6 +274,13 @@ int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema
       s->nodes.push_back(t);
       s->depth = std::max(s->depth, depth[i]);
     }
+  }
+  // flat variable-length schemas wider than the flat kernels: the generic engine (row
+  // interpreter encode, plan-API decode), like nested ones
+  if (s->device_ok && !s->is_fixed && num_fields > kMaxWideVarColsHost) {
+    s->device_ok = 0;
+    s->device_reason = "variable-length schema wider than " + std::to_string(kMaxWideVarColsHost) +
+                       " fields";
   }
   if (!s->device_ok) {
     // nested fields: the generic engine handles them within its table limits

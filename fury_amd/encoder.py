@@ -416,9 +416,12 @@ class RowEncoder:
 
     @property
     def nested(self) -> bool:
-        """True when the schema has STRUCT / MAP / LIST-of-variable-length fields (decoded by the
-        two-step plan API); always for collection schemas."""
+        """True when the schema has STRUCT / MAP / LIST-of-variable-length fields, or more than
+        256 fields of which some are variable-length (decoded by the two-step plan API: the generic
+        engine); always for collection schemas."""
         if getattr(self._schema, "collection", False):
+            return True
+        if len(self._schema.fields) > 256 and not self._schema.is_fixed:
             return True
         def deep(f: Field) -> bool:
             if f.type_id in (STRUCT, MAP):

@@ -222,22 +222,22 @@ def test_collection_schema_create():
     assert L.fury_unframe_rows(m.handle, buf, 64, 1, buf, buf, None) == 2
 
 
-def test_wide_schema_limits_reported_on_host():
-    """Beyond the widest tiles (315 fixed-width / 256 variable-length fields) the device calls
-    report UnsupportedOperationException before touching the GPU."""
+def test_wide_schemas_accepted():
+    """No field limit (RowEncoderBuilder.java:154-217 emits a statement per field for any N): 316+
+    fixed-width fields take the column-block kernels, 257+ variable-length fields the generic
+    engine; argument errors are still reported on the host."""
     import numpy as np
     from fury_amd import _native as N
-    from fury_amd.encoder import Schema
+    from fury_amd.encoder import Encoders, Schema
     L = N.lib()
     buf = np.zeros(64, np.uint64)
-    for n, kind in ((316, T.INT64), (257, T.STRING)):
-        s = Schema([T.field(f"f{i:03d}", kind) for i in range(n)])
+    for n, kind in ((400, T.INT64), (300, T.STRING)):
+        fields = [T.field(f"f{i:03d}", kind) for i in range(n)]
+        s = Schema(fields)
         cols = (N.FuryColumn * n)()
         for k in range(n):
             cols[k].values = buf.ctypes.data
             cols[k].offsets = buf.ctypes.data
-        if kind == T.INT64:
-            assert L.fury_row_encode(s.handle, cols, 1, None, buf.ctypes.data, None) == 2
-        else:
-            assert L.fury_row_encode(s.handle, cols, 1, buf.ctypes.data, buf.ctypes.data, None) == 2
-        assert "at most" in N.last_error()
+        assert L.fury_row_encode(s.handle, cols, 1, buf.ctypes.data, None, None) == 1   # rows null
+        assert "rows is null" in N.last_error()
+        assert Encoders.bean(fields, device="cpu").nested == (kind == T.STRING)

@@ -1148,18 +1148,20 @@ def test_map_encoder_batch_vs_oracle(oracle, dev):
 
 
 # ---- round 2: schemas wider than the kernel argument block (column table in device memory) ----
-def test_wide_fixed_300_fields(oracle, dev):
-    """300 fixed-width fields (int8..int64, float, double, bool, date, timestamp; every third one
-    nullable): beyond the argument block's 128 columns the general tile kernel reads the column
-    table the host uploaded for the call.  Encode / decode / rows_to_arrow oracle-exact."""
+@pytest.mark.parametrize("ncols,n", [(300, 1500), (316, 777), (400, 1500), (1000, 129)])
+def test_wide_fixed_fields(oracle, dev, ncols, n):
+    """300 .. 1000 fixed-width fields (int8..int64, float, double, bool, date, timestamp; every
+    third one nullable): beyond the argument block's 128 columns the general tile kernel reads the
+    column table the host uploaded for the call; beyond 315 the column-block kernels (64 rows x 64
+    fields per workgroup) take over.  Encode / decode / rows_to_arrow oracle-exact."""
     from fury_amd.encoder import ArrowWriter, column_to_host
     kinds = [T.INT64, T.FLOAT64, T.INT32, T.BOOL, T.INT16, T.FLOAT32, T.INT8, T.DATE32, T.TIMESTAMP]
-    fields = [(T.field if i % 3 == 0 else T.not_null_field)(f"f{i:03d}", kinds[i % len(kinds)])
-              for i in range(300)]
-    n = 1500
-    host = gen_columns("wide", fields, n, seed=30, null_pct=15)
+    fields = [(T.field if i % 3 == 0 else T.not_null_field)(f"f{i:04d}", kinds[i % len(kinds)])
+              for i in range(ncols)]
+    host = gen_columns("wide", fields, n, seed=ncols, null_pct=15)
     enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
-    assert enc.schema().is_fixed and enc.schema().fixed_size == 40 + 8 * 300
+    assert enc.schema().is_fixed
+    assert enc.schema().fixed_size == (ncols + 63) // 64 * 8 + 8 * ncols
     want, offs = oracle.encode(fields, host, n)
     w = ArrowWriter(enc)
     w.write(batch)
@@ -1167,10 +1169,11 @@ def test_wide_fixed_300_fields(oracle, dev):
                          oracle.decode(fields, want, offs, n), n)
 
 
-@pytest.mark.parametrize("ncols,n", [(100, 2000), (200, 700), (256, 300)])
+@pytest.mark.parametrize("ncols,n", [(100, 2000), (200, 700), (256, 300), (257, 500), (300, 900)])
 def test_wide_var_schemas_beyond_arg_block(oracle, dev, ncols, n):
-    """100 / 200 / 256-field schemas with strings, lists, bools and nulls (multi-word row null
-    bitmaps): encode (measure + encode), encode_measured, decode and rows_to_arrow oracle-exact."""
+    """100 .. 300-field schemas with strings, lists, bools and nulls (multi-word row null bitmaps):
+    encode (measure + encode), encode_measured, decode and rows_to_arrow oracle-exact.  Beyond 256
+    fields the generic engine (row interpreter encode, plan-API decode) runs them."""
     from fury_amd.encoder import ArrowWriter, column_to_host
     fields = _wide_fields(ncols)
     host = gen_columns("wide", fields, n, seed=ncols, null_pct=20, str_max=48, list_max=9,
