@@ -4,7 +4,8 @@ encode / decode pipelines (C3 mixed, C4 nested bench workloads).
 Per kernel: median FETCH_SIZE / WRITE_SIZE (KB per dispatch) over the bench's dispatches, with the
 gfx950 corrections of MI355X_MICROARCH.md §HBM as calibrated on tools/hbm_probe in
 profiles/pmc_struct100.json (FETCH_SIZE counts half of the bytes of 8- and 16-B-per-lane reads:
-x2; WRITE_SIZE exact: x1).  Encode = measure_tiles (or measure_kernel + add_group_prefix) + encode_var_reg + the scan kernels;
+x2; WRITE_SIZE exact: x1).  Encode = measure_tiles + encode_var_reg + the scan kernels (the bench's untimed
+pre-size, measure_kernel + add_group_prefix, is listed but not counted);
 decode = decode_var_reg (decode_measure_* run only in the untimed sizing path).  Algorithmic bytes per launch come from the bench line in the same
 pass's log (encode and decode both move column bytes + row bytes: half of a step).
 
@@ -58,9 +59,12 @@ def main():
         kernels[short(k)] = {"kernel": k, "FETCH_SIZE_KB": fetch.get(k), "WRITE_SIZE_KB": write.get(k),
                              "fetch_bytes_corrected": round(fb), "write_bytes_corrected": round(wb),
                              "hbm_bytes_per_launch": round(fb + wb)}
-    enc = sum(v["hbm_bytes_per_launch"] for n, v in kernels.items()
-              if n.startswith(("encode_var", "measure_kernel", "measure_tiles", "add_group_prefix",
-                                   "scan_", "add_groups")))
+    # the timed encode is fury_row_encode_measured: measure_tiles + scans + encode_var_reg; the
+    # row-sized measure_kernel + add_group_prefix only pre-size the bench's buffer (untimed)
+    timed = ("encode_var", "measure_tiles", "scan_", "add_groups") if any(
+        n.startswith("measure_tiles") for n in kernels) else (
+        "encode_var", "measure_kernel", "add_group_prefix", "scan_", "add_groups")
+    enc = sum(v["hbm_bytes_per_launch"] for n, v in kernels.items() if n.startswith(timed))
     dec = sum(v["hbm_bytes_per_launch"] for n, v in kernels.items()
               if n.startswith("decode_var"))
     res = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
