@@ -434,13 +434,76 @@ bool view_inputs(const fury_schema* s, const fury_column* host, int64_t n,
   return true;
 }
 
+// Device views of a generic (nested / collection / very wide) schema's host input column tree,
+// breadth-first like the schema nodes (a node's children contiguous: child = &d[first_child]);
+// every node's entry count follows from its parent's (STRUCT: the same; LIST / MAP: the parent's
+// offsets[m], read on the host).  False when a buffer is pageable, misaligned or missing (the call
+// is then staged, which reports argument errors).
+bool view_gen_inputs(const fury_schema* s, const fury_column* host, int64_t n,
+                     std::vector<fury_column>& d) {
+  const int nn = static_cast<int>(s->nodes.size());
+  std::vector<const fury_column*> hc(nn, nullptr);
+  std::vector<int64_t> m(nn, 0);
+  d.assign(nn, fury_column{});
+  for (int k = 0; k < s->num_fields; k++) {
+    hc[k] = &host[k];
+    m[k] = n;
+  }
+  for (int i = 0; i < nn; i++) {
+    const GenTpl& t = s->nodes[i];
+    if (!hc[i]) return false;
+    const fury_column& h = *hc[i];
+    fury_column& c = d[i];
+    const int64_t mi = m[i];
+    uint8_t* v = nullptr;
+    if (h.validity) {
+      if (!(v = device_view(h.validity, (mi + 7) / 8 > 0 ? (mi + 7) / 8 : 1))) return false;
+      c.validity = v;
+    }
+    const int t_id = t.type_id;
+    const bool var = t_id == FURY_TYPE_STRING || t_id == FURY_TYPE_BINARY ||
+                     t_id == FURY_TYPE_LIST || t_id == FURY_TYPE_MAP;
+    int64_t end = 0;                                    // offsets[m]: payload bytes / elements
+    if (var) {
+      if (!h.offsets) return false;
+      if (!(v = device_view(h.offsets, (mi + 1) * 4)) || !aligned_to(v, 4)) return false;
+      c.offsets = reinterpret_cast<int32_t*>(v);
+      end = h.offsets[mi];
+      if (end < 0) return false;
+    }
+    const int w = type_width_of(t_id);
+    if (t_id == FURY_TYPE_BOOL) {
+      if (h.values && !(c.values = device_view(h.values, std::max<int64_t>((mi + 7) / 8, 1)))) return false;
+    } else if (w > 0) {
+      if (mi > 0 && (!(v = device_view(h.values, mi * w)) || !aligned_to(v, w))) return false;
+      c.values = v;
+    } else if (t_id == FURY_TYPE_DECIMAL) {
+      if (mi > 0 && (!(v = device_view(h.values, 16 * mi)) || !aligned_to(v, 8))) return false;
+      c.values = v;
+    } else if (t_id == FURY_TYPE_STRING || t_id == FURY_TYPE_BINARY) {
+      if (end > 0 && !(c.values = device_view(h.values, end))) return false;
+    }
+    if (t.num_children > 0) {
+      if (!h.child) return false;
+      const int64_t cm = t_id == FURY_TYPE_STRUCT ? mi : end;
+      for (int j = 0; j < t.num_children; j++) {
+        hc[t.first_child + j] = &h.child[j];
+        m[t.first_child + j] = cm;
+      }
+      c.child = &d[t.first_child];
+    }
+  }
+  return true;
+}
+
 int var_encode_direct(const fury_schema* s, const fury_column* host, int64_t n, uint8_t* rows,
                       int64_t cap, int64_t* row_offsets, int64_t* row_bytes, int32_t device,
                       bool* used) {
   *used = false;
-  if (s->generic || n == 0 || cap <= 0) return FURY_OK;
+  if (n == 0 || cap <= 0) return FURY_OK;
   std::vector<fury_column> d, dchild;
-  if (!view_inputs(s, host, n, d, dchild)) return FURY_OK;
+  if (s->generic ? !view_gen_inputs(s, host, n, d) : !view_inputs(s, host, n, d, dchild))
+    return FURY_OK;
   uint8_t* drows = device_view(rows, cap);
   if (!drows || !aligned_to(drows, 16) || !device_view(row_offsets, (n + 1) * 8)) return FURY_OK;
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
@@ -789,9 +852,29 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
   hipStream_t hs = nullptr;
   if ((st = check_hip(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking), "hipStreamCreate")))
     return st;
-  // stage the rows and their offsets (fixed-width rows: offsets i * fixed_size) in HBM
   const int64_t total = nrows == 0 ? 0 : s->is_fixed && !row_offsets ? nrows * s->fixed_size
                                                                       : row_offsets[nrows];
+  // pinned rows and offsets: the prepare (and later the execute) kernels read them in place over
+  // PCIe -- every read an 8-byte word or a 16-byte LDS-DMA block holding a byte of the batch
+  if (nrows > 0 && row_offsets && total > 0) {
+    const uint8_t* drows = device_view(rows, total);
+    const uint8_t* doffs = device_view(row_offsets, (nrows + 1) * 8);
+    if (drows && doffs && aligned_to(drows, 8) && aligned_to(doffs, 8)) {
+      fury_decode_plan* p = nullptr;
+      st = fury_decode_prepare(s, drows, reinterpret_cast<const int64_t*>(doffs), nrows,
+                               node_entries, node_bytes, &p, hs);
+      if (st) {
+        (void)hipStreamDestroy(hs);
+        return st;
+      }
+      p->owned_stream = hs;
+      p->device = device;
+      p->direct = true;
+      *plan = p;
+      return FURY_OK;
+    }
+  }
+  // stage the rows and their offsets (fixed-width rows: offsets i * fixed_size) in HBM
   uint8_t* d = nullptr;
   const int64_t rb = (total + 255) & ~int64_t(255);
   keep_pool(device);
@@ -853,6 +936,10 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
   }
   DeviceArena arena(hs);
   std::vector<fury_column> dc(nn);
+  // Outputs the kernels write exactly (values, offsets, payloads) go straight into pinned host
+  // buffers; bitmaps (written as words / by atomics) and pageable buffers through HBM + a copy.
+  std::vector<uint8_t> copy_off(nn, 1), copy_val(nn, 1);
+  bool all_direct = p->direct;
   for (int i = 0; i < nn; i++) {
     const GenTpl& t = s->nodes[i];
     const fury_column& h = *hc[i];
@@ -867,8 +954,15 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     }
     if (node_has_offsets(t.type_id)) {
       if (!h.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": output offsets is null");
-      if ((st = arena.alloc((m + 1) * 4, &v))) return st;
-      d.offsets = static_cast<int32_t*>(v);
+      uint8_t* view = device_view(h.offsets, (m + 1) * 4);
+      if (view && aligned_to(view, 4)) {
+        d.offsets = reinterpret_cast<int32_t*>(view);
+        copy_off[i] = 0;
+      } else {
+        all_direct = false;
+        if ((st = arena.alloc((m + 1) * 4, &v))) return st;
+        d.offsets = static_cast<int32_t*>(v);
+      }
     }
     const int64_t vb = node_values_bytes(t.type_id, m, b);
     if (t.type_id != FURY_TYPE_LIST && t.type_id != FURY_TYPE_MAP && t.type_id != FURY_TYPE_STRUCT) {
@@ -877,10 +971,19 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
       if ((t.type_id == FURY_TYPE_STRING || t.type_id == FURY_TYPE_BINARY) && h.capacity < vb)
         return set_error(FURY_ERR_CAPACITY, "node " + std::to_string(i) + " needs " +
                                                 std::to_string(vb) + " payload bytes");
-      const int64_t alloc = t.type_id == FURY_TYPE_BOOL ? bitmap_alloc(m) : vb + 16;
-      if ((st = arena.alloc(alloc, &v))) return st;
-      if (t.type_id == FURY_TYPE_BOOL) (void)hipMemsetAsync(v, 0, alloc, hs);
-      d.values = v;
+      const int w = type_width_of(t.type_id);
+      const int al = t.type_id == FURY_TYPE_DECIMAL ? 8 : w > 0 ? w : 1;
+      uint8_t* view = t.type_id != FURY_TYPE_BOOL && vb > 0 ? device_view(h.values, vb) : nullptr;
+      if (view && aligned_to(view, al)) {
+        d.values = view;
+        copy_val[i] = 0;
+      } else {
+        if (t.type_id != FURY_TYPE_BOOL && vb > 0) all_direct = false;
+        const int64_t alloc = t.type_id == FURY_TYPE_BOOL ? bitmap_alloc(m) : vb + 16;
+        if ((st = arena.alloc(alloc, &v))) return st;
+        if (t.type_id == FURY_TYPE_BOOL) (void)hipMemsetAsync(v, 0, alloc, hs);
+        d.values = v;
+      }
       d.capacity = vb;
     }
     if (t.num_children > 0) d.child = &dc[t.first_child];
@@ -893,10 +996,13 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     const int64_t m = p->totals[2 * i], b = p->totals[2 * i + 1];
     if (h.validity && m > 0)
       (void)hipMemcpyAsync(h.validity, d.validity, (m + 7) / 8, hipMemcpyDeviceToHost, hs);
-    if (d.offsets) (void)hipMemcpyAsync(h.offsets, d.offsets, (m + 1) * 4, hipMemcpyDeviceToHost, hs);
+    if (d.offsets && copy_off[i])
+      (void)hipMemcpyAsync(h.offsets, d.offsets, (m + 1) * 4, hipMemcpyDeviceToHost, hs);
     const int64_t vb = node_values_bytes(t.type_id, m, b);
-    if (d.values && vb > 0) (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
+    if (d.values && vb > 0 && copy_val[i])
+      (void)hipMemcpyAsync(h.values, d.values, vb, hipMemcpyDeviceToHost, hs);
   }
+  if (all_direct) g_host_direct.fetch_add(1);
   st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
   return st ? st : take_device_error(hs);
 }

@@ -54,6 +54,8 @@ struct TreeArgs {
   uint32_t* rowpre;         // [K][nrows]: a row's in-tile exclusive prefix of counted slot k
   int32_t K;                // counted slots
   uint32_t pool_cap;        // LDS bytes of the bitmap windows (write pass)
+  int32_t prefetch;         // write pass: each wave first pulls its rows' lines (tuning)
+  int32_t pad2_;
   int32_t knode[64];        // counted slot -> node
 };
 

@@ -41,15 +41,16 @@ struct WShared {
   uint32_t* req;            // [2][nn + 1]: window words, scanned into window offsets
   uint64_t* wsum;           // [K][NT / 64] (pass 1) / [16] (pass 2) scan scratch
   uint32_t* pool;           // window words
+  uint8_t* pf;              // prefetch landing zone
   uint8_t* stg;             // staged rows
 };
 
 struct WLayout {
-  size_t cur, kb, win, w0, req, wsum, pool, stg, end;
+  size_t cur, kb, win, w0, req, wsum, pool, pf, stg, end;
 };
 
 __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t stage, uint32_t pool,
-                                               bool write) {
+                                               bool write, bool prefetch) {
   WLayout l{};
   size_t b = 0;
   l.cur = b;
@@ -70,6 +71,8 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   l.pool = b;
   b += write ? pool : 0;
   b = (b + 15) & ~size_t(15);
+  l.pf = b;                                   // prefetch landing zone: 1 KB per wave
+  b += write && prefetch ? 1024 * static_cast<size_t>(nt / 64) : 0;
   l.stg = b;
   b += stage;
   l.end = (b + 15) & ~size_t(15);
@@ -77,7 +80,7 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
 }
 
 __device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, bool write) {
-  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write);
+  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0);
   WShared s;
   s.cur = reinterpret_cast<uint32_t*>(base + l.cur);
   s.kb = reinterpret_cast<int64_t*>(base + l.kb);
@@ -86,6 +89,7 @@ __device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, 
   s.req = reinterpret_cast<uint32_t*>(base + l.req);
   s.wsum = reinterpret_cast<uint64_t*>(base + l.wsum);
   s.pool = reinterpret_cast<uint32_t*>(base + l.pool);
+  s.pf = base + l.pf;
   s.stg = base + l.stg;
   return s;
 }
@@ -427,6 +431,22 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   }
   if (tid == 0) sh.req[2 * nn] = 0;
   const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
+  if (a.prefetch) {
+    // the wave's 64 rows are one contiguous byte range: pull its lines into the caches with
+    // coalesced 16-B LDS-DMA loads into a scratch zone (data discarded), so the walk's dependent
+    // reads below hit L2 instead of each paying an HBM round trip
+    const int64_t wr0 = r0 + (tid & ~63);
+    if (wr0 < a.nrows) {
+      const int64_t wr1 = min<int64_t>(wr0 + 64, a.nrows);
+      const int64_t g0 = min<int64_t>(max<int64_t>(gl(a.offs)[wr0], 0), total);
+      const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[wr1], g0), total);
+      const uintptr_t lo = reinterpret_cast<uintptr_t>(a.rows + g0) & ~uintptr_t(15);
+      const uintptr_t hi = (reinterpret_cast<uintptr_t>(a.rows + g1) + 15) & ~uintptr_t(15);
+      uint8_t* land = sh.pf + 1024 * (tid >> 6);
+      for (uintptr_t q = lo + 16 * (tid & 63); q < hi; q += 1024)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q), land, 16, 0, 0);
+    }
+  }
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
   const uint32_t pool_words = a.pool_cap / 4;
@@ -472,7 +492,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
 }  // namespace
 
 size_t walk_lds(const TreeArgs& a, int nt, bool write) {
-  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write).end;
+  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0).end;
 }
 
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {

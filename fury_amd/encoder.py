@@ -630,13 +630,14 @@ class RowEncoder:
         return rows[:nb.value], row_offsets
 
     def decode_host(self, rows, row_offsets, nrows: int, out: Optional[List[Column]] = None,
-                    device_index: int = 0) -> List[Column]:
-        """Host rows -> host columns through HBM (``fury_row_decode_host``).  Without ``out``,
-        numpy columns are allocated: validity for nullable fields, and payload / element
-        buffers bounded by the row bytes (a row holds every byte it decodes to)."""
+                    device_index: int = 0, pinned: bool = False) -> List[Column]:
+        """Host rows -> host columns (``fury_row_decode_host``; nested schemas through the
+        two-step host decode).  Without ``out``, numpy columns are allocated (pinned ones with
+        ``pinned``, nested schemas): validity for nullable fields, and payload / element buffers
+        bounded by the row bytes (a row holds every byte it decodes to)."""
         from .workloads import Column as C
         if self.nested and out is None:
-            return self._decode_host_nested(rows, row_offsets, nrows, device_index)
+            return self._decode_host_nested(rows, row_offsets, nrows, device_index, pinned)
         if out is None:
             out = []
             rb = max(_nbytes(rows), 16)
@@ -663,9 +664,11 @@ class RowEncoder:
                                             nrows, _c_host_columns(out, keep), device_index))
         return out
 
-    def _decode_host_nested(self, rows, row_offsets, nrows: int, device_index: int = 0):
+    def _decode_host_nested(self, rows, row_offsets, nrows: int, device_index: int = 0,
+                            pinned: bool = False):
         """Nested schemas through fury_decode_host_prepare / fury_decode_host_execute: node
-        sizes first, then numpy buffers of exactly those sizes, filled in one call."""
+        sizes first, then host buffers of exactly those sizes (pinned: written in place by the
+        kernels), filled in one call."""
         L = N.lib()
         h = self._schema.handle
         nn = L.fury_schema_num_nodes(h)
@@ -676,7 +679,8 @@ class RowEncoder:
                                           nbytes, ctypes.byref(plan), device_index))
         try:
             order = _bfs(self._schema.fields)
-            cols = [_alloc_host_node(f, int(entries[i]), int(nbytes[i]))
+            zeros = _pinned_zeros if pinned else np.zeros
+            cols = [_alloc_host_node(f, int(entries[i]), int(nbytes[i]), zeros)
                     for i, (f, _) in enumerate(order)]
             for i, (f, first) in enumerate(order):
                 if f.children:
@@ -798,22 +802,28 @@ def _node_sizes(order, cols: List[Column], n: int, stream=None):
     return m, b
 
 
-def _alloc_host_node(f: Field, m: int, nbytes: int) -> Column:
-    """Host (numpy) buffers for one schema node with m Arrow entries (fury_decode_host_execute
-    contract: exact sizes)."""
-    vb = np.zeros((m + 7) // 8 + 8, np.uint8)
+def _pinned_zeros(n: int, dtype=np.uint8) -> np.ndarray:
+    a = host_empty(max(int(n), 1) * np.dtype(dtype).itemsize, dtype)
+    a[:] = 0
+    return a[:n]
+
+
+def _alloc_host_node(f: Field, m: int, nbytes: int, zeros=np.zeros) -> Column:
+    """Host buffers for one schema node with m Arrow entries (fury_decode_host_execute contract:
+    exact sizes); ``zeros=_pinned_zeros`` gives pinned ones (the execute writes them in place)."""
+    vb = zeros((m + 7) // 8 + 8, np.uint8)
     t = f.type_id
     if t == BOOL:
-        return Column(values=np.zeros((m + 7) // 8 + 8, np.uint8), validity=vb)
+        return Column(values=zeros((m + 7) // 8 + 8, np.uint8), validity=vb)
     if type_width(t) > 0:
-        return Column(values=np.zeros(m * type_width(t) + 8, np.uint8), validity=vb)
+        return Column(values=zeros(m * type_width(t) + 8, np.uint8), validity=vb)
     if t in (STRING, BINARY):
-        return Column(values=np.zeros(max(nbytes, 1), np.uint8), validity=vb,
-                      offsets=np.zeros(m + 1, np.int32))
+        return Column(values=zeros(max(nbytes, 1), np.uint8), validity=vb,
+                      offsets=zeros(m + 1, np.int32))
     if t == DECIMAL:
-        return Column(values=np.zeros(16 * m + 16, np.uint8), validity=vb)
+        return Column(values=zeros(16 * m + 16, np.uint8), validity=vb)
     if t in (LIST, MAP):
-        return Column(validity=vb, offsets=np.zeros(m + 1, np.int32))
+        return Column(validity=vb, offsets=zeros(m + 1, np.int32))
     if t == STRUCT:
         return Column(validity=vb)
     raise UnsupportedOperationException(f"no device decode for {f}")

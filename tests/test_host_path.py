@@ -306,3 +306,59 @@ def test_host_direct_var_capacity_short(oracle):
         enc.decode_host(rows, roffs, n, out=out)
     assert N.lib().fury_get_tuning(b"host_direct") == d0 + 1, "decode did not take the direct path"
     assert bool((guard[full.nbytes - 1:] == 0xAB).all()), "decode wrote past the capacity"
+
+
+def _page_zeros(n, dtype=np.uint8):
+    a = _page_tail(max(int(n), 1) * np.dtype(dtype).itemsize, dtype)
+    a[:] = 0
+    return a[:n]
+
+
+@pytest.mark.parametrize("name,n", [("foo", 3001), ("beana", 1200), ("nested7", 5000),
+                                    ("maps", 777), ("nested7", 1)])
+def test_host_direct_nested_page_edge(oracle, name, n):
+    """Nested schemas (RowEncoderTest's Foo and BeanA among them) on pinned buffers run their
+    kernels on host memory: the encode reads the column tree and writes rows in place, the decode
+    plan reads the pinned rows in place and the execute writes values / offsets / payloads into
+    the pinned outputs (bitmaps through HBM) -- host_direct counts both.  Every buffer ends at a
+    page edge; rows, offsets and columns bit-exact vs the oracle."""
+    import ctypes
+    from fury_amd import _native as N
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, _alloc_host_node, _bfs, _c_host_columns
+    from tests.test_tree import _beans, _schemas
+    fields = _schemas()[name]
+    beans = _beans(fields, n, n + len(name))
+    host = beans_to_columns(fields, beans)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    enc = Encoders.bean(fields, device="cuda:0")
+    L = N.lib()
+    d0 = L.fury_get_tuning(b"host_direct")
+    cols = [_tail_tree(c, True) for c in host]
+    rows = _page_tail((want.size + 15) // 16 * 16)
+    roffs = _page_tail(8 * (n + 1), np.int64)
+    got, offs = enc.encode_host(cols, n, rows=rows, row_offsets=roffs)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 1, "encode did not take the direct path"
+    assert np.array_equal(got, want) and np.array_equal(offs, want_offs)
+    nn = L.fury_schema_num_nodes(enc.schema().handle)
+    e = (ctypes.c_int64 * nn)()
+    b = (ctypes.c_int64 * nn)()
+    plan = ctypes.c_void_p()
+    assert L.fury_decode_host_prepare(enc.schema().handle, rows.ctypes.data, roffs.ctypes.data,
+                                      n, e, b, ctypes.byref(plan), 0) == 0, N.last_error()
+    try:
+        order = _bfs(fields)
+        out = [_alloc_host_node(f, int(e[i]), int(b[i]), _page_zeros) for i, (f, _) in enumerate(order)]
+        for i, (f, first) in enumerate(order):
+            if f.children:
+                out[i].child = [out[first + j] for j in range(len(f.children))]
+        keep = []
+        assert L.fury_decode_host_execute(plan, _c_host_columns(out[:len(fields)], keep)) == 0, \
+            N.last_error()
+    finally:
+        L.fury_decode_plan_destroy(plan)
+    assert L.fury_get_tuning(b"host_direct") == d0 + 2, "decode did not take the direct path"
+    top = out[:len(fields)]
+    assert_columns_equal(fields, top, ref, n)
+    assert columns_to_beans(fields, top, n) == beans
