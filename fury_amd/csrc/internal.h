@@ -80,7 +80,6 @@ struct fury_decode_plan {
   void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)
   void* owned_stream = nullptr;    // host flavour: its stream
   int32_t device = 0;
-  bool direct = false;             // host flavour: the kernels read the pinned host rows in place
 };
 
 namespace fury {

@@ -216,6 +216,8 @@ int workspace_reserve(size_t bytes, void** out);
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
 int64_t lookback_timeouts();
+int var_wide_mode();                  // tuning "var_wide" (var.hip)
+void set_var_wide_mode(int v);
 int lookback_help_mode();
 void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);

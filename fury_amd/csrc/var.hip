@@ -65,6 +65,11 @@ int64_t lookback_timeouts() { return device_error_count(); }
 // Test hook (tuning "lookback_help"): every look-back computes a silent predecessor's aggregate
 // at once -- the path a late-dispatched predecessor takes -- instead of polling first.
 static int g_help_now = 0;
+// Tuning "var_wide": decode of schemas wider than kRegCols -- 4 / 8 / 16: the row-staged kernel
+// in chunks of that many fields (default 8), 0: the 256-row tile kernel (decode_var_kernel).
+static int g_var_wide = 8;
+int var_wide_mode() { return g_var_wide; }
+void set_var_wide_mode(int v) { g_var_wide = v; }
 int lookback_help_mode() { return g_help_now; }
 void set_lookback_help_mode(int v) { g_help_now = v; }
 // Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
@@ -183,24 +188,30 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 // bound sizing); a tile whose payload outgrows its image stores that column straight to HBM and
 // rows past the stage are read from HBM (both correct, slower), so the estimate only moves speed.
 // mixed (C3): 512-row tiles.
-void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) {
+void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage, int chunk = kRegCols) {
   constexpr int64_t kBudget = 80 * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
-  double row = a.fixed_size, img_row = 0, img_fix = 0;
+  // images: the largest chunk's (schemas wider than kRegCols decode kRegCols fields at a time)
+  double row = a.fixed_size, img_row = 0, img_fix = 0, chunk_row = 0, chunk_fix = 0;
   for (int k = 0; k < a.ncols; k++) {
+    if (k % chunk == 0) {
+      chunk_row = chunk_fix = 0;
+    }
     const VarCol& c = hcol(a, k);
     const double per = a.nrows > 0 && c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 16.0;
     if (c.kind == kDecimal) row += 16;
     if (c.kind == kBytes) {
       row += per + 4;
-      if (c.values) { img_row += per; img_fix += 80; }
+      if (c.values) { chunk_row += per; chunk_fix += 80; }
     }
     if (c.kind == kListFixed) {
       row += 12 + per * (c.width == 0 ? 1 : c.width) + 4;
       if (c.values) {
-        img_row += per * (c.width == 0 ? 0.125 : c.width) + (c.elem_validity ? per / 8 : 0);
-        img_fix += c.elem_validity ? 160 : 80;
+        chunk_row += per * (c.width == 0 ? 0.125 : c.width) + (c.elem_validity ? per / 8 : 0);
+        chunk_fix += c.elem_validity ? 160 : 80;
       }
     }
+    if (chunk_row > img_row) img_row = chunk_row;
+    if (chunk_fix > img_fix) img_fix = chunk_fix;
   }
   // headroom over the estimates: 8 % on the images, 2 % on the stage (a 512-row tile's bytes
   // vary by ~1 %; C4 0.252 -> 0.229 ms against 15 % / 5 %, mixed unchanged)
@@ -238,6 +249,23 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     if (!st) st = launch_decode_var_reg(b, rows, offs, ws, img, stage, mode, nt, stream);
+    dev_free(ws, stream);
+    return st;
+  }
+  if (var_wide_mode() > 0) {
+    // wider than kRegCols: the row-staged kernel in chunks of kc fields (one row read)
+    const int kc = var_wide_mode();
+    VarArgs b = a;
+    uint32_t img = 0, stage = 0;
+    dec_tile_plan(a, &b.tile_rows, &img, &stage, kc);
+    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
+    const int64_t nch = (a.ncols + kc - 1) / kc;
+    const size_t wsb = static_cast<size_t>(nt) * kc * nch * 8;
+    uint64_t* ws = nullptr;
+    int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
+    if (st) return st;
+    st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
+    if (!st) st = launch_decode_var_reg_wide(b, rows, offs, ws, img, stage, mode, nt, kc, stream);
     dev_free(ws, stream);
     return st;
   }

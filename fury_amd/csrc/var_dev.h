@@ -655,16 +655,16 @@ constexpr int kSeqBytes = 0, kSeqLists = 1, kSeqAll = 2;
 // fields (kSeqLists), as the host checks (reg_mode), map every kind onto those three, so the
 // compiler drops the other kinds' code from the unrolled K-column bodies (mixed decode, K = 6:
 // 7.1k instead of 18k instructions; the full body cost it ~10 % in instruction-cache misses).
-template <int M>
-__device__ __forceinline__ int kind_of(const VarCol& c) {
+template <int M, class C>
+__device__ __forceinline__ int kind_of(const C& c) {
   const int kd = c.kind;
   if (M == kSeqAll) return kd;
   const int seq = M == kSeqBytes ? kBytes : kListFixed;
   return kd == seq ? seq : (kd == kBool ? kBool : kFixed);
 }
 // a sequence column's payload is bytes (else list elements)
-template <int M>
-__device__ __forceinline__ bool bytes_seq(const VarCol& c) {
+template <int M, class C>
+__device__ __forceinline__ bool bytes_seq(const C& c) {
   return M == kSeqBytes || (M == kSeqAll && c.kind == kBytes);
 }
 __device__ __forceinline__ bool seq_kind(int kd) { return kd == kBytes || kd == kListFixed; }
@@ -1366,7 +1366,19 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 
 #ifdef FURY_VAR_DEC
 // (K <= 4: at most 128 VGPRs, so two 512-thread workgroups share a CU -- the LDS plan assumes two)
-template <int K, int M>
+// Column k of the chunk starting at c0: the argument block's record (one chunk, K >= the field
+// count), or -- chunked instances for schemas wider than kRegCols -- record c0 + k of the block or
+// the uploaded table.
+template <bool CH>
+__device__ __forceinline__ auto& vcol(const VarArgs& a, int c0, int k) {
+  if constexpr (CH) return vc(a, c0 + k);
+  else return a.col[k];
+}
+
+// CH (chunked): the schema's fields in chunks of K = kRegCols, decoded one chunk after the other
+// from the same staged tile (one row read for all chunks); each chunk has its own status words
+// (tiles x K, after the previous chunk's) and reuses the images, zeroed again between chunks.
+template <int K, int M, bool CH = false>
 __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <= 4 ? 4 : 1))) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               uint64_t* __restrict__ status,
@@ -1415,6 +1427,17 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
     __syncthreads();
   }
+  const int nchunks = CH ? (a.ncols + K - 1) / K : 1;
+  for (int ch = 0; ch < nchunks; ch++) {
+  const int c0 = CH ? ch * K : 0;
+  const int ncc = CH ? min(K, a.ncols - c0) : a.ncols;  // fields of this chunk
+  uint64_t* const stc = status + (CH ? static_cast<int64_t>(ch) * nb * K : 0);
+  if (CH && ch > 0) {                             // the images again, zeroed
+    __syncthreads();
+    for (uint32_t i = 16 * tid; i < img_cap; i += 16 * NT)
+      *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
+    __syncthreads();
+  }
   const int64_t lim = total - a.fixed_size;       // last byte a row header may start at
   // the header is read at a clamped (always readable) start; a row outside the batch decodes as
   // all-null and is reported
@@ -1425,6 +1448,9 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // are only 8-aligned, the words are selected afterwards.  Blocks past the header's last word
   // are not read (the last block may extend 8 bytes past the header: inside the same 16-byte
   // block, never used).
+  uint64_t nullw;
+  uint64_t slot[K];
+  if constexpr (!CH) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
   constexpr int kNch = (K + 3) / 2;
   const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
@@ -1453,18 +1479,39 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       hw[2 * c + 1] = x.y;
     }
   }
-  uint64_t nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
+  nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
   nullw |= a.ncols >= 64 ? 0ull : (~0ull << a.ncols);
-  uint64_t slot[K];
 #pragma unroll
   for (int k = 0; k < K; k++) slot[k] = mis ? hw[k + 2] : hw[k + 1];
+  } else {
+    // chunk c0: null word c0 / 64 (c0 % 64 + K <= 64: K divides 64) and slots c0 .. c0 + ncc,
+    // from the stage when the row's header lies in it, else from HBM
+    const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
+    const bool hin = ra >= sa_lo && ra + a.fixed_size <= sa_hi && !(ra & 7);
+    const bool rd = lim >= 0;
+    const int sw = (a.bitmap_bytes >> 3) + c0;      // word of slot c0
+    uint64_t nw = ~0ull;
+    if (hin) {
+      const uint64_t* hp = reinterpret_cast<const uint64_t*>(stg + (ra - sa_lo));
+      if (rd) nw = hp[c0 >> 6];
+#pragma unroll
+      for (int k = 0; k < K; k++) slot[k] = rd && k < ncc ? hp[sw + k] : 0;
+    } else {
+      const auto hp = gl(reinterpret_cast<const uint64_t*>(row));
+      if (rd) nw = hp[c0 >> 6];
+#pragma unroll
+      for (int k = 0; k < K; k++) slot[k] = rd && k < ncc ? hp[sw + k] : 0;
+    }
+    nullw = live && rok ? (nw >> (c0 & 63)) : ~0ull;
+    nullw |= ncc >= 64 ? 0ull : (~0ull << ncc);
+  }
   // counts (LIST: the array header's element count), bounds-checked: a value outside the batch
   // decodes as null and is reported (slot_count / list_count)
   uint32_t cnt[K];
   uint64_t badw = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     const int kd = kind_of<M>(c);
     cnt[k] = 0;
     if (((nullw >> k) & 1) || kd < kBytes) continue;
@@ -1487,7 +1534,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
 #pragma unroll
   for (int k = 0; k < K; k++) {
     ex[k] = tot[k] = 0;
-    if (!seq_kind(kind_of<M>(a.col[k]))) continue;
+    if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
     const uint32_t inc = wave_scan_u32(cnt[k]);
     if (lane == 63) wtot[k][wave] = inc;
     ex[k] = inc - cnt[k];
@@ -1495,7 +1542,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    if (!seq_kind(kind_of<M>(a.col[k]))) continue;
+    if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
     uint32_t pre = 0, t = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -1509,8 +1556,8 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   if (tid == 0) {
 #pragma unroll
     for (int k = 0; k < K; k++)
-      if (seq_kind(kind_of<M>(a.col[k])))
-        st_status(status + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
+      if (seq_kind(kind_of<M>(vcol<CH>(a, c0, k))))
+        st_status(stc + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
   }
   // tile-relative LDS images of every variable-length column (image byte / bit i = the tile's
   // i-th output byte / element); laid out from the tile totals alone, so the rows are scattered
@@ -1519,7 +1566,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   uint32_t used = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     const int kd = kind_of<M>(c);
     img_at[k] = kNone;
     if (!seq_kind(kd) || !c.values || tot[k] == 0) continue;
@@ -1536,7 +1583,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // (the images were zeroed while the rows were staged)
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     if (img_at[k] == kNone || !live || cnt[k] == 0) continue;
     if (static_cast<uint64_t>(ex[k]) + cnt[k] > tot[k]) {   // the tile's 32-bit total wrapped
       raise_oob(a.err, r);
@@ -1640,7 +1687,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   const int nwords = nvalid >= 64 ? 2 : nvalid <= 0 ? 0 : static_cast<int>((nvalid + 31) >> 5);
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     const bool isnull = (nullw >> k) & 1;
     if (c.validity) {
       const uint64_t ok = __ballot(live && !isnull);
@@ -1680,12 +1727,12 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     int q = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      if (!seq_kind(kind_of<M>(a.col[k]))) continue;
+      if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err, TR);
+      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, c0 + k, rows, offs, stc, b, K, k, a.err, TR);
       if (lane == 0) {
         sbase[k] = pre;
-        if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
+        if (b > 0) st_status(stc + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
       }
     }
   }
@@ -1693,7 +1740,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     if (!seq_kind(kind_of<M>(c))) continue;
     const int64_t gb = sbase[k];
     if (live) c.offsets[r] = static_cast<int32_t>(gb + ex[k]);
@@ -1744,7 +1791,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // images -> HBM at the resolved positions
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const VarCol& c = a.col[k];
+    auto& c = vcol<CH>(a, c0, k);
     if (img_at[k] == kNone) continue;
     const int64_t gb = sbase[k];
     uint8_t* dst = const_cast<uint8_t*>(c.values);
@@ -1765,7 +1812,9 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     if (c.elem_validity)
       store_bits_shifted<NT>(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
   }
+  }  // chunks
 }
+
 #endif  // FURY_VAR_DEC
 
 // Decode / row->Arrow, single pass: 256 rows per workgroup.  Arrow offsets of STRING/BINARY and
@@ -2085,5 +2134,9 @@ int launch_decode_var_reg_mid(const VarArgs& a, const uint8_t* rows, const int64
 int launch_decode_var_reg_hi(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                              uint64_t* status, uint32_t img, uint32_t stage, int mode, int64_t nt,
                              hipStream_t stream);
+// schemas wider than kRegCols: decode_var_reg<kc, M, chunked>, kc in {4, 8, 16} fields per chunk
+int launch_decode_var_reg_wide(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
+                               uint64_t* status, uint32_t img, uint32_t stage, int mode, int64_t nt,
+                               int kc, hipStream_t stream);
 
 }  // namespace fury

@@ -214,7 +214,10 @@ class _PinnedBlock:
 
     def __del__(self):
         if self._ptr.value:
-            N.lib().fury_host_free(self._ptr)
+            try:
+                N.lib().fury_host_free(self._ptr)
+            except TypeError:           # interpreter shutdown: the module is already torn down
+                pass
             self._ptr = ctypes.c_void_p()
 
 

@@ -1,0 +1,71 @@
+"""Wide flat variable-length schemas (17..256 fields): the 33-field schema of
+tests/test_device.py::_wide_fields at --rows rows, timed with HIP events over bound-free calls:
+encode (fury_row_encode_measured), flat decode (fury_row_decode: decode_var_kernel) and the plan
+decode (fury_decode_prepare + execute: the row walk) -- GB/s of column + row bytes.
+
+    python scripts/ab_wide.py --rows 5000000 --ncols 33
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=5_000_000)
+    ap.add_argument("--ncols", type=int, default=33)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--str-max", type=int, default=24)
+    args = ap.parse_args()
+    import torch
+    from fury_amd.encoder import Encoders, _tree_bytes, column_to_device
+    from fury_amd.workloads import gen_columns
+    from tests.test_device import _wide_fields
+    fields = _wide_fields(args.ncols)
+    n = args.rows
+    host = gen_columns("wide", fields, n, seed=7, null_pct=10, str_max=args.str_max, list_max=6)
+    dev = torch.device("cuda:0")
+    cols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch(cols, n)
+    row_bytes = int(batch.rows.numel())
+    col_bytes = _tree_bytes(host)
+    alg = row_bytes + col_bytes
+    rows = torch.empty_like(batch.rows)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best = 1e9
+        for _ in range(args.iters):
+            s.record()
+            fn()
+            e.record()
+            e.synchronize()
+            best = min(best, s.elapsed_time(e))
+        return best
+    res = {"ncols": args.ncols, "rows": n, "row_bytes": row_bytes, "column_bytes": col_bytes}
+    res["encode_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
+    out = enc.decode_batch(batch)                       # allocated once (bound sizing)
+    from fury_amd import _native as N
+    L = N.lib()
+    for kc in (0, 4, 8, 16):
+        assert L.fury_set_tuning(b"var_wide", kc) == 0
+        res[f"decode_flat_kc{kc}_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
+        res[f"decode_flat_kc{kc}_TBps"] = round(alg / (res[f"decode_flat_kc{kc}_ms"] * 1e-3) / 1e12, 3)
+    assert L.fury_set_tuning(b"var_wide", 8) == 0
+    res["decode_flat_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
+    res["decode_plan_ms"] = timed(lambda: enc._decode_nested(batch, True, False, None))
+    for k in ("encode", "decode_flat", "decode_plan"):
+        res[k + "_TBps"] = round(alg / (res[k + "_ms"] * 1e-3) / 1e12, 3)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -236,7 +236,7 @@ def _tail_copy(a, dtype):
     if a is None:
         return None
     src = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
-    b = _page_tail(src.nbytes)
+    b = _page_tail(src.nbytes)[:src.nbytes]
     b[:] = src
     return b.view(dtype)
 
