@@ -69,6 +69,8 @@ static int g_help_now = 0;
 // in chunks of that many fields (default 8), 0: the 256-row tile kernel (decode_var_kernel).
 static int g_var_wide = 8;
 int var_wide_mode() { return g_var_wide; }
+// the chunked encode's fields per chunk: 16-field chunks spill (3.6 KB of scratch), so at most 8
+static int wide_enc_chunk() { return g_var_wide > 8 ? 8 : g_var_wide; }
 void set_var_wide_mode(int v) { g_var_wide = v; }
 int lookback_help_mode() { return g_help_now; }
 void set_lookback_help_mode(int v) { g_help_now = v; }
@@ -104,11 +106,28 @@ int reg_mode(const VarArgs& a) {
 // the encode's own tiles (measure_tiles, one wave per tile), their exclusive scan, then the encode
 // scans each tile's row sizes itself and writes the final row offsets once (the row-sized measure
 // wrote and the prefix pass re-read and re-wrote all 8 B/row of them).  -1: not this path.
+// Rows per chunked-encode tile (schemas wider than kRegCols): the estimated tile bytes fit the
+// kWideImgBytes image with headroom.
+int wide_tile_rows(const VarArgs& a) {
+  double img_row = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = hcol(a, k);
+    if (c.kind == kDecimal) img_row += 16;
+    if (c.kind != kBytes && c.kind != kListFixed) continue;
+    const double per = c.capacity > 0 && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
+    img_row += c.kind == kBytes ? per + 7 : 16 + per * (c.width == 0 ? 1 : c.width) + 7;
+  }
+  for (int R = kEncRows; R > 64; R -= 64)
+    if (R * img_row * 1.08 <= kWideImgBytes) return R;
+  return 64;
+}
+
 int launch_encode_measured_var(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
                                hipStream_t stream) {
-  if (a.ncols > kRegCols || a.nrows <= 0) return -1;
+  const bool wide = a.ncols > kRegCols;
+  if ((wide && var_wide_mode() == 0) || a.nrows <= 0) return -1;
   VarArgs b = a;
-  b.tile_rows = reg_tile_rows(a);
+  b.tile_rows = wide ? wide_tile_rows(a) : reg_tile_rows(a);
   const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
   int64_t* ws = nullptr;          // [tile totals x nt][total][scan scratch]
   int st = dev_alloc((nt + 1 + scan_workspace(nt)) * 8, stream, reinterpret_cast<void**>(&ws));
@@ -116,7 +135,8 @@ int launch_encode_measured_var(const VarArgs& a, int64_t* offs, uint8_t* rows, i
   st = launch_measure_tiles(b, ws, nt, stream);
   if (!st) {
     device_scan(ws, nt, ws + nt, ws + nt + 1, stream);
-    st = launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), ws, stream);
+    st = wide ? launch_encode_var_wide(b, offs, rows, cap, nt, reg_mode(a), ws, wide_enc_chunk(), stream)
+              : launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), ws, stream);
   }
   dev_free(ws, stream);
   return st;
@@ -132,6 +152,12 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     return launch_encode_var_reg(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
                                  stream);
+  } else if (var_wide_mode() > 0) {   // column chunks of the register-staged encode
+    VarArgs b = a;
+    b.tile_rows = wide_tile_rows(a);
+    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
+    return launch_encode_var_wide(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
+                                  wide_enc_chunk(), stream);
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);

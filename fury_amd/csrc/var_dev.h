@@ -886,6 +886,155 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* _
   }
 }
 
+// ---- column-chunked encode (schemas wider than kRegCols) ---------------------------------
+// The fields in chunks of K: a chunk's per-row inputs are loaded into registers (one batch of
+// loads), sized, then written into the row at the running cursor (the row's variable-length
+// section is in field order, so chunks append in turn); the row null bitmap gets one word per 64
+// fields (K divides 64: a chunk never straddles a word).  The tile's row image lives in a larger
+// static LDS block (two workgroups per CU) since wide rows are long.
+constexpr int kWideImg = 64 * 1024;
+
+template <int K, int M>
+__device__ __forceinline__ void wide_load(const VarArgs& a, int c0, int ncc, int64_t r, uint64_t* v,
+                                          uint64_t* valid) {
+  *valid = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    v[k] = 0;
+    if (k >= ncc) continue;
+    CVarCol& c = vc(a, c0 + k);
+    const bool ok = !c.validity || bit_at_g(c.validity, r);
+    *valid |= static_cast<uint64_t>(ok) << k;
+    uint64_t x = 0;
+    switch (kind_of<M>(c)) {
+      case kFixed: x = load_fixed(c.values, r, c.width); break;
+      case kBool: x = bit_at_g(c.values, r); break;
+      case kBytes:
+      case kListFixed:
+        x = static_cast<uint32_t>(gl(c.offsets)[r]) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(gl(c.offsets)[r + 1])) << 32);
+        break;
+      default: break;
+    }
+    v[k] = x;
+  }
+}
+
+// variable-length bytes of a chunk (reg_row_size without the fixed part)
+template <int K, int M>
+__device__ __forceinline__ int64_t wide_var_bytes(const VarArgs& a, int c0, int ncc, const uint64_t* v,
+                                                  uint64_t valid) {
+  int64_t sz = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    if (k >= ncc || !((valid >> k) & 1)) continue;
+    CVarCol& c = vc(a, c0 + k);
+    const int kd = kind_of<M>(c);
+    if (kd == kDecimal) {
+      sz += 16;
+    } else if (kd == kBytes || kd == kListFixed) {
+      const int64_t n = static_cast<int64_t>(static_cast<int32_t>(v[k] >> 32)) - static_cast<int32_t>(v[k]);
+      sz += kd == kBytes ? rnd8(n) : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
+    }
+  }
+  return sz;
+}
+
+// reg_build_row for fields [c0, c0 + ncc), appending at *cursor
+template <int K, int M, typename D>
+__device__ __forceinline__ void wide_build(const VarArgs& a, int c0, int ncc, int64_t r,
+                                           const uint64_t* v, uint64_t valid, D* d64, int64_t* cursor) {
+  const int nslot0 = a.bitmap_bytes >> 3;
+  uint64_t nullbits = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    if (k >= ncc) continue;
+    CVarCol& c = vc(a, c0 + k);
+    const int kd = kind_of<M>(c);
+    uint64_t slot = 0;
+    if (!((valid >> k) & 1)) {
+      nullbits |= 1ull << k;
+    } else if (kd == kFixed || kd == kBool) {
+      slot = v[k];
+    } else if (kd == kBytes) {
+      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
+      const int64_t len = o1 - o0;
+      put_string(d64 + (*cursor >> 3), c.values + o0, len);
+      slot = (static_cast<uint64_t>(*cursor) << 32) | static_cast<uint32_t>(len);
+      *cursor += rnd8(len);
+    } else if (kd == kDecimal) {
+      const auto s = gl(reinterpret_cast<const uint64_t*>(c.values)) + 2 * r;
+      d64[*cursor >> 3] = s[0];
+      d64[(*cursor >> 3) + 1] = s[1];
+      slot = (static_cast<uint64_t>(*cursor) << 32) | 16u;
+      *cursor += 16;
+    } else {   // kListFixed
+      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
+      const int64_t n = o1 - o0;
+      const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + int64_t(o0) * c.width;
+      const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
+      const int64_t sz = put_array(d64 + (*cursor >> 3), c.width, vals, vb, o0 & 7, n);
+      slot = (static_cast<uint64_t>(*cursor) << 32) | static_cast<uint32_t>(sz);
+      *cursor += sz;
+    }
+    d64[nslot0 + c0 + k] = slot;
+  }
+  if ((c0 & 63) == 0) d64[c0 >> 6] = nullbits << (c0 & 63);
+  else d64[c0 >> 6] |= nullbits << (c0 & 63);
+}
+
+template <int K, int M>
+__global__ __launch_bounds__(kEncRows) void encode_var_wide(VarArgs a, int64_t* __restrict__ offs,
+                                                            uint8_t* __restrict__ rows, int64_t cap,
+                                                            const int64_t* __restrict__ tbase) {
+  __shared__ __attribute__((aligned(16))) uint64_t img[kWideImg / 8];
+  __shared__ int64_t tmp[kEncRows / 64];
+  const int tid = threadIdx.x;
+  const int R = a.tile_rows;
+  const int64_t b = blockIdx.x;
+  const int64_t r0 = b * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t r = live ? r0 + tid : r0;
+  const int nch = (a.ncols + K - 1) / K;
+  uint64_t v[K];
+  uint64_t valid = 0;
+  int64_t base, bytes, ex, sz;
+  if (tbase) {
+    sz = a.fixed_size;
+    for (int ch = 0; ch < nch; ch++) {
+      const int c0 = ch * K, ncc = min(K, a.ncols - c0);
+      wide_load<K, M>(a, c0, ncc, r, v, &valid);
+      sz += wide_var_bytes<K, M>(a, c0, ncc, v, valid);
+    }
+    if (!live) sz = 0;
+    base = tbase[b];
+    ex = block_excl_scan<kEncRows>(sz, &bytes, tmp);
+    if (live) offs[r] = base + ex;
+    if (r0 + nr == a.nrows && tid == nr - 1) offs[a.nrows] = base + ex + sz;
+  } else {
+    base = offs[r0];
+    bytes = offs[r0 + nr] - base;
+    ex = offs[r] - base;
+    sz = offs[r + 1] - offs[r];
+  }
+  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
+  const bool inimg = bytes <= kWideImg;
+  if (live && (inimg || ex + sz <= room)) {
+    int64_t cursor = a.fixed_size;
+    for (int ch = 0; ch < nch; ch++) {
+      const int c0 = ch * K, ncc = min(K, a.ncols - c0);
+      wide_load<K, M>(a, c0, ncc, r, v, &valid);
+      if (inimg) wide_build<K, M>(a, c0, ncc, r, v, valid, img + (ex >> 3), &cursor);
+      else wide_build<K, M>(a, c0, ncc, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex), &cursor);
+    }
+  }
+  if (inimg) {
+    __syncthreads();
+    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
+  }
+}
+
 #endif  // FURY_VAR_ENC
 
 // ---- measure: row sizes (writerIndex growth of toRow) and their exclusive scan.  Each thread
@@ -2120,6 +2269,10 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
                           int64_t ntiles, int mode, const int64_t* tbase, hipStream_t stream);
 int launch_measure_tiles(const VarArgs& b, int64_t* tsum, int64_t ntiles, hipStream_t stream);
+// schemas wider than kRegCols: encode_var_wide<kc, M>, kc in {4, 8, 16}
+int launch_encode_var_wide(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
+                           int64_t ntiles, int mode, const int64_t* tbase, int kc, hipStream_t stream);
+constexpr int kWideImgBytes = 64 * 1024;
 // The register-staged instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded
 // up; the decode's look-back status words are tiles x K) x mode (kind_of, from reg_mode).
 inline int reg_dec_k(int ncols) {
