@@ -254,7 +254,7 @@ struct GenArgs {
   int64_t nrows;
   int32_t* err;            // optional device flag (never NULL when set by the host)
   int32_t root;            // fury_schema.root: 0 rows, 1 top-level arrays, 2 top-level maps
-  int32_t pad_;
+  int32_t prefetch;        // row-interpreter encode: pull each tile's input ranges first (tuning)
   const GenNode* tab;      // device node table for > kGenMaxNodes nodes, else NULL
   const GenNode* htab;     // its host copy (launchers only; never read on the device)
 };
@@ -262,6 +262,8 @@ struct GenArgs {
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
+void set_gen_prefetch(int v);        // tuning "gen_prefetch": 0 / 1
+int gen_prefetch_mode();
 // Nested encode engine (generic.hip): tuning "nested_encode" 0 = tree tiles (default), 1 = the
 // thread-per-row interpreter; "tree_enc_lds" / "tree_measure_lds" = their LDS budgets (bytes).
 void set_tree_encode_mode(int v);
