@@ -827,15 +827,9 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_tree_mode(value);
     return FURY_OK;
   }
-  if (std::string(key) == "gen_prefetch") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "gen_prefetch: 0..1");
-    set_gen_prefetch(value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "var_wide") {
-    if (value != 0 && value != 4 && value != 8 && value != 16)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "var_wide: 0, 4, 8 or 16");
-    set_var_wide_mode(value);
+  if (std::string(key) == "host_decode_inplace") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "host_decode_inplace: 0..1");
+    set_host_decode_inplace(value);
     return FURY_OK;
   }
   if (std::string(key) == "walk_prefetch") {
@@ -905,8 +899,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_pool") return static_cast<int32_t>(walk_tuning(2));
   if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
-  if (key && std::string(key) == "var_wide") return var_wide_mode();
-  if (key && std::string(key) == "gen_prefetch") return gen_prefetch_mode();
+  if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
   if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);
   if (key && std::string(key) == "tree_measure_rows") return tree_encode_rows(0);

@@ -309,73 +309,6 @@ __global__ __launch_bounds__(kEncThreads) void gen_measure_kernel(GenArgs g, int
 // A tile larger than the image (or past `cap`) takes the direct path.
 constexpr int64_t kGenImg = 76 * 1024;
 
-// Pulls the tile's input bytes into the caches before the rows are built (tuning
-// "gen_prefetch"): every node's Arrow entry range for rows [r0, r1) is found top-down (a struct
-// child's = its parent's, a list / map child's = the parent's offsets at its range ends; one
-// level per round), then each node's validity bits, offsets, values and string payload are read
-// with coalesced 16-B LDS-DMA loads into a scratch zone (data discarded) -- one round trip for the
-// whole tile, after which the interpreter's dependent gathers hit L2 instead of HBM.
-template <class NP>
-__device__ void gen_prefetch(const GenArgs& g, NP nodes, int64_t r0, int64_t r1, uint8_t* land) {
-  __shared__ int32_t par[kGenMaxNodes], rdy[kGenMaxNodes];
-  __shared__ int64_t lo[kGenMaxNodes], hi[kGenMaxNodes];
-  const int nn = g.nnodes, tid = threadIdx.x;
-  if (nn > kGenMaxNodes) return;
-  if (tid < nn) {
-    rdy[tid] = tid < g.ntop;
-    lo[tid] = r0;
-    hi[tid] = r1;
-    const auto& N = nodes[tid];
-    for (int j = 0; j < N.num_children; j++) par[N.first_child + j] = tid;
-  }
-  __syncthreads();
-  for (int it = 0; it < kGenMaxDepth; it++) {
-    bool now = false;
-    if (tid < nn && !rdy[tid] && rdy[par[tid]]) {
-      const int p = par[tid];
-      const auto& P = nodes[p];
-      if (P.type == FURY_TYPE_STRUCT || !P.offsets) {
-        lo[tid] = lo[p];
-        hi[tid] = hi[p];
-      } else {
-        lo[tid] = gl(P.offsets)[lo[p]];
-        hi[tid] = gl(P.offsets)[hi[p]];
-      }
-      now = true;
-    }
-    __syncthreads();
-    if (now) rdy[tid] = 1;
-    __syncthreads();
-  }
-  uint8_t* zone = land + 1024 * (tid >> 6);
-  auto pull = [&](const uint8_t* p, int64_t b0, int64_t b1) {
-    if (!p || b1 <= b0) return;
-    const uintptr_t a0 = reinterpret_cast<uintptr_t>(p + b0) & ~uintptr_t(15);
-    const uintptr_t a1 = (reinterpret_cast<uintptr_t>(p + b1) + 15) & ~uintptr_t(15);
-    for (uintptr_t q = a0 + 16 * tid; q < a1; q += 16 * kEncThreads)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q), zone, 16, 0, 0);
-  };
-  for (int n = 0; n < nn; n++) {
-    const auto& N = nodes[n];
-    const int64_t e0 = lo[n], e1 = hi[n];
-    if (e1 <= e0) continue;
-    pull(N.validity, e0 >> 3, (e1 + 7) >> 3);
-    const int w = gwidth(N.type);
-    if (N.type == FURY_TYPE_BOOL) {
-      pull(N.values, e0 >> 3, (e1 + 7) >> 3);
-    } else if (w > 0) {
-      pull(N.values, e0 * w, e1 * w);
-    } else if (N.type == FURY_TYPE_DECIMAL) {
-      pull(N.values, 16 * e0, 16 * e1);
-    } else if (N.offsets) {
-      pull(reinterpret_cast<const uint8_t*>(N.offsets), 4 * e0, 4 * e1 + 4);
-      if (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY)
-        pull(N.values, gl(N.offsets)[e0], gl(N.offsets)[e1]);
-    }
-  }
-  __syncthreads();
-}
-
 template <bool kWide, int kRoot>
 __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
                                                                  const int64_t* __restrict__ offs,
@@ -389,7 +322,6 @@ __global__ __launch_bounds__(kEncThreads, 2) void gen_encode_kernel(GenArgs g,
   const int64_t rend = min(r0 + kEncThreads, g.nrows);
   const int64_t b0 = offs[r0], b1 = offs[rend];
   if (b1 - b0 <= kGenImg && b1 <= cap) {
-    if (!kWide && g.prefetch) gen_prefetch(g, nodes, r0, rend, img);
     if (r < g.nrows) put_row<true, kRoot>(nodes, g.ntop, r, (LdsU8*)(img + (offs[r] - b0)));
     __syncthreads();
     const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
@@ -1305,20 +1237,14 @@ int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
   return check_hip(hipGetLastError(), "gen_measure launch");
 }
 
-int g_gen_prefetch = 0;          // tuning "gen_prefetch" (gen_prefetch above)
-void set_gen_prefetch(int v) { g_gen_prefetch = v; }
-int gen_prefetch_mode() { return g_gen_prefetch; }
-
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   if (g.nrows > 0) {
     const int t = launch_tree_encode(g, offs, nullptr, rows, cap, stream);
     if (t != 1) return t;
   }
-  GenArgs g2 = g;
-  g2.prefetch = g_gen_prefetch;
-  if (g.tab) gen_encode_root<true>(g2, offs, nullptr, rows, cap, stream);
-  else gen_encode_root<false>(g2, offs, nullptr, rows, cap, stream);
+  if (g.tab) gen_encode_root<true>(g, offs, nullptr, rows, cap, stream);
+  else gen_encode_root<false>(g, offs, nullptr, rows, cap, stream);
   return check_hip(hipGetLastError(), "gen_encode launch");
 }
 

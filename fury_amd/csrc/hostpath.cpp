@@ -816,6 +816,9 @@ bool node_has_offsets(int32_t t) {
 }  // namespace
 
 int64_t host_direct_count() { return g_host_direct.load(); }
+static std::atomic<int> g_host_decode_inplace{0};
+void set_host_decode_inplace(int v) { g_host_decode_inplace.store(v); }
+int host_decode_inplace() { return g_host_decode_inplace.load(); }
 
 // The stream-ordered pool of `device` keeps freed workspace memory instead of returning it at
 // every synchronisation (the default release threshold 0 re-mapped ~1.7 GB per call).  Once per
@@ -919,10 +922,13 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
   }
   DeviceArena arena(hs);
   std::vector<fury_column> dc(nn);
-  // Outputs the kernels write exactly (values, offsets, payloads) go straight into pinned host
-  // buffers; bitmaps (written as words / by atomics) and pageable buffers through HBM + a copy.
+  // Tuning "host_decode_inplace": outputs the kernels write exactly (values, offsets, payloads)
+  // go straight into pinned host buffers (bitmaps through HBM + a copy).  Off by default: the
+  // decode's scattered 4-8 byte stores over PCIe ran at 27.5 GB/s end to end against 40.4 GB/s for
+  // HBM outputs + copies (1M nested rows, scripts/ab_host_nested.py).
   std::vector<uint8_t> copy_off(nn, 1), copy_val(nn, 1);
-  bool all_direct = true;
+  const bool inplace = host_decode_inplace();
+  bool all_direct = inplace;
   for (int i = 0; i < nn; i++) {
     const GenTpl& t = s->nodes[i];
     const fury_column& h = *hc[i];
@@ -937,7 +943,7 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
     }
     if (node_has_offsets(t.type_id)) {
       if (!h.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "node " + std::to_string(i) + ": output offsets is null");
-      uint8_t* view = device_view(h.offsets, (m + 1) * 4);
+      uint8_t* view = inplace ? device_view(h.offsets, (m + 1) * 4) : nullptr;
       if (view && aligned_to(view, 4)) {
         d.offsets = reinterpret_cast<int32_t*>(view);
         copy_off[i] = 0;
@@ -956,7 +962,7 @@ int fury_decode_host_execute(fury_decode_plan* p, fury_column* host) {
                                                 std::to_string(vb) + " payload bytes");
       const int w = type_width_of(t.type_id);
       const int al = t.type_id == FURY_TYPE_DECIMAL ? 8 : w > 0 ? w : 1;
-      uint8_t* view = t.type_id != FURY_TYPE_BOOL && vb > 0 ? device_view(h.values, vb) : nullptr;
+      uint8_t* view = inplace && t.type_id != FURY_TYPE_BOOL && vb > 0 ? device_view(h.values, vb) : nullptr;
       if (view && aligned_to(view, al)) {
         d.values = view;
         copy_val[i] = 0;

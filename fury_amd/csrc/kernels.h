@@ -216,8 +216,8 @@ int workspace_reserve(size_t bytes, void** out);
 // Rows per encode tile for this column set (the staged per-row inputs must fit the LDS pool).
 int encode_tile_rows(const VarArgs& a);
 int64_t lookback_timeouts();
-int var_wide_mode();                  // tuning "var_wide" (var.hip)
-void set_var_wide_mode(int v);
+void set_host_decode_inplace(int v);   // tuning "host_decode_inplace" (hostpath.cpp)
+int host_decode_inplace();
 int lookback_help_mode();
 void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
@@ -254,7 +254,7 @@ struct GenArgs {
   int64_t nrows;
   int32_t* err;            // optional device flag (never NULL when set by the host)
   int32_t root;            // fury_schema.root: 0 rows, 1 top-level arrays, 2 top-level maps
-  int32_t prefetch;        // row-interpreter encode: pull each tile's input ranges first (tuning)
+  int32_t pad_;
   const GenNode* tab;      // device node table for > kGenMaxNodes nodes, else NULL
   const GenNode* htab;     // its host copy (launchers only; never read on the device)
 };
@@ -262,8 +262,6 @@ struct GenArgs {
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
-void set_gen_prefetch(int v);        // tuning "gen_prefetch": 0 / 1
-int gen_prefetch_mode();
 // Nested encode engine (generic.hip): tuning "nested_encode" 0 = tree tiles (default), 1 = the
 // thread-per-row interpreter; "tree_enc_lds" / "tree_measure_lds" = their LDS budgets (bytes).
 void set_tree_encode_mode(int v);

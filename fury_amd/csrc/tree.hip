@@ -432,12 +432,15 @@ int tree_host_width(int32_t t) {
 }
 
 int g_tree_mode = 2;             // tuning "nested_decode": 0 tree tiles, 1 level engine, 2 row walk
-int g_walk_threads = 256;        // tuning "walk_threads": rows (= threads) per row-walk tile
-uint32_t g_walk_stage = 48 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
+// Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row tiles with a
+// 20 KB count-pass stage (prepare 1.35 -> 1.17 ms: more tiles resident), write-pass prefetch
+// (execute 2.00 -> 1.91 ms).
+int g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per row-walk tile
+uint32_t g_walk_stage = 20 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
 uint32_t g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
 uint32_t g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
-int g_walk_prefetch = 0;            // tuning "walk_prefetch": write-pass waves pull their rows first
+int g_walk_prefetch = 1;            // tuning "walk_prefetch": write-pass waves pull their rows first
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 uint32_t g_tree_stage = 32 * 1024, g_tree_arena = 24 * 1024;
 int g_tree_threads = 256;        // tuning "tree_threads": workgroup size of the decode (256/512/1024)

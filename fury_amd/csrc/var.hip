@@ -65,13 +65,6 @@ int64_t lookback_timeouts() { return device_error_count(); }
 // Test hook (tuning "lookback_help"): every look-back computes a silent predecessor's aggregate
 // at once -- the path a late-dispatched predecessor takes -- instead of polling first.
 static int g_help_now = 0;
-// Tuning "var_wide": decode of schemas wider than kRegCols -- 4 / 8 / 16: the row-staged kernel
-// in chunks of that many fields (default 8), 0: the 256-row tile kernel (decode_var_kernel).
-static int g_var_wide = 8;
-int var_wide_mode() { return g_var_wide; }
-// the chunked encode's fields per chunk: 16-field chunks spill (3.6 KB of scratch), so at most 8
-static int wide_enc_chunk() { return g_var_wide > 8 ? 8 : g_var_wide; }
-void set_var_wide_mode(int v) { g_var_wide = v; }
 int lookback_help_mode() { return g_help_now; }
 void set_lookback_help_mode(int v) { g_help_now = v; }
 // Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
@@ -106,28 +99,11 @@ int reg_mode(const VarArgs& a) {
 // the encode's own tiles (measure_tiles, one wave per tile), their exclusive scan, then the encode
 // scans each tile's row sizes itself and writes the final row offsets once (the row-sized measure
 // wrote and the prefix pass re-read and re-wrote all 8 B/row of them).  -1: not this path.
-// Rows per chunked-encode tile (schemas wider than kRegCols): the estimated tile bytes fit the
-// kWideImgBytes image with headroom.
-int wide_tile_rows(const VarArgs& a) {
-  double img_row = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = hcol(a, k);
-    if (c.kind == kDecimal) img_row += 16;
-    if (c.kind != kBytes && c.kind != kListFixed) continue;
-    const double per = c.capacity > 0 && a.nrows > 0 ? static_cast<double>(c.capacity) / a.nrows : 32.0;
-    img_row += c.kind == kBytes ? per + 7 : 16 + per * (c.width == 0 ? 1 : c.width) + 7;
-  }
-  for (int R = kEncRows; R > 64; R -= 64)
-    if (R * img_row * 1.08 <= kWideImgBytes) return R;
-  return 64;
-}
-
 int launch_encode_measured_var(const VarArgs& a, int64_t* offs, uint8_t* rows, int64_t cap,
                                hipStream_t stream) {
-  const bool wide = a.ncols > kRegCols;
-  if ((wide && var_wide_mode() == 0) || a.nrows <= 0) return -1;
+  if (a.ncols > kRegCols || a.nrows <= 0) return -1;
   VarArgs b = a;
-  b.tile_rows = wide ? wide_tile_rows(a) : reg_tile_rows(a);
+  b.tile_rows = reg_tile_rows(a);
   const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
   int64_t* ws = nullptr;          // [tile totals x nt][total][scan scratch]
   int st = dev_alloc((nt + 1 + scan_workspace(nt)) * 8, stream, reinterpret_cast<void**>(&ws));
@@ -135,8 +111,7 @@ int launch_encode_measured_var(const VarArgs& a, int64_t* offs, uint8_t* rows, i
   st = launch_measure_tiles(b, ws, nt, stream);
   if (!st) {
     device_scan(ws, nt, ws + nt, ws + nt + 1, stream);
-    st = wide ? launch_encode_var_wide(b, offs, rows, cap, nt, reg_mode(a), ws, wide_enc_chunk(), stream)
-              : launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), ws, stream);
+    st = launch_encode_var_reg(b, offs, rows, cap, nt, reg_mode(a), ws, stream);
   }
   dev_free(ws, stream);
   return st;
@@ -152,12 +127,6 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     return launch_encode_var_reg(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
                                  stream);
-  } else if (var_wide_mode() > 0) {   // column chunks of the register-staged encode
-    VarArgs b = a;
-    b.tile_rows = wide_tile_rows(a);
-    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
-    return launch_encode_var_wide(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
-                                  wide_enc_chunk(), stream);
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);
@@ -214,30 +183,24 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 // bound sizing); a tile whose payload outgrows its image stores that column straight to HBM and
 // rows past the stage are read from HBM (both correct, slower), so the estimate only moves speed.
 // mixed (C3): 512-row tiles.
-void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage, int chunk = kRegCols) {
+void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) {
   constexpr int64_t kBudget = 80 * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
-  // images: the largest chunk's (schemas wider than kRegCols decode kRegCols fields at a time)
-  double row = a.fixed_size, img_row = 0, img_fix = 0, chunk_row = 0, chunk_fix = 0;
+  double row = a.fixed_size, img_row = 0, img_fix = 0;
   for (int k = 0; k < a.ncols; k++) {
-    if (k % chunk == 0) {
-      chunk_row = chunk_fix = 0;
-    }
     const VarCol& c = hcol(a, k);
     const double per = a.nrows > 0 && c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 16.0;
     if (c.kind == kDecimal) row += 16;
     if (c.kind == kBytes) {
       row += per + 4;
-      if (c.values) { chunk_row += per; chunk_fix += 80; }
+      if (c.values) { img_row += per; img_fix += 80; }
     }
     if (c.kind == kListFixed) {
       row += 12 + per * (c.width == 0 ? 1 : c.width) + 4;
       if (c.values) {
-        chunk_row += per * (c.width == 0 ? 0.125 : c.width) + (c.elem_validity ? per / 8 : 0);
-        chunk_fix += c.elem_validity ? 160 : 80;
+        img_row += per * (c.width == 0 ? 0.125 : c.width) + (c.elem_validity ? per / 8 : 0);
+        img_fix += c.elem_validity ? 160 : 80;
       }
     }
-    if (chunk_row > img_row) img_row = chunk_row;
-    if (chunk_fix > img_fix) img_fix = chunk_fix;
   }
   // headroom over the estimates: 8 % on the images, 2 % on the stage (a 512-row tile's bytes
   // vary by ~1 %; C4 0.252 -> 0.229 ms against 15 % / 5 %, mixed unchanged)
@@ -275,23 +238,6 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     if (st) return st;
     st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
     if (!st) st = launch_decode_var_reg(b, rows, offs, ws, img, stage, mode, nt, stream);
-    dev_free(ws, stream);
-    return st;
-  }
-  if (var_wide_mode() > 0) {
-    // wider than kRegCols: the row-staged kernel in chunks of kc fields (one row read)
-    const int kc = var_wide_mode();
-    VarArgs b = a;
-    uint32_t img = 0, stage = 0;
-    dec_tile_plan(a, &b.tile_rows, &img, &stage, kc);
-    const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
-    const int64_t nch = (a.ncols + kc - 1) / kc;
-    const size_t wsb = static_cast<size_t>(nt) * kc * nch * 8;
-    uint64_t* ws = nullptr;
-    int st = dev_alloc(wsb, stream, reinterpret_cast<void**>(&ws));
-    if (st) return st;
-    st = check_hip(hipMemsetAsync(ws, 0, wsb, stream), "memset");
-    if (!st) st = launch_decode_var_reg_wide(b, rows, offs, ws, img, stage, mode, nt, kc, stream);
     dev_free(ws, stream);
     return st;
   }

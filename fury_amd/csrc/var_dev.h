@@ -655,16 +655,16 @@ constexpr int kSeqBytes = 0, kSeqLists = 1, kSeqAll = 2;
 // fields (kSeqLists), as the host checks (reg_mode), map every kind onto those three, so the
 // compiler drops the other kinds' code from the unrolled K-column bodies (mixed decode, K = 6:
 // 7.1k instead of 18k instructions; the full body cost it ~10 % in instruction-cache misses).
-template <int M, class C>
-__device__ __forceinline__ int kind_of(const C& c) {
+template <int M>
+__device__ __forceinline__ int kind_of(const VarCol& c) {
   const int kd = c.kind;
   if (M == kSeqAll) return kd;
   const int seq = M == kSeqBytes ? kBytes : kListFixed;
   return kd == seq ? seq : (kd == kBool ? kBool : kFixed);
 }
 // a sequence column's payload is bytes (else list elements)
-template <int M, class C>
-__device__ __forceinline__ bool bytes_seq(const C& c) {
+template <int M>
+__device__ __forceinline__ bool bytes_seq(const VarCol& c) {
   return M == kSeqBytes || (M == kSeqAll && c.kind == kBytes);
 }
 __device__ __forceinline__ bool seq_kind(int kd) { return kd == kBytes || kd == kListFixed; }
@@ -883,155 +883,6 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* _
     store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
     if (ex + sz <= room) reg_build_row<K, M>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
-  }
-}
-
-// ---- column-chunked encode (schemas wider than kRegCols) ---------------------------------
-// The fields in chunks of K: a chunk's per-row inputs are loaded into registers (one batch of
-// loads), sized, then written into the row at the running cursor (the row's variable-length
-// section is in field order, so chunks append in turn); the row null bitmap gets one word per 64
-// fields (K divides 64: a chunk never straddles a word).  The tile's row image lives in a larger
-// static LDS block (two workgroups per CU) since wide rows are long.
-constexpr int kWideImg = 64 * 1024;
-
-template <int K, int M>
-__device__ __forceinline__ void wide_load(const VarArgs& a, int c0, int ncc, int64_t r, uint64_t* v,
-                                          uint64_t* valid) {
-  *valid = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    v[k] = 0;
-    if (k >= ncc) continue;
-    CVarCol& c = vc(a, c0 + k);
-    const bool ok = !c.validity || bit_at_g(c.validity, r);
-    *valid |= static_cast<uint64_t>(ok) << k;
-    uint64_t x = 0;
-    switch (kind_of<M>(c)) {
-      case kFixed: x = load_fixed(c.values, r, c.width); break;
-      case kBool: x = bit_at_g(c.values, r); break;
-      case kBytes:
-      case kListFixed:
-        x = static_cast<uint32_t>(gl(c.offsets)[r]) |
-            (static_cast<uint64_t>(static_cast<uint32_t>(gl(c.offsets)[r + 1])) << 32);
-        break;
-      default: break;
-    }
-    v[k] = x;
-  }
-}
-
-// variable-length bytes of a chunk (reg_row_size without the fixed part)
-template <int K, int M>
-__device__ __forceinline__ int64_t wide_var_bytes(const VarArgs& a, int c0, int ncc, const uint64_t* v,
-                                                  uint64_t valid) {
-  int64_t sz = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    if (k >= ncc || !((valid >> k) & 1)) continue;
-    CVarCol& c = vc(a, c0 + k);
-    const int kd = kind_of<M>(c);
-    if (kd == kDecimal) {
-      sz += 16;
-    } else if (kd == kBytes || kd == kListFixed) {
-      const int64_t n = static_cast<int64_t>(static_cast<int32_t>(v[k] >> 32)) - static_cast<int32_t>(v[k]);
-      sz += kd == kBytes ? rnd8(n) : 8 + bm_bytes(n) + rnd8(n * (c.width == 0 ? 1 : c.width));
-    }
-  }
-  return sz;
-}
-
-// reg_build_row for fields [c0, c0 + ncc), appending at *cursor
-template <int K, int M, typename D>
-__device__ __forceinline__ void wide_build(const VarArgs& a, int c0, int ncc, int64_t r,
-                                           const uint64_t* v, uint64_t valid, D* d64, int64_t* cursor) {
-  const int nslot0 = a.bitmap_bytes >> 3;
-  uint64_t nullbits = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    if (k >= ncc) continue;
-    CVarCol& c = vc(a, c0 + k);
-    const int kd = kind_of<M>(c);
-    uint64_t slot = 0;
-    if (!((valid >> k) & 1)) {
-      nullbits |= 1ull << k;
-    } else if (kd == kFixed || kd == kBool) {
-      slot = v[k];
-    } else if (kd == kBytes) {
-      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
-      const int64_t len = o1 - o0;
-      put_string(d64 + (*cursor >> 3), c.values + o0, len);
-      slot = (static_cast<uint64_t>(*cursor) << 32) | static_cast<uint32_t>(len);
-      *cursor += rnd8(len);
-    } else if (kd == kDecimal) {
-      const auto s = gl(reinterpret_cast<const uint64_t*>(c.values)) + 2 * r;
-      d64[*cursor >> 3] = s[0];
-      d64[(*cursor >> 3) + 1] = s[1];
-      slot = (static_cast<uint64_t>(*cursor) << 32) | 16u;
-      *cursor += 16;
-    } else {   // kListFixed
-      const int32_t o0 = static_cast<int32_t>(v[k]), o1 = static_cast<int32_t>(v[k] >> 32);
-      const int64_t n = o1 - o0;
-      const uint8_t* vals = c.width == 0 ? c.values + (o0 >> 3) : c.values + int64_t(o0) * c.width;
-      const uint8_t* vb = c.elem_validity ? c.elem_validity + (o0 >> 3) : nullptr;
-      const int64_t sz = put_array(d64 + (*cursor >> 3), c.width, vals, vb, o0 & 7, n);
-      slot = (static_cast<uint64_t>(*cursor) << 32) | static_cast<uint32_t>(sz);
-      *cursor += sz;
-    }
-    d64[nslot0 + c0 + k] = slot;
-  }
-  if ((c0 & 63) == 0) d64[c0 >> 6] = nullbits << (c0 & 63);
-  else d64[c0 >> 6] |= nullbits << (c0 & 63);
-}
-
-template <int K, int M>
-__global__ __launch_bounds__(kEncRows) void encode_var_wide(VarArgs a, int64_t* __restrict__ offs,
-                                                            uint8_t* __restrict__ rows, int64_t cap,
-                                                            const int64_t* __restrict__ tbase) {
-  __shared__ __attribute__((aligned(16))) uint64_t img[kWideImg / 8];
-  __shared__ int64_t tmp[kEncRows / 64];
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;
-  const int64_t b = blockIdx.x;
-  const int64_t r0 = b * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t r = live ? r0 + tid : r0;
-  const int nch = (a.ncols + K - 1) / K;
-  uint64_t v[K];
-  uint64_t valid = 0;
-  int64_t base, bytes, ex, sz;
-  if (tbase) {
-    sz = a.fixed_size;
-    for (int ch = 0; ch < nch; ch++) {
-      const int c0 = ch * K, ncc = min(K, a.ncols - c0);
-      wide_load<K, M>(a, c0, ncc, r, v, &valid);
-      sz += wide_var_bytes<K, M>(a, c0, ncc, v, valid);
-    }
-    if (!live) sz = 0;
-    base = tbase[b];
-    ex = block_excl_scan<kEncRows>(sz, &bytes, tmp);
-    if (live) offs[r] = base + ex;
-    if (r0 + nr == a.nrows && tid == nr - 1) offs[a.nrows] = base + ex + sz;
-  } else {
-    base = offs[r0];
-    bytes = offs[r0 + nr] - base;
-    ex = offs[r] - base;
-    sz = offs[r + 1] - offs[r];
-  }
-  const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
-  const bool inimg = bytes <= kWideImg;
-  if (live && (inimg || ex + sz <= room)) {
-    int64_t cursor = a.fixed_size;
-    for (int ch = 0; ch < nch; ch++) {
-      const int c0 = ch * K, ncc = min(K, a.ncols - c0);
-      wide_load<K, M>(a, c0, ncc, r, v, &valid);
-      if (inimg) wide_build<K, M>(a, c0, ncc, r, v, valid, img + (ex >> 3), &cursor);
-      else wide_build<K, M>(a, c0, ncc, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex), &cursor);
-    }
-  }
-  if (inimg) {
-    __syncthreads();
-    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   }
 }
 
@@ -1515,19 +1366,7 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 
 #ifdef FURY_VAR_DEC
 // (K <= 4: at most 128 VGPRs, so two 512-thread workgroups share a CU -- the LDS plan assumes two)
-// Column k of the chunk starting at c0: the argument block's record (one chunk, K >= the field
-// count), or -- chunked instances for schemas wider than kRegCols -- record c0 + k of the block or
-// the uploaded table.
-template <bool CH>
-__device__ __forceinline__ auto& vcol(const VarArgs& a, int c0, int k) {
-  if constexpr (CH) return vc(a, c0 + k);
-  else return a.col[k];
-}
-
-// CH (chunked): the schema's fields in chunks of K = kRegCols, decoded one chunk after the other
-// from the same staged tile (one row read for all chunks); each chunk has its own status words
-// (tiles x K, after the previous chunk's) and reuses the images, zeroed again between chunks.
-template <int K, int M, bool CH = false>
+template <int K, int M>
 __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <= 4 ? 4 : 1))) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               uint64_t* __restrict__ status,
@@ -1576,17 +1415,6 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
     __syncthreads();
   }
-  const int nchunks = CH ? (a.ncols + K - 1) / K : 1;
-  for (int ch = 0; ch < nchunks; ch++) {
-  const int c0 = CH ? ch * K : 0;
-  const int ncc = CH ? min(K, a.ncols - c0) : a.ncols;  // fields of this chunk
-  uint64_t* const stc = status + (CH ? static_cast<int64_t>(ch) * nb * K : 0);
-  if (CH && ch > 0) {                             // the images again, zeroed
-    __syncthreads();
-    for (uint32_t i = 16 * tid; i < img_cap; i += 16 * NT)
-      *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
-    __syncthreads();
-  }
   const int64_t lim = total - a.fixed_size;       // last byte a row header may start at
   // the header is read at a clamped (always readable) start; a row outside the batch decodes as
   // all-null and is reported
@@ -1597,9 +1425,6 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // are only 8-aligned, the words are selected afterwards.  Blocks past the header's last word
   // are not read (the last block may extend 8 bytes past the header: inside the same 16-byte
   // block, never used).
-  uint64_t nullw;
-  uint64_t slot[K];
-  if constexpr (!CH) {
   using u64x2 = __attribute__((ext_vector_type(2))) unsigned long long;
   constexpr int kNch = (K + 3) / 2;
   const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
@@ -1628,39 +1453,18 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       hw[2 * c + 1] = x.y;
     }
   }
-  nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
+  uint64_t nullw = live && rok ? (mis ? hw[1] : hw[0]) : ~0ull;
   nullw |= a.ncols >= 64 ? 0ull : (~0ull << a.ncols);
+  uint64_t slot[K];
 #pragma unroll
   for (int k = 0; k < K; k++) slot[k] = mis ? hw[k + 2] : hw[k + 1];
-  } else {
-    // chunk c0: null word c0 / 64 (c0 % 64 + K <= 64: K divides 64) and slots c0 .. c0 + ncc,
-    // from the stage when the row's header lies in it, else from HBM
-    const uintptr_t ra = reinterpret_cast<uintptr_t>(row);
-    const bool hin = ra >= sa_lo && ra + a.fixed_size <= sa_hi && !(ra & 7);
-    const bool rd = lim >= 0;
-    const int sw = (a.bitmap_bytes >> 3) + c0;      // word of slot c0
-    uint64_t nw = ~0ull;
-    if (hin) {
-      const uint64_t* hp = reinterpret_cast<const uint64_t*>(stg + (ra - sa_lo));
-      if (rd) nw = hp[c0 >> 6];
-#pragma unroll
-      for (int k = 0; k < K; k++) slot[k] = rd && k < ncc ? hp[sw + k] : 0;
-    } else {
-      const auto hp = gl(reinterpret_cast<const uint64_t*>(row));
-      if (rd) nw = hp[c0 >> 6];
-#pragma unroll
-      for (int k = 0; k < K; k++) slot[k] = rd && k < ncc ? hp[sw + k] : 0;
-    }
-    nullw = live && rok ? (nw >> (c0 & 63)) : ~0ull;
-    nullw |= ncc >= 64 ? 0ull : (~0ull << ncc);
-  }
   // counts (LIST: the array header's element count), bounds-checked: a value outside the batch
   // decodes as null and is reported (slot_count / list_count)
   uint32_t cnt[K];
   uint64_t badw = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     const int kd = kind_of<M>(c);
     cnt[k] = 0;
     if (((nullw >> k) & 1) || kd < kBytes) continue;
@@ -1683,7 +1487,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
 #pragma unroll
   for (int k = 0; k < K; k++) {
     ex[k] = tot[k] = 0;
-    if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
+    if (!seq_kind(kind_of<M>(a.col[k]))) continue;
     const uint32_t inc = wave_scan_u32(cnt[k]);
     if (lane == 63) wtot[k][wave] = inc;
     ex[k] = inc - cnt[k];
@@ -1691,7 +1495,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
+    if (!seq_kind(kind_of<M>(a.col[k]))) continue;
     uint32_t pre = 0, t = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -1705,8 +1509,8 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   if (tid == 0) {
 #pragma unroll
     for (int k = 0; k < K; k++)
-      if (seq_kind(kind_of<M>(vcol<CH>(a, c0, k))))
-        st_status(stc + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
+      if (seq_kind(kind_of<M>(a.col[k])))
+        st_status(status + b * K + k, (b == 0 ? kInc : kAgg) | static_cast<uint64_t>(tot[k]));
   }
   // tile-relative LDS images of every variable-length column (image byte / bit i = the tile's
   // i-th output byte / element); laid out from the tile totals alone, so the rows are scattered
@@ -1715,7 +1519,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   uint32_t used = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     const int kd = kind_of<M>(c);
     img_at[k] = kNone;
     if (!seq_kind(kd) || !c.values || tot[k] == 0) continue;
@@ -1732,7 +1536,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // (the images were zeroed while the rows were staged)
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     if (img_at[k] == kNone || !live || cnt[k] == 0) continue;
     if (static_cast<uint64_t>(ex[k]) + cnt[k] > tot[k]) {   // the tile's 32-bit total wrapped
       raise_oob(a.err, r);
@@ -1836,7 +1640,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   const int nwords = nvalid >= 64 ? 2 : nvalid <= 0 ? 0 : static_cast<int>((nvalid + 31) >> 5);
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     const bool isnull = (nullw >> k) & 1;
     if (c.validity) {
       const uint64_t ok = __ballot(live && !isnull);
@@ -1876,12 +1680,12 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     int q = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      if (!seq_kind(kind_of<M>(vcol<CH>(a, c0, k)))) continue;
+      if (!seq_kind(kind_of<M>(a.col[k]))) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, c0 + k, rows, offs, stc, b, K, k, a.err, TR);
+      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err, TR);
       if (lane == 0) {
         sbase[k] = pre;
-        if (b > 0) st_status(stc + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
+        if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
       }
     }
   }
@@ -1889,7 +1693,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     if (!seq_kind(kind_of<M>(c))) continue;
     const int64_t gb = sbase[k];
     if (live) c.offsets[r] = static_cast<int32_t>(gb + ex[k]);
@@ -1940,7 +1744,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // images -> HBM at the resolved positions
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    auto& c = vcol<CH>(a, c0, k);
+    const VarCol& c = a.col[k];
     if (img_at[k] == kNone) continue;
     const int64_t gb = sbase[k];
     uint8_t* dst = const_cast<uint8_t*>(c.values);
@@ -1961,9 +1765,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     if (c.elem_validity)
       store_bits_shifted<NT>(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
   }
-  }  // chunks
 }
-
 #endif  // FURY_VAR_DEC
 
 // Decode / row->Arrow, single pass: 256 rows per workgroup.  Arrow offsets of STRING/BINARY and
@@ -2269,10 +2071,6 @@ __global__ __launch_bounds__(kThreads) void decode_var_kernel(VarArgs a,
 int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
                           int64_t ntiles, int mode, const int64_t* tbase, hipStream_t stream);
 int launch_measure_tiles(const VarArgs& b, int64_t* tsum, int64_t ntiles, hipStream_t stream);
-// schemas wider than kRegCols: encode_var_wide<kc, M>, kc in {4, 8, 16}
-int launch_encode_var_wide(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
-                           int64_t ntiles, int mode, const int64_t* tbase, int kc, hipStream_t stream);
-constexpr int kWideImgBytes = 64 * 1024;
 // The register-staged instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded
 // up; the decode's look-back status words are tiles x K) x mode (kind_of, from reg_mode).
 inline int reg_dec_k(int ncols) {
@@ -2287,9 +2085,5 @@ int launch_decode_var_reg_mid(const VarArgs& a, const uint8_t* rows, const int64
 int launch_decode_var_reg_hi(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
                              uint64_t* status, uint32_t img, uint32_t stage, int mode, int64_t nt,
                              hipStream_t stream);
-// schemas wider than kRegCols: decode_var_reg<kc, M, chunked>, kc in {4, 8, 16} fields per chunk
-int launch_decode_var_reg_wide(const VarArgs& a, const uint8_t* rows, const int64_t* offs,
-                               uint64_t* status, uint32_t img, uint32_t stage, int mode, int64_t nt,
-                               int kc, hipStream_t stream);
 
 }  // namespace fury

@@ -1,5 +1,5 @@
 // var_reg_enc.hip — instances of the register-staged encode: K = 2, 3, 4, 6, 8, 12, 16 columns
-// (reg_dec_k) x kind mode (kind_of), and the column-chunked encode of wider schemas.
+// (reg_dec_k) x kind mode (kind_of).
 #define FURY_VAR_ENC
 #include "var_dev.h"
 
@@ -28,25 +28,6 @@ int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_
 #undef FURY_REG
 #undef FURY_REG_M
   return check_hip(hipGetLastError(), "encode_var_reg launch");
-}
-
-int launch_encode_var_wide(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_t cap,
-                           int64_t nt, int mode, const int64_t* tbase, int kc, hipStream_t stream) {
-#define FURY_WIDE_M(KC, M) \
-  hipLaunchKernelGGL((encode_var_wide<KC, M>), dim3(nt), dim3(kEncRows), 0, stream, b, offs, rows, cap, tbase);
-#define FURY_WIDE(KC)                                                                          \
-  if (kc == KC) {                                                                              \
-    if (mode == kSeqBytes) { FURY_WIDE_M(KC, kSeqBytes) }                                      \
-    else if (mode == kSeqLists) { FURY_WIDE_M(KC, kSeqLists) }                                 \
-    else { FURY_WIDE_M(KC, kSeqAll) }                                                          \
-    return check_hip(hipGetLastError(), "encode_var_wide launch");                             \
-  }
-  FURY_WIDE(4)
-  FURY_WIDE(8)
-  FURY_WIDE(16)
-#undef FURY_WIDE
-#undef FURY_WIDE_M
-  return set_error(FURY_ERR_INVALID_ARGUMENT, "chunked encode: 4, 8 or 16 fields per chunk");
 }
 
 }  // namespace fury

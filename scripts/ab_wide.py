@@ -52,15 +52,6 @@ def main():
         return best
     res = {"ncols": args.ncols, "rows": n, "row_bytes": row_bytes, "column_bytes": col_bytes}
     out = enc.decode_batch(batch)                       # allocated once (bound sizing)
-    from fury_amd import _native as N
-    L = N.lib()
-    for kc in (0, 4, 8, 16):
-        assert L.fury_set_tuning(b"var_wide", kc) == 0
-        res[f"encode_kc{kc}_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
-        res[f"encode_kc{kc}_TBps"] = round(alg / (res[f"encode_kc{kc}_ms"] * 1e-3) / 1e12, 3)
-        res[f"decode_flat_kc{kc}_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
-        res[f"decode_flat_kc{kc}_TBps"] = round(alg / (res[f"decode_flat_kc{kc}_ms"] * 1e-3) / 1e12, 3)
-    assert L.fury_set_tuning(b"var_wide", 8) == 0
     res["encode_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
     res["decode_flat_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
     res["decode_plan_ms"] = timed(lambda: enc._decode_nested(batch, True, False, None))

@@ -821,35 +821,6 @@ def test_reg_decode_every_width_and_kind_mode(oracle, dev, mode, ncols):
     assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
 
 
-@pytest.mark.parametrize("kc", [0, 4, 8, 16])
-@pytest.mark.parametrize("ncols,n", [(33, 3001), (100, 900), (17, 5000)])
-def test_wide_var_decode_chunk_sizes(oracle, dev, kc, ncols, n):
-    """Schemas wider than 16 fields encode and decode through the register-/row-staged kernels in
-    chunks of 4 / 8 / 16 fields (tuning var_wide; 0 = the 256-row tile kernels): every chunk size
-    == the oracle, through encode, encode_measured, fury_row_decode and rows_to_arrow, with nulls,
-    empty and long strings, lists."""
-    from fury_amd import _native as N
-    from fury_amd.encoder import ArrowWriter, column_to_host
-    L = N.lib()
-    old = L.fury_get_tuning(b"var_wide")
-    assert L.fury_set_tuning(b"var_wide", kc) == 0
-    try:
-        fields = _wide_fields(ncols)
-        host = gen_columns("wide", fields, n, seed=ncols + kc, null_pct=15, str_max=90,
-                           list_max=12, list_null_pct=10, elem_null_pct=10)
-        enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
-        want, want_offs = oracle.encode(fields, host, n)
-        rows, offs, total = _encode_measured(enc, _dev_cols(host, dev), n, dev)
-        assert np.array_equal(offs.cpu().numpy(), want_offs)
-        assert np.array_equal(rows[:total].cpu().numpy(), want)
-        w = ArrowWriter(enc)
-        w.write(batch)
-        assert_columns_equal(fields, [column_to_host(c) for c in w.finish()],
-                             oracle.decode(fields, want, want_offs, n), n)
-    finally:
-        L.fury_set_tuning(b"var_wide", old)
-
-
 def test_wide_var_schema_large_batch(oracle, dev):
     """A 40-field schema over 300k rows (>1,000 workgroups chained by the look-back)."""
     fields = _wide_fields(40)

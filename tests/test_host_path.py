@@ -317,11 +317,11 @@ def _page_zeros(n, dtype=np.uint8):
 @pytest.mark.parametrize("name,n", [("foo", 3001), ("beana", 1200), ("nested7", 5000),
                                     ("maps", 777), ("nested7", 1)])
 def test_host_direct_nested_page_edge(oracle, name, n):
-    """Nested schemas (RowEncoderTest's Foo and BeanA among them) on pinned buffers run their
-    kernels on host memory: the encode reads the column tree and writes rows in place, the decode
-    plan reads the pinned rows in place and the execute writes values / offsets / payloads into
-    the pinned outputs (bitmaps through HBM) -- host_direct counts both.  Every buffer ends at a
-    page edge; rows, offsets and columns bit-exact vs the oracle."""
+    """Nested schemas (RowEncoderTest's Foo and BeanA among them) on pinned buffers: the encode
+    reads the column tree and writes rows in place (kernels on host memory); the decode stages the
+    rows in HBM and, with tuning host_decode_inplace, writes values / offsets / payloads into the
+    pinned outputs (bitmaps through HBM) -- host_direct counts both.  Every buffer ends at a page
+    edge; rows, offsets and columns bit-exact vs the oracle."""
     import ctypes
     from fury_amd import _native as N
     from fury_amd.beans import beans_to_columns, columns_to_beans
@@ -347,6 +347,7 @@ def test_host_direct_nested_page_edge(oracle, name, n):
     plan = ctypes.c_void_p()
     assert L.fury_decode_host_prepare(enc.schema().handle, rows.ctypes.data, roffs.ctypes.data,
                                       n, e, b, ctypes.byref(plan), 0) == 0, N.last_error()
+    assert L.fury_set_tuning(b"host_decode_inplace", 1) == 0
     try:
         order = _bfs(fields)
         out = [_alloc_host_node(f, int(e[i]), int(b[i]), _page_zeros) for i, (f, _) in enumerate(order)]
@@ -357,8 +358,9 @@ def test_host_direct_nested_page_edge(oracle, name, n):
         assert L.fury_decode_host_execute(plan, _c_host_columns(out[:len(fields)], keep)) == 0, \
             N.last_error()
     finally:
+        L.fury_set_tuning(b"host_decode_inplace", 0)
         L.fury_decode_plan_destroy(plan)
-    assert L.fury_get_tuning(b"host_direct") == d0 + 2, "decode did not take the direct path"
+    assert L.fury_get_tuning(b"host_direct") == d0 + 2, "decode did not write in place"
     top = out[:len(fields)]
     assert_columns_equal(fields, top, ref, n)
     assert columns_to_beans(fields, top, n) == beans

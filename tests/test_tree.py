@@ -199,12 +199,6 @@ def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, nam
         b1 = enc.encode_batch(dcols, n)
         assert np.array_equal(b1.row_offsets.cpu().numpy(), want_offs)
         assert np.array_equal(b1.rows.cpu().numpy(), want)
-    _tune("gen_prefetch", 1)          # the interpreter with each tile's inputs pulled first
-    try:
-        b2 = enc.encode_batch(dcols, n)
-        assert np.array_equal(b2.rows.cpu().numpy(), want)
-    finally:
-        _tune("gen_prefetch", 0)
 
 
 def test_tree_encode_capacity(oracle, dev, enc_engines):
