@@ -827,6 +827,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_tree_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "walk_skip") {
+    if (value < 0 || value > 15) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_skip: 0..15");
+    set_walk_tuning(5, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
   if (std::string(key) == "host_decode_inplace") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "host_decode_inplace: 0..1");
     set_host_decode_inplace(value);

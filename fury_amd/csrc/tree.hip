@@ -441,6 +441,7 @@ uint32_t g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for t
                                     // LDS-bound occupancy costs more than HBM row reads save)
 uint32_t g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
 int g_walk_prefetch = 1;            // tuning "walk_prefetch": write-pass waves pull their rows first
+int g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 uint32_t g_tree_stage = 32 * 1024, g_tree_arena = 24 * 1024;
 int g_tree_threads = 256;        // tuning "tree_threads": workgroup size of the decode (256/512/1024)
@@ -472,12 +473,13 @@ void set_walk_tuning(int which, uint32_t v) {
   else if (which == 1) g_walk_stage = (v + 15) & ~15u;
   else if (which == 2) g_walk_pool = (v + 15) & ~15u;
   else if (which == 3) g_walk_stage_w = (v + 15) & ~15u;
-  else g_walk_prefetch = static_cast<int>(v);
+  else if (which == 4) g_walk_prefetch = static_cast<int>(v);
+  else g_walk_skip = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
   return which == 0 ? static_cast<uint32_t>(g_walk_threads) : which == 1 ? g_walk_stage
          : which == 2 ? g_walk_pool : which == 3 ? g_walk_stage_w
-         : static_cast<uint32_t>(g_walk_prefetch);
+         : which == 4 ? static_cast<uint32_t>(g_walk_prefetch) : static_cast<uint32_t>(g_walk_skip);
 }
 
 struct TreePlan {
@@ -532,6 +534,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   if (p.walk) {
     if (write) a.stage_cap = p.arena_cap;        // walk plans: the write pass's stage cap
     a.prefetch = write ? g_walk_prefetch : 0;
+    a.skip = write ? g_walk_skip : 0;
     a.rowpre = p.rowpre;
     a.K = p.K;
     a.pool_cap = p.pool_cap;

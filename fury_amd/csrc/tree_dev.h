@@ -55,7 +55,8 @@ struct TreeArgs {
   int32_t K;                // counted slots
   uint32_t pool_cap;        // LDS bytes of the bitmap windows (write pass)
   int32_t prefetch;         // write pass: each wave first pulls its rows' lines (tuning)
-  int32_t pad2_;
+  int32_t skip;             // diagnostics (tuning "walk_skip", outputs wrong): 1 payload copies,
+                            // 2 bitmaps, 4 scalar values, 8 offsets not written
   int32_t knode[64];        // counted slot -> node
 };
 
@@ -232,34 +233,46 @@ __device__ __forceinline__ void tstore_w(uint8_t* p, int w, uint64_t v) {
   }
 }
 
-// len bytes of the batch at src -> dst (any alignment; only [dst, dst + len) written).
+// len bytes of the batch at src -> dst (any alignment; only [dst, dst + len) written).  The source
+// is read as aligned words (a word past the payload only when the payload reaches into it); the
+// destination takes at most three stores of 1 / 2 / 4 bytes before its first 8-byte boundary and
+// after its last, whole words in between (short strings: ~5 stores instead of ~15 byte stores).
 __device__ void tcopy_out(uint8_t* dst, const Rows& R, int64_t src, int64_t len) {
   if (len <= 0) return;
-  int64_t i = 0;
-  const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
-  for (; i < head; i++) gl(dst)[i] = rd1(R, src + i);
-  const int64_t s = src + head;             // source of the first whole destination word
-  const int o = static_cast<int>(s & 7);
-  const int64_t nw = (len - head) >> 3;
-  if (nw > 0) {
-    const int64_t s0 = s - o;               // aligned source word
-    uint64_t cur = rd8(R, s0);
-    auto d64 = gl(reinterpret_cast<uint64_t*>(dst + head));
-    for (int64_t w = 0; w < nw; w++) {
-      uint64_t v;
-      if (o == 0) {
-        v = cur;
-        if (w + 1 < nw) cur = rd8(R, s0 + 8 * (w + 1));
+  const int64_t s0 = src & ~int64_t(7);
+  const int o = static_cast<int>(src & 7);
+  // 8 payload bytes from payload byte i (bytes past len are garbage, never stored)
+  auto word_at = [&](int64_t i) -> uint64_t {
+    const int64_t p = o + i;
+    const int64_t q = s0 + (p & ~int64_t(7));
+    const int sh = static_cast<int>(p & 7) * 8;
+    const uint64_t a = rd8(R, q);
+    if (!sh || (p & 7) + min<int64_t>(8, len - i) <= 8) return sh ? a >> sh : a;
+    return (a >> sh) | (rd8(R, q + 8) << (64 - sh));
+  };
+  auto put_small = [&](uint8_t* d, uint64_t v, int n) {   // n < 8 bytes, d + n 8-aligned or end
+    int k = 0;
+    while (k < n) {
+      const uintptr_t ad = reinterpret_cast<uintptr_t>(d + k);
+      if ((ad & 1) || n - k < 2) {
+        gl(d)[k] = static_cast<uint8_t>(v >> (8 * k));
+        k += 1;
+      } else if ((ad & 2) || n - k < 4) {
+        *gl(reinterpret_cast<uint16_t*>(d + k)) = static_cast<uint16_t>(v >> (8 * k));
+        k += 2;
       } else {
-        const uint64_t nxt = rd8(R, s0 + 8 * (w + 1));
-        v = (cur >> (8 * o)) | (nxt << (64 - 8 * o));
-        cur = nxt;
+        *gl(reinterpret_cast<uint32_t*>(d + k)) = static_cast<uint32_t>(v >> (8 * k));
+        k += 4;
       }
-      d64[w] = v;
     }
-    i = head + 8 * nw;
-  }
-  for (; i < len; i++) gl(dst)[i] = rd1(R, src + i);
+  };
+  const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
+  if (head > 0) put_small(dst, word_at(0), static_cast<int>(head));
+  const int64_t nw = (len - head) >> 3;
+  auto d64 = gl(reinterpret_cast<uint64_t*>(dst + head));
+  for (int64_t w = 0; w < nw; w++) d64[w] = word_at(head + 8 * w);
+  const int64_t t0 = head + 8 * nw;
+  if (t0 < len) put_small(dst + t0, word_at(t0), static_cast<int>(len - t0));
 }
 
 // Where an error of a nested entry is reported in pass 1: the node and the first row of the

@@ -141,14 +141,73 @@ __device__ __forceinline__ void wbit(const WCtx& c, CTNode& N, int n, int which,
   }
 }
 
+// Bits of consecutive entries e0, e0 + 1, ... (mask bit q = entry e0 + q, q < 32) OR-ed into node
+// n's window (or the bitmap in HBM): at most two words.  Not for row-aligned nodes.
+__device__ __forceinline__ void wbits_run(const WCtx& c, int n, int which, uint8_t* bits,
+                                          int64_t e0, uint32_t mask) {
+  if (!mask) return;
+  const int sh = static_cast<int>(e0 & 31);
+  const uint32_t lo = mask << sh;
+  const uint32_t hi = sh ? static_cast<uint32_t>(static_cast<uint64_t>(mask) >> (32 - sh)) : 0u;
+  const int64_t w = e0 >> 5;
+  const int wi = c.sh->win[which * c.a->nn + n];
+  if (wi >= 0) {
+    uint32_t* p = c.sh->pool + wi + (w - c.sh->w0[n]);
+    if (lo) atomicOr(p, lo);
+    if (hi) atomicOr(p + 1, hi);
+  } else {
+    auto g = gl(reinterpret_cast<uint32_t*>(bits)) + w;
+    if (lo) __hip_atomic_fetch_or(g, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (hi) __hip_atomic_fetch_or(g + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// m fixed-width elements of a LIST / MAP side (write pass) at entries cs, cs + 1, ...: values one
+// by one, validity / BOOL bits batched 32 elements to an atomic pair, null bits read a word at a
+// time.
+__device__ __forceinline__ void welems(const WCtx& c, CTNode& C, int cn, int64_t cs, int64_t arr,
+                                       int64_t hb, uint32_t m) {
+  const Rows& R = *c.R;
+  const int es = C.esize;
+  const int64_t ev = arr + 8 + hb;
+  const bool bits = !(c.a->skip & 2);
+  uint64_t nb = 0;
+  uint32_t vm = 0, bm = 0;
+  int64_t eb = cs;
+  for (uint32_t j = 0; j < m; j++) {
+    if ((j & 63) == 0) nb = rd8(R, arr + 8 + (j >> 3));
+    const bool cnul = (nb >> (j & 63)) & 1;
+    const uint64_t x = cnul ? 0 : rdw(R, ev + static_cast<int64_t>(es) * j, es);
+    const int q = static_cast<int>(j & 31);
+    if (C.type == FURY_TYPE_BOOL) {
+      if (!cnul && (x & 0xff)) bm |= 1u << q;
+    } else if (C.values && !(c.a->skip & 4)) {
+      tstore_w(C.values + (cs + j) * C.width, C.width, x);
+    }
+    if (!cnul) vm |= 1u << q;
+    if (q == 31 || j + 1 == m) {
+      if (bits) {
+        if (C.validity) wbits_run(c, cn, 0, C.validity, eb, vm);
+        if (C.type == FURY_TYPE_BOOL && C.values) wbits_run(c, cn, 1, C.values, eb, bm);
+      }
+      eb += q + 1;
+      vm = bm = 0;
+    }
+  }
+}
+
 // A fixed-width entry (write pass): value (0 when null), BOOL bit, validity bit.
 __device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t e, bool nul,
                                         int64_t slotp, int rw) {
   const uint64_t x = nul ? 0 : rdw(*c.R, slotp, rw);
+  if (c.a->skip & 2) {
+    if (N.type != FURY_TYPE_BOOL && N.values && !(c.a->skip & 4)) tstore_w(N.values + e * N.width, N.width, x);
+    return;
+  }
   if (N.type == FURY_TYPE_BOOL) {
     if (N.values) wbit(c, N, n, 1, N.values, e, !nul && (x & 0xff));
   } else if (N.values) {
-    tstore_w(N.values + e * N.width, N.width, x);
+    if (!(c.a->skip & 4)) tstore_w(N.values + e * N.width, N.width, x);
   }
   if (N.validity) wbit(c, N, n, 0, N.validity, e, !nul);
 }
@@ -184,7 +243,7 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       if (!tcheck(a, R, N, pos, size, c.total, &cnt, static_cast<uint64_t>(c.row))) pos = kNullPos;
     }
     const bool valid = pos >= 0;
-    if (W && D > 0 && N.validity) wbit(c, N, n, 0, N.validity, e, valid);
+    if (W && D > 0 && N.validity && !(a.skip & 2)) wbit(c, N, n, 0, N.validity, e, valid);
     if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
       uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
       const uint32_t c0 = *cu;
@@ -192,10 +251,10 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       if (W) {
         const int64_t bp = c.sh->kb[N.k] + c0;
         if (N.offsets) {
-          gl(N.offsets)[e + 1] = static_cast<int32_t>(bp + cnt);
+          if (!(a.skip & 8)) gl(N.offsets)[e + 1] = static_cast<int32_t>(bp + cnt);
           if (e == 0) gl(N.offsets)[0] = 0;
         }
-        if (valid && N.values) tcopy_out(N.values + bp, R, pos, cnt);
+        if (valid && N.values && !(a.skip & 1)) tcopy_out(N.values + bp, R, pos, cnt);
       }
       return valid;
     }
@@ -222,7 +281,7 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       if (W) {
         cs = c.sh->kb[N.k] + c0;
         if (N.offsets) {
-          gl(N.offsets)[e + 1] = static_cast<int32_t>(cs + m);
+          if (!(a.skip & 8)) gl(N.offsets)[e + 1] = static_cast<int32_t>(cs + m);
           if (e == 0) gl(N.offsets)[0] = 0;
         }
       }
@@ -236,6 +295,10 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       if (!strc) {
         CTNode& C = tn(a, N.first_child + sd);
         if (!W && !C.walk) continue;              // nothing to count below
+        if (W && C.width > 0) {                   // fixed-width elements: batched bits
+          welems(c, C, N.first_child + sd, cs, arr, hb, m);
+          continue;
+        }
       }
       for (uint32_t j = 0; j < m; j++) {
         const int cn = strc ? N.first_child + static_cast<int>(j) : N.first_child + sd;
