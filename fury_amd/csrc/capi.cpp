@@ -827,6 +827,18 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_tree_mode(value);
     return FURY_OK;
   }
+  if (std::string(key) == "var_dec_cover") {
+    if (value != 0 && (value < 50 || value > 100))
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_cover: 50..100 (0 = default)");
+    set_var_dec_cover(value ? value : 95);
+    return FURY_OK;
+  }
+  if (std::string(key) == "var_dec_rows") {
+    if (value != 0 && (value < 64 || value > 512 || value % 64))
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_rows: 0 or 64..512 in steps of 64");
+    set_var_dec_rows(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "walk_skip") {
     if (value < 0 || value > 15) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_skip: 0..15");
     set_walk_tuning(5, static_cast<uint32_t>(value));
@@ -905,6 +917,8 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
+  if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
+  if (key && std::string(key) == "var_dec_cover") return var_dec_cover();
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
   if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);
   if (key && std::string(key) == "tree_measure_rows") return tree_encode_rows(0);

@@ -218,6 +218,10 @@ int encode_tile_rows(const VarArgs& a);
 int64_t lookback_timeouts();
 void set_host_decode_inplace(int v);   // tuning "host_decode_inplace" (hostpath.cpp)
 int host_decode_inplace();
+int var_dec_rows();                   // tuning "var_dec_rows" (var.hip): 0 = planned
+void set_var_dec_rows(int v);
+int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
+void set_var_dec_cover(int v);
 int lookback_help_mode();
 void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);

@@ -177,6 +177,16 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   return st;
 }
 
+static int g_dec_rows = 0;
+int var_dec_rows() { return g_dec_rows; }
+void set_var_dec_rows(int v) { g_dec_rows = v; }
+// tuning "var_dec_cover": percent of a tile's estimated row bytes the stage must hold (the rest
+// is read from HBM by the rows' threads).  95 (scripts/ab_dec.py legs, interleaved): mixed 10M
+// 0.542 -> 0.508 ms (its tiles grow 448 -> 512 rows), C4 4M unchanged (0.229 ms); 80 or less slows C4.
+static int g_dec_cover = 95;
+int var_dec_cover() { return g_dec_cover; }
+void set_var_dec_cover(int v) { g_dec_cover = v; }
+
 // Tile plan of decode_var_reg: rows per tile (a multiple of 64, <= kDecThreads), LDS bytes of the
 // output images and of the row stage, within the LDS of two workgroups per CU.  Per-row sizes are
 // estimated from the output capacities (exact after fury_row_decode_measure, an over-estimate under
@@ -205,10 +215,18 @@ void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) 
   // headroom over the estimates: 8 % on the images, 2 % on the stage (a 512-row tile's bytes
   // vary by ~1 %; C4 0.252 -> 0.229 ms against 15 % / 5 %, mixed unchanged)
   const double mi = 1.08, mr = 1.02;
+  if (g_dec_rows > 0) {                         // tuning "var_dec_rows": forced tile rows (A/B)
+    const int R = g_dec_rows;
+    const int64_t im = (static_cast<int64_t>(img_row * R * mi + img_fix) + 1023) & ~int64_t(1023);
+    *tile = R;
+    *img = static_cast<uint32_t>(std::min<int64_t>(im, kBudget / 2));
+    *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
+    return;
+  }
   for (int R = kDecThreads; R >= 64; R -= 64) {
     const int64_t im = (static_cast<int64_t>(img_row * R * mi + img_fix) + 1023) & ~int64_t(1023);
     const int64_t st = (kBudget - im) & ~int64_t(15);
-    if (st >= static_cast<int64_t>(row * R * mr) + 64 || R == 64) {
+    if (st >= static_cast<int64_t>(row * R * mr * g_dec_cover / 100.0) + 64 || R == 64) {
       *tile = R;
       *img = static_cast<uint32_t>(std::min<int64_t>(im, kBudget / 2));
       *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
