@@ -186,7 +186,10 @@ int fury_row_decode_measure(const fury_schema* schema, const void* rows,
  * offsets are computed here (fury_row_decode_measure is only needed to size the buffers); when
  * offsets[nrows] exceeds a column's capacity the payload past the capacity is not written —
  * grow the buffer and decode again.  Malformed rows are reported asynchronously, on `stream`
- * (fury_device_status below). */
+ * (fury_device_status below).  Nested schemas, and flat ones with more than 256 fields of which
+ * some are variable-length (the generic engine), decode through fury_decode_prepare /
+ * fury_decode_execute instead: these calls (and fury_row_decode_measure) return
+ * FURY_ERR_INVALID_ARGUMENT for them, naming the plan API. */
 int fury_row_decode(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                     int64_t nrows, fury_column* columns, void* stream);
 /* ArrowWriter.write(row) for every row + finishAsRecordBatch: as fury_row_decode but every
@@ -271,12 +274,22 @@ int fury_device_status(void* stream);
 int fury_trim_workspace(int32_t device);
 
 /* ---- tuning (no reference equivalent) ---------------------------------------------------- */
-/* Process-wide knobs for tests and A/B measurement (results are identical under every value).
+/* Process-wide knobs for tests and A/B measurement (results are identical under every value,
+ * except the diagnostic "walk_skip").
  * Key "lookback_help": 1 = every look-back of the variable-length decode computes a silent
  * predecessor tile's aggregate at once (the path a late-dispatched predecessor takes).
  * Key "unframe": 0 speculative parallel stream parse (a stream that does not verify -- a payload
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.
+ * Nested engines: "nested_decode" 2 row walk (default), 1 level engine, 0 tree tiles;
+ * "nested_encode" 2 tree-tile measure + row interpreter (default), 1 interpreter, 0 tree tiles;
+ * row walk "walk_threads" (128 / 256), "walk_stage" / "walk_stage_write" / "walk_pool" (LDS
+ * bytes), "walk_prefetch" (0 / 1); tree tiles "tree_stage" / "tree_arena" / "tree_threads",
+ * "tree_enc_lds" / "tree_measure_lds" / "tree_enc_rows" / "tree_measure_rows"; diagnostics
+ * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
+ * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's
+ * row bytes the LDS stage must hold, default 95), "var_dec_rows" (forced tile rows, 0 = plan).
+ * Host path: "host_decode_inplace" (0 / 1).
  * fury_get_tuning only: "unframe_walks" = streams the walk parsed (wholly or from the first frame
  * the repair could not place), "unframe_repairs" = streams the parallel repair parsed,
  * "host_direct" = fury_row_encode_host / _decode_host calls that ran their kernels directly on
@@ -307,7 +320,8 @@ int fury_unframe_rows(const fury_schema* schema, const void* stream_bytes, int64
  * the kernel directly on host memory — loads and stores cross PCIe in both directions at once,
  * no HBM staging ("host_direct" counts these calls); otherwise they are staged through HBM
  * (chunked over three HIP streams).  Flat variable-length schemas on pinned buffers run direct
- * too (bitmaps through HBM); otherwise, and nested schemas always, they are staged whole.  `device` is the
+ * too (bitmaps through HBM), and so does the ENCODE of nested schemas (the column tree read and
+ * the rows written in place); otherwise they are staged whole.  `device` is the
  * HIP device ordinal.  Buffers from fury_host_alloc (hipHostMalloc) run fastest; registering
  * ordinary 4 KB-page memory (fury_host_register, hipHostRegister) pins it in place but the GPU
  * then walks 4 KB translations (host path). */
@@ -325,8 +339,10 @@ int fury_row_encode_host(const fury_schema* schema, const fury_column* columns, 
 /* Host rows -> host columns (fromRow semantics, like fury_row_decode).  Variable-length flat
  * schemas: STRING/BINARY payload capacity in fury_column.capacity, LIST element bytes in the
  * child's capacity (FURY_ERR_CAPACITY when short: staged calls size first and write nothing,
- * direct calls write nothing past a capacity and leave offsets[nrows] = the size needed); nested schemas: FURY_ERR_UNSUPPORTED (their
- * output sizes depend on the data: fury_decode_host_prepare / fury_decode_host_execute below). */
+ * direct calls write nothing past a capacity and leave offsets[nrows] = the size needed); nested
+ * schemas and flat ones with more than 256 fields of which some are variable-length:
+ * FURY_ERR_UNSUPPORTED (their output sizes depend on the data: fury_decode_host_prepare /
+ * fury_decode_host_execute below). */
 int fury_row_decode_host(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
                          int64_t nrows, fury_column* columns, int32_t device);
 
@@ -337,7 +353,9 @@ int fury_row_decode_host(const fury_schema* schema, const void* rows, const int6
  * host buffers from them (validity (entries + 7) / 8 bytes, offsets entries + 1 int32, values
  * entries * width / (entries + 7) / 8 for BOOL / node_bytes for STRING-BINARY (checked against
  * fury_column.capacity) / 16 * entries for DECIMAL) and calls fury_decode_host_execute, which
- * decodes in HBM and copies every buffer back (synchronous).  The plan is freed by
+ * decodes in HBM and copies every buffer back (synchronous; with tuning "host_decode_inplace" the
+ * values / offsets / payloads of pinned outputs are written in place -- slower).
+ * The plan is freed by
  * fury_decode_plan_destroy.  Replaces generated fromRow + ArrowWriter for nested beans
  * (FMT/encoder/BaseBinaryEncoderBuilder.java:459-706, FMT/vectorized/ArrowWriter.java:519-640). */
 int fury_decode_host_prepare(const fury_schema* schema, const void* rows, const int64_t* row_offsets,
