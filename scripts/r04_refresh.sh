@@ -4,12 +4,12 @@
 # stats of each workload.  Each GPU step has its own time limit; stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r04c
+OUT=gpurun_out/${R04_OUT:-r04c}
 mkdir -p $OUT
 export TMPDIR=/tmp
 for w in struct100 mixed nested; do
   timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 3 > $OUT/bench_$w.json 2> $OUT/bench_$w.err || { tail -5 $OUT/bench_$w.err; exit 1; }
-  echo "[r04c] bench $w: $(cut -c1-160 $OUT/bench_$w.json)"
+  echo "[refresh] bench $w: $(cut -c1-160 $OUT/bench_$w.json)"
   timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $OUT/prof_$w -o $w --output-format csv \
     -- python3 bench.py --workload $w --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
     > $OUT/prof_$w.log 2>&1 || { tail -5 $OUT/prof_$w.log; exit 1; }
@@ -17,5 +17,5 @@ done
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --share-gpus --steps 10 --warmup 2 --no-cpu-baseline --no-e2e \
   > $OUT/bench_2rank.json 2> $OUT/bench_2rank.err || { tail -5 $OUT/bench_2rank.err; exit 1; }
-echo "[r04c] 2-rank: $(cut -c1-200 $OUT/bench_2rank.json)"
-echo "[r04c] done"
+echo "[refresh] 2-rank: $(cut -c1-200 $OUT/bench_2rank.json)"
+echo "[refresh] done"
