@@ -839,6 +839,12 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_dec_rows(value);
     return FURY_OK;
   }
+  if (std::string(key) == "walk_threads_write") {
+    if (value != 128 && value != 256)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads_write: 128 or 256");
+    set_walk_tuning(6, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
   if (std::string(key) == "walk_skip") {
     if (value < 0 || value > 15) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_skip: 0..15");
     set_walk_tuning(5, static_cast<uint32_t>(value));
@@ -916,6 +922,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_pool") return static_cast<int32_t>(walk_tuning(2));
   if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
+  if (key && std::string(key) == "walk_threads_write") return static_cast<int32_t>(walk_tuning(6));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
   if (key && std::string(key) == "var_dec_cover") return var_dec_cover();

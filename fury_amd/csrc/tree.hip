@@ -432,11 +432,12 @@ int tree_host_width(int32_t t) {
 }
 
 int g_tree_mode = 2;             // tuning "nested_decode": 0 tree tiles, 1 level engine, 2 row walk
-// Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row tiles with a
-// 20 KB count-pass stage (prepare 1.35 -> 1.17 ms: more tiles resident), write-pass prefetch
-// (execute 2.00 -> 1.91 ms).
-int g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per row-walk tile
-uint32_t g_walk_stage = 20 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
+// Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row count tiles with
+// a 12 KB stage (prepare 1.35 -> 1.08 ms: more tiles resident), 256-row write tiles (1.87 -> 1.78
+// ms) with the prefetch.
+int g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per count tile
+int g_walk_threads_w = 256;      // tuning "walk_threads_write": rows per write tile (a multiple)
+uint32_t g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
 uint32_t g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
 uint32_t g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
@@ -474,12 +475,14 @@ void set_walk_tuning(int which, uint32_t v) {
   else if (which == 2) g_walk_pool = (v + 15) & ~15u;
   else if (which == 3) g_walk_stage_w = (v + 15) & ~15u;
   else if (which == 4) g_walk_prefetch = static_cast<int>(v);
-  else g_walk_skip = static_cast<int>(v);
+  else if (which == 5) g_walk_skip = static_cast<int>(v);
+  else g_walk_threads_w = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
   return which == 0 ? static_cast<uint32_t>(g_walk_threads) : which == 1 ? g_walk_stage
          : which == 2 ? g_walk_pool : which == 3 ? g_walk_stage_w
-         : which == 4 ? static_cast<uint32_t>(g_walk_prefetch) : static_cast<uint32_t>(g_walk_skip);
+         : which == 4 ? static_cast<uint32_t>(g_walk_prefetch)
+         : which == 5 ? static_cast<uint32_t>(g_walk_skip) : static_cast<uint32_t>(g_walk_threads_w);
 }
 
 struct TreePlan {
@@ -495,7 +498,7 @@ struct TreePlan {
   bool walk = false;
   int64_t stride = 0;              // ntiles (tree tiles) / ntiles + 1 (row walk)
   uint32_t* rowpre = nullptr;      // [K][nrows]
-  int32_t K = 0, nt = 0;
+  int32_t K = 0, nt = 0, ntw = 0;   // count / write tile rows
   uint32_t pool_cap = 0;
   int32_t knode[kWalkMaxK] = {};
 };
@@ -539,7 +542,10 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
     a.K = p.K;
     a.pool_cap = p.pool_cap;
     for (int k = 0; k < p.K; k++) a.knode[k] = p.knode[k];
-    return walk_launch(a, p.nt, write, hs);
+    a.ctr = p.nt;
+    a.tmul = write ? p.ntw / p.nt : 1;
+    if (write) a.ntiles = (p.nrows + p.ntw - 1) / p.ntw;
+    return walk_launch(a, write ? p.ntw : p.nt, write, hs);
   }
   for (int i = 0; i <= a.nlevels; i++) a.level_start[i] = p.level_start[i];
   int maxw = 0;
@@ -651,6 +657,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     // a thread per row; the stage holds the tile's rows up to walk_stage bytes (the rest are read
     // from HBM), the bitmap-window pool walk_pool bytes
     p->nt = g_walk_threads;
+    p->ntw = g_walk_threads_w % p->nt == 0 && g_walk_threads_w >= p->nt ? g_walk_threads_w : p->nt;
     p->tile_rows = p->nt;
     const double want = avg * p->nt * 1.04 + 64;
     p->stage_cap = static_cast<uint32_t>(std::min<double>(g_walk_stage, want) + 15) & ~15u;

@@ -57,6 +57,8 @@ struct TreeArgs {
   int32_t prefetch;         // write pass: each wave first pulls its rows' lines (tuning)
   int32_t skip;             // diagnostics (tuning "walk_skip", outputs wrong): 1 payload copies,
                             // 2 bitmaps, 4 scalar values, 8 offsets not written
+  int32_t tmul;             // write pass: count tiles per write tile (1 or 2)
+  int32_t ctr;              // rows per count tile
   int32_t knode[64];        // counted slot -> node
 };
 

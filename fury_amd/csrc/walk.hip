@@ -470,14 +470,22 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   __shared__ uint64_t tacc[16];
   const WClock clk{a.dbg ? tacc : nullptr};
   clk.start();
-  for (int k = 0; k < a.K; k++)
-    sh.cur[k * NT + tid] = live ? gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] : 0u;
-  for (int k = tid; k < a.K; k += NT) {
+  // A write tile spans tmul count tiles [tc0, tc1): a row's cursor = its in-count-tile prefix +
+  // its count tile's base - the write tile's base (kb).
+  const int64_t tc0 = t * a.tmul, tc1 = min<int64_t>(tc0 + a.tmul, a.stride - 1);
+  const int64_t tcr = live ? (r0 + tid) / a.ctr : tc0;
+  auto slot_base = [&](int k, int64_t tc) -> int64_t {
     const int n = a.knode[k];
     CTNode& N = tn(a, n);
-    sh.kb[k] = (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY)
-                   ? a.byt[n * a.stride + t] : a.cnt[N.first_child * a.stride + t];
+    return (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY)
+               ? a.byt[n * a.stride + tc] : a.cnt[N.first_child * a.stride + tc];
+  };
+  for (int k = 0; k < a.K; k++) {
+    uint32_t c = live ? gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] : 0u;
+    if (tcr != tc0) c += static_cast<uint32_t>(slot_base(k, tcr) - slot_base(k, tc0));
+    sh.cur[k * NT + tid] = c;
   }
+  for (int k = tid; k < a.K; k += NT) sh.kb[k] = slot_base(k, tc0);
   // bitmap windows of the nodes that are not row-aligned: words covering the tile's entries
   for (int i = tid; i < 2 * nn; i += NT) {
     const int n = i < nn ? i : i - nn;
@@ -486,7 +494,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
                                            : (N.type == FURY_TYPE_BOOL && N.values != nullptr));
     uint32_t words = 0;
     if (want) {
-      const int64_t e0 = a.cnt[n * a.stride + t], e1 = a.cnt[n * a.stride + t + 1];
+      const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
       if (e1 > e0) words = static_cast<uint32_t>(((e1 - 1) >> 5) - (e0 >> 5) + 1);
       if (i < nn) sh.w0[n] = e0 >> 5;
     }

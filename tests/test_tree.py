@@ -34,7 +34,7 @@ def engines():
     L = N.lib()
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena",
                                                        "walk_threads", "walk_stage", "walk_pool",
-                                                       "walk_stage_write")}
+                                                       "walk_stage_write", "walk_threads_write")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -90,6 +90,7 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         _tune("walk_stage_write", 2048)
         _tune("walk_pool", 0)
         _tune("walk_threads", 128)
+        _tune("walk_threads_write", 128)
     _tune("nested_decode", 2)
     walk = _decode_plan(enc, batch)
     assert_columns_equal(fields, walk, ref, n)
