@@ -636,21 +636,34 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   p->level_start[0] = 0;
   for (int L = 1; L <= nlev; L++)               // BFS: levels are contiguous and increasing
     if (p->level_start[L] < p->level_start[L - 1]) p->level_start[L] = p->level_start[L - 1];
-  // tile rows from the batch's average row size (one small read)
-  int64_t* pin = nullptr;
-  if (hipHostMalloc(reinterpret_cast<void**>(&pin), 8 * (2 * nn + 2), hipHostMallocDefault) != hipSuccess) {
-    delete p;
-    return set_error(FURY_ERR_DEVICE, "hipHostMalloc (tree plan)");
+  // pinned landing zone of the totals: one per host thread, kept (a hipHostMalloc / hipHostFree
+  // pair per call cost more host time than the small kernels)
+  static thread_local int64_t* pin = nullptr;
+  static thread_local size_t pin_words = 0;
+  if (pin_words < static_cast<size_t>(2 * nn + 2)) {
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_words = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&pin), 8 * (2 * kTreeMaxNodes + 2), hipHostMallocDefault) != hipSuccess) {
+      pin = nullptr;
+      delete p;
+      return set_error(FURY_ERR_DEVICE, "hipHostMalloc (tree plan)");
+    }
+    pin_words = 2 * kTreeMaxNodes + 2;
   }
-  int st = check_hip(hipMemcpyAsync(pin, offs + nrows, 8, hipMemcpyDeviceToHost, hs), "hipMemcpyAsync");
-  if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
-  if (st) {
-    (void)hipHostFree(pin);
-    delete p;
-    return st;
+  int st = FURY_OK;
+  double avg = 64.0;
+  if (!walk) {
+    // tile rows from the batch's average row size (one small read; the row walk's tiles are fixed)
+    st = check_hip(hipMemcpyAsync(pin, offs + nrows, 8, hipMemcpyDeviceToHost, hs), "hipMemcpyAsync");
+    if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+    if (st) {
+      delete p;
+      return st;
+    }
+    const int64_t total = std::max<int64_t>(pin[0], 1);
+    avg = std::max(8.0, static_cast<double>(total) / static_cast<double>(nrows));
   }
-  const int64_t total = std::max<int64_t>(pin[0], 1);
-  const double avg = std::max(8.0, static_cast<double>(total) / static_cast<double>(nrows));
   // rows per tile: the tile's bytes fill ~90 % of the stage, its level arrays (~1.5 x the row
   // bytes at worst: 12 B per non-scalar entry, each behind an 8-byte slot) the arena
   if (walk) {
@@ -659,9 +672,8 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     p->nt = g_walk_threads;
     p->ntw = g_walk_threads_w % p->nt == 0 && g_walk_threads_w >= p->nt ? g_walk_threads_w : p->nt;
     p->tile_rows = p->nt;
-    const double want = avg * p->nt * 1.04 + 64;
-    p->stage_cap = static_cast<uint32_t>(std::min<double>(g_walk_stage, want) + 15) & ~15u;
-    p->arena_cap = static_cast<uint32_t>(std::min<double>(g_walk_stage_w, want) + 15) & ~15u;
+    p->stage_cap = (g_walk_stage + 15) & ~15u;
+    p->arena_cap = (g_walk_stage_w + 15) & ~15u;
     p->pool_cap = g_walk_pool;
   } else {
     const double by_stage = 0.9 * p->stage_cap / avg, by_arena = 0.9 * p->arena_cap / (0.75 * avg);
@@ -699,7 +711,6 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
       (*totals)[2 * i + 1] = pin[nn + i];
     }
   }
-  (void)hipHostFree(pin);
   dev_free(tot, hs);
   if (st || over) {
     tree_free(p);
