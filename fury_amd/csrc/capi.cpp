@@ -856,7 +856,7 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "walk_prefetch") {
-    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_prefetch: 0..1");
+    if (value < 0 || value > 3) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_prefetch: 0..3 (bit 0 write pass, bit 1 count pass)");
     set_walk_tuning(4, static_cast<uint32_t>(value));
     return FURY_OK;
   }
@@ -884,8 +884,24 @@ int fury_set_tuning(const char* key, int32_t value) {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "tree_debug: 0..1");
     return set_tree_debug(value) ? set_error(FURY_ERR_DEVICE, "tree_debug buffer") : FURY_OK;
   }
+  if (std::string(key) == "rowenc_rows") {
+    if (value != 128 && value != 256) return set_error(FURY_ERR_INVALID_ARGUMENT, "rowenc_rows: 128 or 256");
+    set_rowenc_tuning(0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "rowenc_tile") {
+    if (value < 0 || value > 256) return set_error(FURY_ERR_INVALID_ARGUMENT, "rowenc_tile: 0..256");
+    set_rowenc_tuning(2, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "rowenc_img") {
+    if (value < 1024 || value > 152 * 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "rowenc_img: 1024..155648 bytes");
+    set_rowenc_tuning(1, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
   if (std::string(key) == "nested_encode") {
-    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..2");
+    if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..4");
     set_tree_encode_mode(value);
     return FURY_OK;
   }
@@ -916,6 +932,9 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "nested_decode") return tree_mode();
   if (key && std::string(key) == "nested_encode") return tree_encode_mode();
+  if (key && std::string(key) == "rowenc_rows") return static_cast<int32_t>(rowenc_tuning(0));
+  if (key && std::string(key) == "rowenc_img") return static_cast<int32_t>(rowenc_tuning(1));
+  if (key && std::string(key) == "rowenc_tile") return static_cast<int32_t>(rowenc_tuning(2));
   if (key && std::string(key) == "tree_threads") return tree_threads();
   if (key && std::string(key) == "walk_threads") return static_cast<int32_t>(walk_tuning(0));
   if (key && std::string(key) == "walk_stage") return static_cast<int32_t>(walk_tuning(1));

@@ -1085,8 +1085,9 @@ void gen_encode_root(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint
 
 namespace {
 // tuning "nested_encode": 0 tree tiles (measure + encode), 1 the row interpreter (both), 2 tree
-// measure + interpreter encode (default: the fastest pair measured, scripts/ab_generic.py).
-// Schemas nested deeper than the interpreter unrolls (kGenMaxDepth) always take the tree tiles.
+// measure + interpreter encode, 3 tree measure + row-walk encode (rowenc.hip), 4 row walk (both).
+// Schemas nested deeper than the interpreter unrolls (kGenMaxDepth) always take the tree tiles;
+// the row walk covers up to kRowEncMaxDepth levels (deeper: the interpreter).
 int g_tree_encode = 2;
 uint32_t g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
 int g_te_rows[2] = {256, 256};                   // rows per workgroup tile: measure, encode
@@ -1134,7 +1135,8 @@ int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, ui
   const int nlev = level[nn - 1] + 1;
   if (nlev > kTEMaxLevels) return 1;
   const bool deep = nlev >= kGenMaxDepth;       // beyond the row interpreter
-  if (!deep && (g_tree_encode == 1 || (g_tree_encode == 2 && sizes == nullptr))) return 1;
+  if (!deep && (g_tree_encode == 1 || g_tree_encode == 4 || (g_tree_encode >= 2 && sizes == nullptr)))
+    return 1;
   TEArgs a{};
   a.deep = deep ? 1 : 0;
   a.err = device_error_word(stream);
@@ -1229,7 +1231,8 @@ int tree_encode_rows(int which) { return g_te_rows[which ? 1 : 0]; }
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
   if (g.nrows > 0) {
-    const int t = launch_tree_encode(g, nullptr, sizes, nullptr, 0, stream);
+    int t = launch_tree_encode(g, nullptr, sizes, nullptr, 0, stream);
+    if (t == 1 && g_tree_encode == 4) t = rowenc_launch(g, nullptr, sizes, nullptr, 0, stream);
     if (t != 1) return t;
   }
   if (g.tab) gen_encode_root<true>(g, nullptr, sizes, nullptr, 0, stream);
@@ -1240,7 +1243,8 @@ int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream) {
   if (g.nrows > 0) {
-    const int t = launch_tree_encode(g, offs, nullptr, rows, cap, stream);
+    int t = launch_tree_encode(g, offs, nullptr, rows, cap, stream);
+    if (t == 1 && g_tree_encode >= 3) t = rowenc_launch(g, offs, nullptr, rows, cap, stream);
     if (t != 1) return t;
   }
   if (g.tab) gen_encode_root<true>(g, offs, nullptr, rows, cap, stream);

@@ -264,6 +264,13 @@ struct GenArgs {
 };
 
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
+// Row-walk encode (rowenc.hip): measure (sizes != NULL) or build pass for schemas of up to
+// kRowEncMaxDepth levels; returns 1 when the schema is deeper (left to the interpreter).
+constexpr int kRowEncMaxDepth = 5;
+int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
+                  int64_t cap, hipStream_t stream);
+void set_rowenc_tuning(int which, uint32_t v);   // 0 "rowenc_rows", 1 "rowenc_img", 2 "rowenc_tile"
+uint32_t rowenc_tuning(int which);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
 // Nested encode engine (generic.hip): tuning "nested_encode" 0 = tree tiles (default), 1 = the

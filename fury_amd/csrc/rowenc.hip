@@ -1,0 +1,373 @@
+// rowenc.hip — nested encode with a thread per ROW, the schema walk inlined per depth: the
+// default build pass (and optional measure pass) of fury_encode for schemas of up to
+// kRowEncMaxDepth levels.  generic.hip's interpreter (put_value / put_array, called level by
+// level) stays for deeper schemas; the tree tiles (generic.hip, te_kernel) for the deepest.
+//
+// Reference semantics are the interpreter's (generic.hip header): BaseBinaryEncoderBuilder
+// .serializeFor (FMT/encoder/BaseBinaryEncoderBuilder.java:138-453) -- primitives in 8-byte slots
+// (narrow in arrays), var values appended at the writer index and zero-padded to 8
+// (BinaryWriter.java:106-121,187-194), List -> [int64 n][bitmap][n x elemSize, tail zeroed][var
+// section] (BinaryArrayWriter.java:91-163), bean -> nested BinaryRowWriter row (:363-417), Map ->
+// [int64 keyBytes][key array][value array] (:298-357), null -> setNullAt (bit only).  The bytes
+// written are identical to the interpreter's (tests/test_tree.py runs every nested_encode mode
+// against the oracle).
+//
+// MI355X design.  The interpreter's depth templates call each other (put_value -> put_array ->
+// put_value): every level is a call frame, and the build kernel kept 256 VGPRs plus ~870 B of
+// scratch per lane live.  Here a container's children -- a STRUCT's fields, a LIST's elements, a
+// MAP's keys then values -- go through ONE loop with ONE call of the next level, so the levels
+// inline into straight code (as walk.hip's decode walk); scalar children are stored at the call
+// site, so a schema of L levels needs L instances.  Every active lane of a wave is at the same
+// schema node at the same time (the loops are schema-driven), so node records come from a device
+// table through scalar loads (readfirstlane'd index).  The build pass writes a workgroup's rows
+// (rowenc_rows) into an LDS image of their contiguous output range and stores it coalesced (as
+// the interpreter's build kernel), in chunks of rows that fit the image (rowenc_img): thread-per-
+// row stores straight to HBM wrote several times the row bytes (partial lines); only a row larger
+// than the whole image is built in HBM.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "internal.h"
+#include "kernels.h"
+
+namespace fury {
+
+namespace {
+
+constexpr int kRwThreads = 256;                 // measure pass rows per workgroup
+int g_rw_rows = 256;                            // tuning "rowenc_rows": build-pass rows per workgroup
+uint32_t g_rw_img = 76 * 1024;                  // tuning "rowenc_img": its LDS image bytes
+int g_rw_tile = 0;                              // tuning "rowenc_tile": rows per workgroup (0: all)
+
+template <class T>
+using Lds = __attribute__((address_space(3))) T;
+using LdsU8 = Lds<uint8_t>;
+using CGNode = __attribute__((address_space(4))) const GenNode;
+
+struct RwArgs {
+  const GenNode* tab;       // device node table (scalar loads)
+  int64_t img;              // build pass: LDS image bytes
+  int64_t tile;             // build pass: rows per workgroup (<= its threads)
+  const int64_t* offs;      // build pass: row offsets
+  int64_t* sizes;           // measure pass: row sizes
+  uint8_t* rows;
+  int64_t nrows;
+  int64_t cap;
+  int32_t ntop;
+};
+
+__device__ __forceinline__ CGNode& rn(const RwArgs& a, int n) { return ((CGNode*)(a.tab))[n]; }
+
+__device__ __forceinline__ bool rbit(const uint8_t* bits, int64_t i) {
+  return (gl(bits)[i >> 3] >> (i & 7)) & 1;
+}
+__device__ __forceinline__ int64_t r8(int64_t n) { return (n + 7) & ~int64_t(7); }
+__device__ __forceinline__ int64_t rbm(int64_t n) { return ((n + 63) >> 6) << 3; }
+__device__ __forceinline__ int rwidth(int t) {
+  switch (t) {
+    case FURY_TYPE_BOOL: case FURY_TYPE_INT8: return 1;
+    case FURY_TYPE_INT16: return 2;
+    case FURY_TYPE_INT32: case FURY_TYPE_FLOAT32: case FURY_TYPE_DATE32: return 4;
+    case FURY_TYPE_INT64: case FURY_TYPE_FLOAT64: case FURY_TYPE_TIMESTAMP: return 8;
+    default: return -1;
+  }
+}
+
+// Stores into the LDS image or (past it) HBM; every store is aligned to its width by the format.
+__device__ __forceinline__ void s8(LdsU8* p, uint64_t v) { *reinterpret_cast<Lds<uint64_t>*>(p) = v; }
+__device__ __forceinline__ void s8(uint8_t* p, uint64_t v) { *gl(reinterpret_cast<uint64_t*>(p)) = v; }
+__device__ __forceinline__ void s4(LdsU8* p, uint32_t v) { *reinterpret_cast<Lds<uint32_t>*>(p) = v; }
+__device__ __forceinline__ void s4(uint8_t* p, uint32_t v) { *gl(reinterpret_cast<uint32_t*>(p)) = v; }
+__device__ __forceinline__ void s2(LdsU8* p, uint16_t v) { *reinterpret_cast<Lds<uint16_t>*>(p) = v; }
+__device__ __forceinline__ void s2(uint8_t* p, uint16_t v) { *gl(reinterpret_cast<uint16_t*>(p)) = v; }
+__device__ __forceinline__ void s1(LdsU8* p, uint8_t v) { *p = v; }
+__device__ __forceinline__ void s1(uint8_t* p, uint8_t v) { *gl(p) = v; }
+__device__ __forceinline__ void o1(LdsU8* p, uint8_t v) { *p |= v; }
+__device__ __forceinline__ void o1(uint8_t* p, uint8_t v) { *gl(p) |= v; }
+
+template <class P>
+__device__ __forceinline__ void rzero(P p, int64_t n) {       // 8-aligned, n a multiple of 8
+  for (int64_t i = 0; i < n; i += 8) s8(p + i, 0);
+}
+
+// len bytes from an unaligned source at dst (8-aligned), zero-padded to 8: aligned source words
+// funnel-shifted into place; no word past the last source byte is read.
+template <class P>
+__device__ __forceinline__ void rappend(P dst, const uint8_t* src, int64_t len) {
+  const uintptr_t so = reinterpret_cast<uintptr_t>(src) & 7;
+  const auto ap = gl(reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(src) - so));
+  const int64_t nw = (len + 7) >> 3;
+  const int64_t nsrc = (static_cast<int64_t>(so) + len + 7) >> 3;
+  const int sh = static_cast<int>(so) * 8;
+  uint64_t cur = nsrc > 0 ? ap[0] : 0;
+  for (int64_t w = 0; w < nw; w++) {
+    const uint64_t nxt = w + 1 < nsrc ? ap[w + 1] : 0;
+    uint64_t x = sh ? (cur >> sh) | (nxt << (64 - sh)) : cur;
+    const int64_t rem = len - 8 * w;
+    if (rem < 8) x &= (~0ull) >> (8 * (8 - rem));
+    s8(dst + 8 * w, x);
+    cur = nxt;
+  }
+}
+
+// A non-null fixed-width value: a row / struct slot takes the whole 8 bytes (putInt64(0) + narrow
+// put), an array slot its element width.
+template <class P>
+__device__ __forceinline__ void rscalar(CGNode& n, int w, int64_t idx, P buf, int64_t slot,
+                                        int es, bool in_array) {
+  uint64_t v;
+  if (n.type == FURY_TYPE_BOOL) v = rbit(n.values, idx);
+  else if (w == 8) v = *gl(reinterpret_cast<const uint64_t*>(n.values + idx * 8));
+  else if (w == 4) v = *gl(reinterpret_cast<const uint32_t*>(n.values + idx * 4));
+  else if (w == 2) v = *gl(reinterpret_cast<const uint16_t*>(n.values + idx * 2));
+  else v = gl(n.values)[idx];
+  if (!in_array || es == 8) s8(buf + slot, v);
+  else if (es == 4) s4(buf + slot, static_cast<uint32_t>(v));
+  else if (es == 2) s2(buf + slot, static_cast<uint16_t>(v));
+  else s1(buf + slot, static_cast<uint8_t>(v));
+}
+
+template <int D, int MD, bool W, class P>
+__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int64_t idx, P buf,
+                                       int64_t container, int64_t slot, int64_t& cursor);
+
+// The image of container entry idx of node ni (type ty: STRUCT, LIST or MAP) at buf + start;
+// returns the end of its bytes.  Children at level D + 1.
+template <int D, int MD, bool W, class P>
+__device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_t idx, P buf,
+                                         int64_t start) {
+  CGNode& n = rn(a, ni);
+  const bool strc = ty == FURY_TYPE_STRUCT;
+  int64_t b = 0, m = 0;
+  if (!strc) {
+    b = gl(n.offsets)[idx];
+    m = gl(n.offsets)[idx + 1] - b;
+  }
+  int64_t c2 = start + (ty == FURY_TYPE_MAP ? 8 : 0);   // a map's key-array size word first
+  const int sides = ty == FURY_TYPE_MAP ? 2 : 1;
+  for (int sd = 0; sd < sides; sd++) {
+    int64_t arr, hb, items;
+    int ces = 8;
+    if (strc) {                                 // [bitmap][8-byte slots]
+      items = n.num_children;
+      arr = start;
+      hb = rbm(items);
+      if (W) rzero(buf + start, hb + 8 * items);
+      c2 = start + hb + 8 * items;
+    } else {                                    // [int64 m][bitmap][m x es, tail zeroed]
+      if (sd == 1 && W) s8(buf + start, static_cast<uint64_t>(c2 - (start + 8)));
+      CGNode& C = rn(a, n.first_child + sd);
+      const int cw = rwidth(C.type);
+      ces = cw > 0 ? cw : 8;
+      arr = c2;
+      hb = 8 + rbm(m);
+      items = m;
+      const int64_t fp = r8(m * ces);
+      if (W) {
+        s8(buf + arr, static_cast<uint64_t>(m));
+        rzero(buf + arr + 8, hb - 8 + fp);
+      }
+      c2 = arr + hb + fp;
+    }
+    const int64_t bm = strc ? arr : arr + 8;
+    for (int64_t j = 0; j < items; j++) {
+      const int cn = __builtin_amdgcn_readfirstlane(
+          strc ? n.first_child + static_cast<int>(j) : n.first_child + sd);
+      CGNode& C = rn(a, cn);
+      const int64_t cidx = strc ? idx : b + j;
+      const int64_t cslot = arr + hb + (strc ? 8 : ces) * j;
+      if (C.validity && !rbit(C.validity, cidx)) {     // setNullAt: bit only
+        if (W) o1(buf + bm + (j >> 3), static_cast<uint8_t>(1u << (j & 7)));
+        continue;
+      }
+      const int cw = rwidth(C.type);
+      if (cw > 0) {
+        if (W) rscalar(C, cw, cidx, buf, cslot, strc ? 8 : ces, !strc);
+        continue;
+      }
+      rvalue<D + 1, MD, W>(a, cn, cidx, buf, arr, cslot, c2);
+    }
+  }
+  return c2;
+}
+
+// A non-null, non-scalar entry idx of node ni (level D): its bytes at the cursor, its slot
+// (offset from the container, size).
+template <int D, int MD, bool W, class P>
+__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int64_t idx, P buf,
+                                       int64_t container, int64_t slot, int64_t& cursor) {
+  if constexpr (D >= MD) {
+    return;
+  } else {
+    CGNode& n = rn(a, ni);
+    const int ty = n.type;
+    const int64_t start = cursor;
+    if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
+      const int64_t b = gl(n.offsets)[idx];
+      const int64_t len = gl(n.offsets)[idx + 1] - b;
+      if (W) {
+        rappend(buf + start, n.values + b, len);
+        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
+      }
+      cursor = start + r8(len);
+      return;
+    }
+    if (ty == FURY_TYPE_DECIMAL) {
+      if (W) {
+        const auto v = gl(reinterpret_cast<const uint64_t*>(n.values + 16 * idx));
+        s8(buf + start, v[0]);
+        s8(buf + start + 8, v[1]);
+        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | 16u);
+      }
+      cursor = start + 16;
+      return;
+    }
+    if (ty != FURY_TYPE_STRUCT && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
+    cursor = rcont<D, MD, W>(a, ni, ty, idx, buf, start);
+    if (W) s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) |
+                              static_cast<uint32_t>(cursor - start));
+  }
+}
+
+// Entry r of the batch (generic.hip put_row): a row of the ntop top-level fields, or the
+// top-level BinaryArray / BinaryMap of node 0's entry r (ArrayEncoder.toArray / MapEncoder.toMap,
+// ArrayEncoderBuilder.java:118-140, MapEncoderBuilder.java:152-208).  Returns its size.
+template <bool W, int kRoot, int MD, class P>
+__device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
+  if constexpr (kRoot != 0) {
+    return rcont<0, MD, W>(a, 0, kRoot == 1 ? FURY_TYPE_LIST : FURY_TYPE_MAP, r, buf, 0);
+  } else {
+    const int ntop = a.ntop;
+    const int64_t bmb = rbm(ntop);
+    const int64_t fixed = bmb + 8 * static_cast<int64_t>(ntop);
+    if (W) rzero(buf, fixed);
+    int64_t cursor = fixed;
+    for (int k = 0; k < ntop; k++) {
+      CGNode& N = rn(a, k);
+      const int64_t slot = bmb + 8 * static_cast<int64_t>(k);
+      if (N.validity && !rbit(N.validity, r)) {
+        if (W) o1(buf + (k >> 3), static_cast<uint8_t>(1u << (k & 7)));
+        continue;
+      }
+      const int w = rwidth(N.type);
+      if (w > 0) {
+        if (W) rscalar(N, w, r, buf, slot, 8, false);
+        continue;
+      }
+      rvalue<0, MD, W>(a, k, r, buf, 0, slot, cursor);
+    }
+    return cursor;
+  }
+}
+
+template <int kRoot, int MD>
+__global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
+  if (r < a.nrows) a.sizes[r] = rrow<false, kRoot, MD>(a, r, static_cast<LdsU8*>(nullptr));
+}
+
+// Build pass: the workgroup's NT rows in chunks of consecutive rows whose bytes fit the image
+// (a.img bytes of LDS): each chunk's rows are built in the image, then stored with coalesced
+// 8-byte stores.  A row larger than the image alone is built straight in HBM.  Rows past the
+// capacity (encode_measured) are not written.
+template <int NT, int kRoot, int MD>
+__global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t img[];
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile;
+  const int64_t r = r0 + threadIdx.x;
+  const int64_t rend = min(r0 + a.tile, a.nrows);
+  const bool live = r < rend;
+  const int64_t my0 = live ? a.offs[r] : 0, my1 = live ? a.offs[r + 1] : 0;
+  int64_t s0 = r0;
+  while (s0 < rend) {
+    const int64_t b0 = a.offs[s0];
+    // rows from s0 whose end fits the image: a prefix of the tile (offsets ascend)
+    const int fit = __syncthreads_count(live && r >= s0 && my1 - b0 <= a.img && my1 <= a.cap);
+    if (fit == 0) {                              // row s0 alone exceeds the image (or the cap)
+      if (r == s0 && my1 <= a.cap) rrow<true, kRoot, MD>(a, r, a.rows + my0);
+      s0++;
+      continue;
+    }
+    const int64_t s1 = s0 + fit;
+    if (r >= s0 && r < s1) rrow<true, kRoot, MD>(a, r, (LdsU8*)(img + (my0 - b0)));
+    __syncthreads();
+    const int64_t nw = (a.offs[s1] - b0) >> 3;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
+    uint64_t* d = reinterpret_cast<uint64_t*>(a.rows + b0);
+    for (int64_t i = threadIdx.x; i < nw; i += NT) d[i] = s[i];
+    s0 = s1;
+    __syncthreads();                             // the image is reused by the next chunk
+  }
+}
+
+}  // namespace
+
+int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
+                  int64_t cap, hipStream_t stream) {
+  const int nn = g.nnodes;
+  const GenNode* hn = g.htab ? g.htab : g.node;
+  if (nn <= 0 || !hn) return 1;
+  std::vector<int32_t> level(nn, 0);
+  int nlev = 1;
+  for (int i = 0; i < nn; i++)
+    for (int j = 0; j < hn[i].num_children; j++) {
+      level[hn[i].first_child + j] = level[i] + 1;
+      nlev = std::max(nlev, level[i] + 2);
+    }
+  if (nlev > kRowEncMaxDepth) return 1;
+  DeviceTable dt;
+  const GenNode* tab = g.tab;
+  if (!tab) {
+    const int st = upload_table(g.node, nn * sizeof(GenNode), stream, &dt);
+    if (st) return st;
+    tab = static_cast<const GenNode*>(dt.dev);
+  }
+  RwArgs a{};
+  a.tab = tab;
+  a.offs = offs;
+  a.sizes = sizes;
+  a.rows = rows;
+  a.nrows = g.nrows;
+  a.cap = cap;
+  a.ntop = g.ntop;
+  a.img = g_rw_img;
+  const int nt = sizes ? kRwThreads : g_rw_rows;
+  a.tile = sizes ? nt : (g_rw_tile > 0 && g_rw_tile < nt ? g_rw_tile : nt);
+  const dim3 grid(static_cast<unsigned>((g.nrows + a.tile - 1) / a.tile));
+  auto go = [&](auto meas, auto enc128, auto enc256) {
+    if (sizes) {
+      hipLaunchKernelGGL(meas, grid, dim3(nt), 0, stream, a);
+      return;
+    }
+    auto run = [&](auto enc) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(a.img));
+      hipLaunchKernelGGL(enc, grid, dim3(nt), a.img, stream, a);
+    };
+    if (nt == 128) run(enc128);
+    else run(enc256);
+  };
+#define FURY_RW(R, MD)                                                                         \
+  if (g.root == R && nlev <= MD) {                                                             \
+    go(rw_measure_kernel<R, MD>, rw_encode_kernel<128, R, MD>, rw_encode_kernel<256, R, MD>);  \
+    return check_hip(hipGetLastError(), "row-walk encode launch");                             \
+  }
+  FURY_RW(0, 2) FURY_RW(0, 3) FURY_RW(0, 4) FURY_RW(0, 5)
+  FURY_RW(1, 2) FURY_RW(1, 3) FURY_RW(1, 4) FURY_RW(1, 5)
+  FURY_RW(2, 2) FURY_RW(2, 3) FURY_RW(2, 4) FURY_RW(2, 5)
+#undef FURY_RW
+  return 1;
+}
+
+void set_rowenc_tuning(int which, uint32_t v) {
+  if (which == 0) g_rw_rows = static_cast<int>(v);
+  else if (which == 1) g_rw_img = (v + 15) & ~15u;
+  else g_rw_tile = static_cast<int>(v);
+}
+uint32_t rowenc_tuning(int which) {
+  return which == 0 ? static_cast<uint32_t>(g_rw_rows) : which == 1 ? g_rw_img
+                                                                   : static_cast<uint32_t>(g_rw_tile);
+}
+
+}  // namespace fury

@@ -441,7 +441,8 @@ uint32_t g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS stage cap of a r
 uint32_t g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
 uint32_t g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
-int g_walk_prefetch = 1;            // tuning "walk_prefetch": write-pass waves pull their rows first
+int g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
+                                    // (bit 0: write pass, bit 1: count pass)
 int g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 uint32_t g_tree_stage = 32 * 1024, g_tree_arena = 24 * 1024;
@@ -536,7 +537,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.stride = p.stride;
   if (p.walk) {
     if (write) a.stage_cap = p.arena_cap;        // walk plans: the write pass's stage cap
-    a.prefetch = write ? g_walk_prefetch : 0;
+    a.prefetch = (g_walk_prefetch >> (write ? 0 : 1)) & 1;
     a.skip = write ? g_walk_skip : 0;
     a.rowpre = p.rowpre;
     a.K = p.K;

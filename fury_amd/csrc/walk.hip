@@ -72,7 +72,7 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   b += write ? pool : 0;
   b = (b + 15) & ~size_t(15);
   l.pf = b;                                   // prefetch landing zone: 1 KB per wave
-  b += write && prefetch ? 1024 * static_cast<size_t>(nt / 64) : 0;
+  b += prefetch ? 1024 * static_cast<size_t>(nt / 64) : 0;
   l.stg = b;
   b += stage;
   l.end = (b + 15) & ~size_t(15);
@@ -109,6 +109,23 @@ __device__ inline Rows walk_stage(const TreeArgs& a, uint8_t* stg, int64_t r0, i
   if (R.hi > R.lo) tstage<NT>(stg, a.rows + R.lo_al, a.rows + R.hi);
   else R.hi = R.lo;
   return R;
+}
+
+// The wave's 64 rows are one contiguous byte range: pull its lines past the stage (from `from`)
+// into the caches with coalesced 16-B LDS-DMA loads into a scratch zone (data discarded), so the
+// walk's dependent reads hit L2 instead of each paying an HBM round trip.
+__device__ inline void walk_prefetch(const TreeArgs& a, const WShared& sh, int64_t r0, int tid,
+                                     int64_t total, int64_t from) {
+  const int64_t wr0 = r0 + (tid & ~63);
+  if (wr0 >= a.nrows) return;
+  const int64_t wr1 = min<int64_t>(wr0 + 64, a.nrows);
+  const int64_t g0 = min<int64_t>(max<int64_t>(max<int64_t>(gl(a.offs)[wr0], from), 0), total);
+  const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[wr1], g0), total);
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(a.rows + g0) & ~uintptr_t(15);
+  const uintptr_t hi = (reinterpret_cast<uintptr_t>(a.rows + g1) + 15) & ~uintptr_t(15);
+  uint8_t* land = sh.pf + 1024 * (tid >> 6);
+  for (uintptr_t q = lo + 16 * (tid & 63); q < hi; q += 1024)
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q), land, 16, 0, 0);
 }
 
 // Walk context of one thread.
@@ -413,6 +430,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   clk.start();
   for (int k = 0; k < a.K; k++) sh.cur[k * NT + tid] = 0;
   const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
+  if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
   __syncthreads();
   clk.mark(0);
   WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid};
@@ -502,22 +520,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   }
   if (tid == 0) sh.req[2 * nn] = 0;
   const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
-  if (a.prefetch) {
-    // the wave's 64 rows are one contiguous byte range: pull its lines into the caches with
-    // coalesced 16-B LDS-DMA loads into a scratch zone (data discarded), so the walk's dependent
-    // reads below hit L2 instead of each paying an HBM round trip
-    const int64_t wr0 = r0 + (tid & ~63);
-    if (wr0 < a.nrows) {
-      const int64_t wr1 = min<int64_t>(wr0 + 64, a.nrows);
-      const int64_t g0 = min<int64_t>(max<int64_t>(gl(a.offs)[wr0], 0), total);
-      const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[wr1], g0), total);
-      const uintptr_t lo = reinterpret_cast<uintptr_t>(a.rows + g0) & ~uintptr_t(15);
-      const uintptr_t hi = (reinterpret_cast<uintptr_t>(a.rows + g1) + 15) & ~uintptr_t(15);
-      uint8_t* land = sh.pf + 1024 * (tid >> 6);
-      for (uintptr_t q = lo + 16 * (tid & 63); q < hi; q += 1024)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q), land, 16, 0, 0);
-    }
-  }
+  if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
   const uint32_t pool_words = a.pool_cap / 4;

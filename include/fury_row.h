@@ -284,7 +284,7 @@ int fury_trim_workspace(int32_t device);
  * Nested engines: "nested_decode" 2 row walk (default), 1 level engine, 0 tree tiles;
  * "nested_encode" 2 tree-tile measure + row interpreter (default), 1 interpreter, 0 tree tiles;
  * row walk "walk_threads" (128 / 256), "walk_stage" / "walk_stage_write" / "walk_pool" (LDS
- * bytes), "walk_prefetch" (0 / 1); tree tiles "tree_stage" / "tree_arena" / "tree_threads",
+ * bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); tree tiles "tree_stage" / "tree_arena" / "tree_threads",
  * "tree_enc_lds" / "tree_measure_lds" / "tree_enc_rows" / "tree_measure_rows"; diagnostics
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
  * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's

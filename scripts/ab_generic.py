@@ -78,8 +78,11 @@ def main():
         if ref is None:
             ref = got
         else:
+            # value buffers carry an uninitialised pad past the last entry (<= 16 B): not compared
             same = torch.equal(ref[0], got[0]) and all(
-                (x is None and y is None) or (x is not None and y is not None and torch.equal(x, y))
+                (x is None and y is None) or (x is not None and y is not None and x.shape == y.shape
+                                              and torch.equal(x[:max(x.numel() - 16, 0)],
+                                                              y[:max(y.numel() - 16, 0)]))
                 for x, y in zip(ref[1], got[1]))
             print(json.dumps({"leg": leg, "equal_to_first": same}), flush=True)
         leg_run(args, t, enc, cols, n, batch, out, leg)

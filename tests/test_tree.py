@@ -158,7 +158,8 @@ def enc_engines():
     from fury_amd import _native as N
     L = N.lib()
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_encode", "tree_enc_lds",
-                                                       "tree_measure_lds")}
+                                                       "tree_measure_lds", "rowenc_rows",
+                                                       "rowenc_img")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -179,12 +180,15 @@ def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, nam
     dcols = [column_to_device(c, dev) for c in host]
     enc = Encoders.bean(fields, device=dev)
     want, want_offs = oracle.encode(fields, host, n)
-    if budget == "small":
+    if budget == "small":             # row walk: 128-row tiles built in 8 KB chunks
         _tune("tree_enc_lds", 8192)
         _tune("tree_measure_lds", 4096)
-    elif budget == "tiny":
+        _tune("rowenc_rows", 128)
+        _tune("rowenc_img", 8192)
+    elif budget == "tiny":            # row walk: most rows alone exceed the image (HBM direct)
         _tune("tree_enc_lds", 1024)
         _tune("tree_measure_lds", 1024)
+        _tune("rowenc_img", 1024)
     _tune("nested_encode", 0)
     b = enc.encode_batch(dcols, n)
     assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
@@ -195,16 +199,17 @@ def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, nam
     enc.encode_measured_into(dcols, n, rows, offs)
     torch.cuda.synchronize()
     assert np.array_equal(rows[:total].cpu().numpy(), want)
-    for mode in (1, 2):               # interpreter; tree measure + interpreter encode
-        _tune("nested_encode", mode)
+    for mode in (1, 2, 3, 4):         # interpreter; tree measure + interpreter / row-walk encode;
+        _tune("nested_encode", mode)  # row walk (measure + encode)
         b1 = enc.encode_batch(dcols, n)
         assert np.array_equal(b1.row_offsets.cpu().numpy(), want_offs)
         assert np.array_equal(b1.rows.cpu().numpy(), want)
 
 
-def test_tree_encode_capacity(oracle, dev, enc_engines):
+@pytest.mark.parametrize("mode", [0, 2, 3, 4])
+def test_tree_encode_capacity(oracle, dev, enc_engines, mode):
     """encode_measured with a short buffer: offsets complete, no byte at or past the capacity
-    written (guard bytes intact), the bytes before it equal to the oracle's."""
+    written (guard bytes intact), the bytes before it equal to the oracle's; every encode engine."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     fields = _schemas()["nested7"]
@@ -213,6 +218,7 @@ def test_tree_encode_capacity(oracle, dev, enc_engines):
     dcols = [column_to_device(c, dev) for c in host]
     enc = Encoders.bean(fields, device=dev)
     want, want_offs = oracle.encode(fields, host, n)
+    _tune("nested_encode", mode)
     cap = (int(want_offs[n // 2]) + 13) & ~7
     rows = torch.full((cap + 4096,), 0xAB, dtype=torch.uint8, device=dev)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
@@ -274,7 +280,7 @@ def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_m
     enc = Encoders.bean(fields, device=dev)
     assert enc.nested
     want, want_offs = oracle.encode(fields, host, n)
-    for mode in (2, 1, 0):            # deep schemas ignore "nested_encode": always the tree tiles
+    for mode in (4, 3, 2, 1, 0):      # deep schemas ignore "nested_encode": always the tree tiles
         _tune("nested_encode", mode)
         b = enc.encode_batch(dcols, n)
         assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
@@ -284,6 +290,37 @@ def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_m
     got = _decode_plan(enc, b)
     assert_columns_equal(fields, got, ref, n)
     assert columns_to_beans(fields, got, n) == beans
+
+
+@pytest.mark.parametrize("levels", [2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("mode", [3, 4])
+def test_row_walk_encode_depths(oracle, dev, enc_engines, levels, mode):
+    """The row-walk encode (rowenc.hip, one inlined instance per depth up to 5 levels; 6 and 7
+    fall back to the interpreter) == the oracle's bytes and offsets."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _deep_fields(levels)
+    assert _schema_levels(fields) == levels
+    n = 2100
+    host = beans_to_columns(fields, _beans(fields, n, levels * 11 + mode))
+    enc = Encoders.bean(fields, device=dev)
+    want, want_offs = oracle.encode(fields, host, n)
+    _tune("nested_encode", mode)
+    b = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
+    assert np.array_equal(b.rows.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
+def test_collections_encode_engines(oracle, dev, enc_engines, mode, kind):
+    """ArrayEncoder / MapEncoder batches (root 1 / 2) encoded by every engine == the oracle."""
+    from tests.test_device import test_array_encoder_batch_vs_oracle, test_map_encoder_batch_vs_oracle
+    _tune("nested_encode", mode)
+    if kind == "map":
+        test_map_encoder_batch_vs_oracle(oracle, dev)
+    else:
+        test_array_encoder_batch_vs_oracle(oracle, dev, kind)
 
 
 def test_deep_schema_row_too_large_for_chip_raises(oracle, dev, enc_engines):
