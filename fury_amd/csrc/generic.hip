@@ -1088,7 +1088,7 @@ namespace {
 // measure + interpreter encode, 3 tree measure + row-walk encode (rowenc.hip), 4 row walk (both).
 // Schemas nested deeper than the interpreter unrolls (kGenMaxDepth) always take the tree tiles;
 // the row walk covers up to kRowEncMaxDepth levels (deeper: the interpreter).
-int g_tree_encode = 2;
+int g_tree_encode = 4;
 uint32_t g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
 int g_te_rows[2] = {256, 256};                   // rows per workgroup tile: measure, encode
 

@@ -307,7 +307,7 @@ void set_tree_threads(int v);        // tuning "tree_threads": 256 / 512 / 1024
 int tree_threads();
 // tunings of the row-walk decode (walk.hip): 0 "walk_threads" (128 / 256 rows per tile),
 // 1 "walk_stage" (LDS stage cap of the count pass, bytes), 2 "walk_pool" (LDS bitmap-window
-// bytes), 3 "walk_stage_write" (LDS stage cap of the write pass), 4 "walk_prefetch" (0 / 1)
+// bytes), 3 "walk_stage_write" (LDS stage cap of the write pass), 4 "walk_prefetch" (bit 0 write pass, bit 1 count pass)
 void set_walk_tuning(int which, uint32_t v);
 uint32_t walk_tuning(int which);
 uint64_t* tree_debug_buffer();

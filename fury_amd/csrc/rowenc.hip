@@ -21,9 +21,8 @@
 // schema node at the same time (the loops are schema-driven), so node records come from a device
 // table through scalar loads (readfirstlane'd index).  The build pass writes a workgroup's rows
 // (rowenc_rows) into an LDS image of their contiguous output range and stores it coalesced (as
-// the interpreter's build kernel), in chunks of rows that fit the image (rowenc_img): thread-per-
-// row stores straight to HBM wrote several times the row bytes (partial lines); only a row larger
-// than the whole image is built in HBM.
+// the interpreter's build kernel): thread-per-row stores straight to HBM wrote several times the
+// row bytes (partial lines); only the rows past the image (rowenc_img) are built in HBM.
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -59,9 +58,6 @@ struct RwArgs {
 
 __device__ __forceinline__ CGNode& rn(const RwArgs& a, int n) { return ((CGNode*)(a.tab))[n]; }
 
-__device__ __forceinline__ bool rbit(const uint8_t* bits, int64_t i) {
-  return (gl(bits)[i >> 3] >> (i & 7)) & 1;
-}
 __device__ __forceinline__ int64_t r8(int64_t n) { return (n + 7) & ~int64_t(7); }
 __device__ __forceinline__ int64_t rbm(int64_t n) { return ((n + 63) >> 6) << 3; }
 __device__ __forceinline__ int rwidth(int t) {
@@ -83,8 +79,8 @@ __device__ __forceinline__ void s2(LdsU8* p, uint16_t v) { *reinterpret_cast<Lds
 __device__ __forceinline__ void s2(uint8_t* p, uint16_t v) { *gl(reinterpret_cast<uint16_t*>(p)) = v; }
 __device__ __forceinline__ void s1(LdsU8* p, uint8_t v) { *p = v; }
 __device__ __forceinline__ void s1(uint8_t* p, uint8_t v) { *gl(p) = v; }
-__device__ __forceinline__ void o1(LdsU8* p, uint8_t v) { *p |= v; }
-__device__ __forceinline__ void o1(uint8_t* p, uint8_t v) { *gl(p) |= v; }
+__device__ __forceinline__ void o1_(LdsU8* p, uint8_t v) { *p |= v; }
+__device__ __forceinline__ void o1_(uint8_t* p, uint8_t v) { *gl(p) |= v; }
 
 template <class P>
 __device__ __forceinline__ void rzero(P p, int64_t n) {       // 8-aligned, n a multiple of 8
@@ -111,39 +107,68 @@ __device__ __forceinline__ void rappend(P dst, const uint8_t* src, int64_t len) 
   }
 }
 
-// A non-null fixed-width value: a row / struct slot takes the whole 8 bytes (putInt64(0) + narrow
-// put), an array slot its element width.
-template <class P>
-__device__ __forceinline__ void rscalar(CGNode& n, int w, int64_t idx, P buf, int64_t slot,
-                                        int es, bool in_array) {
-  uint64_t v;
-  if (n.type == FURY_TYPE_BOOL) v = rbit(n.values, idx);
-  else if (w == 8) v = *gl(reinterpret_cast<const uint64_t*>(n.values + idx * 8));
-  else if (w == 4) v = *gl(reinterpret_cast<const uint32_t*>(n.values + idx * 4));
-  else if (w == 2) v = *gl(reinterpret_cast<const uint16_t*>(n.values + idx * 2));
-  else v = gl(n.values)[idx];
-  if (!in_array || es == 8) s8(buf + slot, v);
-  else if (es == 4) s4(buf + slot, static_cast<uint32_t>(v));
-  else if (es == 2) s2(buf + slot, static_cast<uint16_t>(v));
-  else s1(buf + slot, static_cast<uint8_t>(v));
+template <int D, int MD, bool W, class P>
+__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
+                                       int64_t o1, P buf, int64_t container, int64_t slot,
+                                       int64_t& cursor);
+
+// Entry idx of node ni at level D, in slot `slot` (es bytes; in_array: an array element) of a
+// container starting at `container`, null bit `ord` of the bitmap at bm.  Every load of the entry
+// -- its validity byte, its value or its offsets pair -- is issued before any branch on them: one
+// memory round trip per entry instead of one per dependent read (the walk is latency-bound).
+// (Issuing entry j + 1's loads before finishing entry j measured slower: more VGPRs, 1.34 ->
+// 1.45 ms build at 4M depth-3 rows.)
+template <int D, int MD, bool W, class P>
+__device__ __forceinline__ void ritem(const RwArgs& a, int ni, int64_t idx, P buf,
+                                      int64_t container, int64_t slot, int es, bool in_array,
+                                      int64_t bm, int64_t ord, int64_t& cursor) {
+  if constexpr (D >= MD) {
+    return;
+  } else {
+    CGNode& n = rn(a, ni);
+    const int ty = n.type;
+    const int w = rwidth(ty);
+    const uint32_t vb = n.validity ? gl(n.validity)[idx >> 3] : 0xffu;
+    uint64_t v = 0;
+    int64_t o0 = 0, o1 = 0;
+    if (w > 0) {
+      if (W) {
+        if (ty == FURY_TYPE_BOOL) v = gl(n.values)[idx >> 3];
+        else if (w == 8) v = *gl(reinterpret_cast<const uint64_t*>(n.values + idx * 8));
+        else if (w == 4) v = *gl(reinterpret_cast<const uint32_t*>(n.values + idx * 4));
+        else if (w == 2) v = *gl(reinterpret_cast<const uint16_t*>(n.values + idx * 2));
+        else v = gl(n.values)[idx];
+      }
+    } else if (n.offsets) {
+      o0 = gl(n.offsets)[idx];
+      o1 = gl(n.offsets)[idx + 1];
+    }
+    if (!((vb >> (idx & 7)) & 1)) {              // setNullAt: bit only, slot stays 0
+      if (W) o1_(buf + bm + (ord >> 3), static_cast<uint8_t>(1u << (ord & 7)));
+      return;
+    }
+    if (w > 0) {                                 // putInt64(0) + narrow put / element width
+      if (W) {
+        if (ty == FURY_TYPE_BOOL) v = (v >> (idx & 7)) & 1;
+        if (!in_array || es == 8) s8(buf + slot, v);
+        else if (es == 4) s4(buf + slot, static_cast<uint32_t>(v));
+        else if (es == 2) s2(buf + slot, static_cast<uint16_t>(v));
+        else s1(buf + slot, static_cast<uint8_t>(v));
+      }
+      return;
+    }
+    rvalue<D, MD, W>(a, ni, ty, idx, o0, o1, buf, container, slot, cursor);
+  }
 }
 
+// The image of container entry idx of node ni (type ty: STRUCT, or LIST / MAP with elements
+// [b, b + m) of its child nodes) at buf + start; returns the end of its bytes.  Children at level
+// D + 1.
 template <int D, int MD, bool W, class P>
-__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int64_t idx, P buf,
-                                       int64_t container, int64_t slot, int64_t& cursor);
-
-// The image of container entry idx of node ni (type ty: STRUCT, LIST or MAP) at buf + start;
-// returns the end of its bytes.  Children at level D + 1.
-template <int D, int MD, bool W, class P>
-__device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_t idx, P buf,
-                                         int64_t start) {
+__device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_t idx, int64_t b,
+                                         int64_t m, P buf, int64_t start) {
   CGNode& n = rn(a, ni);
   const bool strc = ty == FURY_TYPE_STRUCT;
-  int64_t b = 0, m = 0;
-  if (!strc) {
-    b = gl(n.offsets)[idx];
-    m = gl(n.offsets)[idx + 1] - b;
-  }
   int64_t c2 = start + (ty == FURY_TYPE_MAP ? 8 : 0);   // a map's key-array size word first
   const int sides = ty == FURY_TYPE_MAP ? 2 : 1;
   for (int sd = 0; sd < sides; sd++) {
@@ -174,60 +199,44 @@ __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_
     for (int64_t j = 0; j < items; j++) {
       const int cn = __builtin_amdgcn_readfirstlane(
           strc ? n.first_child + static_cast<int>(j) : n.first_child + sd);
-      CGNode& C = rn(a, cn);
-      const int64_t cidx = strc ? idx : b + j;
-      const int64_t cslot = arr + hb + (strc ? 8 : ces) * j;
-      if (C.validity && !rbit(C.validity, cidx)) {     // setNullAt: bit only
-        if (W) o1(buf + bm + (j >> 3), static_cast<uint8_t>(1u << (j & 7)));
-        continue;
-      }
-      const int cw = rwidth(C.type);
-      if (cw > 0) {
-        if (W) rscalar(C, cw, cidx, buf, cslot, strc ? 8 : ces, !strc);
-        continue;
-      }
-      rvalue<D + 1, MD, W>(a, cn, cidx, buf, arr, cslot, c2);
+      ritem<D + 1, MD, W>(a, cn, strc ? idx : b + j, buf, arr, arr + hb + (strc ? 8 : ces) * j,
+                          strc ? 8 : ces, !strc, bm, j, c2);
     }
   }
   return c2;
 }
 
-// A non-null, non-scalar entry idx of node ni (level D): its bytes at the cursor, its slot
-// (offset from the container, size).
+// A non-null, non-scalar entry idx of node ni (level D; o0 / o1: its offsets pair): its bytes at
+// the cursor, its slot (offset from the container, size).
 template <int D, int MD, bool W, class P>
-__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int64_t idx, P buf,
-                                       int64_t container, int64_t slot, int64_t& cursor) {
-  if constexpr (D >= MD) {
+__device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
+                                       int64_t o1, P buf, int64_t container, int64_t slot,
+                                       int64_t& cursor) {
+  CGNode& n = rn(a, ni);
+  const int64_t start = cursor;
+  if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
+    const int64_t len = o1 - o0;
+    if (W) {
+      rappend(buf + start, n.values + o0, len);
+      s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
+    }
+    cursor = start + r8(len);
     return;
-  } else {
-    CGNode& n = rn(a, ni);
-    const int ty = n.type;
-    const int64_t start = cursor;
-    if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
-      const int64_t b = gl(n.offsets)[idx];
-      const int64_t len = gl(n.offsets)[idx + 1] - b;
-      if (W) {
-        rappend(buf + start, n.values + b, len);
-        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
-      }
-      cursor = start + r8(len);
-      return;
-    }
-    if (ty == FURY_TYPE_DECIMAL) {
-      if (W) {
-        const auto v = gl(reinterpret_cast<const uint64_t*>(n.values + 16 * idx));
-        s8(buf + start, v[0]);
-        s8(buf + start + 8, v[1]);
-        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | 16u);
-      }
-      cursor = start + 16;
-      return;
-    }
-    if (ty != FURY_TYPE_STRUCT && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
-    cursor = rcont<D, MD, W>(a, ni, ty, idx, buf, start);
-    if (W) s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) |
-                              static_cast<uint32_t>(cursor - start));
   }
+  if (ty == FURY_TYPE_DECIMAL) {
+    if (W) {
+      const auto v = gl(reinterpret_cast<const uint64_t*>(n.values + 16 * idx));
+      s8(buf + start, v[0]);
+      s8(buf + start + 8, v[1]);
+      s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | 16u);
+    }
+    cursor = start + 16;
+    return;
+  }
+  if (ty != FURY_TYPE_STRUCT && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
+  cursor = rcont<D, MD, W>(a, ni, ty, idx, o0, o1 - o0, buf, start);
+  if (W) s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) |
+                            static_cast<uint32_t>(cursor - start));
 }
 
 // Entry r of the batch (generic.hip put_row): a row of the ntop top-level fields, or the
@@ -236,27 +245,18 @@ __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int64_t idx, P b
 template <bool W, int kRoot, int MD, class P>
 __device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
   if constexpr (kRoot != 0) {
-    return rcont<0, MD, W>(a, 0, kRoot == 1 ? FURY_TYPE_LIST : FURY_TYPE_MAP, r, buf, 0);
+    const auto offs = gl(rn(a, 0).offsets);
+    const int64_t b = offs[r];
+    return rcont<0, MD, W>(a, 0, kRoot == 1 ? FURY_TYPE_LIST : FURY_TYPE_MAP, r, b, offs[r + 1] - b,
+                           buf, 0);
   } else {
     const int ntop = a.ntop;
     const int64_t bmb = rbm(ntop);
     const int64_t fixed = bmb + 8 * static_cast<int64_t>(ntop);
     if (W) rzero(buf, fixed);
     int64_t cursor = fixed;
-    for (int k = 0; k < ntop; k++) {
-      CGNode& N = rn(a, k);
-      const int64_t slot = bmb + 8 * static_cast<int64_t>(k);
-      if (N.validity && !rbit(N.validity, r)) {
-        if (W) o1(buf + (k >> 3), static_cast<uint8_t>(1u << (k & 7)));
-        continue;
-      }
-      const int w = rwidth(N.type);
-      if (w > 0) {
-        if (W) rscalar(N, w, r, buf, slot, 8, false);
-        continue;
-      }
-      rvalue<0, MD, W>(a, k, r, buf, 0, slot, cursor);
-    }
+    for (int k = 0; k < ntop; k++)
+      ritem<0, MD, W>(a, k, r, buf, 0, bmb + 8 * static_cast<int64_t>(k), 8, false, 0, k, cursor);
     return cursor;
   }
 }
@@ -267,10 +267,12 @@ __global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
   if (r < a.nrows) a.sizes[r] = rrow<false, kRoot, MD>(a, r, static_cast<LdsU8*>(nullptr));
 }
 
-// Build pass: the workgroup's NT rows in chunks of consecutive rows whose bytes fit the image
-// (a.img bytes of LDS): each chunk's rows are built in the image, then stored with coalesced
-// 8-byte stores.  A row larger than the image alone is built straight in HBM.  Rows past the
-// capacity (encode_measured) are not written.
+// Build pass: the workgroup's rows are built in the LDS image by whole waves as long as their
+// bytes fit it (a.img), then stored with coalesced 8-byte stores; the waves past that build their
+// rows straight in HBM in the same pass.  Per wave, not per row: a wave whose lanes took both
+// paths ran both instruction streams one after the other (a 72 KB image on ~75 KB tiles: 2.1 ms
+// per-row vs 1.33 ms when everything fit), and a second image round costs a whole walk latency.
+// Rows past the capacity (encode_measured) are not written.
 template <int NT, int kRoot, int MD>
 __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t img[];
@@ -279,26 +281,19 @@ __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   const int64_t rend = min(r0 + a.tile, a.nrows);
   const bool live = r < rend;
   const int64_t my0 = live ? a.offs[r] : 0, my1 = live ? a.offs[r + 1] : 0;
-  int64_t s0 = r0;
-  while (s0 < rend) {
-    const int64_t b0 = a.offs[s0];
-    // rows from s0 whose end fits the image: a prefix of the tile (offsets ascend)
-    const int fit = __syncthreads_count(live && r >= s0 && my1 - b0 <= a.img && my1 <= a.cap);
-    if (fit == 0) {                              // row s0 alone exceeds the image (or the cap)
-      if (r == s0 && my1 <= a.cap) rrow<true, kRoot, MD>(a, r, a.rows + my0);
-      s0++;
-      continue;
-    }
-    const int64_t s1 = s0 + fit;
-    if (r >= s0 && r < s1) rrow<true, kRoot, MD>(a, r, (LdsU8*)(img + (my0 - b0)));
-    __syncthreads();
-    const int64_t nw = (a.offs[s1] - b0) >> 3;
-    const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
-    uint64_t* d = reinterpret_cast<uint64_t*>(a.rows + b0);
-    for (int64_t i = threadIdx.x; i < nw; i += NT) d[i] = s[i];
-    s0 = s1;
-    __syncthreads();                             // the image is reused by the next chunk
+  const int64_t b0 = a.offs[r0];
+  // rows whose end fits the image: a prefix of the tile (offsets ascend), cut to whole waves
+  const int fit = __syncthreads_count(live && my1 - b0 <= a.img && my1 <= a.cap);
+  const int64_t in_img = min<int64_t>(fit == rend - r0 ? fit : fit & ~63, rend - r0);
+  if (live && my1 <= a.cap) {
+    if (r < r0 + in_img) rrow<true, kRoot, MD>(a, r, (LdsU8*)(img + (my0 - b0)));
+    else rrow<true, kRoot, MD>(a, r, a.rows + my0);
   }
+  __syncthreads();
+  const int64_t nw = (a.offs[r0 + in_img] - b0) >> 3;
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(img);
+  uint64_t* d = reinterpret_cast<uint64_t*>(a.rows + b0);
+  for (int64_t i = threadIdx.x; i < nw; i += NT) d[i] = s[i];
 }
 
 }  // namespace
@@ -316,6 +311,7 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
       nlev = std::max(nlev, level[i] + 2);
     }
   if (nlev > kRowEncMaxDepth) return 1;
+  RwArgs a{};
   DeviceTable dt;
   const GenNode* tab = g.tab;
   if (!tab) {
@@ -323,7 +319,6 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
     if (st) return st;
     tab = static_cast<const GenNode*>(dt.dev);
   }
-  RwArgs a{};
   a.tab = tab;
   a.offs = offs;
   a.sizes = sizes;
@@ -341,9 +336,10 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
       return;
     }
     auto run = [&](auto enc) {
+      const size_t lds = a.img;
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(enc),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(a.img));
-      hipLaunchKernelGGL(enc, grid, dim3(nt), a.img, stream, a);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+      hipLaunchKernelGGL(enc, grid, dim3(nt), lds, stream, a);
     };
     if (nt == 128) run(enc128);
     else run(enc256);
@@ -367,7 +363,7 @@ void set_rowenc_tuning(int which, uint32_t v) {
 }
 uint32_t rowenc_tuning(int which) {
   return which == 0 ? static_cast<uint32_t>(g_rw_rows) : which == 1 ? g_rw_img
-                                                                   : static_cast<uint32_t>(g_rw_tile);
+         : static_cast<uint32_t>(g_rw_tile);
 }
 
 }  // namespace fury

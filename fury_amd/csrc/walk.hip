@@ -194,7 +194,8 @@ __device__ __forceinline__ void welems(const WCtx& c, CTNode& C, int cn, int64_t
   for (uint32_t j = 0; j < m; j++) {
     if ((j & 63) == 0) nb = rd8(R, arr + 8 + (j >> 3));
     const bool cnul = (nb >> (j & 63)) & 1;
-    const uint64_t x = cnul ? 0 : rdw(R, ev + static_cast<int64_t>(es) * j, es);
+    uint64_t x = rdw(R, ev + static_cast<int64_t>(es) * j, es);   // in the array: load, then mask
+    if (cnul) x = 0;
     const int q = static_cast<int>(j & 31);
     if (C.type == FURY_TYPE_BOOL) {
       if (!cnul && (x & 0xff)) bm |= 1u << q;
@@ -213,10 +214,11 @@ __device__ __forceinline__ void welems(const WCtx& c, CTNode& C, int cn, int64_t
   }
 }
 
-// A fixed-width entry (write pass): value (0 when null), BOOL bit, validity bit.
+// A fixed-width entry (write pass): value sv (loaded with its null bit; 0 when null), BOOL bit,
+// validity bit.
 __device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t e, bool nul,
-                                        int64_t slotp, int rw) {
-  const uint64_t x = nul ? 0 : rdw(*c.R, slotp, rw);
+                                        uint64_t sv) {
+  const uint64_t x = nul ? 0 : sv;
   if (c.a->skip & 2) {
     if (N.type != FURY_TYPE_BOOL && N.values && !(c.a->skip & 4)) tstore_w(N.values + e * N.width, N.width, x);
     return;
@@ -229,14 +231,15 @@ __device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t
   if (N.validity) wbit(c, N, n, 0, N.validity, e, !nul);
 }
 
-// Entry e of node n (non-scalar; scalars go through wscalar): slot at slotp in a container that
-// starts at cont (vpos >= 0: the value is AT vpos -- a collection batch's top-level entry).
+// Entry e of node n (non-scalar; scalars go through wscalar): slot word `slot` (loaded by the
+// caller together with the null bit: one round trip) in a container that starts at cont (vpos >=
+// 0: the value is AT vpos -- a collection batch's top-level entry).
 // Returns whether the value is valid.  Top-level callers (D == 0) set the validity themselves.
 // Every child item -- a STRUCT's fields, a LIST's elements, a MAP's keys then values -- goes
 // through ONE loop with one call of the next level, so the levels inline into straight code (no
 // call frames: a recursive call per level would keep every register of the walk live in scratch).
 template <int D, bool W, int MD>
-__device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul, int64_t slotp,
+__device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul, uint64_t slot,
                                        int64_t cont, int64_t vpos) {
   if constexpr (D >= MD) {
     return false;
@@ -253,7 +256,6 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       if (vpos >= 0) {
         pos = vpos;
       } else {
-        const uint64_t slot = rd8(R, slotp);
         pos = cont + static_cast<int32_t>(slot >> 32);
         size = static_cast<int32_t>(slot);
       }
@@ -320,27 +322,26 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       for (uint32_t j = 0; j < m; j++) {
         const int cn = strc ? N.first_child + static_cast<int>(j) : N.first_child + sd;
         CTNode& C = tn(a, __builtin_amdgcn_readfirstlane(cn));
-        int64_t ce, cslot, ccont;
-        bool cnul;
-        int crw;
-        if (strc) {
-          ce = e;
-          cnul = !valid || rdbit(R, pos, j);
-          cslot = pos + hb + 8 * static_cast<int64_t>(j);
-          ccont = pos;
-          crw = C.width;
-        } else {
-          ce = cs + j;
-          cnul = rdbit(R, arr + 8, j);
-          cslot = arr + 8 + hb + static_cast<int64_t>(C.esize) * j;
-          ccont = arr;
-          crw = C.esize;
+        const int64_t ce = strc ? e : cs + static_cast<int64_t>(j);
+        const int64_t cbm = strc ? pos : arr + 8;
+        const int64_t cslot = strc ? pos + hb + 8 * static_cast<int64_t>(j)
+                                   : arr + 8 + hb + static_cast<int64_t>(C.esize) * j;
+        const int64_t ccont = strc ? pos : arr;
+        const int crw = strc ? C.width : C.esize;
+        const bool scal = C.width > 0;
+        if (scal ? !W : !(W || C.walk)) continue;
+        // the null bit and the slot / value together (inside the checked container: a struct's
+        // fields only when it is valid, a list's elements only exist then)
+        const bool can = !strc || valid;
+        uint32_t nb = 1;
+        uint64_t sv = 0;
+        if (can) {
+          nb = rd1(R, cbm + (j >> 3)) >> (j & 7);
+          sv = scal ? rdw(R, cslot, crw) : rd8(R, cslot);
         }
-        if (C.width > 0) {
-          if (W) wscalar(c, C, cn, ce, cnul, cslot, crw);
-        } else if (W || C.walk) {
-          wvalue<D + 1, W, MD>(c, cn, ce, cnul, cslot, ccont, kNullPos);
-        }
+        const bool cnul = !can || (nb & 1);
+        if (scal) wscalar(c, C, cn, ce, cnul, sv);
+        else wvalue<D + 1, W, MD>(c, cn, ce, cnul, sv, ccont, kNullPos);
       }
     }
     return valid;
@@ -368,11 +369,19 @@ __device__ inline void walk_row(const WCtx& c, bool live) {
   const int64_t hb = tbm(a.ntop);
   for (int f = 0; f < a.ntop; f++) {
     CTNode& N = tn(a, f);
-    const bool nul = !rowok || rdbit(R, base, f);
+    if (N.width > 0 ? !W : !(W || N.walk)) continue;
     const int64_t slotp = base + hb + 8 * f;
+    // the null bit and the slot / value together: one round trip
+    uint32_t nb = 1;
+    uint64_t sv = 0;
+    if (rowok) {
+      nb = rd1(R, base + (f >> 3)) >> (f & 7);
+      sv = N.width > 0 ? rdw(R, slotp, N.width) : rd8(R, slotp);
+    }
+    const bool nul = !rowok || (nb & 1);
     if (N.width > 0) {
       if (W) {
-        const uint64_t x = (live && !nul) ? rdw(R, slotp, N.width) : 0;
+        const uint64_t x = (live && !nul) ? sv : 0;
         if (N.type == FURY_TYPE_BOOL) {
           if (N.values) tballot_or(N.values, c.wave_row, live && !nul && (x & 0xff));
         } else if (live && N.values) {
@@ -382,9 +391,8 @@ __device__ inline void walk_row(const WCtx& c, bool live) {
       }
       continue;
     }
-    if (!W && !N.walk) continue;
     bool valid = false;
-    if (live) valid = wvalue<0, W, MD>(c, f, c.row, nul, slotp, base, kNullPos);
+    if (live) valid = wvalue<0, W, MD>(c, f, c.row, nul, sv, base, kNullPos);
     if (W && N.validity) tballot_or(N.validity, c.wave_row, live && valid);
   }
 }
