@@ -161,6 +161,47 @@ __device__ __forceinline__ void ritem(const RwArgs& a, int ni, int64_t idx, P bu
   }
 }
 
+// Elements [b, b + m) of a fixed-width node C (es bytes each) into an array's slots at buf + sp
+// (null bits at buf + bm): validity bytes and values of four elements loaded together, then
+// stored -- one memory round trip per four elements instead of one per element.
+template <class P>
+__device__ __forceinline__ void relems(CGNode& C, int es, int64_t b, int64_t m, P buf, int64_t sp,
+                                       int64_t bm) {
+  const bool boo = C.type == FURY_TYPE_BOOL;
+  for (int64_t j0 = 0; j0 < m; j0 += 4) {
+    uint64_t v[4];
+    uint32_t vb[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t i = b + j0 + q;
+      v[q] = 0;
+      vb[q] = 0xffu;
+      if (j0 + q < m) {
+        if (C.validity) vb[q] = gl(C.validity)[i >> 3];
+        if (boo) v[q] = gl(C.values)[i >> 3];
+        else if (es == 8) v[q] = *gl(reinterpret_cast<const uint64_t*>(C.values + i * 8));
+        else if (es == 4) v[q] = *gl(reinterpret_cast<const uint32_t*>(C.values + i * 4));
+        else if (es == 2) v[q] = *gl(reinterpret_cast<const uint16_t*>(C.values + i * 2));
+        else v[q] = gl(C.values)[i];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t j = j0 + q, i = b + j;
+      if (j >= m) continue;
+      if (!((vb[q] >> (i & 7)) & 1)) {
+        o1_(buf + bm + (j >> 3), static_cast<uint8_t>(1u << (j & 7)));
+        continue;
+      }
+      const uint64_t x = boo ? (v[q] >> (i & 7)) & 1 : v[q];
+      if (es == 8) s8(buf + sp + 8 * j, x);
+      else if (es == 4) s4(buf + sp + 4 * j, static_cast<uint32_t>(x));
+      else if (es == 2) s2(buf + sp + 2 * j, static_cast<uint16_t>(x));
+      else s1(buf + sp + j, static_cast<uint8_t>(x));
+    }
+  }
+}
+
 // The image of container entry idx of node ni (type ty: STRUCT, or LIST / MAP with elements
 // [b, b + m) of its child nodes) at buf + start; returns the end of its bytes.  Children at level
 // D + 1.
@@ -196,6 +237,11 @@ __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_
       c2 = arr + hb + fp;
     }
     const int64_t bm = strc ? arr : arr + 8;
+    if (!strc && ces == rwidth(rn(a, n.first_child + sd).type)) {
+      // fixed-width elements: four at a time, every load of the four issued before any store
+      if (W) relems(rn(a, n.first_child + sd), ces, b, items, buf, arr + hb, bm);
+      continue;
+    }
     for (int64_t j = 0; j < items; j++) {
       const int cn = __builtin_amdgcn_readfirstlane(
           strc ? n.first_child + static_cast<int>(j) : n.first_child + sd);
