@@ -282,9 +282,13 @@ int fury_trim_workspace(int32_t device);
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.
  * Nested engines: "nested_decode" 2 row walk (default), 1 level engine, 0 tree tiles;
- * "nested_encode" 2 tree-tile measure + row interpreter (default), 1 interpreter, 0 tree tiles;
- * row walk "walk_threads" (128 / 256), "walk_stage" / "walk_stage_write" / "walk_pool" (LDS
- * bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); tree tiles "tree_stage" / "tree_arena" / "tree_threads",
+ * "nested_encode" 4 row-walk measure + encode (default, <= 5 levels), 3 tree-tile measure +
+ * row-walk encode, 2 tree-tile measure + row interpreter, 1 interpreter, 0 tree tiles (deeper
+ * schemas fall back by themselves); row-walk encode "rowenc_rows" (128 / 256 threads per group),
+ * "rowenc_tile" (rows per group, 0 = threads), "rowenc_img" (LDS image bytes);
+ * row walk "walk_threads" / "walk_threads_write" (128 / 256), "walk_stage" / "walk_stage_write" /
+ * "walk_pool" (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); tree tiles
+ * "tree_stage" / "tree_arena" / "tree_threads",
  * "tree_enc_lds" / "tree_measure_lds" / "tree_enc_rows" / "tree_measure_rows"; diagnostics
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
  * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's
