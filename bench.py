@@ -190,6 +190,7 @@ def run(args):
     if ndev < world and not args.share_gpus:
         raise SystemExit(f"bench.py: {world} ranks but {ndev} visible GPUs "
                          "(--share-gpus for a rehearsal)")
+    shared = ndev < world                       # --share-gpus rehearsal: ranks share devices
     local = local % ndev if ndev else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -318,7 +319,11 @@ def run(args):
         "metric": METRIC,
         "value": round(all_bytes * args.steps / dt_max / 1e9, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        # distinct devices: a --share-gpus rehearsal runs `world` ranks on fewer GPUs and is marked
+        # so that it cannot be read as a scaling point
+        "n_gpus": min(world, ndev) if shared else world,
+        "ranks": world,
+        "shared_gpus": shared,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt_max * 1e3 / args.steps, 4),
@@ -339,6 +344,9 @@ def run(args):
                      "encode_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
                      "decode_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
     }
+    if shared:
+        line["rehearsal"] = (f"{world} ranks shared {min(world, ndev)} GPU(s) (--share-gpus): a "
+                             "check of the multi-rank path, not a multi-GPU measurement")
     if e2e is not None:
         line["e2e_pcie"] = e2e
     if world == 1 and not args.no_cpu_baseline:     # the CPU baseline is an N=1 figure

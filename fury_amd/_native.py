@@ -73,6 +73,7 @@ SIGNATURES = {
     "fury_decode_execute": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I32, _P]),
     "fury_decode_plan_destroy": (None, [_P]),
     "fury_device_status": (ctypes.c_int, [_P]),
+    "fury_stream_release": (ctypes.c_int, [_P]),
     "fury_trim_workspace": (ctypes.c_int, [_I32]),
     "fury_set_tuning": (ctypes.c_int, [ctypes.c_char_p, _I32]),
     "fury_get_tuning": (_I32, [ctypes.c_char_p]),

@@ -26,8 +26,12 @@ int check_hip(int hip_status, const char* what) {
 // memory.  A kernel raises into the slot of the stream it was launched on, and a call takes (reads
 // and clears) only the slot of its own stream, so a malformed decode on one stream is never
 // reported by -- or swallowed into -- an unrelated call on another stream / thread.
-// The legacy null stream is keyed per host thread.  Slots are assigned on first use; past
-// kErrSlots distinct streams the overflow streams share slot 0.
+// The legacy null stream and hipStreamPerThread are keyed per host thread (two keys per thread,
+// released when the thread exits).  Slots are assigned on first launch and go back to a free list
+// when their stream is released: by the library when it destroys a stream it created (decode
+// plans, host-path plans), by the caller through fury_stream_release before it destroys one of
+// its own.  A call that needs a slot when all kErrSlots are held fails with FURY_ERR_DEVICE --
+// slots are never shared, so an error is reported on its own stream or not at all.
 namespace {
 constexpr int kErrSlots = 1024;
 uint32_t* g_err_host = nullptr;     // host view of the slots
@@ -35,12 +39,25 @@ uint32_t* g_err_dev = nullptr;      // the same memory as kernels address it
 std::once_flag g_err_once;
 std::mutex g_slot_mu;
 std::unordered_map<uintptr_t, int> g_slot_of;
-int g_slot_next = 1;
+std::vector<int> g_slot_free;       // released slots (words cleared)
+int g_slot_next = 0;                // slots [0, g_slot_next) have been handed out at least once
+
+void release_key(uintptr_t k);
+
+// Per-thread keys of the null stream and of hipStreamPerThread (odd: never a stream handle, which
+// is aligned); their slots are released when the thread exits.
+struct ThreadKeys {
+  char null_key = 0, per_thread_key = 0;
+  ~ThreadKeys() {
+    release_key(reinterpret_cast<uintptr_t>(&null_key) | 1);
+    release_key(reinterpret_cast<uintptr_t>(&per_thread_key) | 1);
+  }
+};
 
 uintptr_t stream_key(hipStream_t s) {
-  if (s) return reinterpret_cast<uintptr_t>(s);
-  thread_local char key;              // odd keys: never a stream handle (handles are aligned)
-  return reinterpret_cast<uintptr_t>(&key) | 1;
+  if (s && s != hipStreamPerThread) return reinterpret_cast<uintptr_t>(s);
+  thread_local ThreadKeys keys;
+  return reinterpret_cast<uintptr_t>(s ? &keys.per_thread_key : &keys.null_key) | 1;
 }
 
 void init_err() {
@@ -59,21 +76,67 @@ void init_err() {
   });
 }
 
-int error_slot(hipStream_t s) {
-  const uintptr_t k = stream_key(s);
+// The slot of stream key k: its own, else a free or never-used one (-1: all kErrSlots held).
+// `assign` false: lookup only (a stream that never launched has nothing to report).
+int error_slot(uintptr_t k, bool assign) {
   std::lock_guard<std::mutex> lock(g_slot_mu);
   auto it = g_slot_of.find(k);
   if (it != g_slot_of.end()) return it->second;
-  const int slot = g_slot_next < kErrSlots ? g_slot_next++ : 0;
+  if (!assign) return -1;
+  int slot = -1;
+  if (!g_slot_free.empty()) {
+    slot = g_slot_free.back();
+    g_slot_free.pop_back();
+  } else if (g_slot_next < kErrSlots) {
+    slot = g_slot_next++;
+  } else {
+    return -1;
+  }
   g_slot_of.emplace(k, slot);
   return slot;
 }
+
+std::atomic<int64_t> g_err_dropped{0};   // look-back flags cleared by a release, never taken
+
+void release_key(uintptr_t k) {
+  std::lock_guard<std::mutex> lock(g_slot_mu);
+  auto it = g_slot_of.find(k);
+  if (it == g_slot_of.end()) return;
+  const int slot = it->second;
+  g_slot_of.erase(it);
+  if (g_err_host) {
+    uint32_t* w = g_err_host + size_t(kErrWords) * slot;
+    if (__atomic_exchange_n(w + kErrLookBack, 0u, __ATOMIC_ACQ_REL)) g_err_dropped.fetch_add(1);
+    for (int i = 0; i < kErrWords; i++) __atomic_store_n(w + i, 0u, __ATOMIC_RELEASE);
+  }
+  g_slot_free.push_back(slot);
+}
 }  // namespace
 
-uint32_t* device_error_word(hipStream_t stream) {
+int device_error_word(hipStream_t stream, uint32_t** out) {
+  *out = nullptr;
   init_err();
-  if (!g_err_dev) return nullptr;
-  return g_err_dev + size_t(kErrWords) * error_slot(stream);
+  if (!g_err_dev) return FURY_OK;     // no mapped memory: kernels run without error reporting
+  const int slot = error_slot(stream_key(stream), true);
+  if (slot < 0)
+    return set_error(FURY_ERR_DEVICE,
+                     "device error slots exhausted: " + std::to_string(kErrSlots) +
+                         " streams hold one; call fury_stream_release(stream) before destroying a "
+                         "stream passed to this library");
+  *out = g_err_dev + size_t(kErrWords) * slot;
+  return FURY_OK;
+}
+
+// Forgets `stream`'s slot after the work on it has finished (its pending errors are dropped);
+// `sync` false: the caller knows the stream is idle (thread exit: no HIP call).
+void release_error_slot(hipStream_t stream, bool sync) {
+  if (sync && stream && stream != hipStreamPerThread) (void)hipStreamSynchronize(stream);
+  release_key(stream_key(stream));
+}
+
+int error_slots_in_use() {
+  std::lock_guard<std::mutex> lock(g_slot_mu);
+  return static_cast<int>(g_slot_of.size());
 }
 
 std::atomic<int64_t> g_err_taken{0};
@@ -85,7 +148,7 @@ int64_t device_error_count() {
     for (int i = 0; i < g_slot_next; i++)
       pending += __atomic_load_n(g_err_host + size_t(kErrWords) * i + kErrLookBack, __ATOMIC_ACQUIRE) ? 1 : 0;
   }
-  return g_err_taken.load() + pending;
+  return g_err_taken.load() + g_err_dropped.load() + pending;
 }
 
 // Where a kernel found the problem: a row index, or (bit 63 set) a nested schema node and Arrow
@@ -106,7 +169,9 @@ static bool take_flag(uint32_t* w, int flag, uint64_t* where) {
 
 int take_device_error(hipStream_t stream) {
   if (!g_err_host) return FURY_OK;
-  uint32_t* w = g_err_host + size_t(kErrWords) * error_slot(stream);
+  const int slot = error_slot(stream_key(stream), false);
+  if (slot < 0) return FURY_OK;       // nothing was ever launched on this stream
+  uint32_t* w = g_err_host + size_t(kErrWords) * slot;
   uint64_t oob_at = 0, map_at = 0;
   const bool lb = take_flag(w, kErrLookBack, nullptr);
   const bool oob = take_flag(w, kErrBounds, &oob_at);
@@ -462,7 +527,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   } else {
     a->tile_rows = encode_tile_rows(*a);
   }
-  a->err = device_error_word(hs);
+  if (const int e = device_error_word(hs, &a->err)) return e;
   a->help_now = lookback_help_mode();
   return FURY_OK;
 }
@@ -787,7 +852,10 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (p->lv) lv_free(p->lv);
   if (p->tree) tree_free(p->tree);
   if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
-  if (p->owned_stream) (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
+  if (p->owned_stream) {
+    release_error_slot(static_cast<hipStream_t>(p->owned_stream));
+    (void)hipStreamDestroy(static_cast<hipStream_t>(p->owned_stream));
+  }
   delete p;
 }
 
@@ -808,6 +876,11 @@ int fury_device_status(void* stream) {
                            "hipStreamSynchronize");
   if (st) return st;
   return take_device_error(static_cast<hipStream_t>(stream));
+}
+
+int fury_stream_release(void* stream) {
+  release_error_slot(static_cast<hipStream_t>(stream));
+  return FURY_OK;
 }
 
 int fury_set_tuning(const char* key, int32_t value) {
@@ -957,6 +1030,8 @@ int32_t fury_get_tuning(const char* key) {
     return static_cast<int32_t>(unframe_walk_count());
   if (key && std::string(key) == "host_direct")
     return static_cast<int32_t>(host_direct_count());
+  if (key && std::string(key) == "err_slots") return error_slots_in_use();
+  if (key && std::string(key) == "var_dec_rows_rejected") return var_dec_rows_rejected();
   if (key && std::string(key) == "unframe_repairs")
     return static_cast<int32_t>(unframe_repair_count());
   return -1;

@@ -568,7 +568,7 @@ __global__ __launch_bounds__(kThreads) void unframe_copy(StreamView sv,
 
 std::atomic<int64_t> g_unframe_walks{0};     // streams parsed (partly) by the sequential walk
 std::atomic<int64_t> g_unframe_repairs{0};   // streams parsed by the parallel repair
-int g_unframe_mode = 0;   // tuning "unframe": 0 speculative, 1 always walk
+std::atomic<int> g_unframe_mode = 0;   // tuning "unframe": 0 speculative, 1 always walk
 
 struct DevBuf {                               // stream-ordered scratch freed on every exit
   void* p = nullptr;

@@ -21,6 +21,8 @@
 // thread-per-row decode interpreter that lived here was removed in round 3.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1088,9 +1090,9 @@ namespace {
 // measure + interpreter encode, 3 tree measure + row-walk encode (rowenc.hip), 4 row walk (both).
 // Schemas nested deeper than the interpreter unrolls (kGenMaxDepth) always take the tree tiles;
 // the row walk covers up to kRowEncMaxDepth levels (deeper: the interpreter).
-int g_tree_encode = 4;
-uint32_t g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
-int g_te_rows[2] = {256, 256};                   // rows per workgroup tile: measure, encode
+std::atomic<int> g_tree_encode = 4;
+std::atomic<uint32_t> g_te_lds[2] = {24 * 1024, 60 * 1024};   // LDS budget: measure, encode
+std::atomic<int> g_te_rows[2] = {256, 256};                   // rows per workgroup tile: measure, encode
 
 int host_gwidth(int t) {
   switch (t) {
@@ -1139,7 +1141,7 @@ int launch_tree_encode(const GenArgs& g, const int64_t* offs, int64_t* sizes, ui
     return 1;
   TEArgs a{};
   a.deep = deep ? 1 : 0;
-  a.err = device_error_word(stream);
+  if (const int e = device_error_word(stream, &a.err)) return e;
   a.level_start[0] = 0;
   for (int L = 1; L <= nlev; L++) {
     int i = a.level_start[L - 1];

@@ -63,7 +63,15 @@ struct DeviceArena {
 struct Streams {
   hipStream_t s[kStages] = {};
   int create(int device) {
-    thread_local std::map<int, std::array<hipStream_t, kStages>> pool;
+    // the streams' error slots go back to the free list when the thread exits (the streams
+    // themselves are idle: every call ends with sync())
+    struct Pool : std::map<int, std::array<hipStream_t, kStages>> {
+      ~Pool() {
+        for (auto& kv : *this)
+          for (hipStream_t x : kv.second) release_error_slot(x, false);
+      }
+    };
+    thread_local Pool pool;
     auto it = pool.find(device);
     if (it == pool.end()) {
       std::array<hipStream_t, kStages> a{};
@@ -866,6 +874,7 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
   keep_pool(device);
   st = dev_alloc(rb + (nrows + 1) * 8 + 16, hs, reinterpret_cast<void**>(&d));
   if (st) {
+    release_error_slot(hs);
     (void)hipStreamDestroy(hs);
     return st;
   }
@@ -880,6 +889,7 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
       (void)hipMemcpyAsync(doffs, o.data(), (nrows + 1) * 8, hipMemcpyHostToDevice, hs);
       if ((st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) {
         dev_free(d, hs);
+        release_error_slot(hs);
         (void)hipStreamDestroy(hs);
         return st;
       }
@@ -889,6 +899,7 @@ int fury_decode_host_prepare(const fury_schema* s, const void* rows, const int64
   st = fury_decode_prepare(s, d, doffs, nrows, node_entries, node_bytes, &p, hs);
   if (st) {
     dev_free(d, hs);
+    release_error_slot(hs);
     (void)hipStreamDestroy(hs);
     return st;
   }

@@ -107,12 +107,15 @@ struct VarArgs {
 //   [kErrMapCount], [+2, +3]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
 //   [kErrTooDeep], [+2, +3]   encode: a row too large for on-chip assembly in a schema nested
 //                             deeper than the row interpreter reaches (FURY_ERR_UNSUPPORTED)
-// device_error_word(stream) is the slot kernels launched on `stream` raise into (NULL if the runtime
-// cannot map host memory); take_device_error(stream) takes that slot only (flag exchanged first,
+// device_error_word(stream, &w) gives the slot kernels launched on `stream` raise into (NULL if the
+// runtime cannot map host memory; FURY_ERR_DEVICE when every slot is held by a live stream);
+// release_error_slot(stream) frees it before the stream is destroyed; take_device_error(stream) takes that slot only (flag exchanged first,
 // then its location) and sets the thread's last error when one was raised.
 constexpr int kErrWords = 16;
 constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12;
-uint32_t* device_error_word(hipStream_t stream);
+int device_error_word(hipStream_t stream, uint32_t** out);
+void release_error_slot(hipStream_t stream, bool sync = true);
+int error_slots_in_use();
 int take_device_error(hipStream_t stream);
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
 
@@ -220,6 +223,7 @@ void set_host_decode_inplace(int v);   // tuning "host_decode_inplace" (hostpath
 int host_decode_inplace();
 int var_dec_rows();                   // tuning "var_dec_rows" (var.hip): 0 = planned
 void set_var_dec_rows(int v);
+int var_dec_rows_rejected();          // forced tiles whose images did not fit (plan used instead)
 int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
 void set_var_dec_cover(int v);
 int lookback_help_mode();
@@ -273,8 +277,9 @@ void set_rowenc_tuning(int which, uint32_t v);   // 0 "rowenc_rows", 1 "rowenc_i
 uint32_t rowenc_tuning(int which);
 int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
                       hipStream_t stream);
-// Nested encode engine (generic.hip): tuning "nested_encode" 0 = tree tiles (default), 1 = the
-// thread-per-row interpreter; "tree_enc_lds" / "tree_measure_lds" = their LDS budgets (bytes).
+// Nested encode engine (generic.hip, rowenc.hip): tuning "nested_encode" (include/fury_row.h) 0 tree
+// tiles, 1 interpreter, 2 tree-tile measure + interpreter, 3 tree-tile measure + row walk, 4 row-walk
+// measure + row walk (default); "tree_enc_lds" / "tree_measure_lds" = the tree tiles' LDS budgets.
 void set_tree_encode_mode(int v);
 int tree_encode_mode();
 void set_tree_encode_lds(int which, uint32_t bytes);   // which: 0 measure, 1 encode
@@ -298,7 +303,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
 int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                  const std::vector<int64_t>& totals, hipStream_t hs);
 void tree_free(TreePlan* p);
-void set_tree_mode(int v);           // tuning "nested_decode": 0 tree tiles (default), 1 levels
+void set_tree_mode(int v);           // tuning "nested_decode": 0 tree tiles, 1 levels, 2 row walk (default)
 int tree_mode();
 void set_tree_lds(uint32_t stage, uint32_t arena);   // tuning "tree_stage" / "tree_arena" (bytes)
 uint32_t tree_lds(int which);

@@ -642,7 +642,7 @@ int upload_args(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t
   a->root = p.root;
   a->nrows = p.nrows;
   a->nlist = static_cast<int32_t>(list.size());
-  a->err = device_error_word(hs);
+  if (const int e = device_error_word(hs, &a->err)) return e;
   return FURY_OK;
 }
 

@@ -25,6 +25,8 @@
 // row bytes (partial lines); only the rows past the image (rowenc_img) are built in HBM.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <vector>
 
 #include "internal.h"
@@ -35,9 +37,9 @@ namespace fury {
 namespace {
 
 constexpr int kRwThreads = 256;                 // measure pass rows per workgroup
-int g_rw_rows = 256;                            // tuning "rowenc_rows": build-pass rows per workgroup
-uint32_t g_rw_img = 76 * 1024;                  // tuning "rowenc_img": its LDS image bytes
-int g_rw_tile = 0;                              // tuning "rowenc_tile": rows per workgroup (0: all)
+std::atomic<int> g_rw_rows = 256;                            // tuning "rowenc_rows": build-pass rows per workgroup
+std::atomic<uint32_t> g_rw_img = 76 * 1024;                  // tuning "rowenc_img": its LDS image bytes
+std::atomic<int> g_rw_tile = 0;                              // tuning "rowenc_tile": rows per workgroup (0: all)
 
 template <class T>
 using Lds = __attribute__((address_space(3))) T;
@@ -373,8 +375,9 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
   a.cap = cap;
   a.ntop = g.ntop;
   a.img = g_rw_img;
-  const int nt = sizes ? kRwThreads : g_rw_rows;
-  a.tile = sizes ? nt : (g_rw_tile > 0 && g_rw_tile < nt ? g_rw_tile : nt);
+  const int nt = sizes ? kRwThreads : g_rw_rows.load();
+  const int rt = g_rw_tile.load();
+  a.tile = sizes ? nt : (rt > 0 && rt < nt ? rt : nt);
   const dim3 grid(static_cast<unsigned>((g.nrows + a.tile - 1) / a.tile));
   auto go = [&](auto meas, auto enc128, auto enc256) {
     if (sizes) {
@@ -408,7 +411,7 @@ void set_rowenc_tuning(int which, uint32_t v) {
   else g_rw_tile = static_cast<int>(v);
 }
 uint32_t rowenc_tuning(int which) {
-  return which == 0 ? static_cast<uint32_t>(g_rw_rows) : which == 1 ? g_rw_img
+  return which == 0 ? static_cast<uint32_t>(g_rw_rows) : which == 1 ? g_rw_img.load()
          : static_cast<uint32_t>(g_rw_tile);
 }
 

@@ -29,6 +29,8 @@
 // stage when the tile's bytes fit it, from HBM otherwise (skewed row sizes).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -431,22 +433,22 @@ int tree_host_width(int32_t t) {
   }
 }
 
-int g_tree_mode = 2;             // tuning "nested_decode": 0 tree tiles, 1 level engine, 2 row walk
+std::atomic<int> g_tree_mode = 2;             // tuning "nested_decode": 0 tree tiles, 1 level engine, 2 row walk
 // Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row count tiles with
 // a 12 KB stage (prepare 1.35 -> 1.08 ms: more tiles resident), 256-row write tiles (1.87 -> 1.78
 // ms) with the prefetch.
-int g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per count tile
-int g_walk_threads_w = 256;      // tuning "walk_threads_write": rows per write tile (a multiple)
-uint32_t g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
-uint32_t g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
+std::atomic<int> g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per count tile
+std::atomic<int> g_walk_threads_w = 256;      // tuning "walk_threads_write": rows per write tile (a multiple)
+std::atomic<uint32_t> g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
+std::atomic<uint32_t> g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
-uint32_t g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
-int g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
+std::atomic<uint32_t> g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
+std::atomic<int> g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
                                     // (bit 0: write pass, bit 1: count pass)
-int g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
+std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
-uint32_t g_tree_stage = 32 * 1024, g_tree_arena = 24 * 1024;
-int g_tree_threads = 256;        // tuning "tree_threads": workgroup size of the decode (256/512/1024)
+std::atomic<uint32_t> g_tree_stage{32 * 1024}, g_tree_arena{24 * 1024};
+std::atomic<int> g_tree_threads = 256;        // tuning "tree_threads": workgroup size of the decode (256/512/1024)
 
 }  // namespace
 
@@ -480,8 +482,8 @@ void set_walk_tuning(int which, uint32_t v) {
   else g_walk_threads_w = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
-  return which == 0 ? static_cast<uint32_t>(g_walk_threads) : which == 1 ? g_walk_stage
-         : which == 2 ? g_walk_pool : which == 3 ? g_walk_stage_w
+  return which == 0 ? static_cast<uint32_t>(g_walk_threads) : which == 1 ? g_walk_stage.load()
+         : which == 2 ? g_walk_pool.load() : which == 3 ? g_walk_stage_w.load()
          : which == 4 ? static_cast<uint32_t>(g_walk_prefetch)
          : which == 5 ? static_cast<uint32_t>(g_walk_skip) : static_cast<uint32_t>(g_walk_threads_w);
 }
@@ -524,7 +526,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.ntiles = p.ntiles;
   a.cnt = p.cnt;
   a.byt = p.byt;
-  a.err = device_error_word(hs);
+  if (const int e = device_error_word(hs, &a.err)) return e;
   a.overflow = overflow;
   a.nn = static_cast<int32_t>(p.nodes.size());
   a.ntop = p.ntop;
@@ -538,7 +540,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   if (p.walk) {
     if (write) a.stage_cap = p.arena_cap;        // walk plans: the write pass's stage cap
     a.prefetch = (g_walk_prefetch >> (write ? 0 : 1)) & 1;
-    a.skip = write ? g_walk_skip : 0;
+    a.skip = write ? g_walk_skip.load() : 0;
     a.rowpre = p.rowpre;
     a.K = p.K;
     a.pool_cap = p.pool_cap;
@@ -671,7 +673,8 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     // a thread per row; the stage holds the tile's rows up to walk_stage bytes (the rest are read
     // from HBM), the bitmap-window pool walk_pool bytes
     p->nt = g_walk_threads;
-    p->ntw = g_walk_threads_w % p->nt == 0 && g_walk_threads_w >= p->nt ? g_walk_threads_w : p->nt;
+    const int tw = g_walk_threads_w.load();
+    p->ntw = tw % p->nt == 0 && tw >= p->nt ? tw : p->nt;
     p->tile_rows = p->nt;
     p->stage_cap = (g_walk_stage + 15) & ~15u;
     p->arena_cap = (g_walk_stage_w + 15) & ~15u;

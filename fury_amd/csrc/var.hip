@@ -3,6 +3,7 @@
 // code is in var_dev.h, the register-staged template instances in var_reg_enc.hip and
 // var_reg_dec_{lo,hi}.hip (separate translation units so they compile in parallel).
 #define FURY_VAR_MAIN
+#include <atomic>
 #include "var_dev.h"
 
 #include <algorithm>
@@ -64,7 +65,7 @@ int64_t lookback_timeouts() { return device_error_count(); }
 
 // Test hook (tuning "lookback_help"): every look-back computes a silent predecessor's aggregate
 // at once -- the path a late-dispatched predecessor takes -- instead of polling first.
-static int g_help_now = 0;
+static std::atomic<int> g_help_now = 0;
 int lookback_help_mode() { return g_help_now; }
 void set_lookback_help_mode(int v) { g_help_now = v; }
 // Rows per register-staged tile: the estimated tile bytes (row sizes from the input buffers' byte
@@ -177,13 +178,15 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   return st;
 }
 
-static int g_dec_rows = 0;
+static std::atomic<int> g_dec_rows = 0;
+static std::atomic<int> g_dec_rows_rejected{0};
+int var_dec_rows_rejected() { return g_dec_rows_rejected.load(); }
 int var_dec_rows() { return g_dec_rows; }
 void set_var_dec_rows(int v) { g_dec_rows = v; }
 // tuning "var_dec_cover": percent of a tile's estimated row bytes the stage must hold (the rest
 // is read from HBM by the rows' threads).  95 (scripts/ab_dec.py legs, interleaved): mixed 10M
 // 0.542 -> 0.508 ms (its tiles grow 448 -> 512 rows), C4 4M unchanged (0.229 ms); 80 or less slows C4.
-static int g_dec_cover = 95;
+static std::atomic<int> g_dec_cover = 95;
 int var_dec_cover() { return g_dec_cover; }
 void set_var_dec_cover(int v) { g_dec_cover = v; }
 
@@ -218,10 +221,16 @@ void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) 
   if (g_dec_rows > 0) {                         // tuning "var_dec_rows": forced tile rows (A/B)
     const int R = g_dec_rows;
     const int64_t im = (static_cast<int64_t>(img_row * R * mi + img_fix) + 1023) & ~int64_t(1023);
-    *tile = R;
-    *img = static_cast<uint32_t>(std::min<int64_t>(im, kBudget / 2));
-    *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
-    return;
+    // a forced tile whose estimated images exceed half the budget is not run with clipped images
+    // (that would change which overflow path an A/B leg measures): the plan below is used and the
+    // rejection counted (fury_get_tuning "var_dec_rows_rejected")
+    if (im <= kBudget / 2) {
+      *tile = R;
+      *img = static_cast<uint32_t>(im);
+      *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
+      return;
+    }
+    g_dec_rows_rejected.fetch_add(1);
   }
   for (int R = kDecThreads; R >= 64; R -= 64) {
     const int64_t im = (static_cast<int64_t>(img_row * R * mi + img_fix) + 1023) & ~int64_t(1023);

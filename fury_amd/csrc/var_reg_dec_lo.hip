@@ -17,6 +17,11 @@ namespace fury {
 
 int launch_decode_var_reg(const VarArgs& a, const uint8_t* rows, const int64_t* offs, uint64_t* status,
                           uint32_t img, uint32_t stage, int mode, int64_t nt, hipStream_t stream) {
+  // The instance reads records a.col[0, K) straight from the argument block, whose records past
+  // ncols are zero (var_args): never a device table, whose bytes past ncols are not ours (the
+  // round-4 column-chunked variant faulted on exactly that).
+  if (a.tab || a.ncols > kRegCols)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "register-staged decode: 1..16 fields, argument-block records");
   switch (reg_dec_k(a.ncols)) {
     FURY_DREG(2) FURY_DREG(3)
     default: return launch_decode_var_reg_mid(a, rows, offs, status, img, stage, mode, nt, stream);

@@ -21,6 +21,9 @@ int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_
     else if (mode == kSeqLists) { FURY_REG_M(KK, kSeqLists) }                                  \
     else { FURY_REG_M(KK, kSeqAll) }                                                           \
     break;
+  // records b.col[0, K) come from the argument block (zero past ncols), never a device table
+  if (b.tab || b.ncols > kRegCols)
+    return set_error(FURY_ERR_INVALID_ARGUMENT, "register-staged encode: 1..16 fields, argument-block records");
   switch (reg_dec_k(b.ncols)) {
     FURY_REG(2) FURY_REG(3) FURY_REG(4) FURY_REG(6) FURY_REG(8) FURY_REG(12) FURY_REG(16)
     default: return set_error(FURY_ERR_UNSUPPORTED, "register-staged encode: 1..16 fields");

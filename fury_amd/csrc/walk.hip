@@ -597,7 +597,6 @@ int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
   FURY_WALK(5)
 #undef FURY_WALK
   return set_error(FURY_ERR_UNSUPPORTED, "walk decode: schema deeper than kWalkMaxDepth");
-  return check_hip(hipGetLastError(), "walk decode launch");
 }
 
 }  // namespace fury

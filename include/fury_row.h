@@ -263,8 +263,15 @@ void fury_decode_plan_destroy(fury_decode_plan* plan);
  * the kernels that have finished).  Either clears it.  Calls on other streams never see it.  When
  * one is reported, every output of the failing call is invalid (the values that failed decode as
  * null; the rest may be incomplete).  fury_decode_prepare and the host-memory entry points
- * synchronise and report their own batch's errors directly. */
+ * synchronise and report their own batch's errors directly.
+ * Each stream that launched work holds one of 1024 error slots until it is released: call
+ * fury_stream_release(stream) (it synchronises the stream and drops any unreported error) before
+ * destroying a stream passed to this library; streams the library creates itself, and the
+ * per-thread keys of the null stream / hipStreamPerThread, are released by the library.  With
+ * every slot held, the next call on a new stream fails with FURY_ERR_DEVICE (slots are never
+ * shared between streams). */
 int fury_device_status(void* stream);
+int fury_stream_release(void* stream);
 
 /* ---- workspace (no reference equivalent) ------------------------------------------------- */
 /* The library caches the device workspaces of its calls (scan scratch, decode plans, column
@@ -298,7 +305,9 @@ int fury_trim_workspace(int32_t device);
  * the repair could not place), "unframe_repairs" = streams the parallel repair parsed,
  * "host_direct" = fury_row_encode_host / _decode_host calls that ran their kernels directly on
  * pinned host buffers (fixed-width and flat variable-length schemas, no staging),
- * "lookback_timeouts" = decoupled look-backs that gave up (must stay 0; synchronous device read). */
+ * "lookback_timeouts" = decoupled look-backs that gave up (must stay 0; synchronous device read),
+ * "err_slots" = device error slots held by live streams (fury_stream_release),
+ * "var_dec_rows_rejected" = forced "var_dec_rows" tiles whose images did not fit (planned tile used). */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 

@@ -21,7 +21,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborow_oracle.so")
+# FURY_ORACLE_LIB: the sanitizer build (tools/sanitize, tests/test_sanitize.py)
+LIB_PATH = os.environ.get("FURY_ORACLE_LIB") or os.path.join(HERE, "liborow_oracle.so")
 
 # fury_type_id (include/fury_row.h) = ArrowType ids (FMT/type/ArrowType.java:25-148)
 BOOL, INT8, INT16, INT32, INT64 = 1, 3, 5, 7, 9

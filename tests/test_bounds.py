@@ -333,3 +333,72 @@ def test_device_errors_stay_on_their_stream(oracle, dev):
     with pytest.raises(IndexOutOfBoundsException, match=f"row {i} "):
         enc.device_status(sa)
     enc.device_status(sa)               # taken once
+
+
+def test_error_slots_recycle_past_1024_streams(oracle, dev):
+    """every stream that launches work holds one of 1024 device error slots until it is
+    released (fury_stream_release), and slots are never shared.  1100 short-lived streams each run
+    a decode and are released: the slots recycle, and an error raised on one of them (left
+    pending, its stream kept) is still reported on that stream alone, after streams that reused
+    other released slots ran clean decodes in between.  With every slot held, a call on a new
+    stream fails loudly (FURY_ERR_DEVICE) instead of sharing a slot."""
+    import ctypes
+    from fury_amd import _native as N
+    from fury_amd.encoder import FuryDeviceError, IndexOutOfBoundsException, column_to_host
+    hip = ctypes.CDLL("libamdhip64.so")
+    L = N.lib()
+    fields = SCHEMAS["mixed"]
+    n = 300
+    enc, host, rows, offs = _encode(oracle, fields, n, 5, dev, null_pct=10, str_max=30)
+    i, k = _victim(fields, rows, offs, n, {T.STRING})
+    bad = _batch(enc, _corrupt(fields, rows, offs, n, i, k, "offset_past_end"), offs, n, dev)
+    good = _batch(enc, rows, offs, n, dev)
+    want = oracle.decode(fields, rows, offs, n)
+    cols = enc.decode_batch(good)                       # outputs reused by every stream below
+    torch.cuda.synchronize()
+    base = L.fury_get_tuning(b"err_slots")
+
+    def new_stream():
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        return h, torch.cuda.ExternalStream(h.value, device=dev)
+
+    def drop(h):
+        assert L.fury_stream_release(h) == 0
+        assert hip.hipStreamDestroy(h) == 0
+
+    held = None
+    for j in range(1100):
+        h, s = new_stream()
+        if j == 700:                                    # the faulting stream stays open
+            enc._decode(bad, True, False, s, None, "bound")
+            s.synchronize()
+            held = (h, s)
+            continue
+        enc.decode_into(good, cols, s)
+        s.synchronize()
+        drop(h)
+    assert L.fury_get_tuning(b"err_slots") == base + 1
+    assert_columns_equal(fields, [column_to_host(c) for c in cols], want, n)
+    enc.device_status()                                 # nothing on this thread's stream
+    with pytest.raises(IndexOutOfBoundsException, match=f"row {i} "):
+        enc.device_status(held[1])
+    enc.device_status(held[1])                          # taken once
+    drop(held[0])
+    assert L.fury_get_tuning(b"err_slots") == base
+    # exhaustion: hold every free slot, then one more stream must fail loudly
+    live = []
+    try:
+        while L.fury_get_tuning(b"err_slots") < 1024:
+            h, s = new_stream()
+            live.append(h)
+            enc.decode_into(good, cols, s)
+        h, s = new_stream()
+        live.append(h)
+        with pytest.raises(FuryDeviceError, match="error slots exhausted"):
+            enc.decode_into(good, cols, s)
+    finally:
+        torch.cuda.synchronize()
+        for h in live:
+            drop(h)
+    assert L.fury_get_tuning(b"err_slots") == base

@@ -234,3 +234,62 @@ def test_cpp_row_test_to_string_from_device_bytes():
     back = enc.from_row(row)
     assert back == bean
     assert B.row_to_string(fields, B.encode_row(fields, back)) == want
+
+
+def _nested_repeately():
+    """RowTest.WriteNestedRepeately's batch (cpp/fury/row/row_test.cc:101-129) as columns."""
+    from fury_amd.workloads import Column
+    ka = _known()["cpp_write_nested_repeately"]["value"]
+    n, m = ka["rows"], ka["f1_num_elements"]
+    fields = [T.field("f0", T.INT32), T.array_field("f1", T.INT32)]
+    host = [Column(values=np.full(n, 2**31 - 1, np.int32)),
+            Column(offsets=np.arange(0, n * m + 1, m, dtype=np.int32),
+                   child=[Column(values=np.full(n * m, -2**31, np.int32))])]
+    return ka, fields, host
+
+
+def _check_nested_repeately(ka, rows: bytes, offs):
+    """The reference's getter answers read from row bytes: GetInt32(0) == 2147483647,
+    GetArray(1)->num_elements() == 50, GetArray(1)->GetInt32(0) == -2147483648 (BinaryRow /
+    BinaryArray getters: 8-byte slot, (offset << 32 | size) var slot, array header
+    [int64 n][bitmap][n x 4 B])."""
+    n, m = ka["rows"], ka["f1_num_elements"]
+    assert len(rows) == n * (8 + 16 + 8 + 8 + 4 * m)   # bitmap, 2 slots, [n][bitmap][50 x 4]
+    hdr = 8 + ((m + 63) // 64) * 8
+    for i in range(n):
+        base = int(offs[i])
+        assert rows[base] == 0                           # no null bits
+        assert struct.unpack_from("<i", rows, base + 8)[0] == ka["f0"]
+        slot = struct.unpack_from("<Q", rows, base + 16)[0]
+        arr = base + (slot >> 32)
+        assert struct.unpack_from("<q", rows, arr)[0] == m          # num_elements
+        assert struct.unpack_from("<i", rows, arr + hdr)[0] == ka["f1_element0"]
+        assert (slot & 0xFFFFFFFF) == hdr + 4 * m
+
+
+def test_cpp_write_nested_repeately_oracle(oracle):
+    """The oracle pinned by RowTest.WriteNestedRepeately's getter answers (row_test.cc:101-129)."""
+    ka, fields, host = _nested_repeately()
+    rows, offs = oracle.encode(fields, host, ka["rows"])
+    _check_nested_repeately(ka, rows.tobytes(), offs)
+
+
+@pytest.mark.gpu
+def test_cpp_write_nested_repeately_getters_from_device_bytes(oracle):
+    """RowTest.WriteNestedRepeately (row_test.cc:101-129): the 100 rows encoded as one device
+    batch, the reference's getter answers read from the DEVICE bytes of every row; the rows equal
+    the oracle's and decode back to the oracle's columns."""
+    torch, dev = _gpu()
+    from fury_amd.encoder import Encoders, column_to_device, column_to_host
+    from tests.helpers import assert_columns_equal
+    ka, fields, host = _nested_repeately()
+    n = ka["rows"]
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    rows = batch.rows.cpu().numpy().tobytes()
+    offs = batch.row_offsets.cpu().numpy()
+    _check_nested_repeately(ka, rows, offs)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert rows == want.tobytes() and np.array_equal(offs, want_offs)
+    dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    assert_columns_equal(fields, dec, oracle.decode(fields, want, want_offs, n), n)
