@@ -529,6 +529,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   }
   if (const int e = device_error_word(hs, &a->err)) return e;
   a->help_now = lookback_help_mode();
+  a->skip = var_skip();
   return FURY_OK;
 }
 
@@ -906,6 +907,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_dec_cover(value ? value : 95);
     return FURY_OK;
   }
+  if (std::string(key) == "var_skip") {
+    if (value < 0 || value > 255) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_skip: 0..255");
+    set_var_skip(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "var_dec_rows") {
     if (value != 0 && (value < 64 || value > 512 || value % 64))
       return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_rows: 0 or 64..512 in steps of 64");
@@ -937,6 +943,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     if (value != 128 && value != 256)
       return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads: 128 or 256");
     set_walk_tuning(0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "walk_out") {
+    if (value < 0 || value > 96 * 1024) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_out: 0..98304 bytes");
+    set_walk_tuning(7, static_cast<uint32_t>(value));
     return FURY_OK;
   }
   if (std::string(key) == "walk_stage" || std::string(key) == "walk_pool" ||
@@ -1015,8 +1026,10 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
   if (key && std::string(key) == "walk_threads_write") return static_cast<int32_t>(walk_tuning(6));
+  if (key && std::string(key) == "walk_out") return static_cast<int32_t>(walk_tuning(7));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
+  if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_dec_cover") return var_dec_cover();
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
   if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);

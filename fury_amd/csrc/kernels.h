@@ -95,6 +95,8 @@ struct VarArgs {
   int32_t tile_rows;         // rows per encode tile (encode_tile_rows)
   int32_t help_now;          // look-backs help a silent predecessor at once (test hook, tuning
                              // "lookback_help"); 0 in production
+  int32_t skip;              // diagnostics (tuning "var_skip"): phases skipped, outputs WRONG
+  int32_t pad_;
   uint32_t* err;             // the launch stream's device error slot (device_error_word) or NULL
 };
 
@@ -227,6 +229,8 @@ int var_dec_rows_rejected();          // forced tiles whose images did not fit (
 int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
 void set_var_dec_cover(int v);
 int lookback_help_mode();
+int var_skip();                       // tuning "var_skip" (diagnostics, timing only)
+void set_var_skip(int v);
 void set_lookback_help_mode(int v);
 int launch_measure_rows(const VarArgs& a, int64_t* row_offsets, hipStream_t stream);
 // Rows at the offsets fury_row_measure produced; never writes row bytes at or past `cap`.

@@ -443,6 +443,7 @@ std::atomic<uint32_t> g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS sta
 std::atomic<uint32_t> g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
 std::atomic<uint32_t> g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
+std::atomic<uint32_t> g_walk_out{16 * 1024};     // tuning "walk_out": LDS output-window bytes (write pass)
 std::atomic<int> g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
                                     // (bit 0: write pass, bit 1: count pass)
 std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
@@ -479,13 +480,15 @@ void set_walk_tuning(int which, uint32_t v) {
   else if (which == 3) g_walk_stage_w = (v + 15) & ~15u;
   else if (which == 4) g_walk_prefetch = static_cast<int>(v);
   else if (which == 5) g_walk_skip = static_cast<int>(v);
+  else if (which == 7) g_walk_out = (v + 15) & ~15u;
   else g_walk_threads_w = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
   return which == 0 ? static_cast<uint32_t>(g_walk_threads) : which == 1 ? g_walk_stage.load()
          : which == 2 ? g_walk_pool.load() : which == 3 ? g_walk_stage_w.load()
          : which == 4 ? static_cast<uint32_t>(g_walk_prefetch)
-         : which == 5 ? static_cast<uint32_t>(g_walk_skip) : static_cast<uint32_t>(g_walk_threads_w);
+         : which == 5 ? static_cast<uint32_t>(g_walk_skip)
+         : which == 7 ? g_walk_out.load() : static_cast<uint32_t>(g_walk_threads_w);
 }
 
 struct TreePlan {
@@ -544,6 +547,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
     a.rowpre = p.rowpre;
     a.K = p.K;
     a.pool_cap = p.pool_cap;
+    a.out_cap = write ? g_walk_out.load() : 0;
     for (int k = 0; k < p.K; k++) a.knode[k] = p.knode[k];
     a.ctr = p.nt;
     a.tmul = write ? p.ntw / p.nt : 1;

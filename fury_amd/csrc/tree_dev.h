@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "internal.h"
 #include "kernels.h"
@@ -60,6 +61,8 @@ struct TreeArgs {
   int32_t tmul;             // write pass: count tiles per write tile (1 or 2)
   int32_t ctr;              // rows per count tile
   int32_t knode[64];        // counted slot -> node
+  uint32_t out_cap;         // write pass: LDS bytes of the output windows (tuning "walk_out")
+  int32_t pad2_;
 };
 
 constexpr int kWalkMaxK = 64;
@@ -182,7 +185,7 @@ __device__ __forceinline__ uint64_t tw_scan64(uint64_t x) {
 // Exclusive scan of the uint32 array a[0, m) in LDS by the whole block (thread t owns a
 // contiguous chunk).  Returns false when the sum does not fit 32 bits (every thread agrees).
 template <int NT>
-__device__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t* wsum) {
+__device__ __forceinline__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t* wsum) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t per = (m + NT - 1) / NT;
   const uint32_t b = min<uint32_t>(tid * per, m), e = min<uint32_t>(b + per, m);
@@ -235,11 +238,39 @@ __device__ __forceinline__ void tstore_w(uint8_t* p, int w, uint64_t v) {
   }
 }
 
+// Pointers into LDS with the address space explicit (ds_* instructions, never flat).
+template <class T>
+using LdsT = __attribute__((address_space(3))) T;
+template <class T>
+__device__ __forceinline__ LdsT<T>* lds_ptr(void* generic_lds) { return (LdsT<T>*)(generic_lds); }
+// A w-byte store through a uint8_t pointer P of any address space: global (gl()), LDS (lds_ptr) or
+// generic (flat: the write pass's output windows and HBM through one instruction stream).
+template <class P, class T>
+using SameAs = typename std::conditional<
+    std::is_same<typename std::remove_pointer<P>::type, LdsT<uint8_t>>::value, LdsT<T>,
+    typename std::conditional<std::is_same<typename std::remove_pointer<P>::type, uint8_t>::value, T,
+                              __attribute__((address_space(1))) T>::type>::type;
+template <class P>
+__device__ __forceinline__ void tstore_wp(P p, int w, uint64_t v) {
+  using AS16 = SameAs<P, uint16_t>;
+  using AS32 = SameAs<P, uint32_t>;
+  using AS64 = SameAs<P, uint64_t>;
+  switch (w) {
+    case 8: *reinterpret_cast<AS64*>(p) = v; break;
+    case 4: *reinterpret_cast<AS32*>(p) = static_cast<uint32_t>(v); break;
+    case 2: *reinterpret_cast<AS16*>(p) = static_cast<uint16_t>(v); break;
+    default: *p = static_cast<uint8_t>(v); break;
+  }
+}
+
 // len bytes of the batch at src -> dst (any alignment; only [dst, dst + len) written).  The source
 // is read as aligned words (a word past the payload only when the payload reaches into it); the
 // destination takes at most three stores of 1 / 2 / 4 bytes before its first 8-byte boundary and
 // after its last, whole words in between (short strings: ~5 stores instead of ~15 byte stores).
-__device__ void tcopy_out(uint8_t* dst, const Rows& R, int64_t src, int64_t len) {
+// P: a global (gl()) or LDS (lds_ptr) uint8_t pointer -- the write pass assembles a tile's
+// payload range in an LDS window (walk.hip) and stores it as whole lines.
+template <class P>
+__device__ void tcopy_to(P dst, const Rows& R, int64_t src, int64_t len) {
   if (len <= 0) return;
   const int64_t s0 = src & ~int64_t(7);
   const int o = static_cast<int>(src & 7);
@@ -252,18 +283,18 @@ __device__ void tcopy_out(uint8_t* dst, const Rows& R, int64_t src, int64_t len)
     if (!sh || (p & 7) + min<int64_t>(8, len - i) <= 8) return sh ? a >> sh : a;
     return (a >> sh) | (rd8(R, q + 8) << (64 - sh));
   };
-  auto put_small = [&](uint8_t* d, uint64_t v, int n) {   // n < 8 bytes, d + n 8-aligned or end
+  auto put_small = [&](P d, uint64_t v, int n) {   // n < 8 bytes, d + n 8-aligned or end
     int k = 0;
     while (k < n) {
       const uintptr_t ad = reinterpret_cast<uintptr_t>(d + k);
       if ((ad & 1) || n - k < 2) {
-        gl(d)[k] = static_cast<uint8_t>(v >> (8 * k));
+        tstore_wp(d + k, 1, v >> (8 * k));
         k += 1;
       } else if ((ad & 2) || n - k < 4) {
-        *gl(reinterpret_cast<uint16_t*>(d + k)) = static_cast<uint16_t>(v >> (8 * k));
+        tstore_wp(d + k, 2, v >> (8 * k));
         k += 2;
       } else {
-        *gl(reinterpret_cast<uint32_t*>(d + k)) = static_cast<uint32_t>(v >> (8 * k));
+        tstore_wp(d + k, 4, v >> (8 * k));
         k += 4;
       }
     }
@@ -271,10 +302,45 @@ __device__ void tcopy_out(uint8_t* dst, const Rows& R, int64_t src, int64_t len)
   const int64_t head = min<int64_t>(len, (8 - (reinterpret_cast<uintptr_t>(dst) & 7)) & 7);
   if (head > 0) put_small(dst, word_at(0), static_cast<int>(head));
   const int64_t nw = (len - head) >> 3;
-  auto d64 = gl(reinterpret_cast<uint64_t*>(dst + head));
-  for (int64_t w = 0; w < nw; w++) d64[w] = word_at(head + 8 * w);
+  for (int64_t w = 0; w < nw; w++) tstore_wp(dst + head + 8 * w, 8, word_at(head + 8 * w));
   const int64_t t0 = head + 8 * nw;
   if (t0 < len) put_small(dst + t0, word_at(t0), static_cast<int>(len - t0));
+}
+__device__ __forceinline__ void tcopy_out(uint8_t* dst, const Rows& R, int64_t src, int64_t len) {
+  tcopy_to(gl(dst), R, src, len);
+}
+
+// One wave stores bytes img[0, n) of an LDS window (16-aligned, >= 16 readable bytes past n) to
+// g[0, n) (any alignment, every byte of the range this wave's): bytes up to g's 16-byte boundary,
+// 16-B non-temporal stores funnel-shifted out of aligned window words, the byte tail.
+__device__ __forceinline__ void wave_store_window(uint8_t* g, const uint8_t* img, int64_t n) {
+  using v4 = __attribute__((ext_vector_type(4))) uint32_t;
+  if (n <= 0) return;
+  const int lane = threadIdx.x & 63;
+  const auto im = lds_ptr<const uint8_t>(const_cast<uint8_t*>(img));
+  const auto i64 = lds_ptr<const uint64_t>(const_cast<uint8_t*>(img));
+  const int64_t head = min<int64_t>(n, (16 - (reinterpret_cast<uintptr_t>(g) & 15)) & 15);
+  const int64_t body = (n - head) >> 4;
+  const int64_t t0 = head + 16 * body;
+  if (lane < head) gl(g)[lane] = im[lane];
+  if (lane < n - t0) gl(g)[t0 + lane] = im[t0 + lane];
+  const int sh = static_cast<int>(head & 7) * 8;
+  for (int64_t m = lane; m < body; m += 64) {
+    const int64_t q = (head + 16 * m) >> 3;
+    uint64_t x, y;
+    if (sh == 0) {
+      x = i64[q];
+      y = i64[q + 1];
+    } else {
+      const uint64_t w0 = i64[q], w1 = i64[q + 1], w2 = i64[q + 2];
+      x = (w0 >> sh) | (w1 << (64 - sh));
+      y = (w1 >> sh) | (w2 << (64 - sh));
+    }
+    v4 vv;
+    vv.x = static_cast<uint32_t>(x); vv.y = static_cast<uint32_t>(x >> 32);
+    vv.z = static_cast<uint32_t>(y); vv.w = static_cast<uint32_t>(y >> 32);
+    __builtin_nontemporal_store(vv, gl(reinterpret_cast<v4*>(g + head + 16 * m)));
+  }
 }
 
 // Where an error of a nested entry is reported in pass 1: the node and the first row of the
@@ -286,7 +352,7 @@ __device__ __forceinline__ uint64_t err_where_tile(int node, int64_t row0) {
 
 // Checked position (and count) of a non-null variable-length value at pos of node `n`
 // (lv_value in levels.hip, the same checks in both passes).  Returns false: decode as null.
-__device__ bool tcheck(const TreeArgs& a, const Rows& R, CTNode& n, int64_t pos,
+__device__ __forceinline__ bool tcheck(const TreeArgs& a, const Rows& R, CTNode& n, int64_t pos,
                        int32_t size, int64_t total, uint32_t* count, uint64_t where) {
   bool ok = true;
   uint32_t c = 0;

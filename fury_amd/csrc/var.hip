@@ -179,6 +179,10 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 }
 
 static std::atomic<int> g_dec_rows = 0;
+// tuning "var_skip" (diagnostics: phases of encode_var_reg skipped, outputs WRONG; timing only)
+static std::atomic<int> g_var_skip{0};
+int var_skip() { return g_var_skip.load(); }
+void set_var_skip(int v) { g_var_skip = v; }
 static std::atomic<int> g_dec_rows_rejected{0};
 int var_dec_rows_rejected() { return g_dec_rows_rejected.load(); }
 int var_dec_rows() { return g_dec_rows; }

@@ -878,11 +878,13 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* _
   }
   const int64_t room = max<int64_t>(0, min<int64_t>(bytes, cap - base));
   if (bytes <= kRegImg) {
-    if (live) reg_build_row<K, M>(a, r, v, valid, img + (ex >> 3));
+    // (a.skip, diagnostics: 1 no string bytes, 2 no row build, 4 no store)
+    if (live && !(a.skip & 2)) reg_build_row<K, M>(a, r, v, (a.skip & 1) ? 0 : valid, img + (ex >> 3));
     __syncthreads();
-    store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
+    if (!(a.skip & 4)) store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
-    if (ex + sz <= room) reg_build_row<K, M>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
+    if (ex + sz <= room)
+      reg_build_row<K, M>(a, r, v, valid, reinterpret_cast<uint64_t*>(rows + base + ex));
   }
 }
 

@@ -41,16 +41,22 @@ struct WShared {
   uint32_t* req;            // [2][nn + 1]: window words, scanned into window offsets
   uint64_t* wsum;           // [K][NT / 64] (pass 1) / [16] (pass 2) scan scratch
   uint32_t* pool;           // window words
+  int32_t* ow;              // [3][nn]: output window (values / offsets / payload) of node n in
+                            // opool, -1: stored straight to HBM
+  uint32_t* olen;           // [3][nn]: its bytes
+  int64_t* oe;              // [2][nn]: the tile's first entry (E0) / payload byte (B0) of node n
+  uint32_t* oreq;           // [3 nn + 1]: window bytes, scanned into window offsets
+  uint8_t* opool;           // output windows
   uint8_t* pf;              // prefetch landing zone
   uint8_t* stg;             // staged rows
 };
 
 struct WLayout {
-  size_t cur, kb, win, w0, req, wsum, pool, pf, stg, end;
+  size_t cur, kb, win, w0, req, wsum, pool, ow, olen, oe, oreq, opool, pf, stg, end;
 };
 
 __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t stage, uint32_t pool,
-                                               bool write, bool prefetch) {
+                                               bool write, bool prefetch, uint32_t out = 0) {
   WLayout l{};
   size_t b = 0;
   l.cur = b;
@@ -71,6 +77,19 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   l.pool = b;
   b += write ? pool : 0;
   b = (b + 15) & ~size_t(15);
+  const bool ow = write && out > 0;
+  l.oe = b;
+  b += ow ? 8 * 2 * static_cast<size_t>(nn) : 0;
+  l.ow = b;
+  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
+  l.olen = b;
+  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
+  l.oreq = b;
+  b += ow ? 4 * (3 * static_cast<size_t>(nn) + 1) : 0;
+  b = (b + 15) & ~size_t(15);
+  l.opool = b;
+  b += ow ? out : 0;
+  b = (b + 15) & ~size_t(15);
   l.pf = b;                                   // prefetch landing zone: 1 KB per wave
   b += prefetch ? 1024 * static_cast<size_t>(nt / 64) : 0;
   l.stg = b;
@@ -80,7 +99,8 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
 }
 
 __device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, bool write) {
-  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0);
+  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0,
+                                a.out_cap);
   WShared s;
   s.cur = reinterpret_cast<uint32_t*>(base + l.cur);
   s.kb = reinterpret_cast<int64_t*>(base + l.kb);
@@ -89,6 +109,11 @@ __device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, 
   s.req = reinterpret_cast<uint32_t*>(base + l.req);
   s.wsum = reinterpret_cast<uint64_t*>(base + l.wsum);
   s.pool = reinterpret_cast<uint32_t*>(base + l.pool);
+  s.ow = reinterpret_cast<int32_t*>(base + l.ow);
+  s.olen = reinterpret_cast<uint32_t*>(base + l.olen);
+  s.oe = reinterpret_cast<int64_t*>(base + l.oe);
+  s.oreq = reinterpret_cast<uint32_t*>(base + l.oreq);
+  s.opool = base + l.opool;
   s.pf = base + l.pf;
   s.stg = base + l.stg;
   return s;
@@ -179,6 +204,37 @@ __device__ __forceinline__ void wbits_run(const WCtx& c, int n, int which, uint8
   }
 }
 
+// Output windows (write pass, a.out_cap > 0): the tile's entries of a node that is not row-aligned
+// (values of fixed-width / DECIMAL nodes, Arrow offsets of LIST / MAP / STRING / BINARY nodes) and
+// the payload bytes of every STRING / BINARY node are assembled in LDS and stored as whole lines at
+// the end of the tile: per-lane 1-8 B stores straight to HBM left partial lines (WRITE_SIZE 1.98x
+// the column bytes at 4M depth-3 rows).  A node whose window did not fit the
+// pool (ow < 0), and the row-aligned ones (coalesced already), store to HBM.
+__device__ __forceinline__ int32_t wwin(const WCtx& c, int which, int n) {
+  return c.a->out_cap ? c.sh->ow[which * c.a->nn + n] : -1;
+}
+// The value x (w bytes) of entry e of fixed-width node n.
+__device__ __forceinline__ void wput_val(const WCtx& c, CTNode& N, int n, int64_t e, int w,
+                                         uint64_t x) {
+  const int32_t o = N.ek >= 0 ? wwin(c, 0, n) : -1;
+  if (o >= 0) tstore_wp(lds_ptr<uint8_t>(c.sh->opool + o + (e - c.sh->oe[n]) * w), w, x);
+  else tstore_w(N.values + e * w, w, x);
+}
+// Arrow offset v of entry e + 1 of node n (offsets[0] = 0 by entry 0, straight to HBM).
+__device__ __forceinline__ void wput_off(const WCtx& c, CTNode& N, int n, int64_t e, int32_t v) {
+  const int32_t o = N.ek >= 0 ? wwin(c, 1, n) : -1;
+  if (o >= 0) *lds_ptr<int32_t>(c.sh->opool + o + 4 * (e - c.sh->oe[n])) = v;
+  else gl(N.offsets)[e + 1] = v;
+  if (e == 0) gl(N.offsets)[0] = 0;
+}
+// cnt payload bytes of the batch at pos -> payload byte bp of STRING / BINARY node n (straight to
+// HBM: a second, LDS-window instance of tcopy_to inlined in the walk took it from 125 to 242
+// VGPRs, out of line still to 143).
+__device__ __forceinline__ void wput_bytes(const WCtx& c, CTNode& N, int n, int64_t bp, int64_t pos,
+                                           uint32_t cnt) {
+  tcopy_out(N.values + bp, *c.R, pos, cnt);
+}
+
 // m fixed-width elements of a LIST / MAP side (write pass) at entries cs, cs + 1, ...: values one
 // by one, validity / BOOL bits batched 32 elements to an atomic pair, null bits read a word at a
 // time.
@@ -200,7 +256,7 @@ __device__ __forceinline__ void welems(const WCtx& c, CTNode& C, int cn, int64_t
     if (C.type == FURY_TYPE_BOOL) {
       if (!cnul && (x & 0xff)) bm |= 1u << q;
     } else if (C.values && !(c.a->skip & 4)) {
-      tstore_w(C.values + (cs + j) * C.width, C.width, x);
+      wput_val(c, C, cn, cs + j, C.width, x);
     }
     if (!cnul) vm |= 1u << q;
     if (q == 31 || j + 1 == m) {
@@ -220,13 +276,13 @@ __device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t
                                         uint64_t sv) {
   const uint64_t x = nul ? 0 : sv;
   if (c.a->skip & 2) {
-    if (N.type != FURY_TYPE_BOOL && N.values && !(c.a->skip & 4)) tstore_w(N.values + e * N.width, N.width, x);
+    if (N.type != FURY_TYPE_BOOL && N.values && !(c.a->skip & 4)) wput_val(c, N, n, e, N.width, x);
     return;
   }
   if (N.type == FURY_TYPE_BOOL) {
     if (N.values) wbit(c, N, n, 1, N.values, e, !nul && (x & 0xff));
   } else if (N.values) {
-    if (!(c.a->skip & 4)) tstore_w(N.values + e * N.width, N.width, x);
+    if (!(c.a->skip & 4)) wput_val(c, N, n, e, N.width, x);
   }
   if (N.validity) wbit(c, N, n, 0, N.validity, e, !nul);
 }
@@ -269,19 +325,24 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       *cu = c0 + cnt;
       if (W) {
         const int64_t bp = c.sh->kb[N.k] + c0;
-        if (N.offsets) {
-          if (!(a.skip & 8)) gl(N.offsets)[e + 1] = static_cast<int32_t>(bp + cnt);
-          if (e == 0) gl(N.offsets)[0] = 0;
-        }
-        if (valid && N.values && !(a.skip & 1)) tcopy_out(N.values + bp, R, pos, cnt);
+        if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(bp + cnt));
+        if (valid && N.values && !(a.skip & 1)) wput_bytes(c, N, n, bp, pos, cnt);
       }
       return valid;
     }
     if (ty == FURY_TYPE_DECIMAL) {
       if (W && N.values) {
-        const auto d = gl(reinterpret_cast<uint64_t*>(N.values + 16 * e));
-        d[0] = valid ? rd8(R, pos) : 0;
-        d[1] = valid ? rd8(R, pos + 8) : 0;
+        const uint64_t lo = valid ? rd8(R, pos) : 0, hi = valid ? rd8(R, pos + 8) : 0;
+        const int32_t o = N.ek >= 0 ? wwin(c, 0, n) : -1;
+        if (o >= 0) {
+          const auto d = lds_ptr<uint64_t>(c.sh->opool + o + 16 * (e - c.sh->oe[n]));
+          d[0] = lo;
+          d[1] = hi;
+        } else {
+          const auto d = gl(reinterpret_cast<uint64_t*>(N.values + 16 * e));
+          d[0] = lo;
+          d[1] = hi;
+        }
       }
       return valid;
     }
@@ -299,10 +360,7 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
       *cu = c0 + m;
       if (W) {
         cs = c.sh->kb[N.k] + c0;
-        if (N.offsets) {
-          if (!(a.skip & 8)) gl(N.offsets)[e + 1] = static_cast<int32_t>(cs + m);
-          if (e == 0) gl(N.offsets)[0] = 0;
-        }
+        if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(cs + m));
       }
     }
     const int64_t hb = tbm(strc ? N.num_children : static_cast<int64_t>(m));
@@ -350,7 +408,7 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
 
 // The top level of one row (every thread of the workgroup, live or not: ballots).
 template <bool W, int MD>
-__device__ inline void walk_row(const WCtx& c, bool live) {
+__device__ __forceinline__ void walk_row(const WCtx& c, bool live) {
   const TreeArgs& a = *c.a;
   const Rows& R = *c.R;
   const int64_t base = live ? gl(a.offs)[c.row] : 0;
@@ -401,17 +459,17 @@ __device__ inline void walk_row(const WCtx& c, bool live) {
 // adds acc to a.dbg[base + id] at the end (count pass base 0, write pass 16; see tree.hip).
 struct WClock {
   uint64_t* acc;            // LDS [16] or NULL
-  __device__ void mark(int id) const {
+  __device__ __forceinline__ void mark(int id) const {
     if (acc && threadIdx.x == 0) {
       const uint64_t t = __builtin_amdgcn_s_memrealtime();
       acc[id] += t - acc[15];
       acc[15] = t;
     }
   }
-  __device__ void start() const {
+  __device__ __forceinline__ void start() const {
     if (acc && threadIdx.x < 16) acc[threadIdx.x] = threadIdx.x == 15 ? __builtin_amdgcn_s_memrealtime() : 0;
   }
-  __device__ void flush(uint64_t* dbg, int base) const {
+  __device__ __forceinline__ void flush(uint64_t* dbg, int base) const {
     if (acc && threadIdx.x < 15)
       atomicAdd(reinterpret_cast<unsigned long long*>(dbg) + base + threadIdx.x,
                 static_cast<unsigned long long>(acc[threadIdx.x]));
@@ -527,10 +585,36 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
     sh.req[i] = words;
   }
   if (tid == 0) sh.req[2 * nn] = 0;
+  // output windows: the tile's range of each node's values / offsets / payload (wput_*)
+  if (a.out_cap) {
+    for (int i = tid; i < 3 * nn; i += NT) {
+      const int which = i / nn, n = i - which * nn;
+      CTNode& N = tn(a, n);
+      const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
+      int64_t bytes = 0;
+      if (which == 0) {
+        if (N.ek >= 0 && N.values && N.type != FURY_TYPE_BOOL &&
+            (N.width > 0 || N.type == FURY_TYPE_DECIMAL))
+          bytes = (e1 - e0) * (N.width > 0 ? N.width : 16);
+      } else if (which == 1) {
+        sh.oe[n] = e0;
+        if (N.ek >= 0 && N.offsets) bytes = 4 * (e1 - e0);
+      }
+      if (bytes > static_cast<int64_t>(a.out_cap)) bytes = 0;     // straight to HBM
+      sh.olen[i] = static_cast<uint32_t>(bytes);
+      sh.oreq[i] = bytes > 0 ? static_cast<uint32_t>((bytes + 31) & ~int64_t(15)) : 0u;
+    }
+    if (tid == 0) sh.oreq[3 * nn] = 0;
+  }
   const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
   if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
+  if (a.out_cap) {
+    block_scan_u32<NT>(sh.oreq, 3 * nn + 1, sh.wsum);
+    for (int i = tid; i < 3 * nn; i += NT)
+      sh.ow[i] = sh.olen[i] > 0 && sh.oreq[i + 1] <= a.out_cap ? static_cast<int32_t>(sh.oreq[i]) : -1;
+  }
   const uint32_t pool_words = a.pool_cap / 4;
   for (int i = tid; i < 2 * nn; i += NT) {
     const uint32_t off = sh.req[i], end = sh.req[i + 1];
@@ -567,6 +651,20 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
       *g = v;
     }
   }
+  // output windows -> HBM, a wave per window: the range [E0, E1) / [B0, B1) is this tile's alone
+  if (a.out_cap) {
+    const int wave = tid >> 6;
+    for (int i = wave; i < 3 * nn; i += NT / 64) {
+      const int32_t o = sh.ow[i];
+      if (o < 0) continue;
+      const int which = i / nn, n = i - which * nn;
+      CTNode& N = tn(a, n);
+      uint8_t* dst = which == 0 ? N.values + sh.oe[n] * (N.width > 0 ? N.width : 16)
+                   : which == 1 ? reinterpret_cast<uint8_t*>(N.offsets + sh.oe[n] + 1)
+                                : N.values + sh.oe[nn + n];
+      wave_store_window(dst, sh.opool + o, sh.olen[i]);
+    }
+  }
   clk.mark(3);
   clk.flush(a.dbg, 16);
 }
@@ -574,7 +672,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
 }  // namespace
 
 size_t walk_lds(const TreeArgs& a, int nt, bool write) {
-  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0).end;
+  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0, a.out_cap).end;
 }
 
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {

@@ -34,7 +34,8 @@ def engines():
     L = N.lib()
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena",
                                                        "walk_threads", "walk_stage", "walk_pool",
-                                                       "walk_stage_write", "walk_threads_write")}
+                                                       "walk_stage_write", "walk_threads_write",
+                                                       "walk_out")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -92,8 +93,12 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         _tune("walk_threads", 128)
         _tune("walk_threads_write", 128)
     _tune("nested_decode", 2)
-    walk = _decode_plan(enc, batch)
-    assert_columns_equal(fields, walk, ref, n)
+    # output windows of the write pass (walk_out bytes): off, too small for most nodes (mixed
+    # LDS / HBM stores), the default
+    for wo in ((0, 256, 16384) if budget == "tiny" else (0, 16384)):
+        _tune("walk_out", wo)
+        walk = _decode_plan(enc, batch)
+        assert_columns_equal(fields, walk, ref, n)
 
 
 @pytest.mark.parametrize("mode", [0, 2])
