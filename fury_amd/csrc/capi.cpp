@@ -907,6 +907,17 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_dec_cover(value ? value : 95);
     return FURY_OK;
   }
+  if (std::string(key) == "var_wide") {
+    if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_wide: 0..1");
+    set_var_wide_mode(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "wide_threads" || std::string(key) == "wide_enc_threads") {
+    if (value != 256 && value != 512 && value != 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 256, 512 or 1024");
+    set_wide_threads(std::string(key) == "wide_enc_threads", value);
+    return FURY_OK;
+  }
   if (std::string(key) == "var_skip") {
     if (value < 0 || value > 255) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_skip: 0..255");
     set_var_skip(value);
@@ -1030,6 +1041,9 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
   if (key && std::string(key) == "var_skip") return var_skip();
+  if (key && std::string(key) == "var_wide") return var_wide_mode();
+  if (key && std::string(key) == "wide_threads") return wide_threads(false);
+  if (key && std::string(key) == "wide_enc_threads") return wide_threads(true);
   if (key && std::string(key) == "var_dec_cover") return var_dec_cover();
   if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
   if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);

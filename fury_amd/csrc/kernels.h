@@ -229,6 +229,15 @@ int var_dec_rows_rejected();          // forced tiles whose images did not fit (
 int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
 void set_var_dec_cover(int v);
 int lookback_help_mode();
+int var_wide_mode();                  // tuning "var_wide" (var.hip): 1 count + write passes, 0 look-back tiles
+void set_var_wide_mode(int v);
+int wide_threads(bool encode);        // tuning "wide_threads" / "wide_enc_threads" (var.hip)
+void set_wide_threads(bool encode, int v);
+// offsets_only: fury_row_decode_measure (the Arrow offsets of the variable-length fields only)
+int launch_decode_wide(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
+                       bool offsets_only);
+int launch_encode_wide(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
+                       hipStream_t stream);
 int var_skip();                       // tuning "var_skip" (diagnostics, timing only)
 void set_var_skip(int v);
 void set_lookback_help_mode(int v);

@@ -128,6 +128,8 @@ int launch_encode_var(const VarArgs& a, const int64_t* offs, uint8_t* rows, int6
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     return launch_encode_var_reg(b, const_cast<int64_t*>(offs), rows, cap, nt, reg_mode(a), nullptr,
                                  stream);
+  } else if (var_wide_mode()) {   // 64-row tiles, fields round robin over the waves (wide.hip)
+    return launch_encode_wide(a, offs, rows, cap, stream);
   } else if (a.tab) {          // wider than the argument block: column table in device memory
     hipLaunchKernelGGL(encode_var_kernel<MetaMapWide>, dim3(nb), dim3(kEncRows), 0, stream, a,
                        offs, rows, cap);
@@ -163,6 +165,7 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
   for (int k = 0; k < a.ncols; k++)
     if (hcol(a, k).kind == kBytes || hcol(a, k).kind == kListFixed) nseq++;
   if (nseq == 0 || a.nrows == 0) return FURY_OK;
+  if (a.ncols > kRegCols && var_wide_mode()) return launch_decode_wide(a, rows, offs, stream, true);
   const int64_t nb = nblocks(a.nrows);
   int64_t* ws = nullptr;
   const int64_t scr = scan_workspace(nb);
@@ -181,6 +184,14 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 static std::atomic<int> g_dec_rows = 0;
 // tuning "var_skip" (diagnostics: phases of encode_var_reg skipped, outputs WRONG; timing only)
 static std::atomic<int> g_var_skip{0};
+static std::atomic<int> g_var_wide{1};
+// threads per 64-row tile of the wide kernels (ab_wide legs, 33 fields x 5M rows): decode 256
+// (3.22 vs 3.37 ms at 512), encode 512 (2.20 vs 2.78 ms at 256)
+static std::atomic<int> g_wide_threads[2] = {256, 512};
+int wide_threads(bool encode) { return g_wide_threads[encode ? 1 : 0].load(); }
+void set_wide_threads(bool encode, int v) { g_wide_threads[encode ? 1 : 0] = v; }
+int var_wide_mode() { return g_var_wide.load(); }
+void set_var_wide_mode(int v) { g_var_wide = v; }
 int var_skip() { return g_var_skip.load(); }
 void set_var_skip(int v) { g_var_skip = v; }
 static std::atomic<int> g_dec_rows_rejected{0};
@@ -272,6 +283,9 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
     dev_free(ws, stream);
     return st;
   }
+  // wider than kRegCols: count pass + scan + write pass (wide.hip); tuning "var_wide" 0 = the
+  // round-4 256-row look-back tile kernel below (A/B)
+  if (var_wide_mode()) return launch_decode_wide(a, rows, offs, stream, false);
   // look-back status words (nb x nseq), zeroed per launch
   const size_t wsb = (nb * nseq + 1) * 8;
   uint64_t* ws = nullptr;

@@ -20,11 +20,18 @@ def main():
     ap.add_argument("--ncols", type=int, default=33)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--str-max", type=int, default=24)
+    ap.add_argument("--tune", action="append", default=[],
+                    help="key=value fury_set_tuning before timing (repeatable)")
+    ap.add_argument("--no-plan", action="store_true", help="skip the plan-API decode leg")
     args = ap.parse_args()
     import torch
     from fury_amd.encoder import Encoders, _tree_bytes, column_to_device
     from fury_amd.workloads import gen_columns
     from tests.test_device import _wide_fields
+    from fury_amd import _native as N
+    for kv in args.tune:
+        k, v = kv.split("=")
+        assert N.lib().fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
     fields = _wide_fields(args.ncols)
     n = args.rows
     host = gen_columns("wide", fields, n, seed=7, null_pct=10, str_max=args.str_max, list_max=6)
@@ -54,8 +61,14 @@ def main():
     out = enc.decode_batch(batch)                       # allocated once (bound sizing)
     res["encode_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
     res["decode_flat_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
-    res["decode_plan_ms"] = timed(lambda: enc._decode_nested(batch, True, False, None))
-    for k in ("encode", "decode_flat", "decode_plan"):
+    # one device pass into the preallocated columns (no sizing pass, no host sync): the kernels
+    res["decode_into_ms"] = timed(lambda: enc.decode_into(batch, out))
+    legs = ["encode", "decode_flat", "decode_into"]
+    if not args.no_plan:
+        res["decode_plan_ms"] = timed(lambda: enc._decode_nested(batch, True, False, None))
+        legs.append("decode_plan")
+    res["tune"] = args.tune
+    for k in legs:
         res[k + "_TBps"] = round(alg / (res[k + "_ms"] * 1e-3) / 1e12, 3)
     print(json.dumps(res))
 
