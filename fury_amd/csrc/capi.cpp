@@ -897,7 +897,8 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "nested_decode") {
-    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 0..2");
+    if (value < 1 || value > 2)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 1 (level engine) or 2 (row walk)");
     set_tree_mode(value);
     return FURY_OK;
   }
@@ -969,12 +970,6 @@ int fury_set_tuning(const char* key, int32_t value) {
                     static_cast<uint32_t>(value));
     return FURY_OK;
   }
-  if (std::string(key) == "tree_threads") {
-    if (value != 256 && value != 512 && value != 1024)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "tree_threads: 256, 512 or 1024");
-    set_tree_threads(value);
-    return FURY_OK;
-  }
   if (std::string(key) == "tree_debug") {
     if (value < 0 || value > 1) return set_error(FURY_ERR_INVALID_ARGUMENT, "tree_debug: 0..1");
     return set_tree_debug(value) ? set_error(FURY_ERR_DEVICE, "tree_debug buffer") : FURY_OK;
@@ -995,30 +990,6 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_rowenc_tuning(1, static_cast<uint32_t>(value));
     return FURY_OK;
   }
-  if (std::string(key) == "nested_encode") {
-    if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_encode: 0..4");
-    set_tree_encode_mode(value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "tree_enc_lds" || std::string(key) == "tree_measure_lds") {
-    if (value < 1024 || value > 96 * 1024)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1024..98304 bytes");
-    set_tree_encode_lds(std::string(key) == "tree_enc_lds" ? 1 : 0, static_cast<uint32_t>(value));
-    return FURY_OK;
-  }
-  if (std::string(key) == "tree_enc_rows" || std::string(key) == "tree_measure_rows") {
-    if (value < 1 || value > 4096)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1..4096 rows");
-    set_tree_encode_rows(std::string(key) == "tree_enc_rows" ? 1 : 0, value);
-    return FURY_OK;
-  }
-  if (std::string(key) == "tree_stage" || std::string(key) == "tree_arena") {
-    if (value < 1024 || value > 96 * 1024)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 1024..98304 bytes");
-    if (std::string(key) == "tree_stage") set_tree_lds(static_cast<uint32_t>(value), 0);
-    else set_tree_lds(0, static_cast<uint32_t>(value));
-    return FURY_OK;
-  }
   return set_error(FURY_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
@@ -1026,11 +997,9 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "lookback_help") return lookback_help_mode();
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "nested_decode") return tree_mode();
-  if (key && std::string(key) == "nested_encode") return tree_encode_mode();
   if (key && std::string(key) == "rowenc_rows") return static_cast<int32_t>(rowenc_tuning(0));
   if (key && std::string(key) == "rowenc_img") return static_cast<int32_t>(rowenc_tuning(1));
   if (key && std::string(key) == "rowenc_tile") return static_cast<int32_t>(rowenc_tuning(2));
-  if (key && std::string(key) == "tree_threads") return tree_threads();
   if (key && std::string(key) == "walk_threads") return static_cast<int32_t>(walk_tuning(0));
   if (key && std::string(key) == "walk_stage") return static_cast<int32_t>(walk_tuning(1));
   if (key && std::string(key) == "walk_pool") return static_cast<int32_t>(walk_tuning(2));
@@ -1045,12 +1014,6 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "wide_threads") return wide_threads(false);
   if (key && std::string(key) == "wide_enc_threads") return wide_threads(true);
   if (key && std::string(key) == "var_dec_cover") return var_dec_cover();
-  if (key && std::string(key) == "tree_enc_lds") return static_cast<int32_t>(tree_encode_lds(1));
-  if (key && std::string(key) == "tree_enc_rows") return tree_encode_rows(1);
-  if (key && std::string(key) == "tree_measure_rows") return tree_encode_rows(0);
-  if (key && std::string(key) == "tree_measure_lds") return static_cast<int32_t>(tree_encode_lds(0));
-  if (key && std::string(key) == "tree_stage") return static_cast<int32_t>(tree_lds(0));
-  if (key && std::string(key) == "tree_arena") return static_cast<int32_t>(tree_lds(1));
   if (key && std::string(key) == "lookback_timeouts")
     return static_cast<int32_t>(lookback_timeouts());
   if (key && std::string(key) == "unframe_walks")

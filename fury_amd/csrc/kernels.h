@@ -256,7 +256,6 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* row_
 // ---- generic (nested) schema engine: generic.hip --------------------------------------------
 constexpr int kGenMaxNodes = 48;      // schema tree nodes in the argument block
 constexpr int kGenMaxWideNodes = 4096;  // beyond 48: node table uploaded per call (GenArgs.tab)
-constexpr int kGenMaxDepth = 8;       // nesting levels (checked at schema creation)
 
 struct GenNode {
   const uint8_t* values;   // fixed values / bytes payload / decimal values (bool: bit-packed)
@@ -280,25 +279,17 @@ struct GenArgs {
   const GenNode* htab;     // its host copy (launchers only; never read on the device)
 };
 
+// Nested encode (rowenc.hip): measure pass (row sizes) / build pass at the given row offsets, for
+// any nesting depth (kRowEncMaxDepth levels inlined, deeper ones on an explicit stack).
 int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream);
-// Row-walk encode (rowenc.hip): measure (sizes != NULL) or build pass for schemas of up to
-// kRowEncMaxDepth levels; returns 1 when the schema is deeper (left to the interpreter).
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
+                      hipStream_t stream);
 constexpr int kRowEncMaxDepth = 5;
+constexpr int kMaxNestLevels = 64;     // schema nesting limit (schema.cpp)
 int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
                   int64_t cap, hipStream_t stream);
 void set_rowenc_tuning(int which, uint32_t v);   // 0 "rowenc_rows", 1 "rowenc_img", 2 "rowenc_tile"
 uint32_t rowenc_tuning(int which);
-int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
-                      hipStream_t stream);
-// Nested encode engine (generic.hip, rowenc.hip): tuning "nested_encode" (include/fury_row.h) 0 tree
-// tiles, 1 interpreter, 2 tree-tile measure + interpreter, 3 tree-tile measure + row walk, 4 row-walk
-// measure + row walk (default); "tree_enc_lds" / "tree_measure_lds" = the tree tiles' LDS budgets.
-void set_tree_encode_mode(int v);
-int tree_encode_mode();
-void set_tree_encode_lds(int which, uint32_t bytes);   // which: 0 measure, 1 encode
-uint32_t tree_encode_lds(int which);
-void set_tree_encode_rows(int which, int rows);        // tuning "tree_enc_rows" / "tree_measure_rows"
-int tree_encode_rows(int which);
 // Level-by-level nested decode (levels.hip): prepare = per-level count / scan / expand passes
 // (totals[2 i] entries, totals[2 i + 1] payload bytes of node i), execute = one write pass into
 // the outputs of gen_args' node table.
@@ -308,7 +299,7 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
 int lv_execute(const LvPlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                hipStream_t hs);
 void lv_free(LvPlan* p);
-// Tile-staged nested decode (tree.hip): prepare = pass 1 + tile scan + one host sync (*out NULL:
+// Row-walk nested decode (tree.hip / walk.hip): prepare = pass 1 + tile scan + one host sync (*out NULL:
 // the batch needs the level engine above), execute = pass 2 into gen_args' node table.
 struct TreePlan;
 int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, int64_t nrows,
@@ -316,13 +307,9 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
 int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                  const std::vector<int64_t>& totals, hipStream_t hs);
 void tree_free(TreePlan* p);
-void set_tree_mode(int v);           // tuning "nested_decode": 0 tree tiles, 1 levels, 2 row walk (default)
+void set_tree_mode(int v);           // tuning "nested_decode": 1 levels, 2 row walk (default)
 int tree_mode();
-void set_tree_lds(uint32_t stage, uint32_t arena);   // tuning "tree_stage" / "tree_arena" (bytes)
-uint32_t tree_lds(int which);
 int set_tree_debug(int on);          // tuning "tree_debug": phase accumulators on / off
-void set_tree_threads(int v);        // tuning "tree_threads": 256 / 512 / 1024
-int tree_threads();
 // tunings of the row-walk decode (walk.hip): 0 "walk_threads" (128 / 256 rows per tile),
 // 1 "walk_stage" (LDS stage cap of the count pass, bytes), 2 "walk_pool" (LDS bitmap-window
 // bytes), 3 "walk_stage_write" (LDS stage cap of the write pass), 4 "walk_prefetch" (bit 0 write pass, bit 1 count pass)

@@ -1,20 +1,21 @@
-// rowenc.hip — nested encode with a thread per ROW, the schema walk inlined per depth: the
-// default build pass (and optional measure pass) of fury_encode for schemas of up to
-// kRowEncMaxDepth levels.  generic.hip's interpreter (put_value / put_array, called level by
-// level) stays for deeper schemas; the tree tiles (generic.hip, te_kernel) for the deepest.
+// rowenc.hip — the encode (measure pass + build pass) of every schema the flat kernels do not
+// take: nested STRUCT / LIST / MAP fields at any depth (up to 64 levels), flat variable-length
+// schemas wider than 256 fields, and ArrayEncoder / MapEncoder collection batches.  A thread per
+// ROW walks the schema, the first kRowEncMaxDepth levels inlined per depth, deeper levels with an
+// explicit stack (rdeep).  (Round 5 removed the row interpreter and the tree-tile encode this
+// replaced: one nested encode engine)
 //
-// Reference semantics are the interpreter's (generic.hip header): BaseBinaryEncoderBuilder
+// Reference semantics: BaseBinaryEncoderBuilder
 // .serializeFor (FMT/encoder/BaseBinaryEncoderBuilder.java:138-453) -- primitives in 8-byte slots
 // (narrow in arrays), var values appended at the writer index and zero-padded to 8
 // (BinaryWriter.java:106-121,187-194), List -> [int64 n][bitmap][n x elemSize, tail zeroed][var
 // section] (BinaryArrayWriter.java:91-163), bean -> nested BinaryRowWriter row (:363-417), Map ->
-// [int64 keyBytes][key array][value array] (:298-357), null -> setNullAt (bit only).  The bytes
-// written are identical to the interpreter's (tests/test_tree.py runs every nested_encode mode
-// against the oracle).
+// [int64 keyBytes][key array][value array] (:298-357), null -> setNullAt (bit only); the bytes are
+// checked against the oracle (tests/test_tree.py, tests/test_reference_beans.py).
 //
-// MI355X design.  The interpreter's depth templates call each other (put_value -> put_array ->
-// put_value): every level is a call frame, and the build kernel kept 256 VGPRs plus ~870 B of
-// scratch per lane live.  Here a container's children -- a STRUCT's fields, a LIST's elements, a
+// MI355X design.  A row interpreter whose depth templates call each other keeps every level's
+// registers live in a call frame (the round-2/3 engine: 256 VGPRs plus ~870 B of scratch per
+// lane).  Here a container's children -- a STRUCT's fields, a LIST's elements, a
 // MAP's keys then values -- go through ONE loop with ONE call of the next level, so the levels
 // inline into straight code (as walk.hip's decode walk); scalar children are stored at the call
 // site, so a schema of L levels needs L instances.  Every active lane of a wave is at the same
@@ -109,10 +110,13 @@ __device__ __forceinline__ void rappend(P dst, const uint8_t* src, int64_t len) 
   }
 }
 
-template <int D, int MD, bool W, class P>
+template <int D, int MD, bool W, bool DEEP, class P>
 __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
                                        int64_t o1, P buf, int64_t container, int64_t slot,
                                        int64_t& cursor);
+template <bool W, class P>
+__device__ void rdeep(const RwArgs& a, int ni, int64_t idx, P buf, int64_t container, int64_t slot,
+                      int es, bool in_array, int64_t bm, int64_t ord, int64_t& cursor);
 
 // Entry idx of node ni at level D, in slot `slot` (es bytes; in_array: an array element) of a
 // container starting at `container`, null bit `ord` of the bitmap at bm.  Every load of the entry
@@ -120,11 +124,13 @@ __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t 
 // memory round trip per entry instead of one per dependent read (the walk is latency-bound).
 // (Issuing entry j + 1's loads before finishing entry j measured slower: more VGPRs, 1.34 ->
 // 1.45 ms build at 4M depth-3 rows.)
-template <int D, int MD, bool W, class P>
+template <int D, int MD, bool W, bool DEEP, class P>
 __device__ __forceinline__ void ritem(const RwArgs& a, int ni, int64_t idx, P buf,
                                       int64_t container, int64_t slot, int es, bool in_array,
                                       int64_t bm, int64_t ord, int64_t& cursor) {
   if constexpr (D >= MD) {
+    // below the inlined levels: the explicit-stack walk (DEEP instances, schemas deeper than MD)
+    if constexpr (DEEP) rdeep<W>(a, ni, idx, buf, container, slot, es, in_array, bm, ord, cursor);
     return;
   } else {
     CGNode& n = rn(a, ni);
@@ -159,7 +165,7 @@ __device__ __forceinline__ void ritem(const RwArgs& a, int ni, int64_t idx, P bu
       }
       return;
     }
-    rvalue<D, MD, W>(a, ni, ty, idx, o0, o1, buf, container, slot, cursor);
+    rvalue<D, MD, W, DEEP>(a, ni, ty, idx, o0, o1, buf, container, slot, cursor);
   }
 }
 
@@ -207,7 +213,7 @@ __device__ __forceinline__ void relems(CGNode& C, int es, int64_t b, int64_t m, 
 // The image of container entry idx of node ni (type ty: STRUCT, or LIST / MAP with elements
 // [b, b + m) of its child nodes) at buf + start; returns the end of its bytes.  Children at level
 // D + 1.
-template <int D, int MD, bool W, class P>
+template <int D, int MD, bool W, bool DEEP, class P>
 __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_t idx, int64_t b,
                                          int64_t m, P buf, int64_t start) {
   CGNode& n = rn(a, ni);
@@ -247,8 +253,8 @@ __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_
     for (int64_t j = 0; j < items; j++) {
       const int cn = __builtin_amdgcn_readfirstlane(
           strc ? n.first_child + static_cast<int>(j) : n.first_child + sd);
-      ritem<D + 1, MD, W>(a, cn, strc ? idx : b + j, buf, arr, arr + hb + (strc ? 8 : ces) * j,
-                          strc ? 8 : ces, !strc, bm, j, c2);
+      ritem<D + 1, MD, W, DEEP>(a, cn, strc ? idx : b + j, buf, arr, arr + hb + (strc ? 8 : ces) * j,
+                                strc ? 8 : ces, !strc, bm, j, c2);
     }
   }
   return c2;
@@ -256,7 +262,7 @@ __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_
 
 // A non-null, non-scalar entry idx of node ni (level D; o0 / o1: its offsets pair): its bytes at
 // the cursor, its slot (offset from the container, size).
-template <int D, int MD, bool W, class P>
+template <int D, int MD, bool W, bool DEEP, class P>
 __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
                                        int64_t o1, P buf, int64_t container, int64_t slot,
                                        int64_t& cursor) {
@@ -282,7 +288,7 @@ __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t 
     return;
   }
   if (ty != FURY_TYPE_STRUCT && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
-  cursor = rcont<D, MD, W>(a, ni, ty, idx, o0, o1 - o0, buf, start);
+  cursor = rcont<D, MD, W, DEEP>(a, ni, ty, idx, o0, o1 - o0, buf, start);
   if (W) s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) |
                             static_cast<uint32_t>(cursor - start));
 }
@@ -290,13 +296,13 @@ __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t 
 // Entry r of the batch (generic.hip put_row): a row of the ntop top-level fields, or the
 // top-level BinaryArray / BinaryMap of node 0's entry r (ArrayEncoder.toArray / MapEncoder.toMap,
 // ArrayEncoderBuilder.java:118-140, MapEncoderBuilder.java:152-208).  Returns its size.
-template <bool W, int kRoot, int MD, class P>
+template <bool W, int kRoot, int MD, bool DEEP, class P>
 __device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
   if constexpr (kRoot != 0) {
     const auto offs = gl(rn(a, 0).offsets);
     const int64_t b = offs[r];
-    return rcont<0, MD, W>(a, 0, kRoot == 1 ? FURY_TYPE_LIST : FURY_TYPE_MAP, r, b, offs[r + 1] - b,
-                           buf, 0);
+    return rcont<0, MD, W, DEEP>(a, 0, kRoot == 1 ? FURY_TYPE_LIST : FURY_TYPE_MAP, r, b,
+                                 offs[r + 1] - b, buf, 0);
   } else {
     const int ntop = a.ntop;
     const int64_t bmb = rbm(ntop);
@@ -304,15 +310,15 @@ __device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
     if (W) rzero(buf, fixed);
     int64_t cursor = fixed;
     for (int k = 0; k < ntop; k++)
-      ritem<0, MD, W>(a, k, r, buf, 0, bmb + 8 * static_cast<int64_t>(k), 8, false, 0, k, cursor);
+      ritem<0, MD, W, DEEP>(a, k, r, buf, 0, bmb + 8 * static_cast<int64_t>(k), 8, false, 0, k, cursor);
     return cursor;
   }
 }
 
-template <int kRoot, int MD>
+template <int kRoot, int MD, bool DEEP>
 __global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
-  if (r < a.nrows) a.sizes[r] = rrow<false, kRoot, MD>(a, r, static_cast<LdsU8*>(nullptr));
+  if (r < a.nrows) a.sizes[r] = rrow<false, kRoot, MD, DEEP>(a, r, static_cast<LdsU8*>(nullptr));
 }
 
 // Build pass: the workgroup's rows are built in the LDS image by whole waves as long as their
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
 // paths ran both instruction streams one after the other (a 72 KB image on ~75 KB tiles: 2.1 ms
 // per-row vs 1.33 ms when everything fit), and a second image round costs a whole walk latency.
 // Rows past the capacity (encode_measured) are not written.
-template <int NT, int kRoot, int MD>
+template <int NT, int kRoot, int MD, bool DEEP>
 __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t img[];
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile;
@@ -334,8 +340,8 @@ __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   const int fit = __syncthreads_count(live && my1 - b0 <= a.img && my1 <= a.cap);
   const int64_t in_img = min<int64_t>(fit == rend - r0 ? fit : fit & ~63, rend - r0);
   if (live && my1 <= a.cap) {
-    if (r < r0 + in_img) rrow<true, kRoot, MD>(a, r, (LdsU8*)(img + (my0 - b0)));
-    else rrow<true, kRoot, MD>(a, r, a.rows + my0);
+    if (r < r0 + in_img) rrow<true, kRoot, MD, DEEP>(a, r, (LdsU8*)(img + (my0 - b0)));
+    else rrow<true, kRoot, MD, DEEP>(a, r, a.rows + my0);
   }
   __syncthreads();
   const int64_t nw = (a.offs[r0 + in_img] - b0) >> 3;
@@ -344,13 +350,155 @@ __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   for (int64_t i = threadIdx.x; i < nw; i += NT) d[i] = s[i];
 }
 
+// ---- schemas nested deeper than kRowEncMaxDepth: the walk below the inlined levels with an
+// explicit stack (per-lane frames in scratch) -- the same entries, in the same order, writing the
+// same bytes as ritem / rvalue / rcont.  Lanes may sit at different depths here (a lane whose
+// list is shorter pops while another pushes), so node records are plain per-lane loads.
+struct RFrame {
+  int64_t idx, b, m, start, slot, container, arr, hb, items, j;
+  int32_t ni, sd;
+};
+
+// Header of side f.sd of the container of frame f at the cursor (a STRUCT: bitmap + slots; a LIST /
+// MAP side: [int64 m][bitmap][m x elemSize, tail zeroed]); returns the items the walk visits (0:
+// fixed-width elements, written here four at a time).
+template <bool W, class P>
+__device__ __forceinline__ int64_t rside(const RwArgs& a, RFrame& f, P buf, int64_t& cursor) {
+  CGNode& n = rn(a, f.ni);
+  if (n.type == FURY_TYPE_STRUCT) {
+    const int64_t items = n.num_children;
+    f.arr = f.start;
+    f.hb = rbm(items);
+    if (W) rzero(buf + f.start, f.hb + 8 * items);
+    cursor = f.start + f.hb + 8 * items;
+    return items;
+  }
+  if (f.sd == 1 && W) s8(buf + f.start, static_cast<uint64_t>(cursor - (f.start + 8)));
+  CGNode& C = rn(a, n.first_child + f.sd);
+  const int cw = rwidth(C.type);
+  const int ces = cw > 0 ? cw : 8;
+  f.arr = cursor;
+  f.hb = 8 + rbm(f.m);
+  const int64_t fp = r8(f.m * ces);
+  if (W) {
+    s8(buf + f.arr, static_cast<uint64_t>(f.m));
+    rzero(buf + f.arr + 8, f.hb - 8 + fp);
+  }
+  cursor = f.arr + f.hb + fp;
+  if (cw > 0) {
+    if (W) relems(C, ces, f.b, f.m, buf, f.arr + f.hb, f.arr + 8);
+    return 0;
+  }
+  return f.m;
+}
+
+template <bool W, class P>
+__device__ void rdeep(const RwArgs& a, int ni0, int64_t idx0, P buf, int64_t container0,
+                      int64_t slot0, int es0, bool in_array0, int64_t bm0, int64_t ord0,
+                      int64_t& cursor) {
+  RFrame st[kMaxNestLevels];
+  int sp = -1;
+  // one entry (ritem + rvalue): leaves written at once, a container pushed with its first side
+  auto enter = [&](int ni, int64_t idx, int64_t container, int64_t slot, int es, bool in_array,
+                   int64_t bm, int64_t ord) {
+    CGNode& n = rn(a, ni);
+    const int ty = n.type;
+    const int w = rwidth(ty);
+    const uint32_t vb = n.validity ? gl(n.validity)[idx >> 3] : 0xffu;
+    uint64_t v = 0;
+    int64_t o0 = 0, o1 = 0;
+    if (w > 0) {
+      if (W) {
+        if (ty == FURY_TYPE_BOOL) v = gl(n.values)[idx >> 3];
+        else if (w == 8) v = *gl(reinterpret_cast<const uint64_t*>(n.values + idx * 8));
+        else if (w == 4) v = *gl(reinterpret_cast<const uint32_t*>(n.values + idx * 4));
+        else if (w == 2) v = *gl(reinterpret_cast<const uint16_t*>(n.values + idx * 2));
+        else v = gl(n.values)[idx];
+      }
+    } else if (n.offsets) {
+      o0 = gl(n.offsets)[idx];
+      o1 = gl(n.offsets)[idx + 1];
+    }
+    if (!((vb >> (idx & 7)) & 1)) {
+      if (W) o1_(buf + bm + (ord >> 3), static_cast<uint8_t>(1u << (ord & 7)));
+      return;
+    }
+    if (w > 0) {
+      if (W) {
+        if (ty == FURY_TYPE_BOOL) v = (v >> (idx & 7)) & 1;
+        if (!in_array || es == 8) s8(buf + slot, v);
+        else if (es == 4) s4(buf + slot, static_cast<uint32_t>(v));
+        else if (es == 2) s2(buf + slot, static_cast<uint16_t>(v));
+        else s1(buf + slot, static_cast<uint8_t>(v));
+      }
+      return;
+    }
+    const int64_t start = cursor;
+    if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
+      const int64_t len = o1 - o0;
+      if (W) {
+        rappend(buf + start, n.values + o0, len);
+        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | static_cast<uint32_t>(len));
+      }
+      cursor = start + r8(len);
+      return;
+    }
+    if (ty == FURY_TYPE_DECIMAL) {
+      if (W) {
+        const auto dv = gl(reinterpret_cast<const uint64_t*>(n.values + 16 * idx));
+        s8(buf + start, dv[0]);
+        s8(buf + start + 8, dv[1]);
+        s8(buf + slot, (static_cast<uint64_t>(start - container) << 32) | 16u);
+      }
+      cursor = start + 16;
+      return;
+    }
+    if (ty != FURY_TYPE_STRUCT && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
+    RFrame& f = st[++sp];
+    f.ni = ni;
+    f.idx = idx;
+    f.b = o0;
+    f.m = o1 - o0;
+    f.start = start;
+    f.slot = slot;
+    f.container = container;
+    f.sd = 0;
+    f.j = 0;
+    f.items = 0;
+    cursor = start + (ty == FURY_TYPE_MAP ? 8 : 0);     // a map's key-array size word first
+    f.items = rside<W>(a, f, buf, cursor);
+  };
+  enter(ni0, idx0, container0, slot0, es0, in_array0, bm0, ord0);
+  while (sp >= 0) {
+    RFrame& f = st[sp];
+    CGNode& n = rn(a, f.ni);
+    if (f.j < f.items) {
+      const int64_t j = f.j++;
+      if (n.type == FURY_TYPE_STRUCT)
+        enter(n.first_child + static_cast<int>(j), f.idx, f.arr, f.arr + f.hb + 8 * j, 8, false, f.arr, j);
+      else
+        enter(n.first_child + f.sd, f.b + j, f.arr, f.arr + f.hb + 8 * j, 8, true, f.arr + 8, j);
+      continue;
+    }
+    if (n.type == FURY_TYPE_MAP && f.sd == 0) {          // the value array after the keys
+      f.sd = 1;
+      f.j = 0;
+      f.items = rside<W>(a, f, buf, cursor);
+      continue;
+    }
+    if (W) s8(buf + f.slot, (static_cast<uint64_t>(f.start - f.container) << 32) |
+                                static_cast<uint32_t>(cursor - f.start));
+    sp--;
+  }
+}
+
 }  // namespace
 
 int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t* rows,
                   int64_t cap, hipStream_t stream) {
   const int nn = g.nnodes;
   const GenNode* hn = g.htab ? g.htab : g.node;
-  if (nn <= 0 || !hn) return 1;
+  if (nn <= 0 || !hn) return set_error(FURY_ERR_INVALID_ARGUMENT, "row-walk encode: empty schema");
   std::vector<int32_t> level(nn, 0);
   int nlev = 1;
   for (int i = 0; i < nn; i++)
@@ -358,7 +506,7 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
       level[hn[i].first_child + j] = level[i] + 1;
       nlev = std::max(nlev, level[i] + 2);
     }
-  if (nlev > kRowEncMaxDepth) return 1;
+  if (nlev > kMaxNestLevels) return set_error(FURY_ERR_UNSUPPORTED, "schema nested deeper than 64 levels");
   RwArgs a{};
   DeviceTable dt;
   const GenNode* tab = g.tab;
@@ -395,14 +543,35 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
   };
 #define FURY_RW(R, MD)                                                                         \
   if (g.root == R && nlev <= MD) {                                                             \
-    go(rw_measure_kernel<R, MD>, rw_encode_kernel<128, R, MD>, rw_encode_kernel<256, R, MD>);  \
+    go(rw_measure_kernel<R, MD, false>, rw_encode_kernel<128, R, MD, false>,                   \
+       rw_encode_kernel<256, R, MD, false>);                                                   \
+    return check_hip(hipGetLastError(), "row-walk encode launch");                             \
+  }
+  // deeper schemas: kRowEncMaxDepth inlined levels, then the explicit stack (rdeep)
+#define FURY_RW_DEEP(R)                                                                        \
+  if (g.root == R) {                                                                           \
+    go(rw_measure_kernel<R, kRowEncMaxDepth, true>,                                            \
+       rw_encode_kernel<128, R, kRowEncMaxDepth, true>, rw_encode_kernel<256, R, kRowEncMaxDepth, true>); \
     return check_hip(hipGetLastError(), "row-walk encode launch");                             \
   }
   FURY_RW(0, 2) FURY_RW(0, 3) FURY_RW(0, 4) FURY_RW(0, 5)
   FURY_RW(1, 2) FURY_RW(1, 3) FURY_RW(1, 4) FURY_RW(1, 5)
   FURY_RW(2, 2) FURY_RW(2, 3) FURY_RW(2, 4) FURY_RW(2, 5)
+  FURY_RW_DEEP(0) FURY_RW_DEEP(1) FURY_RW_DEEP(2)
+#undef FURY_RW_DEEP
 #undef FURY_RW
-  return 1;
+  return set_error(FURY_ERR_UNSUPPORTED, "row-walk encode: collection root");
+}
+
+// fury_row_measure / fury_row_encode(_measured) of the schemas above (capi.cpp).
+int launch_gen_measure(const GenArgs& g, int64_t* sizes, hipStream_t stream) {
+  if (g.nrows == 0) return FURY_OK;
+  return rowenc_launch(g, nullptr, sizes, nullptr, 0, stream);
+}
+int launch_gen_encode(const GenArgs& g, const int64_t* offs, uint8_t* rows, int64_t cap,
+                      hipStream_t stream) {
+  if (g.nrows == 0) return FURY_OK;
+  return rowenc_launch(g, offs, nullptr, rows, cap, stream);
 }
 
 void set_rowenc_tuning(int which, uint32_t v) {

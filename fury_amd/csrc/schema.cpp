@@ -15,11 +15,9 @@
 
 namespace fury {
 
-// keep in sync with kGenMaxNodes / kGenMaxDepth (kernels.h; this TU is host-only C++)
-constexpr int kGenMaxNodesHost = 4096;   // = kGenMaxWideNodes (kernels.h)
-constexpr int kGenMaxDepthHost = 65;     // tree tiles (kTEMaxLevels = 64 levels)
-constexpr int kInterpDepthHost = 8;      // = kGenMaxDepth: the row interpreter's unrolled depth
-constexpr int kTreeEncNodesHost = 256;   // tree-tile encode node table (generic.hip)
+// keep in sync with kernels.h (this TU is host-only C++)
+constexpr int kGenMaxNodesHost = 4096;   // = kGenMaxWideNodes
+constexpr int kGenMaxDepthHost = 65;     // < : kMaxNestLevels = 64 levels (rowenc.hip rdeep stack)
 constexpr int kMaxWideVarColsHost = 256; // = kMaxWideVarCols: the flat variable-length kernels
 
 static thread_local std::string g_last_error;
@@ -284,8 +282,7 @@ int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema
   }
   if (!s->device_ok) {
     // nested fields: the generic engine handles them within its table limits
-    if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost &&
-        (s->depth < kInterpDepthHost || s->nodes.size() <= static_cast<size_t>(kTreeEncNodesHost))) {
+    if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost) {
       s->device_ok = 1;
       s->generic = 1;
       s->device_reason.clear();
@@ -315,8 +312,7 @@ int fury_collection_schema_create(const fury_field* field, fury_schema** out) {
   s->bitmap_bytes = 0;
   s->fixed_size = 0;
   s->schema_hash = 0;
-  if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost &&
-      (s->depth < kInterpDepthHost || s->nodes.size() <= static_cast<size_t>(kTreeEncNodesHost))) {
+  if (s->nodes.size() <= static_cast<size_t>(kGenMaxNodesHost) && s->depth < kGenMaxDepthHost) {
     s->device_ok = 1;
     s->generic = 1;
     s->device_reason.clear();

@@ -1,5 +1,4 @@
-// tree_dev.h — device side shared by the nested decodes over staged rows: tree.hip (tile-staged
-// level walk) and walk.hip (a thread per row).  Node records, the batch reader (LDS stage or HBM),
+// tree_dev.h — device side of the row-walk nested decode (walk.hip; tree.hip plans it).  Node records, the batch reader (LDS stage or HBM),
 // the bounds checks every pass applies identically, block scans and bitmap helpers.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -30,8 +29,6 @@ struct TNode {
 };
 
 constexpr int kTreeMaxNodes = 512;
-constexpr int kTreeMaxLevels = 64;
-constexpr int kTreeThreads = 256;
 
 struct TreeArgs {
   const TNode* nodes;       // device table (scalar loads: every use has a uniform index)
@@ -44,13 +41,9 @@ struct TreeArgs {
   uint32_t* err;            // the stream's device error slot
   int32_t* overflow;        // set when a single row does not fit the arena (pass 1)
   int32_t nn, ntop, root, nlevels;
-  int32_t tile_rows;
-  uint32_t stage_cap, arena_cap;
-  int32_t maxw;             // widest level (nodes)
+  uint32_t stage_cap;       // LDS bytes of the row stage (count / write pass)
   int32_t pad_;
   uint64_t* dbg;            // diagnostics (tuning "tree_debug"): phase times, or NULL
-  int32_t level_start[kTreeMaxLevels + 1];
-  // walk.hip
   int64_t stride;           // row stride of cnt / byt (ntiles + 1: [ntiles] = the node's total)
   uint32_t* rowpre;         // [K][nrows]: a row's in-tile exclusive prefix of counted slot k
   int32_t K;                // counted slots

@@ -288,15 +288,15 @@ int fury_trim_workspace(int32_t device);
  * Key "unframe": 0 speculative parallel stream parse (a stream that does not verify -- a payload
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.
- * Nested engines: "nested_decode" 2 row walk (default), 1 level engine, 0 tree tiles;
- * "nested_encode" 4 row-walk measure + encode (default, <= 5 levels), 3 tree-tile measure +
- * row-walk encode, 2 tree-tile measure + row interpreter, 1 interpreter, 0 tree tiles (deeper
- * schemas fall back by themselves); row-walk encode "rowenc_rows" (128 / 256 threads per group),
- * "rowenc_tile" (rows per group, 0 = threads), "rowenc_img" (LDS image bytes);
- * row walk "walk_threads" / "walk_threads_write" (128 / 256), "walk_stage" / "walk_stage_write" /
- * "walk_pool" (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); tree tiles
- * "tree_stage" / "tree_arena" / "tree_threads",
- * "tree_enc_lds" / "tree_measure_lds" / "tree_enc_rows" / "tree_measure_rows"; diagnostics
+ * Nested engines: "nested_decode" 2 row walk (default), 1 level engine (schemas past the walk's
+ * limits use it by themselves); nested encode is the row walk with an explicit-stack continuation
+ * for deep schemas: "rowenc_rows" (128 / 256 threads per group), "rowenc_tile" (rows per group,
+ * 0 = threads), "rowenc_img" (LDS image bytes); row-walk decode "walk_threads" /
+ * "walk_threads_write" (128 / 256), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
+ * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); flat schemas of 17-256
+ * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_threads" /
+ * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (encode phases skipped: outputs
+ * WRONG, timing only),
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
  * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's
  * row bytes the LDS stage must hold, default 95), "var_dec_rows" (forced tile rows, 0 = plan).

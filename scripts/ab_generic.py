@@ -29,9 +29,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=400_000)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--legs", default="0",
-                    help="engines: 0 tree tiles, 1 interpreter encode + level decode (tunings "
-                         "nested_encode / nested_decode)")
+    ap.add_argument("--legs", default="2",
+                    help="decode engines: 1 level engine, 2 row walk (tuning nested_decode), or a "
+                         "JSON list of {tuning key: value} legs")
     args = ap.parse_args()
     import torch
     from fury_amd.beans import beans_to_columns
@@ -66,7 +66,7 @@ def main():
     if args.legs.startswith("["):          # JSON list of {tuning key: value} legs
         legs = json.loads(args.legs)
     else:
-        legs = [{"nested_encode": int(x), "nested_decode": int(x)} for x in args.legs.split(",")]
+        legs = [{"nested_decode": int(x)} for x in args.legs.split(",")]
     ref = None
     for leg in legs:
         for k, v in leg.items():

@@ -1,4 +1,4 @@
-"""Phase times of the tree-tile kernels (tuning "tree_debug"): thread 0 of every workgroup adds the
+"""Phase times of the row-walk decode passes (tuning "tree_debug"): thread 0 of every workgroup adds the
 time between phase marks; printed as the mean microseconds per workgroup per phase (thread 0's
 timeline: barrier waits included).  Depth-3 nested schema of the tests, --rows rows.
 
@@ -13,15 +13,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEC = {0: "walk start (since previous mark)", 1: "level layout (all threads)", 2: "barrier",
-       3: "thread-0 lists + barrier", 4: "expand", 5: "barrier", 6: "scan + bases", 7: "write",
-       8: "kernel tail", 9: "failed walk"}
 WALK_C = {0: "stage + barrier", 1: "walk (thread 0)", 2: "walk tail + scans", 3: "epilogue"}
 WALK_W = {0: "prologue + stage + windows", 1: "walk (thread 0)", 2: "walk tail (barrier)",
           3: "window flush"}
-ENC = {7: "walk start", 0: "R ranges", 1: "stage + layout + lists", 2: "barrier (staged)",
-       3: "sizes (S)", 4: "rows: sizes / containers", 5: "positions + contents",
-       6: "image store", 8: "kernel tail", 9: "failed walk"}
 
 
 def main():
@@ -38,9 +32,6 @@ def main():
     fn = L.fury_internal_tree_debug
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.POINTER(ctypes.c_int64), ctypes.c_int32]
-    for k in ("nested_encode", "nested_decode"):
-        assert L.fury_set_tuning(k.encode(), 0) == 0
-    walk = any(kv.startswith("nested_decode=2") for kv in args.tune)
     for kv in args.tune:
         k, v = kv.split("=")
         assert L.fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
@@ -60,9 +51,7 @@ def main():
     enc.decode_batch(batch)
     assert fn(out, 80) == 0
     res = {}
-    d1, d2 = (WALK_C, WALK_W) if walk else (DEC, DEC)
-    for name, off, cnt_i, names in (("decode_pass1", 0, 64, d1), ("decode_pass2", 16, 65, d2),
-                                    ("measure", 32, 66, ENC), ("encode", 48, 67, ENC)):
+    for name, off, cnt_i, names in (("decode_pass1", 0, 64, WALK_C), ("decode_pass2", 16, 65, WALK_W)):
         wg = max(out[cnt_i], 1)
         res[name] = {"workgroups": out[cnt_i],
                      "us_per_wg": {names.get(i, str(i)): round(out[off + i] / wg / 100.0, 2)

@@ -113,20 +113,20 @@ def test_device_calls_reject_bad_arguments_without_touching_gpu():
     cols = (N.FuryColumn * 5)()
     assert L.fury_row_encode(s.handle, cols, 1, None, None, None) == 1
     deep = T.field("x", T.INT32)
-    for d in range(9):               # 10 levels of nesting: the tree tiles take it
+    for d in range(9):               # 10 levels of nesting: the row walk's explicit stack
         deep = T.struct_field(f"s{d}", [deep])
     assert L.fury_row_encode(Schema([deep]).handle, cols, 1, None, None, None) == 1  # rows null
-    for d in range(9, 70):           # 71 levels: beyond the schema limit (and the tree tiles' 64)
+    for d in range(9, 70):           # 71 levels: beyond the schema limit (64)
         deep = T.struct_field(f"s{d}", [deep])
     with pytest.raises(UnsupportedOperationException):
         Schema([deep])
     wide = [T.struct_field(f"w{i}", [T.field("a", T.INT32), T.field("b", T.INT64)])
-            for i in range(100)]     # > 256 nodes and nested past the row interpreter
-    deep = T.field("x", T.INT32)
+            for i in range(100)]     # > 256 nodes and 10 levels deep: the row walk (round 5;
+    deep = T.field("x", T.INT32)     # round 4 refused it: no engine took both)
     for d in range(9):
         deep = T.struct_field(f"s{d}", [deep])
-    assert L.fury_row_encode(Schema(wide + [deep]).handle, cols, 1, None, None, None) == 2
-    assert "nested" in N.last_error()
+    assert L.fury_row_encode(Schema(wide + [deep]).handle, cols, 1, None, None, None) == 1  # rows null
+    assert "rows is null" in N.last_error()
     assert L.fury_schema_num_nodes(s.handle) == 5 + 1 + 2 + 2
     s2 = Schema(SCHEMAS["struct100"])
     cols2 = (N.FuryColumn * 100)()

@@ -1,7 +1,9 @@
-"""The tile-staged nested decode (tree.hip) against the oracle and against the level engine
-(levels.hip, tuning "nested_decode" = 1) on the same rows: every nested schema shape the tests
-know, the reference's BeanA, collections (ArrayEncoder / MapEncoder batches), and LDS budgets
-small enough to force the walk in halves and rows read from HBM past the stage.  Marked gpu."""
+"""The nested engines against the oracle: the row-walk decode (walk.hip, tuning "nested_decode" =
+2, the default) and the level engine (levels.hip, "nested_decode" = 1) on the same rows, and the
+row-walk encode (rowenc.hip; deep schemas through its explicit-stack continuation): every nested
+schema shape the tests know, the reference's BeanA, collections (ArrayEncoder / MapEncoder
+batches), schemas nested up to the 64-level limit, and LDS budgets small enough to force rows
+read from HBM past the stage.  Marked gpu."""
 from __future__ import annotations
 
 import numpy as np
@@ -32,8 +34,7 @@ def engines():
     """Restores the default engine and LDS budgets after the test."""
     from fury_amd import _native as N
     L = N.lib()
-    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "tree_stage", "tree_arena",
-                                                       "walk_threads", "walk_stage", "walk_pool",
+    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "walk_threads", "walk_stage", "walk_pool",
                                                        "walk_stage_write", "walk_threads_write",
                                                        "walk_out")}
     yield
@@ -75,17 +76,11 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
-    if budget == "tiny":              # 2 KB stage, 2 KB arena: walks in halves, HBM reads
-        _tune("tree_stage", 2048)
-        _tune("tree_arena", 2048)
     ref = oracle.decode(fields, want, want_offs, n)
-    _tune("nested_decode", 0)
-    tree = _decode_plan(enc, batch)
-    assert_columns_equal(fields, tree, ref, n)
-    assert columns_to_beans(fields, tree, n) == beans
     _tune("nested_decode", 1)
     lv = _decode_plan(enc, batch)
-    assert_columns_equal(fields, lv, tree, n)
+    assert_columns_equal(fields, lv, ref, n)
+    assert columns_to_beans(fields, lv, n) == beans
     if budget == "tiny":              # row walk: 1 KB stage (rows from HBM), no bitmap windows
         _tune("walk_stage", 1024)
         _tune("walk_stage_write", 2048)
@@ -101,10 +96,10 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         assert_columns_equal(fields, walk, ref, n)
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [1, 2])
 def test_tree_decode_large_batch(oracle, dev, engines, mode):
-    """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode, tile
-    walk (0) and row walk (2)."""
+    """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode, level
+    engine (1) and row walk (2)."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     from tests.test_device import _nested_beans, _nested_fields
@@ -120,11 +115,11 @@ def test_tree_decode_large_batch(oracle, dev, engines, mode):
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
 def test_collections_both_engines(oracle, dev, engines, mode, kind):
     """ArrayEncoder / MapEncoder batches (root 1 / 2: each entry a top-level BinaryArray /
-    BinaryMap) through the tile engine (mode 0) and the level engine (mode 1)."""
+    BinaryMap) through the level engine (mode 1) and the row walk (mode 2)."""
     from tests.test_device import test_array_encoder_batch_vs_oracle, test_map_encoder_batch_vs_oracle
     _tune("nested_decode", mode)
     if kind == "map":
@@ -133,7 +128,7 @@ def test_collections_both_engines(oracle, dev, engines, mode, kind):
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
 
 
-@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("mode", [1, 2])
 def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     """Tiles whose bytes exceed the stage (rows of very different sizes): the rows past the stage
     are read from HBM, the result is the oracle's."""
@@ -162,39 +157,15 @@ def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
 def enc_engines():
     from fury_amd import _native as N
     L = N.lib()
-    old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_encode", "tree_enc_lds",
-                                                       "tree_measure_lds", "rowenc_rows",
-                                                       "rowenc_img")}
+    old = {k: L.fury_get_tuning(k.encode()) for k in ("rowenc_rows", "rowenc_img", "rowenc_tile")}
     yield
     for k, v in old.items():
         _tune(k, v)
 
 
-@pytest.mark.parametrize("name", ["nested7", "foo", "deep_lists", "struct_chain", "maps", "beana"])
-@pytest.mark.parametrize("budget", ["default", "small", "tiny"])
-def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, name, budget):
-    """The tile-staged nested encode (measure + encode) == the C restatement's bytes and offsets
-    == the row interpreter's (tuning nested_encode = 1); "small" budgets walk tiles in halves,
-    "tiny" ones leave single rows to the interpreter's fixup kernel."""
-    from fury_amd.beans import beans_to_columns
-    from fury_amd.encoder import Encoders, column_to_device
-    fields = _schemas()[name]
-    n = 3001
-    beans = _beans(fields, n, len(name) * 17 + 5)
-    host = beans_to_columns(fields, beans)
-    dcols = [column_to_device(c, dev) for c in host]
-    enc = Encoders.bean(fields, device=dev)
+def _encode_both_ways(oracle, dev, enc, dcols, host, fields, n):
+    """encode_batch (measure + encode) and encode_measured_into == the oracle's bytes / offsets."""
     want, want_offs = oracle.encode(fields, host, n)
-    if budget == "small":             # row walk: 128-row tiles built in 8 KB chunks
-        _tune("tree_enc_lds", 8192)
-        _tune("tree_measure_lds", 4096)
-        _tune("rowenc_rows", 128)
-        _tune("rowenc_img", 8192)
-    elif budget == "tiny":            # row walk: most rows alone exceed the image (HBM direct)
-        _tune("tree_enc_lds", 1024)
-        _tune("tree_measure_lds", 1024)
-        _tune("rowenc_img", 1024)
-    _tune("nested_encode", 0)
     b = enc.encode_batch(dcols, n)
     assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
     assert np.array_equal(b.rows.cpu().numpy(), want)
@@ -204,17 +175,37 @@ def test_tree_encode_equals_oracle_and_interpreter(oracle, dev, enc_engines, nam
     enc.encode_measured_into(dcols, n, rows, offs)
     torch.cuda.synchronize()
     assert np.array_equal(rows[:total].cpu().numpy(), want)
-    for mode in (1, 2, 3, 4):         # interpreter; tree measure + interpreter / row-walk encode;
-        _tune("nested_encode", mode)  # row walk (measure + encode)
-        b1 = enc.encode_batch(dcols, n)
-        assert np.array_equal(b1.row_offsets.cpu().numpy(), want_offs)
-        assert np.array_equal(b1.rows.cpu().numpy(), want)
+    return b, want, want_offs
 
 
-@pytest.mark.parametrize("mode", [0, 2, 3, 4])
-def test_tree_encode_capacity(oracle, dev, enc_engines, mode):
+@pytest.mark.parametrize("name", ["nested7", "foo", "deep_lists", "struct_chain", "maps", "beana"])
+@pytest.mark.parametrize("budget", ["default", "small", "tiny"])
+def test_tree_encode_equals_oracle(oracle, dev, enc_engines, name, budget):
+    """The row-walk nested encode (measure + encode) == the C restatement's bytes and offsets;
+    "small" budgets build 128-row tiles in 8 KB chunks, "tiny" ones leave most rows to the
+    HBM-direct path (a row alone past the image)."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _schemas()[name]
+    n = 3001
+    beans = _beans(fields, n, len(name) * 17 + 5)
+    host = beans_to_columns(fields, beans)
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    if budget == "small":
+        _tune("rowenc_rows", 128)
+        _tune("rowenc_img", 8192)
+    elif budget == "tiny":
+        _tune("rowenc_img", 1024)
+        _tune("rowenc_tile", 64)
+    _encode_both_ways(oracle, dev, enc, dcols, host, fields, n)
+
+
+@pytest.mark.parametrize("img", [0, 1024])
+def test_tree_encode_capacity(oracle, dev, enc_engines, img):
     """encode_measured with a short buffer: offsets complete, no byte at or past the capacity
-    written (guard bytes intact), the bytes before it equal to the oracle's; every encode engine."""
+    written (guard bytes intact), the bytes before it equal to the oracle's; LDS-built rows and
+    HBM-direct rows (img = 1024)."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     fields = _schemas()["nested7"]
@@ -223,7 +214,8 @@ def test_tree_encode_capacity(oracle, dev, enc_engines, mode):
     dcols = [column_to_device(c, dev) for c in host]
     enc = Encoders.bean(fields, device=dev)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_encode", mode)
+    if img:
+        _tune("rowenc_img", img)
     cap = (int(want_offs[n // 2]) + 13) & ~7
     rows = torch.full((cap + 4096,), 0xAB, dtype=torch.uint8, device=dev)
     offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
@@ -241,7 +233,7 @@ def test_tree_encode_capacity(oracle, dev, enc_engines, mode):
     assert np.array_equal(got[:want_offs[full]], want[:want_offs[full]])
 
 
-# ---- schemas nested past the row interpreter (depth-9 and beyond) -----------
+# ---- schemas nested past the inlined walk (depth 9 .. 64) -------------
 def _deep_fields(levels):
     """`levels` levels of nesting: a struct chain with a LIST every third level and one MAP, so a
     row stays small (at most ~3 entries per collection)."""
@@ -268,28 +260,24 @@ def _schema_levels(fields):
     return max(lv(f) for f in fields)
 
 
-@pytest.mark.parametrize("levels", [9, 12, 20])
-@pytest.mark.parametrize("dec_mode", [0, 1, 2])
+@pytest.mark.parametrize("levels", [6, 9, 12, 20, 64])
+@pytest.mark.parametrize("dec_mode", [1, 2])
 def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_mode):
-    """Depth 9 / 12 / 20 schemas: the encode takes the tree tiles by itself (the row interpreter
-    stops at kGenMaxDepth levels), both decode engines read the rows back; bytes, offsets and
-    columns == the oracle's."""
+    """Depth 6 .. 64 schemas (64 = the schema limit): the row-walk encode continues past its
+    inlined levels on an explicit stack, both decode settings read the rows back (the row walk
+    hands schemas past kWalkMaxDepth to the level engine by itself); bytes, offsets and columns ==
+    the oracle's."""
     from fury_amd.beans import beans_to_columns, columns_to_beans
     from fury_amd.encoder import Encoders, column_to_device
     fields = _deep_fields(levels)
     assert _schema_levels(fields) == levels
-    n = 2500
+    n = 2500 if levels < 64 else 600
     beans = _beans(fields, n, levels * 7 + dec_mode)
     host = beans_to_columns(fields, beans)
     dcols = [column_to_device(c, dev) for c in host]
     enc = Encoders.bean(fields, device=dev)
     assert enc.nested
-    want, want_offs = oracle.encode(fields, host, n)
-    for mode in (4, 3, 2, 1, 0):      # deep schemas ignore "nested_encode": always the tree tiles
-        _tune("nested_encode", mode)
-        b = enc.encode_batch(dcols, n)
-        assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
-        assert np.array_equal(b.rows.cpu().numpy(), want)
+    b, want, want_offs = _encode_both_ways(oracle, dev, enc, dcols, host, fields, n)
     _tune("nested_decode", dec_mode)
     ref = oracle.decode(fields, want, want_offs, n)
     got = _decode_plan(enc, b)
@@ -297,58 +285,59 @@ def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_m
     assert columns_to_beans(fields, got, n) == beans
 
 
-@pytest.mark.parametrize("levels", [2, 3, 4, 5, 6, 7])
-@pytest.mark.parametrize("mode", [3, 4])
-def test_row_walk_encode_depths(oracle, dev, enc_engines, levels, mode):
-    """The row-walk encode (rowenc.hip, one inlined instance per depth up to 5 levels; 6 and 7
-    fall back to the interpreter) == the oracle's bytes and offsets."""
+@pytest.mark.parametrize("levels", [7, 12])
+@pytest.mark.parametrize("img", [0, 2048])
+def test_deep_schema_large_rows(oracle, dev, enc_engines, levels, img):
+    """Deep rows of several KB (long lists at every LIST level): rows past the LDS image take
+    the HBM-direct path of the explicit-stack walk, == the oracle's bytes."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = _deep_fields(levels)
+    n = 700 if levels < 12 else 200
+    rng = np.random.default_rng(levels + img)
+
+    def big(f):
+        if f.type_id == T.LIST:
+            return [big(f.children[0]) for _ in range(int(rng.integers(0, 7)))]
+        if f.type_id == T.MAP:
+            return [(f"k{i}", big(f.children[1])) for i in range(int(rng.integers(0, 4)))]
+        if f.type_id == T.STRUCT:
+            return {c.name: big(c) for c in f.children}
+        if f.type_id == T.STRING:
+            return "s" * int(rng.integers(0, 30))
+        return int(rng.integers(-1000, 1000))
+    beans = [{"id": i, fields[1].name: big(fields[1]), "tail": list(range(i % 20))} for i in range(n)]
+    host = beans_to_columns(fields, beans)
+    dcols = [column_to_device(c, dev) for c in host]
+    enc = Encoders.bean(fields, device=dev)
+    if img:
+        _tune("rowenc_img", img)
+    _, _, want_offs = _encode_both_ways(oracle, dev, enc, dcols, host, fields, n)
+    assert int(np.diff(want_offs).max()) > 2048     # some rows past the small image
+
+
+@pytest.mark.parametrize("levels", [2, 3, 4, 5, 6, 7, 9])
+def test_row_walk_encode_depths(oracle, dev, enc_engines, levels):
+    """The row-walk encode (rowenc.hip: one inlined instance per depth up to 5 levels, the
+    explicit-stack instance past them) == the oracle's bytes and offsets."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     fields = _deep_fields(levels)
     assert _schema_levels(fields) == levels
     n = 2100
-    host = beans_to_columns(fields, _beans(fields, n, levels * 11 + mode))
+    host = beans_to_columns(fields, _beans(fields, n, levels * 11))
     enc = Encoders.bean(fields, device=dev)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_encode", mode)
     b = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     assert np.array_equal(b.row_offsets.cpu().numpy(), want_offs)
     assert np.array_equal(b.rows.cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
-def test_collections_encode_engines(oracle, dev, enc_engines, mode, kind):
-    """ArrayEncoder / MapEncoder batches (root 1 / 2) encoded by every engine == the oracle."""
+def test_collections_encode(oracle, dev, enc_engines, kind):
+    """ArrayEncoder / MapEncoder batches (root 1 / 2) encoded by the row walk == the oracle."""
     from tests.test_device import test_array_encoder_batch_vs_oracle, test_map_encoder_batch_vs_oracle
-    _tune("nested_encode", mode)
     if kind == "map":
         test_map_encoder_batch_vs_oracle(oracle, dev)
     else:
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
-
-
-def test_deep_schema_row_too_large_for_chip_raises(oracle, dev, enc_engines):
-    """A depth-10 row larger than the (shrunk) on-chip budget has no interpreter fallback: the call
-    reports UnsupportedOperationException naming the row instead of writing partial bytes."""
-    from fury_amd.beans import beans_to_columns
-    from fury_amd.encoder import Encoders, UnsupportedOperationException, column_to_device
-    fields = _deep_fields(10)
-    n = 600
-    beans = _beans(fields, n, 3)
-    beans[123]["tail"] = list(range(400))            # ~1 KB row
-    host = beans_to_columns(fields, beans)
-    dcols = [column_to_device(c, dev) for c in host]
-    enc = Encoders.bean(fields, device=dev)
-    from fury_amd import _native as N
-    old = {k: N.lib().fury_get_tuning(k.encode()) for k in ("tree_enc_lds", "tree_measure_lds")}
-    _tune("tree_enc_lds", 1024)
-    _tune("tree_measure_lds", 1024)
-    with pytest.raises(UnsupportedOperationException, match="nested deeper"):
-        enc.encode_batch(dcols, n)
-        enc.device_status()                           # the encode kernel's report (asynchronous)
-    for k, v in old.items():
-        _tune(k, v)
-    b = enc.encode_batch(dcols, n)                    # the stream's error slot is clean again
-    want, _ = oracle.encode(fields, host, n)
-    assert np.array_equal(b.rows.cpu().numpy(), want)
