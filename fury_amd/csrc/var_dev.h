@@ -824,25 +824,10 @@ __device__ __forceinline__ int64_t reg_row_size(const VarArgs& a, const uint64_t
   return sz;
 }
 
-// tbase == nullptr: rows at the given offs.  tbase != nullptr (fury_row_encode_measured): tbase[b]
-// = the exclusive prefix of the tiles' byte totals (measure_tiles + scan); each tile scans its own
-// rows' sizes and writes their final offs -- no per-row sizes pass, no prefix-add pass.
+// Per-row inputs of row r, every column: K independent loads (values, offset pairs, validity).
 template <int K, int M>
-__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* __restrict__ offs,
-                                                           uint8_t* __restrict__ rows, int64_t cap,
-                                                           const int64_t* __restrict__ tbase) {
-  __shared__ __attribute__((aligned(16))) uint64_t img[kRegImg / 8];
-  __shared__ int64_t tmp[kEncRows / 64];
-  const int tid = threadIdx.x;
-  const int R = a.tile_rows;
-  const int64_t b = blockIdx.x;
-  const int64_t r0 = b * R;
-  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t r = live ? r0 + tid : r0;
-  // per-row inputs of every column: one batch of independent loads
-  uint64_t v[K];
-  uint64_t valid = 0;
+__device__ __forceinline__ void reg_load_meta(const VarArgs& a, int64_t r, uint64_t* v, uint64_t& valid) {
+  valid = 0;
 #pragma unroll
   for (int k = 0; k < K; k++) {
     v[k] = 0;
@@ -863,6 +848,28 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* _
     }
     v[k] = x;
   }
+}
+
+// tbase == nullptr: rows at the given offs.  tbase != nullptr (fury_row_encode_measured): tbase[b]
+// = the exclusive prefix of the tiles' byte totals (measure_tiles + scan); each tile scans its own
+// rows' sizes and writes their final offs -- no per-row sizes pass, no prefix-add pass.
+template <int K, int M>
+__global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* __restrict__ offs,
+                                                           uint8_t* __restrict__ rows, int64_t cap,
+                                                           const int64_t* __restrict__ tbase) {
+  __shared__ __attribute__((aligned(16))) uint64_t img[kRegImg / 8];
+  __shared__ int64_t tmp[kEncRows / 64];
+  const int tid = threadIdx.x;
+  const int R = a.tile_rows;
+  const int64_t b = blockIdx.x;
+  const int64_t r0 = b * R;
+  const int nr = static_cast<int>(min<int64_t>(R, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t r = live ? r0 + tid : r0;
+  // per-row inputs of every column: one batch of independent loads
+  uint64_t v[K];
+  uint64_t valid;
+  reg_load_meta<K, M>(a, r, v, valid);
   int64_t base, bytes, ex, sz;
   if (tbase) {
     sz = live ? reg_row_size<K, M>(a, v, valid) : 0;

@@ -1,7 +1,9 @@
 // walk.hip — nested decode with a thread per ROW ("row walk"): the default engine of
 // fury_decode_prepare / fury_decode_execute for schemas of up to kWalkMaxDepth levels and
-// kWalkMaxK counted nodes (tree.hip builds the plan and falls back to the tile-level walk or the
-// level engine beyond that).
+// kWalkMaxK counted nodes (tree.hip builds the plan; the level engine takes the rest).  A deeper
+// walk on an explicit per-lane stack was built and measured 2.5-6.5x slower than the level
+// engine on depth 6-20 schemas (profiles/r05_deep_walk_vs_levels.jsonl), so the level engine is
+// the fallback.
 //
 // Reference semantics are tree.hip's (its header): the getters of BinaryRow / BinaryArray /
 // BinaryMap as the generated fromRow and ArrowWriter walk them (FMT/encoder/
@@ -162,7 +164,31 @@ struct WCtx {
   int64_t row;
   int64_t wave_row;         // the row of lane 0 of this wave (ballots of row-aligned nodes)
   int tid;
+  // count pass: items (fields, elements, keys, values) the row's walk may still visit, 2 x its
+  // bytes + 64.  A row the encoder wrote holds every item in its own bytes (an 8-B slot, or >= 1 B
+  // per fixed-width element), so only a malformed row whose slots alias other bytes runs out --
+  // its walk would otherwise grow with the product of the aliased counts -- and is reported (the
+  // prepare fails, so the write pass, which visits the same items, never meets such a row).
+  mutable int32_t left;
 };
+
+// Charges a container's items to the row's budget (count pass): false, and the row reported, when
+// it is spent.  (Null structs are free: their fields read nothing.)  The level engine (deeper
+// schemas) materialises every level instead: aliased counts there end in an allocation failure.
+template <bool W>
+__device__ __forceinline__ bool wcharge(const WCtx& c, int ty, bool valid, uint32_t m) {
+  if constexpr (W) {
+    return true;
+  } else {
+    const int64_t items = ty == FURY_TYPE_MAP ? 2 * static_cast<int64_t>(m)
+                          : (ty == FURY_TYPE_STRUCT && !valid) ? 0 : m;
+    const int64_t left = static_cast<int64_t>(c.left) - items;
+    c.left = static_cast<int32_t>(max<int64_t>(left, -1));
+    if (left >= 0) return true;
+    if (left + items >= 0) raise_oob(c.a->err, c.row);
+    return false;
+  }
+}
 
 // Bit `e` of node n's validity (which = 0) / BOOL values (which = 1).  Row-aligned nodes (e = the
 // row) take a wave ballot: every active lane calls this at the same node, pred or not.
@@ -287,6 +313,76 @@ __device__ __forceinline__ void wscalar(const WCtx& c, CTNode& N, int n, int64_t
   if (N.validity) wbit(c, N, n, 0, N.validity, e, !nul);
 }
 
+// The entry's own part of entry e of node n (non-scalar): its bounds check, validity bit, cursor
+// of a counted slot, Arrow offset, payload / DECIMAL value.  Returns whether the value is valid;
+// *m = the items a container's walk visits below it (STRUCT: fields, LIST / MAP: elements, 0 for
+// a leaf) and *cs = a LIST / MAP's first element entry.
+template <bool W>
+__device__ __forceinline__ bool wentry(const WCtx& c, CTNode& N, int n, int64_t e, bool nul,
+                                       uint64_t slot, int64_t cont, int64_t vpos, bool top,
+                                       int64_t* ppos, uint32_t* pm, int64_t* pcs) {
+  const TreeArgs& a = *c.a;
+  const Rows& R = *c.R;
+  const int ty = N.type;
+  int64_t pos = kNullPos;
+  uint32_t cnt = 0;
+  if (!nul) {
+    int32_t size = 0;
+    if (vpos >= 0) {
+      pos = vpos;
+    } else {
+      pos = cont + static_cast<int32_t>(slot >> 32);
+      size = static_cast<int32_t>(slot);
+    }
+    if (!tcheck(a, R, N, pos, size, c.total, &cnt, static_cast<uint64_t>(c.row))) pos = kNullPos;
+  }
+  const bool valid = pos >= 0;
+  *ppos = pos;
+  *pm = 0;
+  *pcs = 0;
+  if (W && !top && N.validity && !(a.skip & 2)) wbit(c, N, n, 0, N.validity, e, valid);
+  if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
+    uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+    const uint32_t c0 = *cu;
+    *cu = c0 + cnt;
+    if (W) {
+      const int64_t bp = c.sh->kb[N.k] + c0;
+      if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(bp + cnt));
+      if (valid && N.values && !(a.skip & 1)) wput_bytes(c, N, n, bp, pos, cnt);
+    }
+    return valid;
+  }
+  if (ty == FURY_TYPE_DECIMAL) {
+    if (W && N.values) {
+      const uint64_t lo = valid ? rd8(R, pos) : 0, hi = valid ? rd8(R, pos + 8) : 0;
+      const int32_t o = N.ek >= 0 ? wwin(c, 0, n) : -1;
+      if (o >= 0) {
+        const auto d = lds_ptr<uint64_t>(c.sh->opool + o + 16 * (e - c.sh->oe[n]));
+        d[0] = lo;
+        d[1] = hi;
+      } else {
+        const auto d = gl(reinterpret_cast<uint64_t*>(N.values + 16 * e));
+        d[0] = lo;
+        d[1] = hi;
+      }
+    }
+    return valid;
+  }
+  if (ty == FURY_TYPE_STRUCT) {
+    *pm = (W || valid) ? static_cast<uint32_t>(N.num_children) : 0u;
+  } else if (ty == FURY_TYPE_LIST || ty == FURY_TYPE_MAP) {
+    uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+    const uint32_t c0 = *cu;
+    *pm = cnt;
+    *cu = c0 + cnt;
+    if (W) {
+      *pcs = c.sh->kb[N.k] + c0;
+      if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(*pcs + cnt));
+    }
+  }
+  return valid;
+}
+
 // Entry e of node n (non-scalar; scalars go through wscalar): slot word `slot` (loaded by the
 // caller together with the null bit: one round trip) in a container that starts at cont (vpos >=
 // 0: the value is AT vpos -- a collection batch's top-level entry).
@@ -305,64 +401,13 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
     const Rows& R = *c.R;
     CTNode& N = tn(a, n);
     const int ty = N.type;
-    int64_t pos = kNullPos;
-    uint32_t cnt = 0;
-    if (!nul) {
-      int32_t size = 0;
-      if (vpos >= 0) {
-        pos = vpos;
-      } else {
-        pos = cont + static_cast<int32_t>(slot >> 32);
-        size = static_cast<int32_t>(slot);
-      }
-      if (!tcheck(a, R, N, pos, size, c.total, &cnt, static_cast<uint64_t>(c.row))) pos = kNullPos;
-    }
-    const bool valid = pos >= 0;
-    if (W && D > 0 && N.validity && !(a.skip & 2)) wbit(c, N, n, 0, N.validity, e, valid);
-    if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
-      uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
-      const uint32_t c0 = *cu;
-      *cu = c0 + cnt;
-      if (W) {
-        const int64_t bp = c.sh->kb[N.k] + c0;
-        if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(bp + cnt));
-        if (valid && N.values && !(a.skip & 1)) wput_bytes(c, N, n, bp, pos, cnt);
-      }
-      return valid;
-    }
-    if (ty == FURY_TYPE_DECIMAL) {
-      if (W && N.values) {
-        const uint64_t lo = valid ? rd8(R, pos) : 0, hi = valid ? rd8(R, pos + 8) : 0;
-        const int32_t o = N.ek >= 0 ? wwin(c, 0, n) : -1;
-        if (o >= 0) {
-          const auto d = lds_ptr<uint64_t>(c.sh->opool + o + 16 * (e - c.sh->oe[n]));
-          d[0] = lo;
-          d[1] = hi;
-        } else {
-          const auto d = gl(reinterpret_cast<uint64_t*>(N.values + 16 * e));
-          d[0] = lo;
-          d[1] = hi;
-        }
-      }
-      return valid;
-    }
+    int64_t pos;
+    uint32_t m;
+    int64_t cs;
+    const bool valid = wentry<W>(c, N, n, e, nul, slot, cont, vpos, D == 0, &pos, &m, &cs);
     const bool strc = ty == FURY_TYPE_STRUCT;
     if (!strc && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return valid;
-    // children: STRUCT -> its fields at entry e; LIST / MAP -> m elements from entry cs
-    uint32_t m = 0;
-    int64_t cs = 0;
-    if (strc) {
-      m = (W || valid) ? static_cast<uint32_t>(N.num_children) : 0u;
-    } else {
-      uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
-      const uint32_t c0 = *cu;
-      m = cnt;
-      *cu = c0 + m;
-      if (W) {
-        cs = c.sh->kb[N.k] + c0;
-        if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(cs + m));
-      }
-    }
+    if (!wcharge<W>(c, ty, valid, m)) m = 0;
     const int64_t hb = tbm(strc ? N.num_children : static_cast<int64_t>(m));
     const int sides = ty == FURY_TYPE_MAP ? 2 : 1;
     for (int sd = 0; sd < sides; sd++) {
@@ -412,6 +457,7 @@ __device__ __forceinline__ void walk_row(const WCtx& c, bool live) {
   const TreeArgs& a = *c.a;
   const Rows& R = *c.R;
   const int64_t base = live ? gl(a.offs)[c.row] : 0;
+  if (!W) c.left = live ? static_cast<int32_t>(min<int64_t>(2 * (gl(a.offs)[c.row + 1] - base) + 64, 1 << 30)) : 0;
   if (a.root) {                                  // collection batch: the entry IS the value
     bool valid = false;
     if (live) valid = wvalue<0, W, MD>(c, 0, c.row, false, 0, 0, base);
@@ -499,7 +545,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
   __syncthreads();
   clk.mark(0);
-  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid};
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0};
   walk_row<false, MD>(c, live);
   clk.mark(1);
   // in-tile exclusive prefix of every slot over the rows (row = thread)
@@ -624,7 +670,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   for (uint32_t i = tid; i < used; i += NT) sh.pool[i] = 0;
   __syncthreads();
   clk.mark(0);
-  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid};
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0};
   walk_row<true, MD>(c, live);
   clk.mark(1);
   __syncthreads();

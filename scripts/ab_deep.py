@@ -1,0 +1,76 @@
+"""Deep-schema decode A/B: nested_decode 2 against 1 on the tests' _deep_fields(levels) schema.  A
+base batch of --base beans is encoded once and its rows tiled on the device to --rows rows.
+(profiles/r05_deep_walk_vs_levels.jsonl: a build whose row walk continued past 5 levels on an
+explicit stack -- mode 2 -- against the level engine -- mode 1; that walk was removed.)
+
+    python scripts/ab_deep.py --levels 9,12,20 --rows 1000000
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--levels", default="9,12,20")
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--base", type=int, default=20_000)
+    ap.add_argument("--iters", type=int, default=3)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from fury_amd import _native as N
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, RowBatch, column_to_device
+    from tests.test_tree import _beans, _deep_fields
+    dev = torch.device("cuda:0")
+    L = N.lib()
+    for levels in [int(x) for x in args.levels.split(",")]:
+        fields = _deep_fields(levels)
+        beans = _beans(fields, args.base, levels)
+        enc = Encoders.bean(fields, device=dev)
+        b0 = enc.encode_batch([column_to_device(c, dev) for c in beans_to_columns(fields, beans)],
+                              args.base)
+        reps = max(1, args.rows // args.base)
+        n = reps * args.base
+        tot = int(b0.row_offsets[-1].item())
+        rows = b0.rows.repeat(reps)
+        offs = torch.cat([b0.row_offsets[:-1] + i * tot for i in range(reps)] +
+                         [torch.tensor([reps * tot], dtype=torch.int64, device=dev)])
+        batch = RowBatch(rows, offs, n, enc.schema_hash)
+        res = {"levels": levels, "rows": n, "row_bytes": reps * tot}
+        ref = None
+        for mode in (2, 1):
+            assert L.fury_set_tuning(b"nested_decode", mode) == 0
+            out = enc.decode_batch(batch)
+            torch.cuda.synchronize()
+            got = [x for c in out for x in (c.values, c.validity, c.offsets)]
+            if ref is None:
+                ref = got
+            else:
+                res["equal"] = all((x is None and y is None) or (
+                    x is not None and y is not None and x.shape == y.shape and
+                    torch.equal(x[:max(x.numel() - 16, 0)], y[:max(y.numel() - 16, 0)]))
+                    for x, y in zip(ref, got))
+            xs = []
+            for _ in range(3):
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(args.iters):
+                    enc.decode_batch(batch)
+                b.record()
+                torch.cuda.synchronize()
+                xs.append(a.elapsed_time(b) / args.iters)
+            res[f"decode_ms_mode{mode}"] = round(statistics.median(xs), 3)
+        assert L.fury_set_tuning(b"nested_decode", 2) == 0
+        print(json.dumps(res), flush=True)
+    del np
+
+
+if __name__ == "__main__":
+    main()

@@ -68,7 +68,11 @@ def main():
     else:
         legs = [{"nested_decode": int(x)} for x in args.legs.split(",")]
     ref = None
+    keys = {k for leg in legs for k in leg}
+    defaults = {k: N.lib().fury_get_tuning(k.encode()) for k in keys}
     for leg in legs:
+        for k, v in defaults.items():         # every leg starts from the defaults
+            assert N.lib().fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
         for k, v in leg.items():
             assert N.lib().fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
         b2 = enc.encode_batch(cols, n)

@@ -341,3 +341,42 @@ def test_collections_encode(oracle, dev, enc_engines, kind):
         test_map_encoder_batch_vs_oracle(oracle, dev)
     else:
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
+
+
+@pytest.mark.parametrize("levels", [4, 5, 9])
+def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
+    """Rows of a nested schema with random bytes overwritten: the row walk (nested_decode 2, up to
+    5 levels; deeper schemas take the level engine either way) and the level engine (1) finish --
+    no walk through aliased slots grows without bound (the walk's item budget) -- decode to the
+    same columns when both succeed, read nothing outside the batch (bounds checks shared: tcheck)
+    and leave no error behind for the intact rows."""
+    from fury_amd.encoder import FuryDeviceError, IndexOutOfBoundsException
+    from fury_amd.encoder import UnsupportedOperationException, column_to_host
+    from tests.test_bounds import _batch, _nested_batch
+    fields = _deep_fields(levels)
+    n = 600
+    enc, rows, offs = _nested_batch(oracle, fields, n, levels, dev)
+    rng = np.random.default_rng(levels)
+    for trial in range(4):
+        bad = rows.copy()
+        lo = int(offs[n // 2])
+        pos = rng.integers(lo, len(bad), 24)
+        bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
+        res = {}
+        for mode in (2, 1):
+            _tune("nested_decode", mode)
+            try:
+                res[mode] = [column_to_host(c) for c in enc.decode_batch(_batch(enc, bad, offs, n, dev))]
+            except (IndexOutOfBoundsException, UnsupportedOperationException) as e:
+                res[mode] = type(e)
+            except FuryDeviceError as e:       # the level engine materialises every level:
+                assert mode == 1, e            # aliased counts can exhaust device memory
+                res[mode] = type(e)
+        # a raise need not agree: the walk also reports rows whose aliased slots would make it
+        # visit more items than the row has bytes (its item budget), which the level engine may
+        # decode; two decodes agree
+        if not isinstance(res[2], type) and not isinstance(res[1], type):
+            assert_columns_equal(fields, res[2], res[1], n)
+    _tune("nested_decode", 2)
+    good = [column_to_host(c) for c in enc.decode_batch(_batch(enc, rows, offs, n, dev))]
+    assert_columns_equal(fields, good, oracle.decode(fields, rows, offs, n), n)
