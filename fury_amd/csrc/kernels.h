@@ -152,52 +152,6 @@ __device__ __forceinline__ uint64_t err_where_entry(int node, int64_t entry) {
   return (1ull << 63) | (static_cast<uint64_t>(node) << 40) | static_cast<uint64_t>(entry);
 }
 
-// Exclusive block scans of K parallel sequences over the slots [0, m) by an NT-thread workgroup
-// (thread t owns a contiguous run): f(j, k) is slot j's value in sequence k; ex[k * (m + 1) + j]
-// receives the exclusive prefix and ex[k * (m + 1) + m] the total.  f is evaluated twice per
-// slot; wtot holds K * NT / 64 words.  Two barriers.  (Layouts of per-node arrays in the
-// tree-tile kernels: one parallel pass instead of a serial walk over the schema's nodes.)
-template <int NT, int K, class F>
-__device__ void block_scan_k(int m, F f, uint32_t* ex, uint32_t* wtot) {
-  constexpr int NW = NT / 64;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int per = (m + NT - 1) / NT;
-  const int b = min(tid * per, m), e = min(b + per, m);
-  uint32_t sum[K], inc[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    sum[k] = 0;
-    for (int j = b; j < e; j++) sum[k] += f(j, k);
-    uint32_t x = sum[k];
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(x, d, 64);
-      if (lane >= d) x += y;
-    }
-    inc[k] = x;
-    if (lane == 63) wtot[k * NW + wave] = x;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      const uint32_t v = wtot[k * NW + w];
-      pre += w < wave ? v : 0;
-      tot += v;
-    }
-    uint32_t run = pre + inc[k] - sum[k];
-    uint32_t* o = ex + k * (m + 1);
-    for (int j = b; j < e; j++) {
-      o[j] = run;
-      run += f(j, k);
-    }
-    if (tid == 0) o[m] = tot;
-  }
-  __syncthreads();
-}
-
 // Copies a host column table to device memory on `stream` (stream-ordered: through a pinned
 // staging ring, no host synchronisation); the table is freed stream-ordered when the holder goes.
 struct DeviceTable {

@@ -337,8 +337,8 @@ int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, co
 
 }  // namespace fury
 
-// Diagnostics, not part of include/fury_row.h: copies the tree-tile phase accumulators (80 words:
-// decode pass 1 [0, 16), pass 2 [16, 32), measure [32, 48), encode [48, 64) in 10 ns ticks, then
+// Diagnostics, not part of include/fury_row.h: copies the row-walk phase accumulators (80 words:
+// count pass [0, 16), write pass [16, 32) in 10 ns ticks, then
 // workgroup counts [64, 68)) to out and zeroes them.  Synchronises the device.
 extern "C" int fury_internal_tree_debug(int64_t* out, int32_t n) {
   uint64_t* d = fury::tree_debug_buffer();

@@ -394,37 +394,5 @@ __device__ __forceinline__ bool tcheck(const TreeArgs& a, const Rows& R, CTNode&
   return true;
 }
 
-// Owner of child entry q of a LIST / MAP node whose in-tile exclusive prefix is P[0, m]: the last
-// e with P[e] <= q.
-__device__ __forceinline__ uint32_t towner(const uint32_t* P, uint32_t m, uint32_t q) {
-  uint32_t lo = 0, hi = m;                  // P[lo] <= q < P[hi] (P[m] = total > q)
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (P[mid] <= q) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
-// ORs bit `gi` of a bitmap for every lane with pred: one ballot (<= 3 atomics) when the wave's
-// lanes are consecutive entries of one node (gi0 = lane 0's entry), else per-lane atomics.
-__device__ __forceinline__ void tbits(uint8_t* bits, bool uni, int64_t gi0, int64_t gi, bool pred) {
-  if (uni) {
-    tballot_or(bits, gi0, pred);
-  } else if (pred) {
-    __hip_atomic_fetch_or(gl(reinterpret_cast<uint32_t*>(bits)) + (gi >> 5), 1u << (gi & 31),
-                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// Item i of a level's flattened (node, entry) list: k = the list slot with cum[k] <= i < cum[k+1].
-__device__ __forceinline__ int titem(const uint32_t* cum, int nk, uint32_t i) {
-  int lo = 0, hi = nk;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (cum[mid] <= i) lo = mid; else hi = mid;
-  }
-  return lo;
-}
-
 }  // namespace
 }  // namespace fury

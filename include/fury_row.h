@@ -246,14 +246,14 @@ int fury_decode_execute(fury_decode_plan* plan, fury_column* columns, int32_t ar
 void fury_decode_plan_destroy(fury_decode_plan* plan);
 
 /* ---- asynchronous device errors (no reference equivalent) ------------------------------- */
-/* Decode kernels (and the deep-schema encode) report what they find ASYNCHRONOUSLY: fury_row_decode,
+/* Decode kernels report what they find ASYNCHRONOUSLY: fury_row_decode,
  * fury_rows_to_arrow and fury_decode_execute return before their kernels run, so a malformed
  * batch is reported later --
  *   FURY_ERR_OUT_OF_BOUNDS  a variable-length value, array or map header outside the batch's row
- *                           bytes (MemoryBuffer's IndexOutOfBoundsException);
+ *                           bytes (MemoryBuffer's IndexOutOfBoundsException), or a nested row
+ *                           whose slots alias other bytes so that its walk would visit more
+ *                           items than twice its bytes (found by fury_decode_prepare);
  *   FURY_ERR_UNSUPPORTED    map key / value arrays of different lengths (BinaryMap.pointTo);
- *                           or (encode, fury_row_encode / _measured) a row of a schema nested
- *                           deeper than 7 levels too large to assemble on chip;
  *   FURY_ERR_DEVICE         a decoupled look-back that gave up waiting (by construction -- a
  *                           look-back computes a silent predecessor's aggregate itself -- never
  *                           raised on working hardware).
