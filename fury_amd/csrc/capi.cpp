@@ -931,8 +931,8 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "walk_threads_write") {
-    if (value != 128 && value != 256)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads_write: 128 or 256");
+    if (value != 128 && value != 256 && value != 512)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads_write: 128, 256 or 512 (512: no write stage)");
     set_walk_tuning(6, static_cast<uint32_t>(value));
     return FURY_OK;
   }

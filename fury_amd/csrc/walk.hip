@@ -586,7 +586,10 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
 }
 
 // Pass 2: the walk again, writing every output at its final position.
-template <int NT, int MD>
+// STG false (no write stage, the default): the reader's window is the literal empty range, so every
+// staged-or-HBM branch of the inlined reads folds to the HBM load at compile time (smaller code,
+// fewer live scalars).
+template <int NT, int MD, bool STG>
 __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
   const WShared sh = walk_shared(wsm, a, NT, true);
@@ -652,8 +655,9 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
     }
     if (tid == 0) sh.oreq[3 * nn] = 0;
   }
-  const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
-  if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
+  Rows R{a.rows, sh.stg, 0, 0, 0};
+  if constexpr (STG) R = walk_stage<NT>(a, sh.stg, r0, nr, total);
+  if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, STG ? R.hi : int64_t(0));
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
   if (a.out_cap) {
@@ -731,8 +735,11 @@ int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
   // instances per schema depth (a level of the inlined walk keeps ~30 VGPRs live)
 #define FURY_WALK(MD)                                                                        \
   if (a.nlevels <= MD) {                                                                     \
-    if (nt == 128) write ? go(walk_write_kernel<128, MD>) : go(walk_count_kernel<128, MD>);  \
-    else write ? go(walk_write_kernel<256, MD>) : go(walk_count_kernel<256, MD>);            \
+    if (!write) nt == 128 ? go(walk_count_kernel<128, MD>) : go(walk_count_kernel<256, MD>); \
+    else if (a.stage_cap)                                                                    \
+      nt == 128 ? go(walk_write_kernel<128, MD, true>) : go(walk_write_kernel<256, MD, true>); \
+    else if (nt == 512) go(walk_write_kernel<512, MD, false>);                               \
+    else nt == 128 ? go(walk_write_kernel<128, MD, false>) : go(walk_write_kernel<256, MD, false>); \
     return check_hip(hipGetLastError(), "walk decode launch");                               \
   }
   FURY_WALK(2)

@@ -89,8 +89,11 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         _tune("walk_threads_write", 128)
     _tune("nested_decode", 2)
     # output windows of the write pass (walk_out bytes): off, too small for most nodes (mixed
-    # LDS / HBM stores), the default
-    for wo in ((0, 256, 16384) if budget == "tiny" else (0, 16384)):
+    # LDS / HBM stores), the default; write tiles of 512 (default, unstaged) and 256 rows
+    legs = ([(128, 0), (128, 256), (128, 16384)] if budget == "tiny"
+            else [(512, 0), (512, 24576), (256, 16384)])
+    for tw, wo in legs:
+        _tune("walk_threads_write", tw)
         _tune("walk_out", wo)
         walk = _decode_plan(enc, batch)
         assert_columns_equal(fields, walk, ref, n)
