@@ -975,7 +975,8 @@ int fury_set_tuning(const char* key, int32_t value) {
     return set_tree_debug(value) ? set_error(FURY_ERR_DEVICE, "tree_debug buffer") : FURY_OK;
   }
   if (std::string(key) == "rowenc_rows") {
-    if (value != 128 && value != 256) return set_error(FURY_ERR_INVALID_ARGUMENT, "rowenc_rows: 128 or 256");
+    if (value != 128 && value != 256 && value != 512)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "rowenc_rows: 128, 256 or 512");
     set_rowenc_tuning(0, static_cast<uint32_t>(value));
     return FURY_OK;
   }

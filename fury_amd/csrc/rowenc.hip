@@ -39,6 +39,7 @@ namespace {
 
 constexpr int kRwThreads = 256;                 // measure pass rows per workgroup
 std::atomic<int> g_rw_rows = 256;                            // tuning "rowenc_rows": build-pass rows per workgroup
+                                                             // (512 with a 152 KB image: 1.31 vs 1.33 ms, not the default)
 std::atomic<uint32_t> g_rw_img = 76 * 1024;                  // tuning "rowenc_img": its LDS image bytes
 std::atomic<int> g_rw_tile = 0;                              // tuning "rowenc_tile": rows per workgroup (0: all)
 
@@ -523,11 +524,12 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
   a.cap = cap;
   a.ntop = g.ntop;
   a.img = g_rw_img;
-  const int nt = sizes ? kRwThreads : g_rw_rows.load();
+  int nt = sizes ? kRwThreads : g_rw_rows.load();
+  if (nlev > kRowEncMaxDepth && nt > 256) nt = 256;   // the explicit-stack instances: 128 / 256
   const int rt = g_rw_tile.load();
   a.tile = sizes ? nt : (rt > 0 && rt < nt ? rt : nt);
   const dim3 grid(static_cast<unsigned>((g.nrows + a.tile - 1) / a.tile));
-  auto go = [&](auto meas, auto enc128, auto enc256) {
+  auto go = [&](auto meas, auto enc128, auto enc256, auto enc512) {
     if (sizes) {
       hipLaunchKernelGGL(meas, grid, dim3(nt), 0, stream, a);
       return;
@@ -539,19 +541,21 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
       hipLaunchKernelGGL(enc, grid, dim3(nt), lds, stream, a);
     };
     if (nt == 128) run(enc128);
+    else if (nt == 512) run(enc512);
     else run(enc256);
   };
 #define FURY_RW(R, MD)                                                                         \
   if (g.root == R && nlev <= MD) {                                                             \
     go(rw_measure_kernel<R, MD, false>, rw_encode_kernel<128, R, MD, false>,                   \
-       rw_encode_kernel<256, R, MD, false>);                                                   \
+       rw_encode_kernel<256, R, MD, false>, rw_encode_kernel<512, R, MD, false>);              \
     return check_hip(hipGetLastError(), "row-walk encode launch");                             \
   }
   // deeper schemas: kRowEncMaxDepth inlined levels, then the explicit stack (rdeep)
 #define FURY_RW_DEEP(R)                                                                        \
   if (g.root == R) {                                                                           \
     go(rw_measure_kernel<R, kRowEncMaxDepth, true>,                                            \
-       rw_encode_kernel<128, R, kRowEncMaxDepth, true>, rw_encode_kernel<256, R, kRowEncMaxDepth, true>); \
+       rw_encode_kernel<128, R, kRowEncMaxDepth, true>, rw_encode_kernel<256, R, kRowEncMaxDepth, true>, \
+       rw_encode_kernel<256, R, kRowEncMaxDepth, true>);                                       \
     return check_hip(hipGetLastError(), "row-walk encode launch");                             \
   }
   FURY_RW(0, 2) FURY_RW(0, 3) FURY_RW(0, 4) FURY_RW(0, 5)

@@ -290,9 +290,9 @@ int fury_trim_workspace(int32_t device);
  * errors), 1 always the sequential walk.
  * Nested engines: "nested_decode" 2 row walk (default), 1 level engine (schemas past the walk's
  * limits use it by themselves); nested encode is the row walk with an explicit-stack continuation
- * for deep schemas: "rowenc_rows" (128 / 256 threads per group), "rowenc_tile" (rows per group,
+ * for deep schemas: "rowenc_rows" (128 / 256 / 512 threads per group), "rowenc_tile" (rows per group,
  * 0 = threads), "rowenc_img" (LDS image bytes); row-walk decode "walk_threads" /
- * "walk_threads_write" (128 / 256), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
+ * "walk_threads_write" (128 / 256 / 512), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
  * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); flat schemas of 17-256
  * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_threads" /
  * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (encode phases skipped: outputs
