@@ -819,6 +819,20 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
                        dim3(kLv), 0, hs, buf, dtab, nseg);
     return check_hip(hipGetLastError(), "segmented scan launch");
   };
+  // The batch's row bytes, read with the first level's totals: a node's elements each own at
+  // least one byte of some row, so more elements than row bytes means slots that alias other bytes
+  // (a malformed batch whose level arrays would grow with the product of the aliased counts).
+  static thread_local int64_t* pin_bytes = nullptr;
+  if (!pin_bytes && hipHostMalloc(reinterpret_cast<void**>(&pin_bytes), 8, hipHostMallocDefault) != hipSuccess)
+    pin_bytes = nullptr;
+  if (pin_bytes) {
+    *pin_bytes = -1;
+    if ((st = check_hip(hipMemcpyAsync(pin_bytes, offs + nrows, 8, hipMemcpyDeviceToHost, hs),
+                        "hipMemcpyAsync batch bytes"))) {
+      lv_free(p);
+      return st;
+    }
+  }
   std::vector<int32_t> strings;                     // STRING / BINARY nodes: bytes at the end
   std::vector<int32_t> cnt = counted_at(0);
   if (!(st = alloc_level(cnt)) && !cnt.empty())
@@ -844,10 +858,15 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
         (*totals)[2 * strings[j] + 1] = tot[arrays.size() + j];
       strings.clear();
     }
-    for (size_t j = 0; j < arrays.size(); j++) {
+    const int64_t batch_bytes = pin_bytes ? *pin_bytes : -1;     // synchronised by level_totals
+    for (size_t j = 0; j < arrays.size() && !st; j++) {
+      if (tot[j] < 0 || (batch_bytes >= 0 && tot[j] > batch_bytes))
+        st = set_error(FURY_ERR_OUT_OF_BOUNDS, "nested decode: more elements than the batch has "
+                                               "row bytes (slots that alias other bytes)");
       const LvNode& n = p->nodes[arrays[j]];
       for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = tot[j];
     }
+    if (st) break;
     for (int i = 0; i < nn; i++) {
       const LvNode& n = p->nodes[i];
       if (level[i] != L || n.type != FURY_TYPE_STRUCT) continue;
@@ -882,6 +901,18 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
   }
   for (int i = 0; i < nn; i++) (*totals)[2 * i] = p->nodes[i].m;
   for (size_t j = 0; j < strings.size(); j++) (*totals)[2 * strings[j] + 1] = bytes[j];
+  // payload bytes past the batch's row bytes: strings that alias other bytes (as above)
+  if (pin_bytes && (st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) {
+    lv_free(p);
+    return st;
+  }
+  const int64_t batch_bytes = pin_bytes ? *pin_bytes : -1;
+  for (int i = 0; i < nn && batch_bytes >= 0; i++)
+    if ((*totals)[2 * i + 1] > batch_bytes) {
+      lv_free(p);
+      return set_error(FURY_ERR_OUT_OF_BOUNDS, "nested decode: more payload bytes than the batch "
+                                               "has row bytes (slots that alias other bytes)");
+    }
   *out = p;
   return FURY_OK;
 }
