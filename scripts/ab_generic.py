@@ -1,4 +1,4 @@
-"""Timing of the nested-schema engine (generic.hip: STRUCT / MAP / LIST of var elements), on the
+"""Timing of the nested-schema engines (rowenc.hip encode, walk.hip / levels.hip decode), on the
 tests' 7-field nested schema (struct with list + string, list<list<int>>, map<string,int>,
 list<struct>, list<string>, bool).  Columns come from beans (host, slow), repeated to --rows.
 

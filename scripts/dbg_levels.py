@@ -1,5 +1,5 @@
-"""DEBUG: first mismatching entry of a nested column between the level engine, the row
-interpreter and the oracle (tests/test_device.py _engine_schemas)."""
+"""DEBUG: first mismatching entry of a nested column between the level engine (nested_decode 1),
+the row walk (2) and the oracle (tests/test_device.py _engine_schemas)."""
 import os
 import sys
 
@@ -28,8 +28,8 @@ def main():
     want, offs = O.encode(fields, host, n)
     ref = O.decode(fields, want, offs, n)
     outs = {}
-    for mode in (0, 1):
-        N.lib().fury_set_tuning(b"gen_decode", mode)
+    for mode in (1, 2):
+        N.lib().fury_set_tuning(b"nested_decode", mode)
         outs[mode] = [column_to_host(c) for c in enc.decode_batch(batch)]
 
     def walk(fs, cols_by, path):

@@ -15,7 +15,7 @@ f = glob.glob('gpurun_out/pmc_walk/sq/**/*counter_collection.csv', recursive=Tru
 acc = collections.defaultdict(lambda: collections.defaultdict(float))
 for r in csv.DictReader(open(f)):
     k = r['Kernel_Name'][:70]
-    if 'walk' not in k and 'gen_encode' not in k and 'te_kernel' not in k: continue
+    if 'walk' not in k and 'rw_' not in k: continue
     acc[k][r['Counter_Name']] += float(r['Counter_Value'])
 for k, d in acc.items():
     print(k); print('   ', {c: f"{v:.3g}" for c, v in sorted(d.items())})
