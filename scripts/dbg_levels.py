@@ -50,7 +50,7 @@ def main():
             if f.children and all(c.child for c in cs.values()):
                 walk(f.children, {m: c.child for m, c in cs.items()}, p + ".")
 
-    walk(fields, {0: outs[0], 1: outs[1], "ref": ref}, "")
+    walk(fields, {1: outs[1], 2: outs[2], "ref": ref}, "")
     print("done")
 
 
