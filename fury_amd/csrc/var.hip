@@ -182,7 +182,8 @@ int launch_decode_measure(const VarArgs& a, const uint8_t* rows, const int64_t* 
 }
 
 static std::atomic<int> g_dec_rows = 0;
-// tuning "var_skip" (diagnostics: phases of encode_var_reg skipped, outputs WRONG; timing only)
+// tuning "var_skip" (diagnostics: phases of encode_var_reg (1 / 2 / 4) and decode_var_reg (16 / 32 /
+// 64 / 128) skipped, outputs WRONG; timing only)
 static std::atomic<int> g_var_skip{0};
 static std::atomic<int> g_var_wide{1};
 // threads per 64-row tile of the wide kernels (ab_wide legs, 33 fields x 5M rows): decode 256

@@ -1543,10 +1543,12 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     }
   }
   // (the images were zeroed while the rows were staged)
+  // (a.skip, diagnostics -- outputs WRONG, timing only: 16 no image assembly, 32 no fixed-width /
+  // validity stores, 64 no look-back, 128 no image store-out)
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    if (img_at[k] == kNone || !live || cnt[k] == 0) continue;
+    if (img_at[k] == kNone || !live || cnt[k] == 0 || (a.skip & 16)) continue;
     if (static_cast<uint64_t>(ex[k]) + cnt[k] > tot[k]) {   // the tile's 32-bit total wrapped
       raise_oob(a.err, r);
       continue;
@@ -1651,6 +1653,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
     const bool isnull = (nullw >> k) & 1;
+    if (a.skip & 32) continue;
     if (c.validity) {
       const uint64_t ok = __ballot(live && !isnull);
       if (lane < nwords)
@@ -1691,7 +1694,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     for (int k = 0; k < K; k++) {
       if (!seq_kind(kind_of<M>(a.col[k]))) continue;
       if ((q++ % (NT / 64)) != wave) continue;
-      const int64_t pre = b == 0 ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err, TR);
+      const int64_t pre = b == 0 || (a.skip & 64) ? 0 : look_back_help<NT>(a, k, rows, offs, status, b, K, k, a.err, TR);
       if (lane == 0) {
         sbase[k] = pre;
         if (b > 0) st_status(status + b * K + k, kInc | static_cast<uint64_t>(pre + tot[k]));
@@ -1754,7 +1757,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const VarCol& c = a.col[k];
-    if (img_at[k] == kNone) continue;
+    if (img_at[k] == kNone || (a.skip & 128)) continue;
     const int64_t gb = sbase[k];
     uint8_t* dst = const_cast<uint8_t*>(c.values);
     const uint8_t* im = reinterpret_cast<const uint8_t*>(oimg) + img_at[k];

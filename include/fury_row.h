@@ -295,8 +295,8 @@ int fury_trim_workspace(int32_t device);
  * "walk_threads_write" (128 / 256 / 512), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
  * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass); flat schemas of 17-256
  * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_threads" /
- * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (encode phases skipped: outputs
- * WRONG, timing only),
+ * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (register-staged encode / decode phases
+ * skipped: outputs WRONG, timing only),
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
  * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's
  * row bytes the LDS stage must hold, default 95), "var_dec_rows" (forced tile rows, 0 = plan).
