@@ -1408,3 +1408,42 @@ def test_decode_skewed_row_sizes(oracle, dev, order):
         })
     cols = beans_to_columns(fields, beans)
     _roundtrip(oracle, None, len(beans), dev, fields=fields, cols=cols)
+
+
+def _wide_all_kinds(ncols):
+    """ncols fields cycling through every flat type the row format has -- each scalar, DECIMAL,
+    STRING / BINARY and LIST of every fixed-width element type (nullable and not) -- all nullable
+    at the top, named so Descriptor order = index order."""
+    L = lambda name, e, en=True: T.Field(name, T.LIST, True, (T.Field("item", e, en, ()),))  # noqa: E731
+    kinds = [T.BOOL, T.INT8, T.INT16, T.INT32, T.FLOAT32, T.DATE32, T.TIMESTAMP, T.DECIMAL,
+             T.BINARY, T.STRING, T.FLOAT64, T.INT64, ("list", T.INT32, True),
+             ("list", T.INT16, False), ("list", T.BOOL, True), ("list", T.INT8, True),
+             ("list", T.FLOAT32, False), ("list", T.FLOAT64, True), ("list", T.DATE32, True),
+             ("list", T.TIMESTAMP, True)]
+    out = []
+    for i in range(ncols):
+        k = kinds[i % len(kinds)]
+        name = f"f{i:03d}"
+        out.append(L(name, k[1], k[2]) if isinstance(k, tuple) else T.field(name, k))
+    return out
+
+
+@pytest.mark.parametrize("ncols,n", [(20, 2001), (41, 1300), (100, 300)])
+def test_wide_every_kind_bit_exact(oracle, dev, ncols, n):
+    """17-256-field flat schemas carrying every flat type (the wide tiles: wide.hip): encode,
+    encode_measured, decode, rows_to_arrow and the bound-sized decode == the oracle."""
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    fields = _wide_all_kinds(ncols)
+    host = gen_columns("wide", fields, n, seed=ncols * 3 + n, null_pct=10, str_max=30,
+                       list_max=11, list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    rows, offs, total = _encode_measured(enc, _dev_cols(host, dev), n, dev)
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+    ref = oracle.decode(fields, want, want_offs, n)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
+    dec = [column_to_host(c) for c in enc.decode_batch(batch, sizing="bound")]
+    assert_columns_equal(fields, dec, ref, n)
