@@ -9,6 +9,7 @@ exclusive scan of per-shard byte totals (``global_row_base``).
 from __future__ import annotations
 
 import os
+import sys
 import socket
 from dataclasses import dataclass
 from typing import Callable, List, Sequence, Tuple
@@ -78,6 +79,23 @@ def global_row_base(shard_bytes: List[int]) -> List[int]:
     return out
 
 
+def _with_stdout_on_stderr(fn):
+    """Runs fn with file descriptor 1 duplicated from 2 (C-level prints included: libc's buffers
+    are flushed before fd 1 is restored)."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn()
+    finally:
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class Orchestrator:
     """Barrier + max-over-ranks timing for the bench contract."""
 
@@ -88,7 +106,12 @@ class Orchestrator:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             if not dist.is_initialized():
-                dist.init_process_group("gloo", rank=r.rank, world_size=r.world)
+                # gloo reports its mesh connections on stdout; the bench contract keeps stdout
+                # for rank 0's one JSON line, so the rendezvous (and a first barrier, where the
+                # mesh may be connected lazily) runs with fd 1 pointed at stderr
+                _with_stdout_on_stderr(lambda: (
+                    dist.init_process_group("gloo", rank=r.rank, world_size=r.world),
+                    dist.barrier()))
             self._dist = dist
 
     def barrier(self) -> None:
