@@ -83,14 +83,15 @@ std::atomic<int> g_tree_mode = 2;             // tuning "nested_decode": 1 level
 // Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row count tiles with
 // a 12 KB stage (prepare 1.35 -> 1.08 ms: more tiles resident), 256-row write tiles (1.87 -> 1.78
 // ms) with the prefetch; round 5: 512-row unstaged write tiles with 24 KB output windows (1.67 ->
-// 1.62 ms: the tile prologue -- bases, window layout -- is ~16 % of a 256-row tile's time).
+// 1.62 ms: the tile prologue -- bases, window layout -- is ~16 % of a 256-row tile's time), then
+// 40 KB windows (the same time, WRITE 1.34x -> 1.23x the column bytes).
 std::atomic<int> g_walk_threads = 128;        // tuning "walk_threads": rows (= threads) per count tile
 std::atomic<int> g_walk_threads_w = 512;      // tuning "walk_threads_write": rows per write tile (a multiple)
 std::atomic<uint32_t> g_walk_stage = 12 * 1024;  // tuning "walk_stage": LDS stage cap of a row-walk count tile
 std::atomic<uint32_t> g_walk_stage_w = 0;        // tuning "walk_stage_write": the same for the write pass (its
                                     // LDS-bound occupancy costs more than HBM row reads save)
 std::atomic<uint32_t> g_walk_pool = 8 * 1024;    // tuning "walk_pool": LDS bitmap-window bytes (write pass)
-std::atomic<uint32_t> g_walk_out{24 * 1024};     // tuning "walk_out": LDS output-window bytes (write pass)
+std::atomic<uint32_t> g_walk_out{40 * 1024};     // tuning "walk_out": LDS output-window bytes (write pass)
 std::atomic<int> g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
                                     // (bit 0: write pass, bit 1: count pass)
 std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)

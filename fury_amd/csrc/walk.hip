@@ -92,8 +92,8 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   l.opool = b;
   b += ow ? out : 0;
   b = (b + 15) & ~size_t(15);
-  l.pf = b;                                   // prefetch landing zone: 1 KB per wave
-  b += prefetch ? 1024 * static_cast<size_t>(nt / 64) : 0;
+  l.pf = b;                                   // prefetch landing zone: 1 KB, shared by the waves
+  b += prefetch ? 1024 : 0;                   // (the data is discarded: overlapping writes are harmless)
   l.stg = b;
   b += stage;
   l.end = (b + 15) & ~size_t(15);
@@ -150,7 +150,7 @@ __device__ inline void walk_prefetch(const TreeArgs& a, const WShared& sh, int64
   const int64_t g1 = min<int64_t>(max<int64_t>(gl(a.offs)[wr1], g0), total);
   const uintptr_t lo = reinterpret_cast<uintptr_t>(a.rows + g0) & ~uintptr_t(15);
   const uintptr_t hi = (reinterpret_cast<uintptr_t>(a.rows + g1) + 15) & ~uintptr_t(15);
-  uint8_t* land = sh.pf + 1024 * (tid >> 6);
+  uint8_t* land = sh.pf;
   for (uintptr_t q = lo + 16 * (tid & 63); q < hi; q += 1024)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(q), land, 16, 0, 0);
 }

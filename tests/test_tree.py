@@ -91,7 +91,7 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
     # output windows of the write pass (walk_out bytes): off, too small for most nodes (mixed
     # LDS / HBM stores), the default; write tiles of 512 (default, unstaged) and 256 rows
     legs = ([(128, 0), (128, 256), (128, 16384)] if budget == "tiny"
-            else [(512, 0), (512, 24576), (256, 16384)])
+            else [(512, 0), (512, 40960), (256, 16384)])
     for tw, wo in legs:
         _tune("walk_threads_write", tw)
         _tune("walk_out", wo)
