@@ -380,3 +380,33 @@ def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
     _tune("nested_decode", 2)
     good = [column_to_host(c) for c in enc.decode_batch(_batch(enc, rows, offs, n, dev))]
     assert_columns_equal(fields, good, oracle.decode(fields, rows, offs, n), n)
+
+
+def test_walk_budget_no_false_positive(oracle, dev, engines):
+    """Well-formed rows at the edge of the count pass's item budget (2 x a row's bytes + 64):
+    thousands of 1-byte list elements, lists of null structs (free) and of empty lists, maps of
+    1-byte keys and values -- decoded by the row walk without a report, == the oracle."""
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, column_to_device
+    S = T.struct_field
+    fields = [T.not_null_field("id", T.INT64),
+              T.Field("bits", T.LIST, True, (T.not_null_field("item", T.BOOL),)),
+              T.Field("nulls", T.LIST, True, (S("item", [T.field(f"x{i:02d}", T.INT32) for i in range(20)]),)),
+              T.Field("empties", T.LIST, True, (T.Field("item", T.LIST, True, (T.field("item", T.INT8),)),)),
+              T.map_field("m", T.not_null_field("k", T.INT8), T.not_null_field("v", T.INT8))]
+    rng = np.random.default_rng(3)
+    n = 64
+    beans = [{"id": i,
+              "bits": [bool(x) for x in rng.integers(0, 2, 3000 + 17 * i)],
+              "nulls": [None] * (500 + i),
+              "empties": [[] for _ in range(400 + i)],
+              "m": [(int(k), int(k) // 2) for k in range(-60, 60)]} for i in range(n)]
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    _tune("nested_decode", 2)
+    got = _decode_plan(enc, batch)
+    assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
+    assert columns_to_beans(fields, got, n) == beans
