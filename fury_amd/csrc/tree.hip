@@ -143,7 +143,7 @@ struct TreePlan {
   int64_t stride = 0;              // ntiles + 1: [ntiles] holds the total
   uint32_t* rowpre = nullptr;      // [K][nrows]
   int32_t K = 0, nt = 0, ntw = 0;   // count / write tile rows
-  uint32_t pool_cap = 0;
+  uint32_t pool_cap = 0, out_cap = 0;  // write pass: bitmap-window / output-window LDS bytes
   int32_t knode[kWalkMaxK] = {};
 };
 
@@ -181,7 +181,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.rowpre = p.rowpre;
   a.K = p.K;
   a.pool_cap = p.pool_cap;
-  a.out_cap = write ? g_walk_out.load() : 0;
+  a.out_cap = write ? p.out_cap : 0;
   for (int k = 0; k < p.K; k++) a.knode[k] = p.knode[k];
   a.ctr = p.nt;
   a.tmul = write ? p.ntw / p.nt : 1;
@@ -278,6 +278,18 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   p->stage_cap_w = (g_walk_stage_w + 15) & ~15u;
   if (p->ntw > 256 && p->stage_cap_w) p->ntw = 256;   // 512-row write tiles: unstaged instance only
   p->pool_cap = g_walk_pool;
+  p->out_cap = g_walk_out;
+  // The write pass's LDS (cursors: K x rows, node tables, windows) must fit one workgroup: wide
+  // schemas (many counted nodes / nodes) step down the tile rows, then the windows.
+  const bool pfw = (g_walk_prefetch & 1) != 0;
+  for (;;) {
+    if (walk_write_lds(nn, K, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) <= kWalkLdsMax) break;
+    if (p->ntw > p->nt) p->ntw /= 2;
+    else if (p->out_cap > 0) p->out_cap = p->out_cap > 4096 ? p->out_cap / 2 : 0;
+    else if (p->pool_cap > 0) p->pool_cap = p->pool_cap > 1024 ? p->pool_cap / 2 : 0;
+    else if (p->stage_cap_w > 0) p->stage_cap_w = 0;
+    else break;                                 // cannot happen for K <= kWalkMaxK, nn <= 512
+  }
   p->ntiles = (nrows + p->tile_rows - 1) / p->tile_rows;
   p->stride = p->ntiles + 1;
   int32_t* overflow = nullptr;

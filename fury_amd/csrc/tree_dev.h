@@ -63,6 +63,9 @@ constexpr int kWalkMaxDepth = 5;      // deeper: the level engine (register budg
 
 // walk.hip launchers (tree.hip owns the plan): LDS bytes of a pass, and the launch itself.
 size_t walk_lds(const TreeArgs& a, int nt, bool write);
+size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool prefetch,
+                      uint32_t out);
+constexpr size_t kWalkLdsMax = 159 * 1024;   // LDS of one workgroup (160 KB, static arrays aside)
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs);
 
 // Diagnostics: thread 0 of a workgroup adds the time since its previous mark to tacc[id]

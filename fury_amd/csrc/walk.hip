@@ -724,6 +724,10 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
 size_t walk_lds(const TreeArgs& a, int nt, bool write) {
   return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0, a.out_cap).end;
 }
+size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool prefetch,
+                      uint32_t out) {
+  return walk_layout(nn, K, nt, stage, pool, true, prefetch, out).end;
+}
 
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
   const size_t lds = walk_lds(a, nt, write);

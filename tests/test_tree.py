@@ -410,3 +410,23 @@ def test_walk_budget_no_false_positive(oracle, dev, engines):
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
     assert columns_to_beans(fields, got, n) == beans
+
+
+def test_walk_many_counted_nodes_fits_lds(oracle, dev, engines):
+    """A schema at the row walk's counted-node limit (62 STRING fields + a LIST of a STRING struct:
+    64 counted nodes): the write pass's per-row cursors (64 x rows) would overflow the LDS at the
+    default 512-row tiles, so the plan steps down to 256-row tiles; the decode == the oracle."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = ([T.not_null_field("id", T.INT64)] + [T.field(f"s{i:02d}", T.STRING) for i in range(62)]
+              + [T.Field("t", T.LIST, True, (T.struct_field("item", [T.field("x", T.STRING)]),))])
+    n = 3000
+    beans = _beans(fields, n, 64)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    _tune("nested_decode", 2)
+    got = _decode_plan(enc, batch)
+    assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
