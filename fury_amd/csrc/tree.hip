@@ -32,40 +32,63 @@ namespace fury {
 namespace {
 
 // Exclusive scan over the tiles of each [node] row of cnt (rows 0..nn-1) and byt (rows nn..2nn-1),
-// rows `stride` apart; tot[row] = the row's total.  One 1024-thread workgroup per row.
+// rows `stride` apart; tot[row] = the row's total.  One 1024-thread workgroup per row walks it in
+// chunks of 8192 tiles: a coalesced load into LDS, each thread's 8 consecutive entries scanned
+// there, a block scan of the thread sums, a coalesced store.  (Per-thread contiguous runs read
+// straight from HBM touched one line per lane per load: 72 us at 31k tiles x 40 rows.)
 constexpr int kScanT = 1024;
+constexpr int kScanPer = 8;
 __global__ __launch_bounds__(kScanT) void tree_tile_scan(int64_t* cnt, int64_t* byt, int64_t ntiles,
                                                          int64_t stride, int32_t nn, int64_t* tot) {
+  __shared__ int64_t buf[kScanT * kScanPer];
   __shared__ int64_t ws[kScanT / 64];
   const int row = blockIdx.x;
   int64_t* v = row < nn ? cnt + static_cast<int64_t>(row) * stride : byt + static_cast<int64_t>(row - nn) * stride;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t per = (ntiles + kScanT - 1) / kScanT;
-  const int64_t b = min<int64_t>(tid * per, ntiles), e = min<int64_t>(b + per, ntiles);
-  int64_t s = 0;
-  for (int64_t i = b; i < e; i++) s += v[i];
-  int64_t x = s;
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < ntiles; c0 += kScanT * kScanPer) {
+    const int64_t len = min<int64_t>(ntiles - c0, kScanT * kScanPer);
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) ws[wave] = x;
-  __syncthreads();
-  int64_t pre = 0, all = 0;
-  for (int w = 0; w < kScanT / 64; w++) {
-    pre += w < wave ? ws[w] : 0;
-    all += ws[w];
-  }
-  int64_t run = pre + x - s;
-  for (int64_t i = b; i < e; i++) {
-    const int64_t c = v[i];
-    v[i] = run;
-    run += c;
+    for (int j = 0; j < kScanPer; j++) {
+      const int64_t i = j * kScanT + tid;
+      buf[i] = i < len ? v[c0 + i] : 0;
+    }
+    __syncthreads();
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanPer; j++) s += buf[tid * kScanPer + j];
+    int64_t x = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int64_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    int64_t pre = 0, all = 0;
+    for (int w = 0; w < kScanT / 64; w++) {
+      pre += w < wave ? ws[w] : 0;
+      all += ws[w];
+    }
+    int64_t run = carry + pre + x - s;
+#pragma unroll
+    for (int j = 0; j < kScanPer; j++) {
+      const int64_t c = buf[tid * kScanPer + j];
+      buf[tid * kScanPer + j] = run;
+      run += c;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kScanPer; j++) {
+      const int64_t i = j * kScanT + tid;
+      if (i < len) v[c0 + i] = buf[i];
+    }
+    carry += all;
+    __syncthreads();                             // buf / ws are reused by the next chunk
   }
   if (tid == 0) {
-    tot[row] = all;
-    if (stride > ntiles) v[ntiles] = all;       // walk plans: [ntiles] = the total
+    tot[row] = carry;
+    if (stride > ntiles) v[ntiles] = carry;     // walk plans: [ntiles] = the total
   }
 }
 
