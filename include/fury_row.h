@@ -154,6 +154,9 @@ int fury_sort_bean_fields(const char* const* java_names, int32_t n, int32_t* ord
 /* StringUtils.lowerCamelToLowerUnderscore (fury-core util/StringUtils.java:252-271).
  * Returns the length written (excluding NUL); out must hold 2*strlen(in)+1 bytes. */
 int32_t fury_lower_camel_to_lower_underscore(const char* in, char* out, size_t out_len);
+/* Any number of fields; nested STRUCT / LIST / MAP up to 64 levels and 4096 nodes (a deeper or
+ * larger schema is created, and its encode / decode calls return FURY_ERR_UNSUPPORTED).  Every
+ * row of a schema within those limits encodes and decodes on the device, whatever its size. */
 int fury_schema_create(const fury_field* fields, int32_t num_fields, fury_schema** out);
 void fury_schema_destroy(fury_schema* schema);
 int fury_schema_get_info(const fury_schema* schema, fury_schema_info* info);
