@@ -27,7 +27,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--sweep", default="", help="fixed_variant values to time zc_enc/zc_dec at")
     args = ap.parse_args()
     import torch
     from fury_amd import _native as N
@@ -162,25 +161,6 @@ def main():
     ms = {k: round(statistics.median(v) * 1e3, 3) for k, v in res.items()}
     gb = {k: round(b / (ms[k] * 1e-3) / 1e9, 1) for k in legs}
     line = {"rows": n, "ms": ms, "GBps_algorithmic": gb}
-    if args.sweep:
-        v0 = lib.fury_get_tuning(b"fixed_variant")
-        sw = {}
-        for v in [int(x) for x in args.sweep.split(",")]:
-            lib.fury_set_tuning(b"fixed_variant", v)
-            t = {}
-            for k, f in (("enc", zc_enc), ("dec", zc_dec)):
-                f()
-                xs = []
-                for _ in range(args.reps):
-                    t0 = time.perf_counter()
-                    f()
-                    xs.append(time.perf_counter() - t0)
-                t[k] = round(b / statistics.median(xs) / 1e9, 1)
-            sw[v] = t
-        lib.fury_set_tuning(b"fixed_variant", v0)
-        zc_dec()
-        assert all(torch.equal(o.values, h.values) for o, h in zip(out, host)), "sweep decode"
-        line["sweep_GBps"] = sw
     print(json.dumps(line), flush=True)
 
 
