@@ -430,3 +430,55 @@ def test_walk_many_counted_nodes_fits_lds(oracle, dev, engines):
     _tune("nested_decode", 2)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
+
+
+def _random_schema(rng, depth_left, nfields, prefix="f"):
+    """Random fields: scalars of every width, STRING / BINARY / DECIMAL, and (while depth_left)
+    STRUCT / LIST / MAP of random children."""
+    scal = [T.BOOL, T.INT8, T.INT16, T.INT32, T.INT64, T.FLOAT32, T.FLOAT64, T.DATE32,
+            T.TIMESTAMP, T.STRING, T.BINARY, T.DECIMAL]
+    out = []
+    for i in range(nfields):
+        name = f"{prefix}{i:02d}"
+        kind = int(rng.integers(0, 6)) if depth_left > 0 else 0
+        nullable = bool(rng.integers(0, 4))
+        if kind <= 2:
+            out.append(T.Field(name, scal[int(rng.integers(0, len(scal)))], nullable, ()))
+        elif kind == 3:
+            out.append(T.Field(name, T.STRUCT, nullable,
+                               tuple(_random_schema(rng, depth_left - 1, int(rng.integers(1, 4)), name + "s"))))
+        elif kind == 4:
+            e = _random_schema(rng, depth_left - 1, 1, name + "e")[0]
+            out.append(T.Field(name, T.LIST, nullable, (T.Field("item", e.type_id, e.nullable, e.children),)))
+        else:
+            k = T.Field("key", [T.INT32, T.STRING, T.INT64][int(rng.integers(0, 3))], False, ())
+            v = _random_schema(rng, depth_left - 1, 1, name + "v")[0]
+            out.append(T.Field(name, T.MAP, nullable, (k, T.Field("value", v.type_id, v.nullable, v.children))))
+    return out
+
+
+@pytest.mark.parametrize("seed", list(range(40)))
+def test_random_nested_schemas(oracle, dev, engines, seed):
+    """Random nested schemas (up to 5 levels, every type) with random beans: the device encode ==
+    the oracle's bytes, and the row walk and the level engine both decode them to the oracle's
+    columns."""
+    from fury_amd.beans import beans_to_columns, columns_to_beans
+    from fury_amd.encoder import Encoders, column_to_device
+    rng = np.random.default_rng(1000 + seed)
+    fields = _random_schema(rng, int(rng.integers(1, 5)), int(rng.integers(2, 9)))
+    n = int(rng.integers(1, 900))
+    beans = _beans(fields, n, seed)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    ref = oracle.decode(fields, want, want_offs, n)
+    for mode in (2, 1):
+        _tune("nested_decode", mode)
+        got = _decode_plan(enc, batch) if enc.nested else None
+        if got is None:
+            from fury_amd.encoder import column_to_host
+            got = [column_to_host(c) for c in enc.decode_batch(batch)]
+        assert_columns_equal(fields, got, ref, n)
+    assert columns_to_beans(fields, got, n) == beans
