@@ -1447,3 +1447,38 @@ def test_wide_every_kind_bit_exact(oracle, dev, ncols, n):
     assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
     dec = [column_to_host(c) for c in enc.decode_batch(batch, sizing="bound")]
     assert_columns_equal(fields, dec, ref, n)
+
+
+@pytest.mark.parametrize("seed", list(range(30)))
+def test_random_flat_schemas(oracle, dev, seed):
+    """Random flat schemas (1-120 fields of every flat type, lists of fixed-width elements,
+    random nullability): the fixed-width, register-staged and wide kernels, whichever the field
+    count picks -- encode, decode and rows_to_arrow == the oracle."""
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    rng = np.random.default_rng(5000 + seed)
+    scal = [T.BOOL, T.INT8, T.INT16, T.INT32, T.INT64, T.FLOAT32, T.FLOAT64, T.DATE32,
+            T.TIMESTAMP, T.STRING, T.BINARY, T.DECIMAL]
+    elem = [T.BOOL, T.INT8, T.INT16, T.INT32, T.INT64, T.FLOAT32, T.FLOAT64]
+    nf = int(rng.choice([1, 3, 7, 16, 17, 33, 64, 65, 120]))
+    var_p = float(rng.choice([0.0, 0.3, 0.6]))
+    fields = []
+    for i in range(nf):
+        nullable = bool(rng.integers(0, 3))
+        if rng.random() < var_p:
+            if rng.random() < 0.4:
+                e = elem[int(rng.integers(0, len(elem)))]
+                fields.append(T.Field(f"f{i:03d}", T.LIST, nullable,
+                                      (T.Field("item", e, bool(rng.integers(0, 2)), ()),)))
+            else:
+                fields.append(T.Field(f"f{i:03d}", [T.STRING, T.BINARY, T.DECIMAL][int(rng.integers(0, 3))], nullable, ()))
+        else:
+            fields.append(T.Field(f"f{i:03d}", scal[int(rng.integers(0, 9))], nullable, ()))
+    n = int(rng.integers(1, 1500))
+    host = gen_columns("wide", fields, n, seed=seed, null_pct=10, str_max=int(rng.integers(1, 60)),
+                       list_max=int(rng.integers(1, 20)), list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    w = ArrowWriter(enc)
+    w.write(batch)
+    assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
