@@ -482,3 +482,27 @@ def test_random_nested_schemas(oracle, dev, engines, seed):
             got = [column_to_host(c) for c in enc.decode_batch(batch)]
         assert_columns_equal(fields, got, ref, n)
     assert columns_to_beans(fields, got, n) == beans
+
+
+@pytest.mark.parametrize("seed", list(range(16)))
+def test_random_deep_schemas(oracle, dev, engines, seed):
+    """Random schemas nested 6-10 levels (the encode's explicit-stack levels, the level-engine
+    decode): bytes and columns == the oracle."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    rng = np.random.default_rng(7000 + seed)
+    fields = []
+    while not fields or max(_levels(f) for f in fields) < 6:
+        fields = _random_schema(rng, int(rng.integers(6, 11)), int(rng.integers(1, 4)))
+    n = int(rng.integers(1, 300))
+    beans = _beans(fields, n, seed)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    assert_columns_equal(fields, _decode_plan(enc, batch), oracle.decode(fields, want, want_offs, n), n)
+
+
+def _levels(f):
+    return 1 + max((_levels(c) for c in f.children), default=0)
