@@ -247,6 +247,10 @@ def run(args):
         if ev is not None:
             ev[2].record(stream)
 
+    # the box's achievable streaming copy, same device, same stream, before the timed loop
+    # (VERDICT r5 item 6): separates a slow box from a slow kernel in the roofline line
+    copy = copy_rate(dev, stream)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -342,7 +346,10 @@ def run(args):
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
                      "encode_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1),
-                     "decode_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+                     "decode_GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1),
+                     "copy_GBps": copy["GBps"],
+                     "frac_of_copy": round(achieved / copy["GBps"], 4),
+                     "copy": copy["what"]},
     }
     if shared:
         line["rehearsal"] = (f"{world} ranks shared {min(world, ndev)} GPU(s) (--share-gpus): a "
@@ -354,6 +361,38 @@ def run(args):
                                             args.cpu_rows or min(n, 1_000_000))
     print(json.dumps(line), flush=True)
     orch.close()
+
+
+def copy_rate(dev, stream, nbytes=1 << 30, reps=10):
+    """Achievable HBM copy on this box: fury_hbm_copy (16-B non-temporal loads + stores, the
+    library's own kernel) of a 1 GiB buffer, read + write bytes per second, HIP events on the bench
+    stream, median of `reps` launches after one warm-up."""
+    import statistics
+    import torch
+    from fury_amd import _native as N
+    src = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    src.fill_(7)
+    L = N.lib()
+    sh = stream.cuda_stream
+
+    def launch():
+        assert L.fury_hbm_copy(dst.data_ptr(), src.data_ptr(), nbytes, sh) == 0, N.last_error()
+    launch()
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        launch()
+        b.record(stream)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    t = statistics.median(ms)
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"GBps": round(2 * nbytes / (t * 1e-3) / 1e9, 1),
+            "what": f"fury_hbm_copy of {nbytes >> 20} MiB (read + write bytes / s, 16-B "
+                    f"non-temporal, median of {reps} launches, same device and stream)"}
 
 
 def end_to_end(enc, cols, n, dev, stream):

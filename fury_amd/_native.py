@@ -100,6 +100,7 @@ SIGNATURES = {
     "fury_jni_decode_host_prepare": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(_I64), _I64,
                                                     ctypes.POINTER(_P), _I32]),
     "fury_jni_decode_host_execute": (ctypes.c_int, [_P, _P, ctypes.POINTER(_I64), _I64]),
+    "fury_hbm_copy": (ctypes.c_int, [_P, _P, _I64, _P]),
     "fury_arrow_ipc_schema": (ctypes.c_int, [_P, _P, _I64, ctypes.POINTER(_I64)]),
     "fury_arrow_ipc_record_batch": (ctypes.c_int, [_P, ctypes.POINTER(FuryColumn), _I64, _P, _I64,
                                                    ctypes.POINTER(_I64), _P]),

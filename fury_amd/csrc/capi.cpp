@@ -29,9 +29,15 @@ int check_hip(int hip_status, const char* what) {
 // The legacy null stream and hipStreamPerThread are keyed per host thread (two keys per thread,
 // released when the thread exits).  Slots are assigned on first launch and go back to a free list
 // when their stream is released: by the library when it destroys a stream it created (decode
-// plans, host-path plans), by the caller through fury_stream_release before it destroys one of
-// its own.  A call that needs a slot when all kErrSlots are held fails with FURY_ERR_DEVICE --
-// slots are never shared, so an error is reported on its own stream or not at all.
+// plans, host-path plans), by the caller through fury_stream_release (which synchronises the
+// stream first, the null stream and hipStreamPerThread included) before it destroys one of its
+// own.  A thread that exits makes no HIP call, so work it launched on its null-stream /
+// per-thread keys may still be running: those slots go to a QUARANTINE, not the free list, and
+// become free only after a device synchronisation that covers them (when the free slots run out,
+// or fury_trim_workspace) -- a late error lands in the quarantined slot and is dropped there, never
+// on an unrelated stream.  A call that needs a slot when all kErrSlots are held fails
+// with FURY_ERR_DEVICE -- slots are never shared, so an error is reported on its own stream or not
+// at all.
 namespace {
 constexpr int kErrSlots = 1024;
 uint32_t* g_err_host = nullptr;     // host view of the slots
@@ -40,17 +46,18 @@ std::once_flag g_err_once;
 std::mutex g_slot_mu;
 std::unordered_map<uintptr_t, int> g_slot_of;
 std::vector<int> g_slot_free;       // released slots (words cleared)
+std::vector<int> g_slot_quarantine; // released at thread exit, their work maybe still running
 int g_slot_next = 0;                // slots [0, g_slot_next) have been handed out at least once
 
-void release_key(uintptr_t k);
+void release_key(uintptr_t k, bool quarantine = false);
 
 // Per-thread keys of the null stream and of hipStreamPerThread (odd: never a stream handle, which
-// is aligned); their slots are released when the thread exits.
+// is aligned); their slots are quarantined when the thread exits.
 struct ThreadKeys {
   char null_key = 0, per_thread_key = 0;
   ~ThreadKeys() {
-    release_key(reinterpret_cast<uintptr_t>(&null_key) | 1);
-    release_key(reinterpret_cast<uintptr_t>(&per_thread_key) | 1);
+    release_key(reinterpret_cast<uintptr_t>(&null_key) | 1, true);
+    release_key(reinterpret_cast<uintptr_t>(&per_thread_key) | 1, true);
   }
 };
 
@@ -76,13 +83,57 @@ void init_err() {
   });
 }
 
-// The slot of stream key k: its own, else a free or never-used one (-1: all kErrSlots held).
+void clear_slot_words(int slot);
+int assign_slot_locked(uintptr_t k);
+
+// Every device synchronised: the quarantined slots' kernels have finished, so their words can be
+// cleared (late errors dropped) and the slots reused.  Called without g_slot_mu held.
+void drain_quarantine() {
+  {
+    std::lock_guard<std::mutex> lock(g_slot_mu);
+    if (g_slot_quarantine.empty()) return;
+  }
+  int n = 0, cur = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return;
+  (void)hipGetDevice(&cur);
+  std::vector<int> q;
+  {
+    std::lock_guard<std::mutex> lock(g_slot_mu);
+    q.swap(g_slot_quarantine);       // slots quarantined after this point wait for the next drain
+  }
+  for (int d = 0; d < n; d++)
+    if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  (void)hipSetDevice(cur);
+  std::lock_guard<std::mutex> lock(g_slot_mu);
+  for (int slot : q) {
+    clear_slot_words(slot);
+    g_slot_free.push_back(slot);
+  }
+}
+
+// The slot of stream key k: its own, else a free or never-used one; when none is left, the
+// quarantine is drained first (-1: all kErrSlots held by live streams).
 // `assign` false: lookup only (a stream that never launched has nothing to report).
 int error_slot(uintptr_t k, bool assign) {
+  {
+    std::lock_guard<std::mutex> lock(g_slot_mu);
+    auto it = g_slot_of.find(k);
+    if (it != g_slot_of.end()) return it->second;
+    if (!assign) return -1;
+    if (g_slot_free.empty() && g_slot_next >= kErrSlots && !g_slot_quarantine.empty()) {
+      // fall through to the drain below (it synchronises: no lock held)
+    } else {
+      return assign_slot_locked(k);
+    }
+  }
+  drain_quarantine();
   std::lock_guard<std::mutex> lock(g_slot_mu);
   auto it = g_slot_of.find(k);
   if (it != g_slot_of.end()) return it->second;
-  if (!assign) return -1;
+  return assign_slot_locked(k);
+}
+
+int assign_slot_locked(uintptr_t k) {
   int slot = -1;
   if (!g_slot_free.empty()) {
     slot = g_slot_free.back();
@@ -98,20 +149,33 @@ int error_slot(uintptr_t k, bool assign) {
 
 std::atomic<int64_t> g_err_dropped{0};   // look-back flags cleared by a release, never taken
 
-void release_key(uintptr_t k) {
+void clear_slot_words(int slot) {
+  if (!g_err_host) return;
+  uint32_t* w = g_err_host + size_t(kErrWords) * slot;
+  if (__atomic_exchange_n(w + kErrLookBack, 0u, __ATOMIC_ACQ_REL)) g_err_dropped.fetch_add(1);
+  for (int i = 0; i < kErrWords; i++) __atomic_store_n(w + i, 0u, __ATOMIC_RELEASE);
+}
+
+void release_key(uintptr_t k, bool quarantine) {
   std::lock_guard<std::mutex> lock(g_slot_mu);
   auto it = g_slot_of.find(k);
   if (it == g_slot_of.end()) return;
   const int slot = it->second;
   g_slot_of.erase(it);
-  if (g_err_host) {
-    uint32_t* w = g_err_host + size_t(kErrWords) * slot;
-    if (__atomic_exchange_n(w + kErrLookBack, 0u, __ATOMIC_ACQ_REL)) g_err_dropped.fetch_add(1);
-    for (int i = 0; i < kErrWords; i++) __atomic_store_n(w + i, 0u, __ATOMIC_RELEASE);
+  if (quarantine) {
+    g_slot_quarantine.push_back(slot);
+    return;
   }
+  clear_slot_words(slot);
   g_slot_free.push_back(slot);
 }
 }  // namespace
+
+int error_slots_quarantined() {
+  std::lock_guard<std::mutex> lock(g_slot_mu);
+  return static_cast<int>(g_slot_quarantine.size());
+}
+void drain_error_quarantine() { drain_quarantine(); }
 
 int device_error_word(hipStream_t stream, uint32_t** out) {
   *out = nullptr;
@@ -130,7 +194,7 @@ int device_error_word(hipStream_t stream, uint32_t** out) {
 // Forgets `stream`'s slot after the work on it has finished (its pending errors are dropped);
 // `sync` false: the caller knows the stream is idle (thread exit: no HIP call).
 void release_error_slot(hipStream_t stream, bool sync) {
-  if (sync && stream && stream != hipStreamPerThread) (void)hipStreamSynchronize(stream);
+  if (sync) (void)hipStreamSynchronize(stream);   // NULL / hipStreamPerThread: this thread's
   release_key(stream_key(stream));
 }
 
@@ -176,9 +240,10 @@ int take_device_error(hipStream_t stream) {
   const bool lb = take_flag(w, kErrLookBack, nullptr);
   const bool oob = take_flag(w, kErrBounds, &oob_at);
   const bool map = take_flag(w, kErrMapCount, &map_at);
-  uint64_t deep_at = 0;
+  uint64_t deep_at = 0, budget_at = 0;
   const bool deep = take_flag(w, kErrTooDeep, &deep_at);
-  if (!lb && !oob && !map && !deep) return FURY_OK;
+  const bool budget = take_flag(w, kErrBudget, &budget_at);
+  if (!lb && !oob && !map && !deep && !budget) return FURY_OK;
   if (lb) {
     g_err_taken.fetch_add(1);
     return set_error(FURY_ERR_DEVICE,
@@ -196,11 +261,27 @@ int take_device_error(hipStream_t stream) {
                      "encode: " + where_text(deep_at) +
                          " is too large to assemble on chip and the schema is nested deeper than "
                          "the row interpreter reaches; the rows of that call are invalid");
-  return set_error(FURY_ERR_UNSUPPORTED,
-                   "decode: " + where_text(map_at) +
-                       ": map key and value arrays have different element counts "
-                       "(BinaryMap.pointTo); the outputs of that call are invalid");
+  if (map)
+    return set_error(FURY_ERR_UNSUPPORTED,
+                     "decode: " + where_text(map_at) +
+                         ": map key and value arrays have different element counts "
+                         "(BinaryMap.pointTo); the outputs of that call are invalid");
+  return budget_error(where_text(budget_at));
 }
+
+namespace {
+std::atomic<int64_t> g_budget_errors{0};
+}
+int budget_error(const std::string& where) {
+  g_budget_errors.fetch_add(1);
+  return set_error(FURY_ERR_UNSUPPORTED,
+                   "decode budget: " + where +
+                       ": slots alias other bytes of the batch so that decoding would visit more "
+                       "items than the rows hold (a device limit, not a reference exception: "
+                       "the reference would decode such rows); the outputs of that call are "
+                       "invalid");
+}
+int64_t budget_errors() { return g_budget_errors.load(); }
 
 // Pinned staging ring for per-call column tables: the host table is copied into the ring, then
 // DMA-ed to a stream-ordered device allocation on the caller's stream (no host synchronisation);
@@ -812,7 +893,15 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
         st = lv_prepare(s, p->rows, row_offsets, nrows, hs, &p->lv, &totals);
       }
     }
-    if (!st) st = take_device_error(hs);
+    if (!st) {
+      st = take_device_error(hs);
+    } else {
+      // the engine failed on the host (the level engine's element bound): errors its finished
+      // kernels raised on the device come first (out of bounds > map count > budget, as the row
+      // walk reports them), and no flag is left behind for the stream's next call
+      const int e = take_device_error(hs);
+      if (e && st != FURY_ERR_DEVICE) st = e;
+    }
     if (st) {
       if (p->lv) lv_free(p->lv);
       if (p->tree) tree_free(p->tree);
@@ -869,7 +958,9 @@ int fury_trim_workspace(int32_t device) {
   int st = check_hip(hipSetDevice(device), "hipSetDevice");
   if (st) return st;
   release_cached(device);
-  return check_hip(hipSetDevice(cur), "hipSetDevice");
+  st = check_hip(hipSetDevice(cur), "hipSetDevice");
+  if (!st) drain_error_quarantine();
+  return st;
 }
 
 int fury_device_status(void* stream) {
@@ -931,8 +1022,8 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "walk_threads_write") {
-    if (value != 128 && value != 256 && value != 512)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads_write: 128, 256 or 512 (512: no write stage)");
+    if (value != 64 && value != 128 && value != 256 && value != 512)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads_write: 64, 128, 256 or 512 (512: no write stage)");
     set_walk_tuning(6, static_cast<uint32_t>(value));
     return FURY_OK;
   }
@@ -952,8 +1043,8 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "walk_threads") {
-    if (value != 128 && value != 256)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads: 128 or 256");
+    if (value != 64 && value != 128 && value != 256)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_threads: 64, 128 or 256");
     set_walk_tuning(0, static_cast<uint32_t>(value));
     return FURY_OK;
   }
@@ -1022,6 +1113,8 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "host_direct")
     return static_cast<int32_t>(host_direct_count());
   if (key && std::string(key) == "err_slots") return error_slots_in_use();
+  if (key && std::string(key) == "err_slots_quarantined") return error_slots_quarantined();
+  if (key && std::string(key) == "decode_budget_errors") return static_cast<int32_t>(budget_errors());
   if (key && std::string(key) == "var_dec_rows_rejected") return var_dec_rows_rejected();
   if (key && std::string(key) == "unframe_repairs")
     return static_cast<int32_t>(unframe_repair_count());

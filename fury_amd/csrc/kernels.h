@@ -109,17 +109,27 @@ struct VarArgs {
 //   [kErrMapCount], [+2, +3]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
 //   [kErrTooDeep], [+2, +3]   encode: a row too large for on-chip assembly in a schema nested
 //                             deeper than the row interpreter reaches (FURY_ERR_UNSUPPORTED)
+//   [kErrBudget], [+2, +3]    nested decode: a row whose slots alias other bytes so that the row
+//                             walk would visit more than 2 x its bytes + 64 items -- the DEVICE's
+//                             limit, not a reference exception (FURY_ERR_UNSUPPORTED with its own
+//                             message; tuning counter "decode_budget_errors")
 // device_error_word(stream, &w) gives the slot kernels launched on `stream` raise into (NULL if the
 // runtime cannot map host memory; FURY_ERR_DEVICE when every slot is held by a live stream);
 // release_error_slot(stream) frees it before the stream is destroyed; take_device_error(stream) takes that slot only (flag exchanged first,
 // then its location) and sets the thread's last error when one was raised.
-constexpr int kErrWords = 16;
-constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12;
+constexpr int kErrWords = 20;
+constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12, kErrBudget = 16;
 int device_error_word(hipStream_t stream, uint32_t** out);
 void release_error_slot(hipStream_t stream, bool sync = true);
 int error_slots_in_use();
+int error_slots_quarantined();
+void drain_error_quarantine();
 int take_device_error(hipStream_t stream);
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
+// The nested decode's item-budget error (device limit): the status and message every engine
+// reports it with, counted by tuning "decode_budget_errors".
+int budget_error(const std::string& where);
+int64_t budget_errors();
 
 // Cached device workspace (capi.cpp): stream-ordered like hipMallocAsync / hipFreeAsync, without
 // their per-call host cost.

@@ -704,11 +704,14 @@ int64_t* pinned_totals(size_t n) {
   return buf;
 }
 
+// *batch_bytes (when given): the batch's row bytes, offs[nrows], copied with the totals into the
+// same pinned buffer (one word past them).
 int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_t* rows,
-                 const int64_t* offs, hipStream_t hs, int64_t* dev_out, std::vector<int64_t>* out) {
+                 const int64_t* offs, hipStream_t hs, int64_t* dev_out, std::vector<int64_t>* out,
+                 int64_t* batch_bytes) {
   out->assign(list.size(), 0);
   if (list.empty()) return FURY_OK;
-  int64_t* host = pinned_totals(list.size());
+  int64_t* host = pinned_totals(list.size() + 1);
   if (!host) return set_error(FURY_ERR_DEVICE, "hipHostMalloc (decode plan totals)");
   DeviceTable dt;
   LvArgs a;
@@ -721,8 +724,13 @@ int level_totals(const LvPlan& p, const std::vector<int32_t>& list, const uint8_
   if ((st = check_hip(hipMemcpyAsync(host, dev_out, list.size() * 8, hipMemcpyDeviceToHost, hs),
                       "hipMemcpyAsync totals")))
     return st;
+  if (batch_bytes &&
+      (st = check_hip(hipMemcpyAsync(host + list.size(), offs + p.nrows, 8, hipMemcpyDeviceToHost, hs),
+                      "hipMemcpyAsync batch bytes")))
+    return st;
   if ((st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) return st;
   out->assign(host, host + list.size());
+  if (batch_bytes) *batch_bytes = host[list.size()];
   return FURY_OK;
 }
 
@@ -819,20 +827,12 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
                        dim3(kLv), 0, hs, buf, dtab, nseg);
     return check_hip(hipGetLastError(), "segmented scan launch");
   };
-  // The batch's row bytes, read with the first level's totals: a node's elements each own at
-  // least one byte of some row, so more elements than row bytes means slots that alias other bytes
-  // (a malformed batch whose level arrays would grow with the product of the aliased counts).
-  static thread_local int64_t* pin_bytes = nullptr;
-  if (!pin_bytes && hipHostMalloc(reinterpret_cast<void**>(&pin_bytes), 8, hipHostMallocDefault) != hipSuccess)
-    pin_bytes = nullptr;
-  if (pin_bytes) {
-    *pin_bytes = -1;
-    if ((st = check_hip(hipMemcpyAsync(pin_bytes, offs + nrows, 8, hipMemcpyDeviceToHost, hs),
-                        "hipMemcpyAsync batch bytes"))) {
-      lv_free(p);
-      return st;
-    }
-  }
+  // The batch's row bytes, read with every level's totals (one more word of the same pinned copy):
+  // a node's elements each own at least one byte of some row, so more elements than row bytes means
+  // slots that alias other bytes (a malformed batch whose level arrays would grow with the product
+  // of the aliased counts).  Every non-zero total arrives through level_totals, so the check below
+  // always has the byte count it needs.
+  int64_t batch_bytes = -1;
   std::vector<int32_t> strings;                     // STRING / BINARY nodes: bytes at the end
   std::vector<int32_t> cnt = counted_at(0);
   if (!(st = alloc_level(cnt)) && !cnt.empty())
@@ -852,17 +852,16 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
     std::vector<int64_t> tot;
     std::vector<int32_t> ask(arrays);
     if (!arrays.empty()) ask.insert(ask.end(), strings.begin(), strings.end());
-    if ((st = level_totals(*p, ask, rows, offs, hs, dev_tot, &tot))) break;
+    if ((st = level_totals(*p, ask, rows, offs, hs, dev_tot, &tot, &batch_bytes))) break;
     if (!arrays.empty()) {
       for (size_t j = 0; j < strings.size(); j++)
         (*totals)[2 * strings[j] + 1] = tot[arrays.size() + j];
       strings.clear();
     }
-    const int64_t batch_bytes = pin_bytes ? *pin_bytes : -1;     // synchronised by level_totals
     for (size_t j = 0; j < arrays.size() && !st; j++) {
-      if (tot[j] < 0 || (batch_bytes >= 0 && tot[j] > batch_bytes))
-        st = set_error(FURY_ERR_OUT_OF_BOUNDS, "nested decode: more elements than the batch has "
-                                               "row bytes (slots that alias other bytes)");
+      if (tot[j] < 0 || tot[j] > batch_bytes)
+        st = budget_error("nested decode (level engine): more elements of a node than the batch "
+                          "has row bytes");
       const LvNode& n = p->nodes[arrays[j]];
       for (int c = 0; c < n.num_children; c++) p->nodes[n.first_child + c].m = tot[j];
     }
@@ -894,7 +893,7 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
     });
   }
   std::vector<int64_t> bytes;
-  if (!st) st = level_totals(*p, strings, rows, offs, hs, dev_tot, &bytes);
+  if (!st) st = level_totals(*p, strings, rows, offs, hs, dev_tot, &bytes, &batch_bytes);
   if (st) {
     lv_free(p);
     return st;
@@ -902,16 +901,11 @@ int lv_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs, i
   for (int i = 0; i < nn; i++) (*totals)[2 * i] = p->nodes[i].m;
   for (size_t j = 0; j < strings.size(); j++) (*totals)[2 * strings[j] + 1] = bytes[j];
   // payload bytes past the batch's row bytes: strings that alias other bytes (as above)
-  if (pin_bytes && (st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize"))) {
-    lv_free(p);
-    return st;
-  }
-  const int64_t batch_bytes = pin_bytes ? *pin_bytes : -1;
-  for (int i = 0; i < nn && batch_bytes >= 0; i++)
-    if ((*totals)[2 * i + 1] > batch_bytes) {
+  for (int i = 0; i < nn; i++)
+    if ((*totals)[2 * i + 1] > std::max<int64_t>(batch_bytes, 0)) {
       lv_free(p);
-      return set_error(FURY_ERR_OUT_OF_BOUNDS, "nested decode: more payload bytes than the batch "
-                                               "has row bytes (slots that alias other bytes)");
+      return budget_error("nested decode (level engine): more payload bytes of a node than the "
+                          "batch has row bytes");
     }
   *out = p;
   return FURY_OK;

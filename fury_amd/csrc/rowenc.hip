@@ -111,11 +111,11 @@ __device__ __forceinline__ void rappend(P dst, const uint8_t* src, int64_t len) 
   }
 }
 
-template <int D, int MD, bool W, bool DEEP, class P>
+template <int D, int MD, bool W, int DEEP, class P>
 __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
                                        int64_t o1, P buf, int64_t container, int64_t slot,
                                        int64_t& cursor);
-template <bool W, class P>
+template <bool W, int SF, class P>
 __device__ void rdeep(const RwArgs& a, int ni, int64_t idx, P buf, int64_t container, int64_t slot,
                       int es, bool in_array, int64_t bm, int64_t ord, int64_t& cursor);
 
@@ -125,13 +125,14 @@ __device__ void rdeep(const RwArgs& a, int ni, int64_t idx, P buf, int64_t conta
 // memory round trip per entry instead of one per dependent read (the walk is latency-bound).
 // (Issuing entry j + 1's loads before finishing entry j measured slower: more VGPRs, 1.34 ->
 // 1.45 ms build at 4M depth-3 rows.)
-template <int D, int MD, bool W, bool DEEP, class P>
+template <int D, int MD, bool W, int DEEP, class P>
 __device__ __forceinline__ void ritem(const RwArgs& a, int ni, int64_t idx, P buf,
                                       int64_t container, int64_t slot, int es, bool in_array,
                                       int64_t bm, int64_t ord, int64_t& cursor) {
   if constexpr (D >= MD) {
-    // below the inlined levels: the explicit-stack walk (DEEP instances, schemas deeper than MD)
-    if constexpr (DEEP) rdeep<W>(a, ni, idx, buf, container, slot, es, in_array, bm, ord, cursor);
+    // below the inlined levels: the explicit-stack walk (DEEP = its frames; instances for schemas
+    // deeper than MD)
+    if constexpr (DEEP > 0) rdeep<W, DEEP>(a, ni, idx, buf, container, slot, es, in_array, bm, ord, cursor);
     return;
   } else {
     CGNode& n = rn(a, ni);
@@ -214,7 +215,7 @@ __device__ __forceinline__ void relems(CGNode& C, int es, int64_t b, int64_t m, 
 // The image of container entry idx of node ni (type ty: STRUCT, or LIST / MAP with elements
 // [b, b + m) of its child nodes) at buf + start; returns the end of its bytes.  Children at level
 // D + 1.
-template <int D, int MD, bool W, bool DEEP, class P>
+template <int D, int MD, bool W, int DEEP, class P>
 __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_t idx, int64_t b,
                                          int64_t m, P buf, int64_t start) {
   CGNode& n = rn(a, ni);
@@ -263,7 +264,7 @@ __device__ __forceinline__ int64_t rcont(const RwArgs& a, int ni, int ty, int64_
 
 // A non-null, non-scalar entry idx of node ni (level D; o0 / o1: its offsets pair): its bytes at
 // the cursor, its slot (offset from the container, size).
-template <int D, int MD, bool W, bool DEEP, class P>
+template <int D, int MD, bool W, int DEEP, class P>
 __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t idx, int64_t o0,
                                        int64_t o1, P buf, int64_t container, int64_t slot,
                                        int64_t& cursor) {
@@ -297,7 +298,7 @@ __device__ __forceinline__ void rvalue(const RwArgs& a, int ni, int ty, int64_t 
 // Entry r of the batch (generic.hip put_row): a row of the ntop top-level fields, or the
 // top-level BinaryArray / BinaryMap of node 0's entry r (ArrayEncoder.toArray / MapEncoder.toMap,
 // ArrayEncoderBuilder.java:118-140, MapEncoderBuilder.java:152-208).  Returns its size.
-template <bool W, int kRoot, int MD, bool DEEP, class P>
+template <bool W, int kRoot, int MD, int DEEP, class P>
 __device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
   if constexpr (kRoot != 0) {
     const auto offs = gl(rn(a, 0).offsets);
@@ -316,7 +317,7 @@ __device__ __forceinline__ int64_t rrow(const RwArgs& a, int64_t r, P buf) {
   }
 }
 
-template <int kRoot, int MD, bool DEEP>
+template <int kRoot, int MD, int DEEP>
 __global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * kRwThreads + threadIdx.x;
   if (r < a.nrows) a.sizes[r] = rrow<false, kRoot, MD, DEEP>(a, r, static_cast<LdsU8*>(nullptr));
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(kRwThreads) void rw_measure_kernel(RwArgs a) {
 // paths ran both instruction streams one after the other (a 72 KB image on ~75 KB tiles: 2.1 ms
 // per-row vs 1.33 ms when everything fit), and a second image round costs a whole walk latency.
 // Rows past the capacity (encode_measured) are not written.
-template <int NT, int kRoot, int MD, bool DEEP>
+template <int NT, int kRoot, int MD, int DEEP>
 __global__ __launch_bounds__(NT) void rw_encode_kernel(RwArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t img[];
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * a.tile;
@@ -393,11 +394,14 @@ __device__ __forceinline__ int64_t rside(const RwArgs& a, RFrame& f, P buf, int6
   return f.m;
 }
 
-template <bool W, class P>
+// SF frames: one per container level below the inlined ones (rowenc_launch picks the smallest
+// instance that holds the schema's depth, so a 6-level schema does not reserve 64 frames x 88 B of
+// scratch per lane -- ADVICE r5).
+template <bool W, int SF, class P>
 __device__ void rdeep(const RwArgs& a, int ni0, int64_t idx0, P buf, int64_t container0,
                       int64_t slot0, int es0, bool in_array0, int64_t bm0, int64_t ord0,
                       int64_t& cursor) {
-  RFrame st[kMaxNestLevels];
+  RFrame st[SF];
   int sp = -1;
   // one entry (ritem + rvalue): leaves written at once, a container pushed with its first side
   auto enter = [&](int ni, int64_t idx, int64_t container, int64_t slot, int es, bool in_array,
@@ -546,22 +550,25 @@ int rowenc_launch(const GenArgs& g, const int64_t* offs, int64_t* sizes, uint8_t
   };
 #define FURY_RW(R, MD)                                                                         \
   if (g.root == R && nlev <= MD) {                                                             \
-    go(rw_measure_kernel<R, MD, false>, rw_encode_kernel<128, R, MD, false>,                   \
-       rw_encode_kernel<256, R, MD, false>, rw_encode_kernel<512, R, MD, false>);              \
+    go(rw_measure_kernel<R, MD, 0>, rw_encode_kernel<128, R, MD, 0>,                           \
+       rw_encode_kernel<256, R, MD, 0>, rw_encode_kernel<512, R, MD, 0>);                      \
     return check_hip(hipGetLastError(), "row-walk encode launch");                             \
   }
   // deeper schemas: kRowEncMaxDepth inlined levels, then the explicit stack (rdeep)
-#define FURY_RW_DEEP(R)                                                                        \
-  if (g.root == R) {                                                                           \
-    go(rw_measure_kernel<R, kRowEncMaxDepth, true>,                                            \
-       rw_encode_kernel<128, R, kRowEncMaxDepth, true>, rw_encode_kernel<256, R, kRowEncMaxDepth, true>, \
-       rw_encode_kernel<256, R, kRowEncMaxDepth, true>);                                       \
+// (frames: the container levels below the inlined ones, at most nlev - kRowEncMaxDepth)
+#define FURY_RW_DEEP(R, SF)                                                                    \
+  if (g.root == R && nlev - kRowEncMaxDepth <= SF) {                                           \
+    go(rw_measure_kernel<R, kRowEncMaxDepth, SF>,                                              \
+       rw_encode_kernel<128, R, kRowEncMaxDepth, SF>, rw_encode_kernel<256, R, kRowEncMaxDepth, SF>, \
+       rw_encode_kernel<256, R, kRowEncMaxDepth, SF>);                                         \
     return check_hip(hipGetLastError(), "row-walk encode launch");                             \
   }
   FURY_RW(0, 2) FURY_RW(0, 3) FURY_RW(0, 4) FURY_RW(0, 5)
   FURY_RW(1, 2) FURY_RW(1, 3) FURY_RW(1, 4) FURY_RW(1, 5)
   FURY_RW(2, 2) FURY_RW(2, 3) FURY_RW(2, 4) FURY_RW(2, 5)
-  FURY_RW_DEEP(0) FURY_RW_DEEP(1) FURY_RW_DEEP(2)
+  FURY_RW_DEEP(0, 16) FURY_RW_DEEP(1, 16) FURY_RW_DEEP(2, 16)
+  FURY_RW_DEEP(0, kMaxNestLevels - kRowEncMaxDepth) FURY_RW_DEEP(1, kMaxNestLevels - kRowEncMaxDepth)
+  FURY_RW_DEEP(2, kMaxNestLevels - kRowEncMaxDepth)
 #undef FURY_RW_DEEP
 #undef FURY_RW
   return set_error(FURY_ERR_UNSUPPORTED, "row-walk encode: collection root");

@@ -185,7 +185,7 @@ __device__ __forceinline__ bool wcharge(const WCtx& c, int ty, bool valid, uint3
     const int64_t left = static_cast<int64_t>(c.left) - items;
     c.left = static_cast<int32_t>(max<int64_t>(left, -1));
     if (left >= 0) return true;
-    if (left + items >= 0) raise_oob(c.a->err, c.row);
+    if (left + items >= 0) raise_at(c.a->err, kErrBudget, static_cast<uint64_t>(c.row));
     return false;
   }
 }
@@ -739,11 +739,14 @@ int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
   // instances per schema depth (a level of the inlined walk keeps ~30 VGPRs live)
 #define FURY_WALK(MD)                                                                        \
   if (a.nlevels <= MD) {                                                                     \
-    if (!write) nt == 128 ? go(walk_count_kernel<128, MD>) : go(walk_count_kernel<256, MD>); \
+    if (!write) nt == 64 ? go(walk_count_kernel<64, MD>) : nt == 128 ? go(walk_count_kernel<128, MD>) \
+                                                      : go(walk_count_kernel<256, MD>);       \
     else if (a.stage_cap)                                                                    \
-      nt == 128 ? go(walk_write_kernel<128, MD, true>) : go(walk_write_kernel<256, MD, true>); \
+      nt == 64 ? go(walk_write_kernel<64, MD, true>) : nt == 128 ? go(walk_write_kernel<128, MD, true>) \
+                                                  : go(walk_write_kernel<256, MD, true>);     \
     else if (nt == 512) go(walk_write_kernel<512, MD, false>);                               \
-    else nt == 128 ? go(walk_write_kernel<128, MD, false>) : go(walk_write_kernel<256, MD, false>); \
+    else nt == 64 ? go(walk_write_kernel<64, MD, false>) : nt == 128 ? go(walk_write_kernel<128, MD, false>) \
+                                                      : go(walk_write_kernel<256, MD, false>); \
     return check_hip(hipGetLastError(), "walk decode launch");                               \
   }
   FURY_WALK(2)

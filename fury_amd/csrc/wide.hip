@@ -81,6 +81,10 @@ __device__ __forceinline__ WideStage wide_stage(uint8_t* stg, const uint8_t* row
   const int64_t g0 = min<int64_t>(max<int64_t>(gl(offs)[r0], 0), tt);
   const int64_t g1 = min<int64_t>(max<int64_t>(gl(offs)[r0 + nr], g0), tt);
   WideStage s{rows, (LdsC*)(stg), 0, 0};
+  // 16-aligned start: LDS byte 0 = s.lo, so staged reads keep their HBM alignment.  With a rows
+  // pointer that is not 16-aligned the first piece starts up to 15 bytes before the batch -- the
+  // aligned 16-B piece holding its first byte, which never leaves that byte's page (the rule every
+  // kernel's whole-word reads follow); those bytes are never used: staged() admits only [rows+p,..).
   s.lo = reinterpret_cast<uintptr_t>(rows + g0) & ~uintptr_t(15);
   s.hi = min<uintptr_t>(reinterpret_cast<uintptr_t>(rows + g1), s.lo + cap);
   uint32_t at = 0;
@@ -135,14 +139,20 @@ __device__ __forceinline__ int64_t wide_field(const Col& c, int k, const WideSta
   return n;
 }
 
-// len bytes of an 8-byte-aligned source (LDS or HBM, P) to byte q of dst (LDS image or HBM, any
-// alignment): 32-bit words wholly inside the range written whole, the edges byte by byte (the
-// neighbouring bytes belong to other lanes).
+// len bytes of a source (LDS or HBM, P; 8-byte aligned in well-formed rows, any alignment in
+// malformed ones) to byte q of dst (LDS image or HBM, any alignment): 32-bit words wholly inside
+// the range written whole, the edges byte by byte (the neighbouring bytes belong to other lanes).
+// The source is read as ABSOLUTELY aligned 8-byte words (the LDS stage keeps the batch's
+// alignment), so every word read holds a byte of [src, src + len): a misaligned slot ending at the
+// batch's end never reads past it.
 template <class P, class D>
 __device__ __forceinline__ void wcopy(D* dst, int64_t q, P src, int64_t len) {
   if (len <= 0) return;
+  const int a = static_cast<int>(reinterpret_cast<uintptr_t>(src) & 7);
+  src = src - a;                                 // aligned; source byte i = stream byte a + i
   auto sb = [&](int64_t i) -> uint32_t {
-    return static_cast<uint32_t>((ldv<uint64_t>(src + 8 * (i >> 3)) >> (8 * (i & 7))) & 0xff);
+    const int64_t b = a + i;
+    return static_cast<uint32_t>((ldv<uint64_t>(src + 8 * (b >> 3)) >> (8 * (b & 7))) & 0xff);
   };
   const int64_t end = q + len;
   const int64_t w0 = (q + 3) >> 2, w1 = end >> 2;
@@ -154,7 +164,7 @@ __device__ __forceinline__ void wcopy(D* dst, int64_t q, P src, int64_t len) {
   const int64_t d = 4 * w0 - q;
   auto d32 = reinterpret_cast<DstT<D, uint32_t>*>(dst);
   for (int64_t w = w0; w < w1; w++) {
-    const int64_t si = d + 4 * (w - w0);
+    const int64_t si = a + d + 4 * (w - w0);
     const int64_t j = si >> 3;
     const int o = static_cast<int>(si & 7);
     uint64_t x = ldv<uint64_t>(src + 8 * j) >> (8 * o);

@@ -314,6 +314,12 @@ int fury_trim_workspace(int32_t device);
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);
 
+/* ---- measurement (no reference equivalent) ------------------------------------------------ */
+/* Same-device streaming copy of `bytes` (a positive multiple of 16 KB) from src to dst (device,
+ * 16-byte aligned) with 16-B non-temporal loads / stores, asynchronous on `stream`: the box's
+ * achievable copy rate, which bench.py reports beside the codec's roofline fraction. */
+int fury_hbm_copy(void* dst, const void* src, int64_t bytes, void* stream);
+
 /* ---- framing (Encoders.java:201-213 / 165-182) ------------------------------------------ */
 /* Writes the stream RowEncoder.encode(MemoryBuffer, T) produces for each row in turn:
  * [int32 len = 8 + rowSize][int64 schemaHash][row bytes].  frame_offsets (device, nrows+1)

@@ -101,6 +101,10 @@ def lib():
                                               ctypes.POINTER(_CColumn), ctypes.c_int64,
                                               ctypes.c_void_p]
         L.fo_type_width.restype = ctypes.c_int32
+        L.fo_last_flags.restype = ctypes.c_int32
+        L.fo_count_walk.restype = ctypes.c_int32
+        L.fo_count_walk.argtypes = [ctypes.POINTER(_CField), ctypes.c_int32, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_int64]
         _lib = L
     return _lib
 
@@ -307,3 +311,39 @@ def decode(fields: Sequence[F], rows: np.ndarray, row_offsets: Optional[np.ndarr
     if st != 0:
         raise RuntimeError(f"oracle decode failed with status {st}")
     return [_trim(f, c, nrows) for f, c in zip(fields, outs)]
+
+
+# Decode errors (row_oracle.c FO_ERR_*): the reference's exception each stands for
+ERR_OOB, ERR_MAP, ERR_BUDGET = 1, 2, 4
+
+
+def decode_checked(fields: Sequence[F], rows: np.ndarray, row_offsets: Optional[np.ndarray],
+                   nrows: int, with_validity: bool = True):
+    """The decode with the reference's bounds rule (row_oracle.c header: MemoryBuffer.checkPosition
+    / get / slice / copyToUnsafe restated per container): returns (flags, columns) -- flags the
+    ERR_* bits found (ERR_OOB = IndexOutOfBoundsException, ERR_MAP = BinaryMap.pointTo's
+    UnsupportedOperationException); columns None when any was found (the reference throws).  The
+    batch must not alias itself beyond what count_walk_flags admits (nested schemas: call that
+    first; it bounds the walk)."""
+    keep: list = []
+    cf = _c_fields(fields, keep)
+    cur = np.zeros(len(_nodes_dfs(fields)) + 1, np.int64)
+    lib().fo_decode_batch_cur(cf, len(fields), _ptr(rows), _ptr(row_offsets), nrows,
+                              _c_columns([_shape_only(f) for f in fields], keep), cur.ctypes.data)
+    flags = int(lib().fo_last_flags())
+    if flags:
+        return flags, None
+    return 0, decode(fields, rows, row_offsets, nrows, with_validity)
+
+
+def count_walk_flags(fields: Sequence[F], rows: np.ndarray, row_offsets: np.ndarray,
+                     nrows: int) -> int:
+    """ERR_* bits of the device row walk's COUNT pass (fury_decode_prepare), restated in
+    row_oracle.c fo_count_walk: the container checks over the nodes that hold or contain a
+    counted slot, and the per-row item budget (ERR_BUDGET: a device limit)."""
+    keep: list = []
+    if nrows == 0:
+        return 0
+    offs = np.ascontiguousarray(row_offsets, np.int64)
+    return int(lib().fo_count_walk(_c_fields(fields, keep), len(fields), _ptr(rows), _ptr(offs),
+                                   nrows))

@@ -17,6 +17,22 @@
  * out zeroed bytes, like a fresh heap buffer), BinaryRowWriter / BinaryArrayWriter on top of it
  * sharing BinaryWriter's var-length append, and the generated toRow's per-field dispatch
  * (BaseBinaryEncoderBuilder.serializeFor) driven by Arrow-style input columns.
+ *
+ * Decode bounds (round 6, the reference's rule restated): every read of the batch is checked
+ * against the batch buffer as MemoryBuffer does -- checkPosition(index, pos, length) throws
+ * IndexOutOfBoundsException unless 0 <= index and index + length <= size
+ * (CORE/memory/MemoryBuffer.java:303-309), get(index, dst, 0, size) / slice(offset, size) for a
+ * payload (:311-325, :2515-2518), and copyToUnsafe's checkArgument over a primitive array's whole
+ * element range (:2451-2455, reached from BinaryArray.toXxxArray, FMT/row/binary/BinaryArray.java:
+ * 157-197, which the generated fromRow calls for primitive arrays, BaseBinaryEncoderBuilder.java:
+ * 655-670).  Restated at container granularity, the way the device checks it: a row's / struct's
+ * null bitmap + slots, an array's header + null bitmap + element slots, a map's key-size word and
+ * both arrays, a STRING / BINARY payload, a DECIMAL's 16 bytes -- each checked whole when the decode
+ * reaches it (a per-entry getter reads a subset of that range; a container that passes is read
+ * without further checks).  A negative element count is an error too (BinaryArray.pointTo's
+ * assert, :71; new byte[size] / new long[n] throw NegativeArraySizeException).  A value that fails
+ * decodes as null and sets FO_ERR_OOB; map key / value arrays of different lengths set FO_ERR_MAP
+ * (BinaryMap.pointTo, FMT/row/binary/BinaryMap.java:73-75, UnsupportedOperationException).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -393,6 +409,80 @@ int64_t fo_encode_batch(const fury_field* fields, int32_t nfields, const fury_co
  * Output variable-length buffers (values of STRING/BINARY, child columns of LIST/MAP) are
  * appended at the cursors in `cur` — one cursor per column node, depth first.
  * ---------------------------------------------------------------------------------------- */
+/* Decode context: the batch (bounds), the errors found (FO_ERR_* bits), and the count walk's
+ * per-row item budget (fo_count_walk). */
+#define FO_ERR_OOB 1
+#define FO_ERR_MAP 2
+#define FO_ERR_BUDGET 4
+static const uint8_t* g_rows;     /* batch base                 */
+static int64_t g_total;           /* batch bytes                */
+static int32_t g_flags;           /* FO_ERR_* seen              */
+
+/* MemoryBuffer.checkPosition / get / slice restated over [0, g_total): 0 <= p, 0 <= len,
+ * p + len <= size (MemoryBuffer.java:303-309). */
+static int fo_span_ok(int64_t p, int64_t len) { return p >= 0 && len >= 0 && len <= g_total - p; }
+
+/* A BinaryArray at p with elements of es bytes: header word read (getInt64, BinaryArray.pointTo
+ * :69-78), numElements >= 0, the null bitmap and the whole element range inside the batch
+ * (copyToUnsafe :2451-2455).  Returns numElements, or -1 (and FO_ERR_OOB). */
+static int64_t fo_array_ok(int64_t p, int32_t es) {
+  if (!fo_span_ok(p, 8)) { g_flags |= FO_ERR_OOB; return -1; }
+  int64_t m = (int32_t)fo_get_i64(g_rows + p);
+  if (m < 0 || !fo_span_ok(p, 8 + fo_bitmap_bytes(m) + m * (int64_t)es)) {
+    g_flags |= FO_ERR_OOB;
+    return -1;
+  }
+  return m;
+}
+
+static int32_t fo_elem_size(const fury_field* f) {
+  int32_t w = fo_type_width(f->type_id);
+  return w < 0 ? 8 : w;
+}
+
+/* The checked position of a non-null non-scalar value of field f whose slot word is oas, in a
+ * container starting at cont; *count = LIST / MAP elements.  -1: decode as null (the error is
+ * recorded). */
+static int64_t fo_value_pos(const fury_field* f, int64_t cont, int64_t oas, int64_t* count) {
+  int64_t pos = cont + (int32_t)(oas >> 32);
+  int32_t size = (int32_t)oas;
+  *count = 0;
+  switch (f->type_id) {
+    case FURY_TYPE_STRING: case FURY_TYPE_BINARY:
+      if (!fo_span_ok(pos, size)) { g_flags |= FO_ERR_OOB; return -1; }
+      *count = size;
+      return pos;
+    case FURY_TYPE_DECIMAL:
+      if (!fo_span_ok(pos, 16)) { g_flags |= FO_ERR_OOB; return -1; }
+      return pos;
+    case FURY_TYPE_STRUCT:
+      if (!fo_span_ok(pos, fo_bitmap_bytes(f->num_children) + 8LL * f->num_children)) {
+        g_flags |= FO_ERR_OOB;
+        return -1;
+      }
+      return pos;
+    case FURY_TYPE_LIST: {
+      int64_t m = fo_array_ok(pos, fo_elem_size(&f->children[0]));
+      if (m < 0) return -1;
+      *count = m;
+      return pos;
+    }
+    case FURY_TYPE_MAP: {        /* BinaryMap.pointTo :62-77 */
+      if (!fo_span_ok(pos, 8)) { g_flags |= FO_ERR_OOB; return -1; }
+      int64_t kb = (int32_t)fo_get_i64(g_rows + pos);
+      int64_t nk = kb >= 0 ? fo_array_ok(pos + 8, fo_elem_size(&f->children[0])) : -1;
+      int64_t nv = kb >= 0 ? fo_array_ok(pos + 8 + kb, fo_elem_size(&f->children[1])) : -1;
+      if (kb < 0) g_flags |= FO_ERR_OOB;
+      if (nk < 0 || nv < 0) return -1;
+      if (nk != nv) { g_flags |= FO_ERR_MAP; return -1; }
+      *count = nk;
+      return pos;
+    }
+    default:
+      return pos;
+  }
+}
+
 typedef struct fo_view {          /* a BinaryRow or BinaryArray pointed at bytes */
   const uint8_t* base;
   int64_t header;                 /* bytes before the slots                   */
@@ -427,21 +517,20 @@ static int32_t fo_node_count(const fury_field* f) {
 
 static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f,
                           fury_column* c, int64_t out_i, int64_t* cur, int32_t node);
+static void fo_null_entry(const fury_field* f, fury_column* c, int64_t out_i, int64_t* cur,
+                          int32_t node);
 
-static void fo_read_array(const uint8_t* base, const fury_field* elem, fury_column* child,
-                          int64_t* cur, int32_t child_node, int32_t list_node, int32_t* count) {
-  /* BinaryArray.pointTo :69-78 */
-  int64_t n = (int32_t)fo_get_i64(base);
+/* The n elements of a checked BinaryArray at batch position p (BinaryArray.pointTo :69-78). */
+static void fo_read_array(int64_t p, int64_t n, const fury_field* elem, fury_column* child,
+                          int64_t* cur, int32_t child_node, int32_t list_node) {
   fo_view av;
-  av.base = base;
+  av.base = g_rows + p;
   av.bytes_before_bitmap = 8;
   av.header = 8 + fo_bitmap_bytes(n);
-  int32_t width = fo_type_width(elem->type_id);
-  av.elem_size = width < 0 ? 8 : width;
+  av.elem_size = fo_elem_size(elem);
   int64_t start = cur[list_node];
   for (int64_t j = 0; j < n; j++) fo_read_value(&av, j, elem, child, start + j, cur, child_node);
   cur[list_node] = start + n;
-  *count = (int32_t)n;
 }
 
 /* A null entry out_i of node `node` (ArrowWriter appendNull, FMT/vectorized/ArrowWriter.java:
@@ -479,14 +568,15 @@ static void fo_null_entry(const fury_field* f, fury_column* c, int64_t out_i, in
   }
 }
 
+/* Entry `ordinal` of the checked container v (its null bit and slot lie inside it). */
 static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f,
                           fury_column* c, int64_t out_i, int64_t* cur, int32_t node) {
   int is_null = fo_view_is_null(v, ordinal);
-  fo_set_valid(c, out_i, !is_null);
   int32_t width = fo_type_width(f->type_id);
   const uint8_t* slot = fo_view_slot(v, ordinal);
-  switch (f->type_id) {
-    case FURY_TYPE_BOOL: {                    /* getBoolean: byte != 0 */
+  if (width > 0) {
+    fo_set_valid(c, out_i, !is_null);
+    if (f->type_id == FURY_TYPE_BOOL) {      /* getBoolean: byte != 0 */
       uint8_t* bits = (uint8_t*)c->values;
       int bit = !is_null && slot[0] != 0;
       if (!bits) return;
@@ -494,62 +584,43 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
       else bits[out_i >> 3] &= (uint8_t)~(1u << (out_i & 7));
       return;
     }
-    case FURY_TYPE_INT8: case FURY_TYPE_INT16: case FURY_TYPE_INT32: case FURY_TYPE_INT64:
-    case FURY_TYPE_FLOAT32: case FURY_TYPE_FLOAT64: case FURY_TYPE_DATE32:
-    case FURY_TYPE_TIMESTAMP: {
-      if (!c->values) return;
-      uint8_t* dst = (uint8_t*)c->values + out_i * width;
-      if (is_null) memset(dst, 0, (size_t)width);
-      else memcpy(dst, slot, (size_t)width);
-      return;
-    }
+    if (!c->values) return;
+    uint8_t* dst = (uint8_t*)c->values + out_i * width;
+    if (is_null) memset(dst, 0, (size_t)width);
+    else memcpy(dst, slot, (size_t)width);
+    return;
+  }
+  int64_t count = 0;
+  int64_t pos = is_null ? -1 : fo_value_pos(f, v->base - g_rows, fo_get_i64(slot), &count);
+  if (pos < 0) {                              /* null, or decoded as null after a failed check */
+    fo_null_entry(f, c, out_i, cur, node);
+    return;
+  }
+  fo_set_valid(c, out_i, 1);
+  switch (f->type_id) {
     case FURY_TYPE_STRING: case FURY_TYPE_BINARY: {   /* getBinary :118-131 */
       int64_t start = cur[node];
-      int32_t size = 0;
-      if (!is_null) {
-        int64_t oas = fo_get_i64(slot);
-        int32_t rel = (int32_t)(oas >> 32);
-        size = (int32_t)oas;
-        if (c->values) memcpy((uint8_t*)c->values + start, v->base + rel, (size_t)size);
-      }
+      if (c->values) memcpy((uint8_t*)c->values + start, g_rows + pos, (size_t)count);
       if (c->offsets) {
         c->offsets[out_i] = (int32_t)start;
-        c->offsets[out_i + 1] = (int32_t)(start + size);
+        c->offsets[out_i + 1] = (int32_t)(start + count);
       }
-      cur[node] = start + size;
+      cur[node] = start + count;
       return;
     }
-    case FURY_TYPE_DECIMAL: {
-      if (!c->values) return;
-      uint8_t* dst = (uint8_t*)c->values + out_i * 16;
-      if (is_null) memset(dst, 0, 16);
-      else memcpy(dst, v->base + (int32_t)(fo_get_i64(slot) >> 32), 16);
+    case FURY_TYPE_DECIMAL:
+      if (c->values) memcpy((uint8_t*)c->values + out_i * 16, g_rows + pos, 16);
       return;
-    }
-    case FURY_TYPE_LIST: {                    /* getArray :168-178 */
-      int32_t count = 0;
+    case FURY_TYPE_LIST:                      /* getArray :168-178 */
       if (c->offsets) c->offsets[out_i] = (int32_t)cur[node];
-      if (!is_null) {
-        int64_t oas = fo_get_i64(slot);
-        fo_read_array(v->base + (int32_t)(oas >> 32), &f->children[0], c->child, cur, node + 1,
-                      node, &count);
-      }
+      fo_read_array(pos, count, &f->children[0], c->child, cur, node + 1, node);
       if (c->offsets) c->offsets[out_i + 1] = (int32_t)cur[node];
       return;
-    }
     case FURY_TYPE_STRUCT: {                  /* getStruct :148-166 */
       /* child columns are row-aligned with the parent (Arrow struct) */
       int32_t child_node = node + 1;
-      if (is_null) {                          /* StructWriter.appendNull :577-584 */
-        for (int k = 0; k < f->num_children; k++) {
-          fo_null_entry(&f->children[k], &c->child[k], out_i, cur, child_node);
-          child_node += fo_node_count(&f->children[k]);
-        }
-        return;
-      }
-      int64_t oas = fo_get_i64(slot);
       fo_view rv;
-      rv.base = v->base + (int32_t)(oas >> 32);
+      rv.base = g_rows + pos;
       rv.bytes_before_bitmap = 0;
       rv.header = fo_bitmap_bytes(f->num_children);
       rv.elem_size = 8;
@@ -563,25 +634,99 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
       int32_t key_node = node + 1;
       int32_t val_node = key_node + fo_node_count(&f->children[0]);
       if (c->offsets) c->offsets[out_i] = (int32_t)cur[node];
-      if (!is_null) {
-        int64_t oas = fo_get_i64(slot);
-        const uint8_t* mb = v->base + (int32_t)(oas >> 32);
-        int64_t key_bytes = fo_get_i64(mb);
-        int32_t nk = 0, nv = 0;
-        int64_t saved = cur[node];
-        fo_read_array(mb + 8, &f->children[0], &c->child[0], cur, key_node, node, &nk);
-        cur[node] = saved;
-        fo_read_array(mb + 8 + key_bytes, &f->children[1], &c->child[1], cur, val_node, node, &nv);
-        if (nk != nv) g_err = FURY_ERR_UNSUPPORTED;   /* BinaryMap.java:73-75 */
-      }
+      int64_t key_bytes = (int32_t)fo_get_i64(g_rows + pos);
+      int64_t saved = cur[node];
+      fo_read_array(pos + 8, count, &f->children[0], &c->child[0], cur, key_node, node);
+      cur[node] = saved;
+      fo_read_array(pos + 8 + key_bytes, count, &f->children[1], &c->child[1], cur, val_node, node);
       if (c->offsets) c->offsets[out_i + 1] = (int32_t)cur[node];
       return;
     }
     default:
+      g_flags |= FO_ERR_OOB;
       g_err = FURY_ERR_UNSUPPORTED;
-      (void)width;
       return;
   }
+}
+
+/* ------------------------------------------------------------------------------------------
+ * The device's two-phase nested decode (fury_decode_prepare, then fury_decode_execute) reports
+ * the errors of its COUNT walk first: a walk of each row over the nodes that hold or contain a
+ * counted slot (LIST / MAP elements, STRING / BINARY bytes -- walk.hip TNode.walk), with the same
+ * container checks and a per-row item budget of 2 x the row's bytes + 64 (a row the encoder wrote
+ * holds every item in its own bytes; a corrupted row whose slots alias other bytes would make the
+ * walk grow with the product of the aliased counts).  fo_count_walk restates that walk exactly
+ * (walk.hip walk_row / wvalue / wcharge) so a test can predict which error the prepare reports;
+ * FO_ERR_BUDGET is the device's own limit, not a reference exception.
+ * ---------------------------------------------------------------------------------------- */
+static int fo_walks(const fury_field* f) {
+  if (f->type_id == FURY_TYPE_STRING || f->type_id == FURY_TYPE_BINARY ||
+      f->type_id == FURY_TYPE_LIST || f->type_id == FURY_TYPE_MAP)
+    return 1;
+  for (int i = 0; i < f->num_children; i++)
+    if (fo_walks(&f->children[i])) return 1;
+  return 0;
+}
+
+static int64_t g_left;            /* the row's remaining item budget (-1: spent) */
+
+static int fo_charge(const fury_field* f, int valid, int64_t m) {
+  int64_t items = f->type_id == FURY_TYPE_MAP ? 2 * m
+                  : (f->type_id == FURY_TYPE_STRUCT && !valid) ? 0 : m;
+  int64_t left = g_left - items;
+  int64_t was = g_left;
+  g_left = left > -1 ? left : -1;
+  if (left >= 0) return 1;
+  if (was >= 0) g_flags |= FO_ERR_BUDGET;
+  return 0;
+}
+
+static void fo_cwalk(const fury_field* f, int nul, int64_t oas, int64_t cont) {
+  int64_t count = 0;
+  int64_t pos = nul ? -1 : fo_value_pos(f, cont, oas, &count);
+  int valid = pos >= 0;
+  int ty = f->type_id;
+  int strc = ty == FURY_TYPE_STRUCT;
+  if (!strc && ty != FURY_TYPE_LIST && ty != FURY_TYPE_MAP) return;
+  int64_t m = strc ? (valid ? f->num_children : 0) : count;
+  if (!fo_charge(f, valid, m)) m = 0;
+  int64_t hb = fo_bitmap_bytes(strc ? f->num_children : m);
+  int sides = ty == FURY_TYPE_MAP ? 2 : 1;
+  for (int sd = 0; sd < sides; sd++) {
+    int64_t arr = pos;
+    if (ty == FURY_TYPE_MAP && m > 0)
+      arr = sd == 0 ? pos + 8 : pos + 8 + (int32_t)fo_get_i64(g_rows + pos);
+    if (!strc && !fo_walks(&f->children[sd])) continue;
+    for (int64_t j = 0; j < m; j++) {
+      const fury_field* cf = strc ? &f->children[j] : &f->children[sd];
+      if (fo_type_width(cf->type_id) > 0 || !fo_walks(cf)) continue;
+      int64_t cbm = strc ? pos : arr + 8;
+      int64_t cslot = strc ? pos + hb + 8 * j : arr + 8 + hb + 8 * j;
+      int cnul = (g_rows[cbm + (j >> 3)] >> (j & 7)) & 1;
+      fo_cwalk(cf, cnul, fo_get_i64(g_rows + cslot), strc ? pos : arr);
+    }
+  }
+}
+
+int32_t fo_count_walk(const fury_field* fields, int32_t nfields, const uint8_t* rows,
+                      const int64_t* row_offsets, int64_t nrows) {
+  g_rows = rows;
+  g_total = row_offsets[nrows];
+  g_flags = 0;
+  int64_t hb = fo_bitmap_bytes(nfields);
+  for (int64_t i = 0; i < nrows; i++) {
+    int64_t base = row_offsets[i];
+    int64_t budget = 2 * (row_offsets[i + 1] - base) + 64;
+    g_left = budget < (1 << 30) ? budget : (1 << 30);
+    int rowok = fo_span_ok(base, hb + 8LL * nfields);
+    if (!rowok) g_flags |= FO_ERR_OOB;
+    for (int k = 0; k < nfields; k++) {
+      if (fo_type_width(fields[k].type_id) > 0 || !fo_walks(&fields[k])) continue;
+      int nul = !rowok || ((rows[base + (k >> 3)] >> (k & 7)) & 1);
+      fo_cwalk(&fields[k], nul, rowok ? fo_get_i64(rows + base + hb + 8 * k) : 0, base);
+    }
+  }
+  return g_flags;
 }
 
 /* Decode rows [row_offsets[i], row_offsets[i+1]) (or i * fixed_size when row_offsets is NULL)
@@ -606,22 +751,35 @@ int fo_decode_batch_cur(const fury_field* fields, int32_t nfields, const uint8_t
   int64_t* cur = (int64_t*)calloc((size_t)(nodes + 1), sizeof(int64_t));
   if (!cur) return FURY_ERR_ENCODER;
   int32_t fixed = fo_bitmap_bytes(nfields) + 8 * nfields;
+  g_rows = rows;
+  g_total = row_offsets ? row_offsets[nrows] : nrows * (int64_t)fixed;
+  g_flags = 0;
   for (int64_t i = 0; i < nrows; i++) {
     fo_view rv;
-    rv.base = rows + (row_offsets ? row_offsets[i] : i * (int64_t)fixed);
+    int64_t base = row_offsets ? row_offsets[i] : i * (int64_t)fixed;
+    rv.base = rows + base;
     rv.bytes_before_bitmap = 0;
     rv.header = fo_bitmap_bytes(nfields);
     rv.elem_size = 8;
+    /* the row's null bitmap + slots inside the batch (getInt64 / isNullAt of every field) */
+    int rowok = fo_span_ok(base, fixed);
+    if (!rowok) g_flags |= FO_ERR_OOB;
     int32_t node = 0;
     for (int k = 0; k < nfields; k++) {
-      fo_read_value(&rv, k, &fields[k], &cols[k], i, cur, node);
+      if (rowok) fo_read_value(&rv, k, &fields[k], &cols[k], i, cur, node);
+      else fo_null_entry(&fields[k], &cols[k], i, cur, node);
       node += fo_node_count(&fields[k]);
     }
   }
   if (cur_out) memcpy(cur_out, cur, (size_t)nodes * sizeof(int64_t));
   free(cur);
-  return g_err;
+  if (g_err) return g_err;
+  return (g_flags & FO_ERR_OOB) ? FURY_ERR_OUT_OF_BOUNDS
+         : (g_flags & FO_ERR_MAP) ? FURY_ERR_UNSUPPORTED : 0;
 }
+
+/* FO_ERR_* bits of the last fo_decode_batch(_cur) / fo_count_walk call. */
+int32_t fo_last_flags(void) { return g_flags; }
 
 /* Convenience used by the CPU baseline: fixed-width schemas only, tight loop over the same
  * restated writer (toRow semantics, rows written straight into `out` which the caller zeroed).

@@ -402,3 +402,82 @@ def test_error_slots_recycle_past_1024_streams(oracle, dev):
         for h in live:
             drop(h)
     assert L.fury_get_tuning(b"err_slots") == base
+
+
+@pytest.mark.gpu
+def test_thread_exit_slot_quarantine(oracle, dev):
+    """a thread that launches a failing decode on the null stream (torch's default) and
+    exits without synchronising leaves its error slot QUARANTINED, not free: the kernel may still
+    be running and raise into it.  New streams never receive it while it is quarantined; when
+    the free slots run out the library synchronises the devices, drops the late error and reuses
+    the slot -- a clean call on the stream that then gets it reports nothing."""
+    import ctypes
+    import threading
+    from fury_amd import _native as N
+    from fury_amd.encoder import IndexOutOfBoundsException
+    hip = ctypes.CDLL("libamdhip64.so")
+    L = N.lib()
+    fields = SCHEMAS["mixed"]
+    n = 300
+    enc, host, rows, offs = _encode(oracle, fields, n, 6, dev, null_pct=10, str_max=30)
+    i, k = _victim(fields, rows, offs, n, {T.STRING})
+    bad = _batch(enc, _corrupt(fields, rows, offs, n, i, k, "offset_past_end"), offs, n, dev)
+    good = _batch(enc, rows, offs, n, dev)
+    cols = enc.decode_batch(good)
+    torch.cuda.synchronize()
+    assert L.fury_trim_workspace(0) == 0              # start with an empty quarantine
+    assert L.fury_get_tuning(b"err_slots_quarantined") == 0
+    base = L.fury_get_tuning(b"err_slots")
+
+    def worker():
+        torch.cuda.set_device(dev)
+        null = torch.cuda.ExternalStream(0, device=dev)
+        try:      # raises on the device; the call may or may not see it before the thread exits
+            enc._decode(bad, True, False, null, None, "bound")
+        except IndexOutOfBoundsException:
+            pass
+
+    t = threading.Thread(target=worker)
+    t.start()
+    t.join()
+    # join() returns when the Python thread state is gone; the OS thread's C++ thread_local
+    # destructors (which quarantine the slot) run just after
+    import time
+    deadline = time.time() + 10
+    while L.fury_get_tuning(b"err_slots_quarantined") < 1 and time.time() < deadline:
+        time.sleep(0.01)
+    assert L.fury_get_tuning(b"err_slots") == base
+    assert L.fury_get_tuning(b"err_slots_quarantined") == 1
+
+    def new_stream():
+        h = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(h)) == 0
+        return h, torch.cuda.ExternalStream(h.value, device=dev)
+
+    live = []
+    try:
+        # clean calls on new streams while the slot is quarantined: none of them sees the error
+        for _ in range(8):
+            h, s = new_stream()
+            live.append(h)
+            enc.decode_into(good, cols, s)
+            enc.device_status(s)
+        # take every never-used / free slot; the next stream drains the quarantine and gets the
+        # quarantined slot, with the late error dropped
+        while L.fury_get_tuning(b"err_slots") < 1024 - 1:
+            h, s = new_stream()
+            live.append(h)
+            enc.decode_into(good, cols, s)
+        assert L.fury_get_tuning(b"err_slots_quarantined") == 1
+        h, s = new_stream()
+        live.append(h)
+        enc.decode_into(good, cols, s)
+        enc.device_status(s)
+        assert L.fury_get_tuning(b"err_slots_quarantined") == 0
+        assert L.fury_get_tuning(b"err_slots") == 1024
+    finally:
+        torch.cuda.synchronize()
+        for h in live:
+            assert L.fury_stream_release(h) == 0
+            assert hip.hipStreamDestroy(h) == 0
+    assert L.fury_get_tuning(b"err_slots") == base

@@ -1,9 +1,19 @@
-"""Corrupted rows of random schemas through every decode path on the device: random bytes of a
-well-formed batch overwritten (the row offsets stay valid), decoded by the flat kernels, the row
-walk and the level engine.  Each decode either succeeds or raises IndexOutOfBoundsException /
-UnsupportedOperationException; nothing reads outside the batch (guard bytes after it), nothing
-hangs (the walk's item budget, the level engine's element bound), and the stream is clean
-afterwards (the intact rows decode to the oracle's columns).  Marked gpu."""
+"""Corrupted rows of random schemas, device against the oracle's bounds rule.  Random bytes of a
+well-formed batch are overwritten (the row offsets stay valid) and the batch is decoded by the
+flat kernels, the row walk and the level engine.  Per trial the oracle -- the reference's decode
+bounds rule restated in row_oracle.c (MemoryBuffer.checkPosition / get / slice / copyToUnsafe,
+java/fury-core/.../memory/MemoryBuffer.java:303-309,2451-2455,2515-2518, per container) --
+predicts the outcome and the device must produce it:
+  * the oracle raises IndexOutOfBoundsException (or the map-count UnsupportedOperationException,
+    BinaryMap.java:73-75) -> the device raises the same exception;
+  * the oracle decodes -> the device decodes to identical columns, or raises the nested decode's
+    item-budget error (a device limit with its own message, never a bounds error: rows whose slots
+    alias other bytes).  The row walk's budget is restated too (fo_count_walk), so for the walk the
+    budget error is predicted exactly; the level engine bounds each node's elements by the batch's
+    bytes instead and may report it for rows the walk's budget admits.
+The batch sits in a buffer with 0xAB guard bytes after it: a read past the batch would show as a
+difference from the oracle, which never reads there.  The stream is clean afterwards (the intact
+rows decode to the oracle's columns).  Marked gpu."""
 from __future__ import annotations
 
 import numpy as np
@@ -13,7 +23,10 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
+from fury_amd import types as T  # noqa: E402
 from tests.helpers import assert_columns_equal  # noqa: E402
+
+COUNTED = (T.STRING, T.BINARY, T.LIST, T.MAP)
 
 
 @pytest.fixture(scope="module")
@@ -26,8 +39,42 @@ def _decode(enc, batch):
     from fury_amd.encoder import column_to_host
     if enc.nested:
         from tests.test_tree import _decode_plan
-        return _decode_plan(enc, batch)
-    return [column_to_host(c) for c in enc.decode_batch(batch)]
+        cols = _decode_plan(enc, batch)
+    else:
+        cols = [column_to_host(c) for c in enc.decode_batch(batch)]
+    enc.device_status()                      # errors the execute raised asynchronously
+    return cols
+
+
+def _shape(fields):
+    """(levels, counted nodes) of a schema: the row walk takes <= 5 levels, <= 64 counted nodes."""
+    def walk(f, d):
+        lv, k = d + 1, int(f.type_id in COUNTED)
+        for c in f.children:
+            a, b = walk(c, d + 1)
+            lv, k = max(lv, a), k + b
+        return lv, k
+    lv, k = 0, 0
+    for f in fields:
+        a, b = walk(f, 0)
+        lv, k = max(lv, a), k + b
+    return lv, k
+
+
+def _expected(O, fields, nested, walk, rows, offs, n):
+    """What the device must report: "oob", "map", "budget", "any" (the level engine on a batch
+    the walk's budget refuses: the oracle's full walk of it is not bounded), or the oracle's
+    columns."""
+    if nested:
+        cw = O.count_walk_flags(fields, rows, offs, n)
+        if walk and cw:                              # the walk's prepare reports these
+            return "oob" if cw & O.ERR_OOB else "map" if cw & O.ERR_MAP else "budget"
+        if cw & O.ERR_BUDGET:
+            return "any"
+    flags, cols = O.decode_checked(fields, rows, offs, n)
+    if flags:
+        return "oob" if flags & O.ERR_OOB else "map"
+    return cols
 
 
 @pytest.mark.parametrize("seed", list(range(24)))
@@ -35,6 +82,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
     from fury_amd import _native as N
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, IndexOutOfBoundsException, UnsupportedOperationException
+    from oracle import oracle as O
     from tests.test_bounds import _batch
     from tests.test_tree import _beans, _random_schema
     rng = np.random.default_rng(9000 + seed)
@@ -46,8 +94,10 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
     rows = rows.copy()
     offs = np.asarray(offs, np.int64).copy()
     ref = oracle.decode(fields, rows, offs, n)
+    levels, counted = _shape(fields)
     L = N.lib()
     old = L.fury_get_tuning(b"nested_decode")
+    seen = []
     try:
         for trial in range(3):
             bad = rows.copy()
@@ -56,11 +106,29 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
                 bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
             for mode in ((2, 1) if enc.nested else (2,)):
                 L.fury_set_tuning(b"nested_decode", mode)
+                walk = mode == 2 and levels <= 5 and counted <= 64
+                want = _expected(O, fields, enc.nested, walk, bad, offs, n)
                 try:
-                    _decode(enc, _batch(enc, bad, offs, n, dev))
-                except (IndexOutOfBoundsException, UnsupportedOperationException):
-                    pass
+                    got = _decode(enc, _batch(enc, bad, offs, n, dev))
+                    err = None
+                except IndexOutOfBoundsException:
+                    err = "oob"
+                except UnsupportedOperationException as e:
+                    err = "budget" if "decode budget" in str(e) else "map"
+                where = f"trial {trial}, engine {'walk' if walk else 'levels'}"
+                seen.append(err or "decoded")
+                if want == "any" or (err == "budget" and not walk):
+                    # the level engine's own bound (elements of a node vs the batch's bytes) is
+                    # checked level by level and may pre-empt errors in deeper levels
+                    continue
+                if isinstance(want, str):
+                    assert err == want, f"{where}: oracle says {want}, device {err or 'decoded'}"
+                elif err is not None:
+                    raise AssertionError(f"{where}: oracle decodes, device raises {err}")
+                else:
+                    assert_columns_equal(fields, got, want, n)
         L.fury_set_tuning(b"nested_decode", 2)
         assert_columns_equal(fields, _decode(enc, _batch(enc, rows, offs, n, dev)), ref, n)
     finally:
         L.fury_set_tuning(b"nested_decode", old)
+    print(f"seed {seed}: {seen}")

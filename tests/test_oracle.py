@@ -244,3 +244,92 @@ def test_null_struct_chain_decode(oracle):
         cols = beans_to_columns(fields, beans)
         rows, offs = oracle.encode(fields, cols, n)
         assert_columns_equal(fields, oracle.decode(fields, rows, offs, n), cols, n)
+
+
+def test_oracle_decode_bounds_rule():
+    """The oracle's decode checks every container against the batch as the reference's
+    MemoryBuffer does (row_oracle.c header): a STRING slot past the end, a negative element
+    count, a struct header past the end and map arrays of different lengths are each reported
+    (ERR_OOB / ERR_MAP) instead of read; the intact batch decodes with no flag."""
+    from oracle import oracle as O
+    from fury_amd import types as T
+    from fury_amd.beans import beans_to_columns
+    inner = [T.field("a", T.INT32), T.field("s", T.STRING)]
+    fields = [T.field("s", T.STRING), T.array_field("l", T.INT64), T.struct_field("st", inner),
+              T.map_field("m", T.field("key", T.STRING), T.field("value", T.INT32))]
+    beans = [{"s": "hello", "l": [1, 2, 3], "st": {"a": 1, "s": "x"}, "m": [("k", 1), ("j", 2)]}
+             for _ in range(3)]
+    host = beans_to_columns(fields, beans)
+    rows, offs = O.encode(fields, host, 3)
+    flags, cols = O.decode_checked(fields, rows, offs, 3)
+    assert flags == 0 and cols is not None
+    assert O.count_walk_flags(fields, rows, offs, 3) == 0
+    hb, last = 8, int(offs[2])
+    total = int(offs[3])
+
+    def slot(k):
+        return last + hb + 8 * k
+
+    def put(buf, at, v):
+        buf[at:at + 8] = np.frombuffer(np.int64(v).tobytes(), np.uint8)
+
+    def word(buf, at):
+        return int(np.frombuffer(buf[at:at + 8].tobytes(), np.int64)[0])
+
+    # STRING payload past the batch
+    bad = rows.copy()
+    put(bad, slot(0), ((total - last) << 32) | 16)
+    assert O.decode_checked(fields, bad, offs, 3)[0] == O.ERR_OOB
+    # negative element count of the list
+    bad = rows.copy()
+    arr = last + (word(rows, slot(1)) >> 32)
+    put(bad, arr, -2)
+    assert O.decode_checked(fields, bad, offs, 3)[0] == O.ERR_OOB
+    assert O.count_walk_flags(fields, bad, offs, 3) == O.ERR_OOB
+    # struct header straddling the end of the batch
+    bad = rows.copy()
+    put(bad, slot(2), ((total - 8 - last) << 32) | 24)
+    assert O.decode_checked(fields, bad, offs, 3)[0] == O.ERR_OOB
+    # map: the value array claims one element fewer than the key array
+    bad = rows.copy()
+    mp = last + (word(rows, slot(3)) >> 32)
+    vals = mp + 8 + word(rows, mp)
+    put(bad, vals, 1)
+    assert O.decode_checked(fields, bad, offs, 3)[0] == O.ERR_MAP
+    assert O.count_walk_flags(fields, bad, offs, 3) == O.ERR_MAP
+
+
+def test_oracle_count_walk_budget():
+    """The row walk's item budget, restated (fo_count_walk): a list of lists whose inner slots all
+    alias one long inner array visits m x k items from a row of far fewer bytes -> ERR_BUDGET; the
+    full decode (no budget) of the same rows still succeeds."""
+    from oracle import oracle as O
+    from fury_amd import types as T
+    from fury_amd.beans import beans_to_columns
+    fields = [T.Field("ll", T.LIST, True, (T.Field("item", T.LIST, True, (T.field("item", T.INT64),)),))]
+    beans = [{"ll": [list(range(60)), [1]]}]
+    host = beans_to_columns(fields, beans)
+    rows, offs = O.encode(fields, host, 1)
+    assert O.count_walk_flags(fields, rows, offs, 1) == 0
+    # outer array at rel offset from the row's slot; element 1's slot -> element 0's inner array
+    outer = int(np.frombuffer(rows[8:16].tobytes(), np.int64)[0]) >> 32   # row-relative
+    m = int(np.frombuffer(rows[outer:outer + 8].tobytes(), np.int64)[0])
+    assert m == 2
+    slots = outer + 8 + 8
+    s0 = int(np.frombuffer(rows[slots:slots + 8].tobytes(), np.int64)[0])
+    # the outer count raised to 40 elements, all of them pointing at inner array 0 (60 items):
+    # the elements' slots must lie inside the row, so reuse the row's own bytes as slots
+    bad = np.zeros(len(rows) + 40 * 8 + 64, np.uint8)
+    bad[:len(rows)] = rows
+    offs2 = np.array([0, len(bad)], np.int64)
+    newarr = len(rows)
+    bad[newarr:newarr + 8] = np.frombuffer(np.int64(40).tobytes(), np.uint8)
+    for j in range(40):
+        at = newarr + 8 + 8 + 8 * j
+        rel0 = (s0 >> 32) + outer - newarr                  # element slots are array-relative
+        bad[at:at + 8] = np.frombuffer(np.int64((rel0 << 32) | (s0 & 0xffffffff)).tobytes(), np.uint8)
+    slot = (np.int64(newarr - 0) << 32) | np.int64(8 + 8 + 8 * 40)
+    bad[8:16] = np.frombuffer(np.int64(slot).tobytes(), np.uint8)
+    assert O.count_walk_flags(fields, bad, offs2, 1) == O.ERR_BUDGET
+    flags, cols = O.decode_checked(fields, bad, offs2, 1)
+    assert flags == 0 and int(cols[0].offsets[1]) == 40
