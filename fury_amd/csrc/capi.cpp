@@ -53,9 +53,11 @@ void release_key(uintptr_t k, bool quarantine = false);
 
 // Per-thread keys of the null stream and of hipStreamPerThread (odd: never a stream handle, which
 // is aligned); their slots are quarantined when the thread exits.
+std::atomic<int> g_thread_key_exits{0};   // ThreadKeys destructors run (diagnostics)
 struct ThreadKeys {
   char null_key = 0, per_thread_key = 0;
   ~ThreadKeys() {
+    g_thread_key_exits.fetch_add(1);
     release_key(reinterpret_cast<uintptr_t>(&null_key) | 1, true);
     release_key(reinterpret_cast<uintptr_t>(&per_thread_key) | 1, true);
   }
@@ -133,7 +135,10 @@ int error_slot(uintptr_t k, bool assign) {
   return assign_slot_locked(k);
 }
 
+std::atomic<uintptr_t> g_last_assigned_key{0};   // diagnostics ("err_slot_last_key")
+
 int assign_slot_locked(uintptr_t k) {
+  g_last_assigned_key = k;
   int slot = -1;
   if (!g_slot_free.empty()) {
     slot = g_slot_free.back();
@@ -171,6 +176,13 @@ void release_key(uintptr_t k, bool quarantine) {
 }
 }  // namespace
 
+int thread_key_exits() { return g_thread_key_exits.load(); }
+// 0: a stream handle, 1: a thread's null-stream key, 2: a thread's hipStreamPerThread key
+int last_assigned_key_kind() {
+  const uintptr_t k = g_last_assigned_key.load();
+  if (!(k & 1)) return 0;
+  return 1;   // (both thread keys are odd; which one is not distinguished)
+}
 int error_slots_quarantined() {
   std::lock_guard<std::mutex> lock(g_slot_mu);
   return static_cast<int>(g_slot_quarantine.size());
@@ -219,6 +231,9 @@ int64_t device_error_count() {
 // entry (err_where_entry).
 static std::string where_text(uint64_t w) {
   if (!(w >> 63)) return "row " + std::to_string(w);
+  if ((w >> 62) & 1)           // err_where_tile: a nested entry of the tile that starts at a row
+    return "schema node " + std::to_string((w >> 40) & 0x3fffff) + " in the rows from row " +
+           std::to_string(w & ((1ull << 40) - 1));
   return "schema node " + std::to_string((w >> 40) & 0x7fffff) + ", Arrow entry " +
          std::to_string(w & ((1ull << 40) - 1));
 }
@@ -243,7 +258,13 @@ int take_device_error(hipStream_t stream) {
   uint64_t deep_at = 0, budget_at = 0;
   const bool deep = take_flag(w, kErrTooDeep, &deep_at);
   const bool budget = take_flag(w, kErrBudget, &budget_at);
-  if (!lb && !oob && !map && !deep && !budget) return FURY_OK;
+  uint64_t internal_at = 0;
+  const bool internal = take_flag(w, kErrInternal, &internal_at);
+  if (!lb && !oob && !map && !deep && !budget && !internal) return FURY_OK;
+  if (internal)
+    return set_error(FURY_ERR_DEVICE, "decode: the tile from " + where_text(internal_at) +
+                                          " outgrew its on-chip plan (internal error); the outputs "
+                                          "of that call are invalid");
   if (lb) {
     g_err_taken.fetch_add(1);
     return set_error(FURY_ERR_DEVICE,
@@ -519,7 +540,8 @@ int fixed_args(const fury_schema* s, const fury_column* cols, int64_t nrows, boo
 }
 
 int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool decode,
-             bool need_validity, VarArgs* a, DeviceTable* dt, hipStream_t hs) {
+             bool need_validity, VarArgs* a, DeviceTable* dt, hipStream_t hs,
+             bool shape_only = false) {
   if (s->num_fields > kMaxWideVarCols)
     return set_error(FURY_ERR_UNSUPPORTED, "variable-length device path handles at most " +
                                                std::to_string(kMaxWideVarCols) + " fields");
@@ -533,7 +555,8 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
   int nvar = 0;
   for (int k = 0; k < s->num_fields; k++) {
     const FieldPlan& p = s->plan[k];
-    const fury_column& c = cols[k];
+    static const fury_column kNoColumn{};
+    const fury_column& c = shape_only ? kNoColumn : cols[k];
     VarCol& v = wide ? tab[k] : a->col[k];
     const std::string who = "column " + std::to_string(k) + " (" + s->fields[k].name + ")";
     v.kind = p.kind;
@@ -549,7 +572,7 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
       case kBool:
         v.width = p.kind == kBool ? 0 : p.width;
         v.values = static_cast<const uint8_t*>(c.values);
-        if (nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
+        if (!shape_only && nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
         if (v.width > 1 && misaligned(c.values, v.width))
           return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values misaligned");
         break;
@@ -559,21 +582,21 @@ int var_args(const fury_schema* s, const fury_column* cols, int64_t nrows, bool 
         v.offsets = c.offsets;
         v.var_slot = nvar++;
         v.capacity = c.values ? c.capacity : 0;
-        if (nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
+        if (!shape_only && nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
         break;
       case kDecimal:
         v.width = 16;
         v.values = static_cast<const uint8_t*>(c.values);
         v.var_slot = nvar++;
-        if (nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
+        if (!shape_only && nrows > 0 && !c.values) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": values is null");
         break;
       case kListFixed: {
         v.width = p.elem_type == FURY_TYPE_BOOL ? 0 : p.elem_width;
         v.offsets = c.offsets;
         v.var_slot = nvar++;
-        if (nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
+        if (!shape_only && nrows > 0 && !c.offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": offsets is null");
         if (!c.child) {
-          if (!decode || nrows > 0)
+          if (!shape_only && (!decode || nrows > 0))
             return set_error(FURY_ERR_INVALID_ARGUMENT, who + ": list needs a child column");
         } else {
           v.values = static_cast<const uint8_t*>(c.child->values);
@@ -881,7 +904,35 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   p->offs = row_offsets;
   p->nrows = nrows;
   std::vector<int64_t> totals(2 * nn, 0);
-  if (nrows > 0) {
+  // flat variable-length schemas of 17-256 fields: the wide kernels' count pass + scan, kept for
+  // the execute (the tile bases), one host sync for the sequence fields' totals
+  const bool wide = nrows > 0 && !s->generic && !s->is_fixed && s->num_fields > 16 /* kRegCols: the register-staged kernels below */ &&
+                    s->num_fields <= kMaxWideVarCols && var_wide_mode();
+  if (wide) {
+    VarArgs a;
+    DeviceTable dt;
+    std::vector<int64_t> seq;
+    int st = var_args(s, nullptr, nrows, true, false, &a, &dt, hs, true);
+    if (!st) {
+      p->wide = new WidePlan();
+      st = wide_prepare(a, p->rows, row_offsets, hs, p->wide, &seq);
+    }
+    if (!st) st = take_device_error(hs);
+    if (st) {
+      if (p->wide) wide_free(p->wide);
+      delete p;
+      return st;
+    }
+    int q = 0;
+    for (int k = 0; k < s->num_fields; k++) {
+      totals[2 * k] = nrows;
+      const int kind = s->plan[k].kind;
+      if (kind != kBytes && kind != kListFixed) continue;
+      if (kind == kBytes) totals[2 * k + 1] = seq[q];
+      else totals[2 * s->nodes[k].first_child] = seq[q];
+      q++;
+    }
+  } else if (nrows > 0) {
     // both engines synchronise `stream`: rows whose values leave the batch are reported here.
     // The tile-staged engine first; the level engine when it declines the batch.
     int st = tree_prepare(s, p->rows, row_offsets, nrows, hs, &p->tree, &totals);
@@ -933,6 +984,13 @@ int fury_decode_execute(fury_decode_plan* p, fury_column* cols, int32_t arrow, v
     return st;
   }
   const GenNode* outs = g.tab ? reinterpret_cast<const GenNode*>(dt.host.data()) : g.node;
+  if (p->wide) {
+    VarArgs a;
+    DeviceTable vdt;
+    st = var_args(p->schema, cols, p->nrows, true, arrow != 0, &a, &vdt, hs);
+    if (st) return st;
+    return wide_execute(a, p->rows, p->offs, hs, *p->wide);
+  }
   if (p->tree) return tree_execute(p->tree, outs, p->rows, p->offs, p->totals, hs);
   return lv_execute(p->lv, outs, p->rows, p->offs, hs);
 }
@@ -941,6 +999,7 @@ void fury_decode_plan_destroy(fury_decode_plan* p) {
   if (!p) return;
   if (p->lv) lv_free(p->lv);
   if (p->tree) tree_free(p->tree);
+  if (p->wide) wide_free(p->wide);
   if (p->owned) dev_free(p->owned, static_cast<hipStream_t>(p->owned_stream));
   if (p->owned_stream) {
     release_error_slot(static_cast<hipStream_t>(p->owned_stream));
@@ -988,9 +1047,28 @@ int fury_set_tuning(const char* key, int32_t value) {
     return FURY_OK;
   }
   if (std::string(key) == "nested_decode") {
-    if (value < 1 || value > 2)
-      return set_error(FURY_ERR_INVALID_ARGUMENT, "nested_decode: 1 (level engine) or 2 (row walk)");
+    if (value < 1 || value > 4)
+      return set_error(FURY_ERR_INVALID_ARGUMENT,
+                       "nested_decode: 1 (level engine), 2 (row walk, level engine beyond it), 3 (row "
+                       "walk, tile BFS beyond it) or 4 (tile BFS)");
     set_tree_mode(value);
+    return FURY_OK;
+  }
+  if (std::string(key) == "bfs_threads") {
+    if (value != 64 && value != 128 && value != 256 && value != 512)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, "bfs_threads: 64, 128, 256 or 512");
+    set_bfs_tuning(0, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "bfs_rows") {
+    if (value < 1 || value > 4096) return set_error(FURY_ERR_INVALID_ARGUMENT, "bfs_rows: 1..4096");
+    set_bfs_tuning(1, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
+  if (std::string(key) == "bfs_stage" || std::string(key) == "bfs_arena") {
+    if (value < 0 || value > 128 * 1024)
+      return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 0..131072 bytes (0: auto)");
+    set_bfs_tuning(std::string(key) == "bfs_stage" ? 2 : 3, static_cast<uint32_t>(value));
     return FURY_OK;
   }
   if (std::string(key) == "var_dec_cover") {
@@ -1089,6 +1167,11 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "lookback_help") return lookback_help_mode();
   if (key && std::string(key) == "unframe") return unframe_mode();
   if (key && std::string(key) == "nested_decode") return tree_mode();
+  if (key && std::string(key) == "bfs_threads") return static_cast<int32_t>(bfs_tuning(0));
+  if (key && std::string(key) == "bfs_rows") return static_cast<int32_t>(bfs_tuning(1));
+  if (key && std::string(key) == "bfs_stage") return static_cast<int32_t>(bfs_tuning(2));
+  if (key && std::string(key) == "bfs_arena") return static_cast<int32_t>(bfs_tuning(3));
+  if (key && std::string(key) == "bfs_fallbacks") return static_cast<int32_t>(bfs_tuning(4));
   if (key && std::string(key) == "rowenc_rows") return static_cast<int32_t>(rowenc_tuning(0));
   if (key && std::string(key) == "rowenc_img") return static_cast<int32_t>(rowenc_tuning(1));
   if (key && std::string(key) == "rowenc_tile") return static_cast<int32_t>(rowenc_tuning(2));
@@ -1114,6 +1197,8 @@ int32_t fury_get_tuning(const char* key) {
     return static_cast<int32_t>(host_direct_count());
   if (key && std::string(key) == "err_slots") return error_slots_in_use();
   if (key && std::string(key) == "err_slots_quarantined") return error_slots_quarantined();
+  if (key && std::string(key) == "thread_key_exits") return thread_key_exits();
+  if (key && std::string(key) == "err_slot_last_key") return last_assigned_key_kind();
   if (key && std::string(key) == "decode_budget_errors") return static_cast<int32_t>(budget_errors());
   if (key && std::string(key) == "var_dec_rows_rejected") return var_dec_rows_rejected();
   if (key && std::string(key) == "unframe_repairs")

@@ -66,7 +66,7 @@ struct fury_schema {
 };
 
 // Decode plan of the two-step (nested) decode, device and host-memory flavours.
-namespace fury { struct LvPlan; struct TreePlan; }
+namespace fury { struct LvPlan; struct TreePlan; struct WidePlan; }
 
 struct fury_decode_plan {
   const fury_schema* schema = nullptr;
@@ -75,6 +75,7 @@ struct fury_decode_plan {
   int64_t nrows = 0;
   fury::LvPlan* lv = nullptr;      // level-by-level engine state (levels.hip); NULL when nrows = 0
   fury::TreePlan* tree = nullptr;  // tile-staged engine state (tree.hip): used when set
+  fury::WidePlan* wide = nullptr;  // flat schemas of 17-256 fields (wide.hip): used when set
   bool arrow = false;
   std::vector<int64_t> totals;     // per node: Arrow entries, payload bytes
   void* owned = nullptr;           // host flavour: the staged rows + offsets (device memory)

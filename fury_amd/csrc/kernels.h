@@ -109,6 +109,8 @@ struct VarArgs {
 //   [kErrMapCount], [+2, +3]  map key / value arrays of different lengths (FURY_ERR_UNSUPPORTED)
 //   [kErrTooDeep], [+2, +3]   encode: a row too large for on-chip assembly in a schema nested
 //                             deeper than the row interpreter reaches (FURY_ERR_UNSUPPORTED)
+//   [kErrInternal], [+2, +3]  a decode plan the device could not follow (tile BFS: a write tile
+//                             whose records outgrew the arena its count pass fitted) (FURY_ERR_DEVICE)
 //   [kErrBudget], [+2, +3]    nested decode: a row whose slots alias other bytes so that the row
 //                             walk would visit more than 2 x its bytes + 64 items -- the DEVICE's
 //                             limit, not a reference exception (FURY_ERR_UNSUPPORTED with its own
@@ -117,12 +119,15 @@ struct VarArgs {
 // runtime cannot map host memory; FURY_ERR_DEVICE when every slot is held by a live stream);
 // release_error_slot(stream) frees it before the stream is destroyed; take_device_error(stream) takes that slot only (flag exchanged first,
 // then its location) and sets the thread's last error when one was raised.
-constexpr int kErrWords = 20;
-constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12, kErrBudget = 16;
+constexpr int kErrWords = 24;
+constexpr int kErrLookBack = 0, kErrBounds = 4, kErrMapCount = 8, kErrTooDeep = 12, kErrBudget = 16,
+              kErrInternal = 20;
 int device_error_word(hipStream_t stream, uint32_t** out);
 void release_error_slot(hipStream_t stream, bool sync = true);
 int error_slots_in_use();
 int error_slots_quarantined();
+int thread_key_exits();
+int last_assigned_key_kind();
 void drain_error_quarantine();
 int take_device_error(hipStream_t stream);
 int64_t device_error_count();        // failures raised so far (taken or pending), no sync
@@ -147,6 +152,15 @@ void dev_free(void* p, hipStream_t stream);
 __device__ __forceinline__ bool span_ok(int64_t p, int64_t len, int64_t total) {
   return p >= 0 && len >= 0 && len <= total - p;
 }
+// A workgroup barrier that orders LDS only: every wave's LDS / scalar operations complete, then
+// s_barrier.  __syncthreads() adds a workgroup-scope release / acquire fence, which also waits
+// for every outstanding GLOBAL store and atomic of the wave -- a tile whose column stores are in
+// flight then waits out their HBM write latency at the barrier.  Use this one where the barrier
+// only hands LDS data between waves (never after LDS-DMA, whose completion is counted by vmcnt).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // The location is one 64-bit store (concurrent raisers never mix halves), made visible before the
 // flag by a release store of the flag; stores only -- no atomics over PCIe.
 __device__ __forceinline__ void raise_at(uint32_t* err, int slot, uint64_t where) {
@@ -198,6 +212,19 @@ void set_var_wide_mode(int v);
 int wide_threads(bool encode);        // tuning "wide_threads" / "wide_enc_threads" (var.hip)
 void set_wide_threads(bool encode, int v);
 // offsets_only: fury_row_decode_measure (the Arrow offsets of the variable-length fields only)
+// Plan form of the wide decode (fury_decode_prepare / _execute): the count pass + scan once, the
+// per-tile bases kept for the write pass.
+struct WidePlan {
+  int64_t* ws = nullptr;
+  int64_t nt = 0;
+  int nseq = 0;
+  hipStream_t stream = nullptr;
+};
+int wide_prepare(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
+                 WidePlan* wp, std::vector<int64_t>* seq_totals);
+int wide_execute(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
+                 const WidePlan& wp);
+void wide_free(WidePlan* wp);
 int launch_decode_wide(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
                        bool offsets_only);
 int launch_encode_wide(const VarArgs& a, const int64_t* offs, uint8_t* rows, int64_t cap,
@@ -271,7 +298,9 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
 int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                  const std::vector<int64_t>& totals, hipStream_t hs);
 void tree_free(TreePlan* p);
-void set_tree_mode(int v);           // tuning "nested_decode": 1 levels, 2 row walk (default)
+void set_tree_mode(int v);           // tuning "nested_decode": 1 levels, 2 row walk, 3 tile BFS (default)
+void set_bfs_tuning(int which, uint32_t v);   // bfs_threads / bfs_rows / bfs_stage / bfs_arena
+int64_t bfs_tuning(int which);                // ... and 4: bfs_fallbacks
 int tree_mode();
 int set_tree_debug(int on);          // tuning "tree_debug": phase accumulators on / off
 // tunings of the row-walk decode (walk.hip): 0 "walk_threads" (128 / 256 rows per tile),

@@ -102,7 +102,20 @@ int tree_host_width(int32_t t) {
   }
 }
 
-std::atomic<int> g_tree_mode = 2;             // tuning "nested_decode": 1 level engine, 2 row walk
+// tuning "nested_decode": 1 level engine; 2 row walk (the level engine past its limits); 3 row walk,
+// tile BFS (bfs.hip) past its limits (default); 4 tile BFS always (A/B, tests).  The BFS falls back
+// to the walk / level engine for a batch whose tiles overflow its arena.  At depth 3 the walk is
+// 2x faster than the BFS (profiles/r06_bfs_legs.jsonl: the BFS's per-node chain of LDS round
+// trips runs at ~1.5 waves per SIMD, bounded by the LDS its staged tiles take); past the walk's
+// limits the BFS replaces the level engine where it measured faster.
+std::atomic<int> g_tree_mode = 3;
+// Tile BFS defaults (tunings "bfs_threads", "bfs_rows", "bfs_stage" (0: sized from the batch's
+// average row), "bfs_arena" (0: 60 % of the stage + 2 KB)).
+std::atomic<int> g_bfs_threads = 128;
+std::atomic<int> g_bfs_rows = 128;
+std::atomic<uint32_t> g_bfs_stage{0};
+std::atomic<uint32_t> g_bfs_arena{0};
+std::atomic<int64_t> g_bfs_fallbacks{0};      // batches whose tiles overflowed the arena
 // Row-walk defaults from scripts/ab_generic.py legs at 4M depth-3 rows: 128-row count tiles with
 // a 12 KB stage (prepare 1.35 -> 1.08 ms: more tiles resident), 256-row write tiles (1.87 -> 1.78
 // ms) with the prefetch; round 5: 512-row unstaged write tiles with 24 KB output windows (1.67 ->
@@ -123,6 +136,17 @@ uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (dev
 }  // namespace
 
 void set_tree_mode(int v) { g_tree_mode = v; }
+void set_bfs_tuning(int which, uint32_t v) {
+  if (which == 0) g_bfs_threads = static_cast<int>(v);
+  else if (which == 1) g_bfs_rows = static_cast<int>(v);
+  else if (which == 2) g_bfs_stage = (v + 15) & ~15u;
+  else g_bfs_arena = (v + 15) & ~15u;
+}
+int64_t bfs_tuning(int which) {
+  return which == 0 ? g_bfs_threads.load() : which == 1 ? g_bfs_rows.load()
+         : which == 2 ? static_cast<int64_t>(g_bfs_stage.load())
+         : which == 3 ? static_cast<int64_t>(g_bfs_arena.load()) : g_bfs_fallbacks.load();
+}
 uint64_t* tree_debug_buffer() { return g_tree_dbg; }
 int set_tree_debug(int on) {
   if (on && !g_tree_dbg) {
@@ -168,6 +192,11 @@ struct TreePlan {
   int32_t K = 0, nt = 0, ntw = 0;   // count / write tile rows
   uint32_t pool_cap = 0, out_cap = 0;  // write pass: bitmap-window / output-window LDS bytes
   int32_t knode[kWalkMaxK] = {};
+  int32_t lvl[kMaxLevels + 1] = {};   // first node of each level
+  // tile BFS (bfs.hip)
+  bool bfs = false;
+  int32_t bnt = 0;                 // threads per tile
+  uint32_t arena_cap = 0;
 };
 
 void tree_free(TreePlan* p) {
@@ -205,14 +234,97 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.K = p.K;
   a.pool_cap = p.pool_cap;
   a.out_cap = write ? p.out_cap : 0;
-  for (int k = 0; k < p.K; k++) a.knode[k] = p.knode[k];
+  for (int k = 0; k < p.K && k < kWalkMaxK; k++) a.knode[k] = p.knode[k];   // (the walk only)
   a.ctr = p.nt;
+  if (p.bfs) {
+    for (int L = 0; L <= p.nlevels && L <= kMaxLevels; L++) a.lvl[L] = p.lvl[L];
+    a.trows = p.tile_rows;
+    a.arena_cap = p.arena_cap;
+    a.stage_cap = p.stage_cap;
+    a.prefetch = 0;
+    return bfs_launch(a, p.bnt, write, hs);
+  }
   a.tmul = write ? p.ntw / p.nt : 1;
   if (write) a.ntiles = (p.nrows + p.ntw - 1) / p.ntw;
   return walk_launch(a, write ? p.ntw : p.nt, write, hs);
 }
 
 }  // namespace
+
+// Tile BFS prepare: pass 1 + tile scan + the host sync for the totals.  p->bfs stays false (FURY_OK)
+// when a tile's records outgrow the arena (the caller falls back to the row walk / level engine).
+// The stage is sized from the batch's average row (one more 8-byte read: the batch's bytes).
+int bfs_prepare(TreePlan* p, const uint8_t* rows, const int64_t* offs, int64_t nrows,
+                hipStream_t hs, int64_t* pin, std::vector<int64_t>* totals) {
+  const int nn = static_cast<int>(p->nodes.size());
+  int st = check_hip(hipMemcpyAsync(pin + 2 * kTreeMaxNodes + 1, offs + nrows, 8,
+                                    hipMemcpyDeviceToHost, hs), "hipMemcpyAsync batch bytes");
+  if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+  if (st) return st;
+  const int64_t bytes = std::max<int64_t>(pin[2 * kTreeMaxNodes + 1], 0);
+  const int nt = g_bfs_threads.load();
+  const double avg = static_cast<double>(bytes) / static_cast<double>(nrows);
+  DeviceTable dt;
+  st = upload_table(p->nodes.data(), p->nodes.size() * sizeof(TNode), hs, &dt);
+  if (st) return st;
+  // A tile whose records outgrow the arena is retried with half the rows and a larger arena share
+  // (container-heavy rows need ~16 B of records per container entry); after three tries the batch
+  // goes to the row walk / level engine.
+  for (int attempt = 0; attempt < 3; attempt++) {
+    const int trows = std::max(1, g_bfs_rows.load() >> attempt);
+    if (attempt > 0 && trows < 16) break;
+    uint32_t stage = g_bfs_stage.load();
+    if (!stage)
+      stage = static_cast<uint32_t>(std::min<double>(std::max<double>(avg * trows * 1.05 + 64, 2048), 64 * 1024));
+    stage = (stage + 15) & ~15u;
+    uint32_t arena = g_bfs_arena.load();
+    if (!arena)
+      arena = ((static_cast<uint32_t>((attempt == 0 ? 0.6 : 1.5) * stage) + 2048) + 15) & ~15u;
+    while (bfs_lds(nn, nt, stage, arena, trows) > kWalkLdsMax && arena > 1024) arena /= 2;
+    while (bfs_lds(nn, nt, stage, arena, trows) > kWalkLdsMax && stage > 1024) stage /= 2;
+    p->tile_rows = trows;
+    p->bnt = nt;
+    p->stage_cap = stage;
+    p->arena_cap = arena;
+    p->ntiles = (nrows + trows - 1) / trows;
+    p->stride = p->ntiles + 1;
+    int64_t* tot = nullptr;
+    int32_t* overflow = nullptr;
+    if (!st) st = dev_alloc(8 * nn * p->stride, hs, reinterpret_cast<void**>(&p->cnt));
+    if (!st) st = dev_alloc(8 * nn * p->stride, hs, reinterpret_cast<void**>(&p->byt));
+    if (!st) st = dev_alloc(8 * (2 * nn + 2), hs, reinterpret_cast<void**>(&tot));
+    if (!st) {
+      overflow = reinterpret_cast<int32_t*>(tot + 2 * nn);
+      st = check_hip(hipMemsetAsync(overflow, 0, 8, hs), "hipMemsetAsync");
+    }
+    p->bfs = true;                          // (tree_launch dispatches on it)
+    if (!st) st = tree_launch(*p, false, static_cast<const TNode*>(dt.dev), rows, offs, overflow, hs);
+    if (!st) {
+      hipLaunchKernelGGL(tree_tile_scan, dim3(static_cast<unsigned>(2 * nn)), dim3(kScanT), 0, hs,
+                         p->cnt, p->byt, p->ntiles, p->stride, nn, tot);
+      st = check_hip(hipGetLastError(), "tree scan launch");
+    }
+    if (!st) st = check_hip(hipMemcpyAsync(pin, tot, 8 * (2 * nn + 1), hipMemcpyDeviceToHost, hs),
+                            "hipMemcpyAsync totals");
+    if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+    const bool over = !st && reinterpret_cast<const int32_t*>(pin + 2 * nn)[0] != 0;
+    if (!st && !over) {
+      totals->assign(2 * nn, 0);
+      for (int i = 0; i < nn; i++) {
+        (*totals)[2 * i] = pin[i];
+        (*totals)[2 * i + 1] = pin[nn + i];
+      }
+    }
+    dev_free(tot, hs);
+    if (!st && !over) return FURY_OK;
+    p->bfs = false;
+    dev_free(p->cnt, hs);
+    dev_free(p->byt, hs);
+    p->cnt = p->byt = nullptr;
+    if (st) return st;
+  }
+  return FURY_OK;                           // p->bfs false: the caller falls back
+}
 
 // Pass 1 + tile scan + the one host sync.  *out stays NULL (FURY_OK) when the batch needs the
 // level engine: schema beyond the tree tables, or a row whose arrays do not fit the arena.
@@ -228,7 +340,9 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     const int t = s->nodes[i].type_id;
     if (t == FURY_TYPE_LIST || t == FURY_TYPE_MAP || t == FURY_TYPE_STRING || t == FURY_TYPE_BINARY) K++;
   }
-  if (K > kWalkMaxK || s->depth > kWalkMaxDepth) return FURY_OK;   // the level engine
+  const bool walk_ok = K <= kWalkMaxK && s->depth <= kWalkMaxDepth;
+  const bool bfs_ok = !s->root && (g_tree_mode == 4 || (g_tree_mode == 3 && !walk_ok));
+  if (!walk_ok && !bfs_ok) return FURY_OK;                          // the level engine
   TreePlan* p = new TreePlan();
   p->K = K;
   p->stream = hs;
@@ -263,7 +377,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
       const bool counted = n.type == FURY_TYPE_LIST || n.type == FURY_TYPE_MAP ||
                            n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY;
       n.k = counted ? k++ : -1;
-      if (counted) p->knode[n.k] = i;
+      if (counted && n.k < kWalkMaxK) p->knode[n.k] = i;
       if (i < s->num_fields) n.ek = -1;
       for (int j = 0; j < n.num_children; j++)
         p->nodes[n.first_child + j].ek = n.type == FURY_TYPE_STRUCT ? n.ek : n.k;
@@ -275,6 +389,11 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     }
   }
   for (int i = 0; i < nn; i++) p->nlevels = std::max(p->nlevels, level[i] + 1);
+  // breadth-first numbering: each level's nodes are contiguous
+  for (int L = 0, i = 0; L <= p->nlevels && L <= kMaxLevels; L++) {
+    while (i < nn && level[i] < L) i++;
+    p->lvl[L] = i;
+  }
   // pinned landing zone of the totals: one per host thread, kept (a hipHostMalloc / hipHostFree
   // pair per call cost more host time than the small kernels)
   static thread_local int64_t* pin = nullptr;
@@ -291,6 +410,19 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     pin_words = 2 * kTreeMaxNodes + 2;
   }
   int st = FURY_OK;
+  if (bfs_ok) {
+    st = bfs_prepare(p, rows, offs, nrows, hs, pin, totals);
+    if (st || p->bfs) {                   // a plan, or an error
+      if (st) tree_free(p);
+      else *out = p;
+      return st;
+    }
+    g_bfs_fallbacks.fetch_add(1);        // a tile overflowed the arena: the row walk / level engine
+    if (!walk_ok) {
+      tree_free(p);
+      return FURY_OK;
+    }
+  }
   // a thread per row; the stage holds the tile's rows up to walk_stage bytes (the rest are read
   // from HBM), the bitmap-window pool walk_pool bytes
   p->nt = g_walk_threads;

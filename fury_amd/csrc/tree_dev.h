@@ -29,6 +29,7 @@ struct TNode {
 };
 
 constexpr int kTreeMaxNodes = 512;
+constexpr int kMaxLevels = 64;
 
 struct TreeArgs {
   const TNode* nodes;       // device table (scalar loads: every use has a uniform index)
@@ -55,7 +56,10 @@ struct TreeArgs {
   int32_t ctr;              // rows per count tile
   int32_t knode[64];        // counted slot -> node
   uint32_t out_cap;         // write pass: LDS bytes of the output windows (tuning "walk_out")
+  int32_t trows;            // bfs.hip: rows per tile
+  uint32_t arena_cap;       // bfs.hip: LDS bytes of the per-node entry records
   int32_t pad2_;
+  int32_t lvl[kMaxLevels + 1];  // bfs.hip: first node of each level (breadth-first numbering)
 };
 
 constexpr int kWalkMaxK = 64;
@@ -67,6 +71,9 @@ size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool
                       uint32_t out);
 constexpr size_t kWalkLdsMax = 159 * 1024;   // LDS of one workgroup (160 KB, static arrays aside)
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs);
+// bfs.hip (tile BFS decode, the default): LDS bytes of a workgroup, and the launch itself.
+size_t bfs_lds(int nn, int nt, uint32_t stage, uint32_t arena, int trows);
+int bfs_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs);
 
 // Diagnostics: thread 0 of a workgroup adds the time since its previous mark to tacc[id]
 // (s_memrealtime, 100 MHz); the kernel adds tacc to dbg at the end.
@@ -189,7 +196,7 @@ __device__ __forceinline__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t
   for (uint32_t i = b; i < e; i++) s += a[i];
   const uint64_t inc = tw_scan64(s);
   if (lane == 63) wsum[wave] = inc;
-  __syncthreads();
+  lds_barrier();
   uint64_t pre = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < NT / 64; w++) {
@@ -203,7 +210,7 @@ __device__ __forceinline__ bool block_scan_u32(uint32_t* a, uint32_t m, uint64_t
     a[i] = static_cast<uint32_t>(run);
     run += v;
   }
-  __syncthreads();
+  lds_barrier();
   return tot < (1ull << 32);
 }
 

@@ -887,7 +887,7 @@ __global__ __launch_bounds__(kEncRows) void encode_var_reg(VarArgs a, int64_t* _
   if (bytes <= kRegImg) {
     // (a.skip, diagnostics: 1 no string bytes, 2 no row build, 4 no store)
     if (live && !(a.skip & 2)) reg_build_row<K, M>(a, r, v, (a.skip & 1) ? 0 : valid, img + (ex >> 3));
-    __syncthreads();
+    lds_barrier();   // (LDS only: the offsets' stores need not land first)
     if (!(a.skip & 4)) store_image(rows + base, reinterpret_cast<const uint8_t*>(img), room);
   } else if (live) {        // oversized tile: rows straight to HBM (whole rows below the capacity)
     if (ex + sz <= room)
@@ -1501,7 +1501,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     if (lane == 63) wtot[k][wave] = inc;
     ex[k] = inc - cnt[k];
   }
-  __syncthreads();
+  lds_barrier();   // (LDS only)
 #pragma unroll
   for (int k = 0; k < K; k++) {
     if (!seq_kind(kind_of<M>(a.col[k]))) continue;
@@ -1701,7 +1701,7 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       }
     }
   }
-  __syncthreads();
+  lds_barrier();   // (LDS only: the column / status stores need not land first)
   // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
 #pragma unroll
   for (int k = 0; k < K; k++) {

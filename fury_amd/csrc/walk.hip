@@ -556,7 +556,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
     if (lane == 63) wsum[k * (NT / 64) + wave] = inc;
     sh.cur[k * NT + tid] = static_cast<uint32_t>(inc - v);   // wave-exclusive for now
   }
-  __syncthreads();
+  lds_barrier();   // (LDS only)
   bool over = false;
   for (int k = 0; k < a.K; k++) {
     uint64_t pre = 0, tot = 0;
@@ -572,7 +572,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
     if (tid == 0) sh.kb[k] = static_cast<int64_t>(tot);
   }
   if (over && tid == 0) __hip_atomic_store(a.overflow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  lds_barrier();   // (LDS only: the rowpre stores need not land first)
   clk.mark(2);
   for (int n = tid; n < a.nn; n += NT) {
     CTNode& N = tn(a, n);
@@ -672,12 +672,12 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   }
   const uint32_t used = min(sh.req[2 * nn], pool_words);
   for (uint32_t i = tid; i < used; i += NT) sh.pool[i] = 0;
-  __syncthreads();
+  lds_barrier();   // (LDS only)
   clk.mark(0);
   WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0};
   walk_row<true, MD>(c, live);
   clk.mark(1);
-  __syncthreads();
+  lds_barrier();   // (LDS only: the walk's column stores need not land before the flush)
   clk.mark(2);
   // flush the windows: whole words; the first and last of each (shared with the neighbouring
   // tiles) by atomic OR

@@ -648,27 +648,24 @@ namespace {
 constexpr uint32_t kWideImg = 2048;
 }  // namespace
 
+namespace {
+// The decode's LDS plan: the stage (~64 rows of the estimated row size) and the per-wave images.
+struct WideGeom {
+  int nseq = 0, th = 256;
+  uint32_t stage = 0, imgs = 0;
+  int64_t nt = 0;
+};
+WideGeom wide_geom(const VarArgs& a, double avg_row = -1);
+}  // namespace
+
 int launch_decode_wide(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
                        bool offsets_only) {
   if (a.nrows == 0) return FURY_OK;
-  int nseq = 0;
-  double row = a.fixed_size;
-  for (int k = 0; k < a.ncols; k++) {
-    const VarCol& c = a.htab ? a.htab[k] : a.col[k];
-    const double per = a.nrows > 0 && c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 16.0;
-    if (c.kind == kBytes || c.kind == kListFixed) nseq++;
-    if (c.kind == kDecimal) row += 16;
-    if (c.kind == kBytes) row += per + 4;
-    if (c.kind == kListFixed) row += 12 + per * (c.width == 0 ? 1 : c.width) + 4;
-  }
-  const uint32_t bit_cap = ((kWideImg / 8 + 4 * 16) + 15) & ~15u;
-  const int th = wide_threads(false);
-  const uint32_t imgs = static_cast<uint32_t>(th / 64) * (kWideImg + bit_cap);
-  // the stage: the tile's estimated row bytes (+3 %), at least 1 KB, at most 96 KB (rows past it
-  // are read from HBM)
-  const uint32_t want = static_cast<uint32_t>(std::min<double>(row * kWideRows * 1.03 + 64, 96.0 * 1024));
-  const uint32_t stage = (std::max<uint32_t>(want, 1024) + 15) & ~15u;
-  const int64_t nt = (a.nrows + kWideRows - 1) / kWideRows;
+  const WideGeom g = wide_geom(a);
+  const int nseq = g.nseq;
+  const uint32_t stage = g.stage, imgs = g.imgs;
+  const int64_t nt = g.nt;
+  const int th = g.th;
   int64_t* ws = nullptr;                   // [nseq x nt counts][total][scan scratch]
   const int64_t m = static_cast<int64_t>(nseq) * nt;
   int st = dev_alloc((m + 1 + scan_workspace(std::max<int64_t>(m, 1))) * 8, stream,
@@ -695,5 +692,112 @@ int launch_decode_wide(const VarArgs& a, const uint8_t* rows, const int64_t* off
   dev_free(ws, stream);
   return st;
 }
+
+// Plan form (fury_decode_prepare / fury_decode_execute): the count pass and the
+// scan run once in the prepare, whose one host sync reads every sequence field's total (sizing the
+// caller's buffers); the execute runs the write pass alone on the kept tile bases -- the rows are no
+// longer counted twice (fury_row_decode_measure + fury_row_decode).
+__global__ void wide_totals_kernel(const int64_t* ws, int64_t nt, int32_t nseq, int64_t* out) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q <= nseq) out[q] = ws[static_cast<int64_t>(q) * nt];      // q = nseq: the grand total
+}
+
+int wide_prepare(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
+                 WidePlan* wp, std::vector<int64_t>* seq_totals) {
+  // the stage is sized from the batch's average row (one 8-byte read)
+  int64_t bytes = 0;
+  if (a.nrows > 0) {
+    int st = check_hip(hipMemcpyAsync(&bytes, offs + a.nrows, 8, hipMemcpyDeviceToHost, stream),
+                       "hipMemcpyAsync batch bytes");
+    if (!st) st = check_hip(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    if (st) return st;
+  }
+  const WideGeom g = wide_geom(a, a.nrows > 0 ? static_cast<double>(bytes) / a.nrows : -1.0);
+  wp->nt = g.nt;
+  wp->nseq = g.nseq;
+  wp->stream = stream;
+  seq_totals->assign(g.nseq, 0);
+  if (a.nrows == 0 || g.nseq == 0) return FURY_OK;
+  const int64_t m = static_cast<int64_t>(g.nseq) * g.nt;
+  int st = dev_alloc((m + 1 + scan_workspace(std::max<int64_t>(m, 1)) + g.nseq + 1) * 8, stream,
+                     reinterpret_cast<void**>(&wp->ws));
+  if (st) return st;
+  int64_t* ws = wp->ws;
+  int64_t* tot = ws + m + 1 + scan_workspace(std::max<int64_t>(m, 1));
+  auto go = [&](auto count, int threads) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(count),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(g.stage));
+    hipLaunchKernelGGL(count, dim3(static_cast<unsigned>(g.nt)), dim3(threads), g.stage, stream, a,
+                       rows, offs, ws, g.nt, g.stage);
+  };
+  if (g.th == 1024) go(wide_count_kernel<1024>, 1024);
+  else if (g.th == 512) go(wide_count_kernel<512>, 512);
+  else go(wide_count_kernel<256>, 256);
+  device_scan(ws, m, ws + m, ws + m + 1, stream);
+  hipLaunchKernelGGL(wide_totals_kernel, dim3(static_cast<unsigned>((g.nseq + 256) / 256)), dim3(256),
+                     0, stream, ws, g.nt, g.nseq, tot);
+  if ((st = check_hip(hipGetLastError(), "wide prepare launch"))) return st;
+  std::vector<int64_t> h(g.nseq + 1);
+  if ((st = check_hip(hipMemcpyAsync(h.data(), tot, 8 * (g.nseq + 1), hipMemcpyDeviceToHost, stream),
+                      "hipMemcpyAsync wide totals")))
+    return st;
+  if ((st = check_hip(hipStreamSynchronize(stream), "hipStreamSynchronize"))) return st;
+  for (int q = 0; q < g.nseq; q++) (*seq_totals)[q] = h[q + 1] - h[q];
+  return FURY_OK;
+}
+
+int wide_execute(const VarArgs& a, const uint8_t* rows, const int64_t* offs, hipStream_t stream,
+                 const WidePlan& wp) {
+  if (a.nrows == 0) return FURY_OK;
+  const WideGeom g = wide_geom(a);
+  const size_t lds = static_cast<size_t>(g.stage) + g.imgs;
+  auto go = [&](auto write, int threads) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(write),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+    hipLaunchKernelGGL(write, dim3(static_cast<unsigned>(g.nt)), dim3(threads), lds, stream, a, rows,
+                       offs, wp.ws, g.nt, g.stage, kWideImg, 0);
+  };
+  if (g.th == 1024) go(wide_write_kernel<1024>, 1024);
+  else if (g.th == 512) go(wide_write_kernel<512>, 512);
+  else go(wide_write_kernel<256>, 256);
+  return check_hip(hipGetLastError(), "wide execute launch");
+}
+
+void wide_free(WidePlan* wp) {
+  if (!wp) return;
+  dev_free(wp->ws, wp->stream);
+  delete wp;
+}
+
+namespace {
+// avg_row >= 0: the batch's average row bytes (the prepare, which has no output capacities to
+// estimate it from)
+WideGeom wide_geom(const VarArgs& a, double avg_row) {
+  WideGeom g;
+  int nseq = 0;
+  double row = a.fixed_size;
+  for (int k = 0; k < a.ncols; k++) {
+    const VarCol& c = a.htab ? a.htab[k] : a.col[k];
+    const double per = a.nrows > 0 && c.capacity > 0 ? static_cast<double>(c.capacity) / a.nrows : 16.0;
+    if (c.kind == kBytes || c.kind == kListFixed) nseq++;
+    if (c.kind == kDecimal) row += 16;
+    if (c.kind == kBytes) row += per + 4;
+    if (c.kind == kListFixed) row += 12 + per * (c.width == 0 ? 1 : c.width) + 4;
+  }
+  const uint32_t bit_cap = ((kWideImg / 8 + 4 * 16) + 15) & ~15u;
+  const int th = wide_threads(false);
+  const uint32_t imgs = static_cast<uint32_t>(th / 64) * (kWideImg + bit_cap);
+  // the stage: the tile's estimated row bytes (+3 %), at least 1 KB, at most 96 KB (rows past it
+  // are read from HBM)
+  if (avg_row >= 0) row = avg_row;
+  const uint32_t want = static_cast<uint32_t>(std::min<double>(row * kWideRows * 1.03 + 64, 96.0 * 1024));
+  g.stage = (std::max<uint32_t>(want, 1024) + 15) & ~15u;
+  g.nt = (a.nrows + kWideRows - 1) / kWideRows;
+  g.nseq = nseq;
+  g.th = th;
+  g.imgs = imgs;
+  return g;
+}
+}  // namespace
 
 }  // namespace fury

@@ -512,6 +512,10 @@ class RowEncoder:
             return self._decode_nested(batch, validity, arrow, stream)
         if sizing not in ("measure", "bound"):
             raise ValueError(f"sizing must be 'measure' or 'bound', not {sizing!r}")
+        if sizing == "measure" and out is None and self._wide_plan():
+            # 17-256 fields: the plan API keeps the count pass's tile bases for the write pass
+            # (fury_decode_prepare sizes, fury_decode_execute writes; the rows are counted once)
+            return self._decode_nested(batch, validity, arrow, stream)
         if sizing == "bound" and out is None and not self._schema.is_fixed:
             return self._decode_bound(batch, validity, arrow, stream)
         n = batch.nrows
@@ -532,6 +536,12 @@ class RowEncoder:
         _check(fn(self._schema.handle, _ptr(batch.rows), _ptr(batch.row_offsets), n,
                   _c_columns(cols, keep), sh))
         return cols
+
+    def _wide_plan(self) -> bool:
+        """Flat variable-length schemas the wide kernels decode (17-256 fields, tuning var_wide)."""
+        nf = len(self._schema.fields)
+        return (not self._schema.is_fixed and 16 < nf <= 256
+                and N.lib().fury_get_tuning(b"var_wide") == 1)
 
     def _size_var_outputs(self, cols: List[Column], n: int, validity: bool, stream) -> None:
         """Allocates the payload / element buffers of the variable-length outputs from the

@@ -21,6 +21,10 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--base", type=int, default=20_000)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--wide", default="", help="comma list of counted-node counts: a bean of that "
+                    "many STRING fields plus a list of structs (the walk's 64-counted-node limit)")
+    ap.add_argument("--modes", default="3,1", help="nested_decode settings (3 tile BFS, 2 row "
+                    "walk -- at most 5 levels, else the level engine --, 1 level engine)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -30,8 +34,17 @@ def main():
     from tests.test_tree import _beans, _deep_fields
     dev = torch.device("cuda:0")
     L = N.lib()
-    for levels in [int(x) for x in args.levels.split(",")]:
-        fields = _deep_fields(levels)
+    from fury_amd import types as T
+    cases = [("levels", int(x)) for x in args.levels.split(",") if x]
+    cases += [("counted", int(x)) for x in args.wide.split(",") if x]
+    for kind, levels in cases:
+        if kind == "levels":
+            fields = _deep_fields(levels)
+        else:
+            fields = ([T.not_null_field("id", T.INT64)] +
+                      [T.field(f"s{i:03d}", T.STRING) for i in range(levels - 2)] +
+                      [T.Field("t", T.LIST, True, (T.struct_field("item", [T.field("x", T.STRING),
+                                                                         T.field("y", T.INT32)]),))])
         beans = _beans(fields, args.base, levels)
         enc = Encoders.bean(fields, device=dev)
         b0 = enc.encode_batch([column_to_device(c, dev) for c in beans_to_columns(fields, beans)],
@@ -43,9 +56,9 @@ def main():
         offs = torch.cat([b0.row_offsets[:-1] + i * tot for i in range(reps)] +
                          [torch.tensor([reps * tot], dtype=torch.int64, device=dev)])
         batch = RowBatch(rows, offs, n, enc.schema_hash)
-        res = {"levels": levels, "rows": n, "row_bytes": reps * tot}
+        res = {kind: levels, "rows": n, "row_bytes": reps * tot}
         ref = None
-        for mode in (2, 1):
+        for mode in [int(x) for x in args.modes.split(",")]:
             assert L.fury_set_tuning(b"nested_decode", mode) == 0
             out = enc.decode_batch(batch)
             torch.cuda.synchronize()
@@ -53,7 +66,7 @@ def main():
             if ref is None:
                 ref = got
             else:
-                res["equal"] = all((x is None and y is None) or (
+                res[f"equal_mode{mode}"] = all((x is None and y is None) or (
                     x is not None and y is not None and x.shape == y.shape and
                     torch.equal(x[:max(x.numel() - 16, 0)], y[:max(y.numel() - 16, 0)]))
                     for x, y in zip(ref, got))
@@ -67,7 +80,8 @@ def main():
                 torch.cuda.synchronize()
                 xs.append(a.elapsed_time(b) / args.iters)
             res[f"decode_ms_mode{mode}"] = round(statistics.median(xs), 3)
-        assert L.fury_set_tuning(b"nested_decode", 2) == 0
+        assert L.fury_set_tuning(b"nested_decode", 3) == 0
+        res["bfs_fallbacks"] = L.fury_get_tuning(b"bfs_fallbacks")
         print(json.dumps(res), flush=True)
     del np
 

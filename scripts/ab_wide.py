@@ -61,9 +61,11 @@ def main():
     out = enc.decode_batch(batch)                       # allocated once (bound sizing)
     res["encode_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
     res["decode_flat_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
+    # the API users call: sizing included (round 6: the plan API -- count pass once)
+    res["decode_batch_ms"] = timed(lambda: enc.decode_batch(batch))
     # one device pass into the preallocated columns (no sizing pass, no host sync): the kernels
     res["decode_into_ms"] = timed(lambda: enc.decode_into(batch, out))
-    legs = ["encode", "decode_flat", "decode_into"]
+    legs = ["encode", "decode_flat", "decode_batch", "decode_into"]
     if not args.no_plan:
         res["decode_plan_ms"] = timed(lambda: enc._decode_nested(batch, True, False, None))
         legs.append("decode_plan")

@@ -16,6 +16,9 @@ sys.path.insert(0, ROOT)
 WALK_C = {0: "stage + barrier", 1: "walk (thread 0)", 2: "walk tail + scans", 3: "epilogue"}
 WALK_W = {0: "prologue + stage + windows", 1: "walk (thread 0)", 2: "walk tail (barrier)",
           3: "window flush"}
+# tile BFS (nested_decode 3, bfs.hip BClock)
+BFS = {0: "stage + row / node bases", 1: "top-level nodes", 2: "nested nodes", 3: "owner arrays",
+       4: "node table + barrier"}
 
 
 def main():
@@ -51,7 +54,9 @@ def main():
     enc.decode_batch(batch)
     assert fn(out, 80) == 0
     res = {}
-    for name, off, cnt_i, names in (("decode_pass1", 0, 64, WALK_C), ("decode_pass2", 16, 65, WALK_W)):
+    bfs = L.fury_get_tuning(b"nested_decode") == 3 and L.fury_get_tuning(b"bfs_fallbacks") == 0
+    for name, off, cnt_i, names in (("decode_pass1", 0, 64, BFS if bfs else WALK_C),
+                                    ("decode_pass2", 16, 65, BFS if bfs else WALK_W)):
         wg = max(out[cnt_i], 1)
         res[name] = {"workgroups": out[cnt_i],
                      "us_per_wg": {names.get(i, str(i)): round(out[off + i] / wg / 100.0, 2)

@@ -437,6 +437,7 @@ def test_thread_exit_slot_quarantine(oracle, dev):
         except IndexOutOfBoundsException:
             pass
 
+    exits = L.fury_get_tuning(b"thread_key_exits")
     t = threading.Thread(target=worker)
     t.start()
     t.join()
@@ -446,7 +447,10 @@ def test_thread_exit_slot_quarantine(oracle, dev):
     deadline = time.time() + 10
     while L.fury_get_tuning(b"err_slots_quarantined") < 1 and time.time() < deadline:
         time.sleep(0.01)
-    assert L.fury_get_tuning(b"err_slots") == base
+    assert L.fury_get_tuning(b"err_slots") == base, (
+        f"thread_key_exits {exits} -> {L.fury_get_tuning(b'thread_key_exits')}, quarantined "
+        f"{L.fury_get_tuning(b'err_slots_quarantined')}, last key kind "
+        f"{L.fury_get_tuning(b'err_slot_last_key')}")
     assert L.fury_get_tuning(b"err_slots_quarantined") == 1
 
     def new_stream():

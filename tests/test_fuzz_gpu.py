@@ -61,16 +61,20 @@ def _shape(fields):
     return lv, k
 
 
-def _expected(O, fields, nested, walk, rows, offs, n):
-    """What the device must report: "oob", "map", "budget", "any" (the level engine on a batch
-    the walk's budget refuses: the oracle's full walk of it is not bounded), or the oracle's
-    columns."""
+def _expected(O, fields, nested, engine, rows, offs, n):
+    """What the device must report: "oob", "map", "budget", "any" (an engine on a batch the walk's
+    budget refuses: the oracle's full walk of it is not bounded), or the oracle's columns.
+    engine: "walk" (its count pass is restated exactly, budget included), "bfs" (the same count-pass
+    containers without a budget; a batch whose tiles overflow the arena goes to the walk) or
+    "levels"."""
     if nested:
         cw = O.count_walk_flags(fields, rows, offs, n)
-        if walk and cw:                              # the walk's prepare reports these
+        if engine == "walk" and cw:                  # the walk's prepare reports these
             return "oob" if cw & O.ERR_OOB else "map" if cw & O.ERR_MAP else "budget"
         if cw & O.ERR_BUDGET:
             return "any"
+        if engine == "bfs" and cw:                   # the tile BFS count pass: the same checks
+            return "oob" if cw & O.ERR_OOB else "map"
     flags, cols = O.decode_checked(fields, rows, offs, n)
     if flags:
         return "oob" if flags & O.ERR_OOB else "map"
@@ -104,10 +108,13 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
             if len(bad):
                 pos = rng.integers(0, len(bad), int(rng.integers(1, 40)))
                 bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
-            for mode in ((2, 1) if enc.nested else (2,)):
+            for mode in ((4, 3, 2, 1) if enc.nested else (3,)):
                 L.fury_set_tuning(b"nested_decode", mode)
-                walk = mode == 2 and levels <= 5 and counted <= 64
-                want = _expected(O, fields, enc.nested, walk, bad, offs, n)
+                walkable = levels <= 5 and counted <= 64
+                engine = ("bfs" if mode == 4 or (mode == 3 and not walkable)
+                          else "walk" if mode in (2, 3) and walkable else "levels")
+                walk = engine != "levels" and walkable
+                want = _expected(O, fields, enc.nested, engine, bad, offs, n)
                 try:
                     got = _decode(enc, _batch(enc, bad, offs, n, dev))
                     err = None
@@ -115,7 +122,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
                     err = "oob"
                 except UnsupportedOperationException as e:
                     err = "budget" if "decode budget" in str(e) else "map"
-                where = f"trial {trial}, engine {'walk' if walk else 'levels'}"
+                where = f"trial {trial}, engine {engine}"
                 seen.append(err or "decoded")
                 if want == "any" or (err == "budget" and not walk):
                     # the level engine's own bound (elements of a node vs the batch's bytes) is
@@ -127,7 +134,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
                     raise AssertionError(f"{where}: oracle decodes, device raises {err}")
                 else:
                     assert_columns_equal(fields, got, want, n)
-        L.fury_set_tuning(b"nested_decode", 2)
+        L.fury_set_tuning(b"nested_decode", 3)
         assert_columns_equal(fields, _decode(enc, _batch(enc, rows, offs, n, dev)), ref, n)
     finally:
         L.fury_set_tuning(b"nested_decode", old)

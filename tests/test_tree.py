@@ -1,5 +1,6 @@
-"""The nested engines against the oracle: the row-walk decode (walk.hip, tuning "nested_decode" =
-2, the default) and the level engine (levels.hip, "nested_decode" = 1) on the same rows, and the
+"""The nested engines against the oracle: the row-walk decode (walk.hip, tuning "nested_decode" = 2;
+3, the default, takes the walk where it fits and the tile BFS past its limits), the tile-BFS decode
+(bfs.hip, 4) and the level engine (levels.hip, 1) on the same rows, and the
 row-walk encode (rowenc.hip; deep schemas through its explicit-stack continuation): every nested
 schema shape the tests know, the reference's BeanA, collections (ArrayEncoder / MapEncoder
 batches), schemas nested up to the 64-level limit, and LDS budgets small enough to force rows
@@ -36,7 +37,8 @@ def engines():
     L = N.lib()
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "walk_threads", "walk_stage", "walk_pool",
                                                        "walk_stage_write", "walk_threads_write",
-                                                       "walk_out")}
+                                                       "walk_out", "bfs_threads", "bfs_rows",
+                                                       "bfs_stage", "bfs_arena")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -97,12 +99,29 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         _tune("walk_out", wo)
         walk = _decode_plan(enc, batch)
         assert_columns_equal(fields, walk, ref, n)
+    # tile BFS: threads / tile rows, a stage far smaller than the tile (rows read from HBM), an
+    # arena too small for the tile (the batch falls back to the row walk), and the defaults
+    from fury_amd import _native as N
+    L = N.lib()
+    _tune("nested_decode", 4)
+    bfs_legs = ([(64, 64, 1024, 0), (256, 200, 2048, 0), (128, 128, 0, 1024)] if budget == "tiny"
+                else [(128, 128, 0, 0), (64, 64, 0, 0), (256, 256, 0, 0), (128, 300, 0, 0)])
+    for th, tr, stg, arena in bfs_legs:
+        _tune("bfs_threads", th)
+        _tune("bfs_rows", tr)
+        _tune("bfs_stage", stg)
+        _tune("bfs_arena", arena)
+        fb = L.fury_get_tuning(b"bfs_fallbacks")
+        got = _decode_plan(enc, batch)
+        assert_columns_equal(fields, got, ref, n)
+        if arena == 1024 and name in ("nested7", "deep_lists", "maps"):
+            assert L.fury_get_tuning(b"bfs_fallbacks") > fb     # the arena leg really fell back
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 def test_tree_decode_large_batch(oracle, dev, engines, mode):
     """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode, level
-    engine (1) and row walk (2)."""
+    engine (1), row walk (2) and tile BFS (3)."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     from tests.test_device import _nested_beans, _nested_fields
@@ -118,7 +137,7 @@ def test_tree_decode_large_batch(oracle, dev, engines, mode):
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 @pytest.mark.parametrize("kind", ["list_bar", "list_long", "list_str", "list_list", "map"])
 def test_collections_both_engines(oracle, dev, engines, mode, kind):
     """ArrayEncoder / MapEncoder batches (root 1 / 2: each entry a top-level BinaryArray /
@@ -131,7 +150,7 @@ def test_collections_both_engines(oracle, dev, engines, mode, kind):
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
 def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     """Tiles whose bytes exceed the stage (rows of very different sizes): the rows past the stage
     are read from HBM, the result is the oracle's."""
@@ -264,7 +283,7 @@ def _schema_levels(fields):
 
 
 @pytest.mark.parametrize("levels", [6, 9, 12, 20, 64])
-@pytest.mark.parametrize("dec_mode", [1, 2])
+@pytest.mark.parametrize("dec_mode", [1, 2, 3, 4])
 def test_deep_schema_round_trip(oracle, dev, engines, enc_engines, levels, dec_mode):
     """Depth 6 .. 64 schemas (64 = the schema limit): the row-walk encode continues past its
     inlined levels on an explicit stack, both decode settings read the rows back (the row walk
@@ -366,7 +385,7 @@ def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
         pos = rng.integers(lo, len(bad), 24)
         bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
         res = {}
-        for mode in (2, 1):
+        for mode in (4, 3, 2, 1):
             _tune("nested_decode", mode)
             try:
                 res[mode] = [column_to_host(c) for c in enc.decode_batch(_batch(enc, bad, offs, n, dev))]
@@ -377,6 +396,9 @@ def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
         # elements or payload bytes outnumber the batch's row bytes; two decodes agree
         if not isinstance(res[2], type) and not isinstance(res[1], type):
             assert_columns_equal(fields, res[2], res[1], n)
+        for m in (3, 4):
+            if not isinstance(res[m], type) and not isinstance(res[1], type):
+                assert_columns_equal(fields, res[m], res[1], n)
     _tune("nested_decode", 2)
     good = [column_to_host(c) for c in enc.decode_batch(_batch(enc, rows, offs, n, dev))]
     assert_columns_equal(fields, good, oracle.decode(fields, rows, offs, n), n)
@@ -474,7 +496,7 @@ def test_random_nested_schemas(oracle, dev, engines, seed):
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     ref = oracle.decode(fields, want, want_offs, n)
-    for mode in (2, 1):
+    for mode in (4, 3, 2, 1):
         _tune("nested_decode", mode)
         got = _decode_plan(enc, batch) if enc.nested else None
         if got is None:
