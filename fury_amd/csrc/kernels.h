@@ -298,7 +298,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
 int tree_execute(const TreePlan* p, const GenNode* outs, const uint8_t* rows, const int64_t* offs,
                  const std::vector<int64_t>& totals, hipStream_t hs);
 void tree_free(TreePlan* p);
-void set_tree_mode(int v);           // tuning "nested_decode": 1 levels, 2 row walk, 3 tile BFS (default)
+void set_tree_mode(int v);           // tuning "nested_decode": 1 levels, 2 row walk (default), 3 walk + BFS, 4 BFS
 void set_bfs_tuning(int which, uint32_t v);   // bfs_threads / bfs_rows / bfs_stage / bfs_arena
 int64_t bfs_tuning(int which);                // ... and 4: bfs_fallbacks
 int tree_mode();

@@ -102,13 +102,14 @@ int tree_host_width(int32_t t) {
   }
 }
 
-// tuning "nested_decode": 1 level engine; 2 row walk (the level engine past its limits); 3 row walk,
-// tile BFS (bfs.hip) past its limits (default); 4 tile BFS always (A/B, tests).  The BFS falls back
-// to the walk / level engine for a batch whose tiles overflow its arena.  At depth 3 the walk is
-// 2x faster than the BFS (profiles/r06_bfs_legs.jsonl: the BFS's per-node chain of LDS round
-// trips runs at ~1.5 waves per SIMD, bounded by the LDS its staged tiles take); past the walk's
-// limits the BFS replaces the level engine where it measured faster.
-std::atomic<int> g_tree_mode = 3;
+// tuning "nested_decode": 1 level engine; 2 row walk, the level engine past its limits (default);
+// 3 row walk, tile BFS (bfs.hip) past its limits; 4 tile BFS always (A/B, tests).  The BFS falls
+// back to the walk / level engine for a batch whose tiles overflow its arena.  Measured round 6
+// (profiles/r06_*): at depth 3 the walk decodes 4M rows in 2.53 ms, the BFS in 3.06 ms
+// at best (its per-level chains of LDS round trips run at ~2 waves per SIMD, bounded by the LDS
+// its staged tiles take); past the walk's limits the level engine beat the BFS too (depth 6-20,
+// 128 counted nodes), so the BFS is not the default anywhere.
+std::atomic<int> g_tree_mode = 2;
 // Tile BFS defaults (tunings "bfs_threads", "bfs_rows", "bfs_stage" (0: sized from the batch's
 // average row), "bfs_arena" (0: 60 % of the stage + 2 KB)).
 std::atomic<int> g_bfs_threads = 128;
@@ -426,6 +427,11 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   // a thread per row; the stage holds the tile's rows up to walk_stage bytes (the rest are read
   // from HBM), the bitmap-window pool walk_pool bytes
   p->nt = g_walk_threads;
+  // the count pass's per-row counters (4 B x counted nodes x rows) must fit one workgroup too:
+  // a bean of ~200+ STRING fields counts on 64-row tiles
+  while (p->nt > 64 &&
+         walk_count_lds(nn, K, p->nt, (g_walk_stage + 15) & ~15u, (g_walk_prefetch & 2) != 0) > kWalkLdsMax)
+    p->nt /= 2;
   const int tw = g_walk_threads_w.load();
   p->ntw = tw % p->nt == 0 && tw >= p->nt ? tw : p->nt;
   p->tile_rows = p->nt;
@@ -444,6 +450,10 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     else if (p->pool_cap > 0) p->pool_cap = p->pool_cap > 1024 ? p->pool_cap / 2 : 0;
     else if (p->stage_cap_w > 0) p->stage_cap_w = 0;
     else break;                                 // cannot happen for K <= kWalkMaxK, nn <= 512
+  }
+  if (walk_write_lds(nn, K, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) > kWalkLdsMax) {
+    tree_free(p);                               // (defensive) the level engine
+    return FURY_OK;
   }
   p->ntiles = (nrows + p->tile_rows - 1) / p->tile_rows;
   p->stride = p->ntiles + 1;

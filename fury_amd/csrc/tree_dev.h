@@ -54,7 +54,7 @@ struct TreeArgs {
                             // 2 bitmaps, 4 scalar values, 8 offsets not written
   int32_t tmul;             // write pass: count tiles per write tile (1 or 2)
   int32_t ctr;              // rows per count tile
-  int32_t knode[64];        // counted slot -> node
+  int32_t knode[256];       // counted slot -> node (kWalkMaxK)
   uint32_t out_cap;         // write pass: LDS bytes of the output windows (tuning "walk_out")
   int32_t trows;            // bfs.hip: rows per tile
   uint32_t arena_cap;       // bfs.hip: LDS bytes of the per-node entry records
@@ -62,13 +62,14 @@ struct TreeArgs {
   int32_t lvl[kMaxLevels + 1];  // bfs.hip: first node of each level (breadth-first numbering)
 };
 
-constexpr int kWalkMaxK = 64;
+constexpr int kWalkMaxK = 256;     // round 6: was 64 (wide nested beans went to the level engine)
 constexpr int kWalkMaxDepth = 5;      // deeper: the level engine (register budget of the walk)
 
 // walk.hip launchers (tree.hip owns the plan): LDS bytes of a pass, and the launch itself.
 size_t walk_lds(const TreeArgs& a, int nt, bool write);
 size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool prefetch,
                       uint32_t out);
+size_t walk_count_lds(int nn, int K, int nt, uint32_t stage, bool prefetch);
 constexpr size_t kWalkLdsMax = 159 * 1024;   // LDS of one workgroup (160 KB, static arrays aside)
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs);
 // bfs.hip (tile BFS decode, the default): LDS bytes of a workgroup, and the launch itself.

@@ -1,6 +1,6 @@
 // walk.hip — nested decode with a thread per ROW ("row walk"): the default engine of
 // fury_decode_prepare / fury_decode_execute for schemas of up to kWalkMaxDepth levels and
-// kWalkMaxK counted nodes (tree.hip builds the plan; the level engine takes the rest).  A deeper
+// kWalkMaxK (256, round 6) counted nodes (tree.hip builds the plan; the level engine takes the rest).  A deeper
 // walk on an explicit per-lane stack was built and measured 2.5-6.5x slower than the level
 // engine on depth 6-20 schemas (profiles/r05_deep_walk_vs_levels.jsonl), so the level engine is
 // the fallback.
@@ -727,6 +727,9 @@ size_t walk_lds(const TreeArgs& a, int nt, bool write) {
 size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool prefetch,
                       uint32_t out) {
   return walk_layout(nn, K, nt, stage, pool, true, prefetch, out).end;
+}
+size_t walk_count_lds(int nn, int K, int nt, uint32_t stage, bool prefetch) {
+  return walk_layout(nn, K, nt, stage, 0, false, prefetch, 0).end;
 }
 
 int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {

@@ -292,7 +292,10 @@ int fury_trim_workspace(int32_t device);
  * spelling a plausible header -- is repaired in parallel; the sequential walk only reports
  * errors), 1 always the sequential walk.
  * Nested engines: "nested_decode" 2 row walk (default), 1 level engine (schemas past the walk's
- * limits use it by themselves); nested encode is the row walk with an explicit-stack continuation
+ * limits -- 5 levels, 256 counted nodes -- use it by themselves), 3 row walk with the tile BFS past
+ * its limits, 4 tile BFS ("bfs_threads" 64 / 128 / 256 / 512, "bfs_rows", "bfs_stage", "bfs_arena"
+ * bytes, 0 = sized from the batch; fury_get_tuning "bfs_fallbacks" = batches whose tiles outgrew
+ * the arena and went to the walk / level engine); nested encode is the row walk with an explicit-stack continuation
  * for deep schemas: "rowenc_rows" (128 / 256 / 512 threads per group), "rowenc_tile" (rows per group,
  * 0 = threads), "rowenc_img" (LDS image bytes); row-walk decode "walk_threads" /
  * "walk_threads_write" (128 / 256 / 512), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
@@ -310,6 +313,8 @@ int fury_trim_workspace(int32_t device);
  * pinned host buffers (fixed-width and flat variable-length schemas, no staging),
  * "lookback_timeouts" = decoupled look-backs that gave up (must stay 0; synchronous device read),
  * "err_slots" = device error slots held by live streams (fury_stream_release),
+ * "err_slots_quarantined" = slots of exited threads waiting for a device synchronisation,
+ * "decode_budget_errors" = nested decodes refused by the item budget (a device limit),
  * "var_dec_rows_rejected" = forced "var_dec_rows" tiles whose images did not fit (planned tile used). */
 int fury_set_tuning(const char* key, int32_t value);
 int32_t fury_get_tuning(const char* key);

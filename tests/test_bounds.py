@@ -414,7 +414,6 @@ def test_thread_exit_slot_quarantine(oracle, dev):
     import ctypes
     import threading
     from fury_amd import _native as N
-    from fury_amd.encoder import IndexOutOfBoundsException
     hip = ctypes.CDLL("libamdhip64.so")
     L = N.lib()
     fields = SCHEMAS["mixed"]
@@ -429,13 +428,13 @@ def test_thread_exit_slot_quarantine(oracle, dev):
     assert L.fury_get_tuning(b"err_slots_quarantined") == 0
     base = L.fury_get_tuning(b"err_slots")
 
+    class _NullStream:            # the legacy null stream itself (handle 0): this thread's key
+        cuda_stream = 0
+
     def worker():
         torch.cuda.set_device(dev)
-        null = torch.cuda.ExternalStream(0, device=dev)
-        try:      # raises on the device; the call may or may not see it before the thread exits
-            enc._decode(bad, True, False, null, None, "bound")
-        except IndexOutOfBoundsException:
-            pass
+        # one asynchronous launch that raises on the device; the thread exits without taking it
+        enc.decode_into(bad, cols, stream=_NullStream())
 
     exits = L.fury_get_tuning(b"thread_key_exits")
     t = threading.Thread(target=worker)

@@ -1,5 +1,5 @@
-"""The nested engines against the oracle: the row-walk decode (walk.hip, tuning "nested_decode" = 2;
-3, the default, takes the walk where it fits and the tile BFS past its limits), the tile-BFS decode
+"""The nested engines against the oracle: the row-walk decode (walk.hip, tuning "nested_decode" = 2,
+the default: the level engine past its limits; 3 takes the tile BFS past them), the tile-BFS decode
 (bfs.hip, 4) and the level engine (levels.hip, 1) on the same rows, and the
 row-walk encode (rowenc.hip; deep schemas through its explicit-stack continuation): every nested
 schema shape the tests know, the reference's BeanA, collections (ArrayEncoder / MapEncoder
@@ -528,3 +528,26 @@ def test_random_deep_schemas(oracle, dev, engines, seed):
 
 def _levels(f):
     return 1 + max((_levels(c) for c in f.children), default=0)
+
+
+@pytest.mark.parametrize("nstr", [126, 254])
+def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
+    """Beans with 128 / 256 counted nodes (STRING fields + a LIST of a STRING struct): round 6 lifts
+    the row walk's 64-counted-node limit to 256 (per-row cursors sized into the LDS by stepping the
+    tile rows down), so these decode through the walk (nested_decode 2) -- and the tile BFS (4) and
+    the level engine (1) -- to the oracle's columns."""
+    from fury_amd.beans import beans_to_columns
+    from fury_amd.encoder import Encoders, column_to_device
+    fields = ([T.not_null_field("id", T.INT64)] + [T.field(f"s{i:03d}", T.STRING) for i in range(nstr)]
+              + [T.Field("t", T.LIST, True, (T.struct_field("item", [T.field("x", T.STRING)]),))])
+    n = 1500
+    beans = _beans(fields, n, nstr)
+    host = beans_to_columns(fields, beans)
+    enc = Encoders.bean(fields, device=dev)
+    batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
+    want, want_offs = oracle.encode(fields, host, n)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    ref = oracle.decode(fields, want, want_offs, n)
+    for mode in (2, 4, 1):
+        _tune("nested_decode", mode)
+        assert_columns_equal(fields, _decode_plan(enc, batch), ref, n)
