@@ -43,7 +43,7 @@
 /* ------------------------------------------------------------------------------------------
  * Errors
  * ---------------------------------------------------------------------------------------- */
-static int g_err = 0;
+static _Thread_local int g_err = 0;   /* per thread: bench.py's CPU baseline runs threads */
 int fo_last_status(void) { return g_err; }
 
 /* ------------------------------------------------------------------------------------------
@@ -414,9 +414,9 @@ int64_t fo_encode_batch(const fury_field* fields, int32_t nfields, const fury_co
 #define FO_ERR_OOB 1
 #define FO_ERR_MAP 2
 #define FO_ERR_BUDGET 4
-static const uint8_t* g_rows;     /* batch base                 */
-static int64_t g_total;           /* batch bytes                */
-static int32_t g_flags;           /* FO_ERR_* seen              */
+static _Thread_local const uint8_t* g_rows;   /* batch base (per thread, as all decode state) */
+static _Thread_local int64_t g_total;         /* batch bytes                */
+static _Thread_local int32_t g_flags;         /* FO_ERR_* seen              */
 
 /* MemoryBuffer.checkPosition / get / slice restated over [0, g_total): 0 <= p, 0 <= len,
  * p + len <= size (MemoryBuffer.java:303-309). */
@@ -668,7 +668,7 @@ static int fo_walks(const fury_field* f) {
   return 0;
 }
 
-static int64_t g_left;            /* the row's remaining item budget (-1: spent) */
+static _Thread_local int64_t g_left;  /* the row's remaining item budget (-1: spent) */
 
 static int fo_charge(const fury_field* f, int valid, int64_t m) {
   int64_t items = f->type_id == FURY_TYPE_MAP ? 2 * m
