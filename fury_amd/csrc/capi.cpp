@@ -1126,6 +1126,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_walk_tuning(0, static_cast<uint32_t>(value));
     return FURY_OK;
   }
+  if (std::string(key) == "walk_group_k") {
+    if (value < 0 || value > 256) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_group_k: 0..256 (0: one field group)");
+    set_walk_tuning(8, static_cast<uint32_t>(value));
+    return FURY_OK;
+  }
   if (std::string(key) == "walk_out") {
     if (value < 0 || value > 96 * 1024) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_out: 0..98304 bytes");
     set_walk_tuning(7, static_cast<uint32_t>(value));
@@ -1181,6 +1186,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_stage_write") return static_cast<int32_t>(walk_tuning(3));
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
   if (key && std::string(key) == "walk_threads_write") return static_cast<int32_t>(walk_tuning(6));
+  if (key && std::string(key) == "walk_group_k") return static_cast<int32_t>(walk_tuning(8));
   if (key && std::string(key) == "walk_out") return static_cast<int32_t>(walk_tuning(7));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();

@@ -132,6 +132,11 @@ std::atomic<uint32_t> g_walk_out{40 * 1024};     // tuning "walk_out": LDS outpu
 std::atomic<int> g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
                                     // (bit 0: write pass, bit 1: count pass)
 std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
+// tuning "walk_group_k": field groups (round 6) -- a schema with more counted slots than this walks
+// its top-level fields in groups of about this many slots, a workgroup per (tile, group): the LDS
+// cursors (4 B x slots x rows) of a 128-slot bean held one 64-row count tile per ~5 waves of a CU;
+// 0 = one group
+std::atomic<int> g_walk_group_k = 16;
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 
 }  // namespace
@@ -168,6 +173,7 @@ void set_walk_tuning(int which, uint32_t v) {
   else if (which == 4) g_walk_prefetch = static_cast<int>(v);
   else if (which == 5) g_walk_skip = static_cast<int>(v);
   else if (which == 7) g_walk_out = (v + 15) & ~15u;
+  else if (which == 8) g_walk_group_k = static_cast<int>(v);
   else g_walk_threads_w = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
@@ -175,7 +181,8 @@ uint32_t walk_tuning(int which) {
          : which == 2 ? g_walk_pool.load() : which == 3 ? g_walk_stage_w.load()
          : which == 4 ? static_cast<uint32_t>(g_walk_prefetch)
          : which == 5 ? static_cast<uint32_t>(g_walk_skip)
-         : which == 7 ? g_walk_out.load() : static_cast<uint32_t>(g_walk_threads_w);
+         : which == 7 ? g_walk_out.load()
+         : which == 8 ? static_cast<uint32_t>(g_walk_group_k) : static_cast<uint32_t>(g_walk_threads_w);
 }
 
 struct TreePlan {
@@ -193,6 +200,8 @@ struct TreePlan {
   int32_t K = 0, nt = 0, ntw = 0;   // count / write tile rows
   uint32_t pool_cap = 0, out_cap = 0;  // write pass: bitmap-window / output-window LDS bytes
   int32_t knode[kWalkMaxK] = {};
+  int32_t ngrp = 1, Kl = 0;           // field groups (TreeArgs)
+  int32_t gf[kMaxGroups + 1] = {}, gk[kMaxGroups + 1] = {};
   int32_t lvl[kMaxLevels + 1] = {};   // first node of each level
   // tile BFS (bfs.hip)
   bool bfs = false;
@@ -236,6 +245,12 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.pool_cap = p.pool_cap;
   a.out_cap = write ? p.out_cap : 0;
   for (int k = 0; k < p.K && k < kWalkMaxK; k++) a.knode[k] = p.knode[k];   // (the walk only)
+  a.ngrp = p.ngrp;
+  a.Kl = p.Kl;
+  for (int g = 0; g <= p.ngrp && g <= kMaxGroups; g++) {
+    a.gf[g] = p.gf[g];
+    a.gk[g] = p.gk[g];
+  }
   a.ctr = p.nt;
   if (p.bfs) {
     for (int L = 0; L <= p.nlevels && L <= kMaxLevels; L++) a.lvl[L] = p.lvl[L];
@@ -372,12 +387,51 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     }
   }
   {
-    int k = 0;
+    // counted slots numbered subtree by subtree (top-level field order), so that a field group's
+    // slots are contiguous
+    const int ntop = s->root ? 1 : s->num_fields;
+    std::vector<int32_t> kf(std::max(ntop, 1), 0);
+    for (int i = 0; i < nn; i++) {               // breadth-first: a parent before its children
+      TNode& n = p->nodes[i];
+      n.top = i < ntop ? i : p->nodes[n.parent].top;
+      const bool counted = n.type == FURY_TYPE_LIST || n.type == FURY_TYPE_MAP ||
+                           n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY;
+      if (counted) kf[n.top]++;
+    }
+    std::vector<int32_t> kn(kf.size() + 1, 0);  // first slot of each subtree
+    for (size_t f = 0; f < kf.size(); f++) kn[f + 1] = kn[f] + kf[f];
+    // field groups: consecutive top-level fields, about walk_group_k slots each, at most kMaxGroups
+    const int gk0 = g_walk_group_k.load();
+    p->ngrp = 1;
+    p->gf[0] = p->gk[0] = 0;
+    if (gk0 > 0 && K > gk0 && ntop > 1 && !s->root) {
+      for (int target = gk0;; target *= 2) {
+        int g = 0, acc = 0;
+        for (int f = 0; f < ntop && g < kMaxGroups; f++) {
+          if (acc > 0 && acc + kf[f] > target) {
+            g++;
+            if (g >= kMaxGroups) break;
+            p->gf[g] = f;
+            p->gk[g] = kn[f];
+            acc = 0;
+          }
+          acc += kf[f];
+        }
+        if (g < kMaxGroups) {
+          p->ngrp = g + 1;
+          break;
+        }
+      }
+    }
+    p->gf[p->ngrp] = ntop;
+    p->gk[p->ngrp] = K;
+    p->Kl = 0;
+    for (int g = 0; g < p->ngrp; g++) p->Kl = std::max(p->Kl, p->gk[g + 1] - p->gk[g]);
     for (int i = 0; i < nn; i++) {               // breadth-first: a parent before its children
       TNode& n = p->nodes[i];
       const bool counted = n.type == FURY_TYPE_LIST || n.type == FURY_TYPE_MAP ||
                            n.type == FURY_TYPE_STRING || n.type == FURY_TYPE_BINARY;
-      n.k = counted ? k++ : -1;
+      n.k = counted ? kn[n.top]++ : -1;
       if (counted && n.k < kWalkMaxK) p->knode[n.k] = i;
       if (i < s->num_fields) n.ek = -1;
       for (int j = 0; j < n.num_children; j++)
@@ -430,7 +484,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   // the count pass's per-row counters (4 B x counted nodes x rows) must fit one workgroup too:
   // a bean of ~200+ STRING fields counts on 64-row tiles
   while (p->nt > 64 &&
-         walk_count_lds(nn, K, p->nt, (g_walk_stage + 15) & ~15u, (g_walk_prefetch & 2) != 0) > kWalkLdsMax)
+         walk_count_lds(nn, p->Kl, p->nt, (g_walk_stage + 15) & ~15u, (g_walk_prefetch & 2) != 0) > kWalkLdsMax)
     p->nt /= 2;
   const int tw = g_walk_threads_w.load();
   p->ntw = tw % p->nt == 0 && tw >= p->nt ? tw : p->nt;
@@ -444,14 +498,14 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   // schemas (many counted nodes / nodes) step down the tile rows, then the windows.
   const bool pfw = (g_walk_prefetch & 1) != 0;
   for (;;) {
-    if (walk_write_lds(nn, K, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) <= kWalkLdsMax) break;
+    if (walk_write_lds(nn, p->Kl, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) <= kWalkLdsMax) break;
     if (p->ntw > p->nt) p->ntw /= 2;
     else if (p->out_cap > 0) p->out_cap = p->out_cap > 4096 ? p->out_cap / 2 : 0;
     else if (p->pool_cap > 0) p->pool_cap = p->pool_cap > 1024 ? p->pool_cap / 2 : 0;
     else if (p->stage_cap_w > 0) p->stage_cap_w = 0;
     else break;                                 // cannot happen for K <= kWalkMaxK, nn <= 512
   }
-  if (walk_write_lds(nn, K, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) > kWalkLdsMax) {
+  if (walk_write_lds(nn, p->Kl, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) > kWalkLdsMax) {
     tree_free(p);                               // (defensive) the level engine
     return FURY_OK;
   }

@@ -26,10 +26,13 @@ struct TNode {
   int32_t walk;             // walk.hip count pass: the node or a descendant has a counted slot
   int32_t ek;               // walk.hip: counted slot of the LIST / MAP whose elements hold this
                             // node's entries (through STRUCTs); -1: one entry per row
+  int32_t top;              // the top-level field whose subtree holds the node
+  int32_t pad_;
 };
 
 constexpr int kTreeMaxNodes = 512;
 constexpr int kMaxLevels = 64;
+constexpr int kMaxGroups = 32;
 
 struct TreeArgs {
   const TNode* nodes;       // device table (scalar loads: every use has a uniform index)
@@ -60,6 +63,12 @@ struct TreeArgs {
   uint32_t arena_cap;       // bfs.hip: LDS bytes of the per-node entry records
   int32_t pad2_;
   int32_t lvl[kMaxLevels + 1];  // bfs.hip: first node of each level (breadth-first numbering)
+  // walk.hip field groups (round 6): group g walks top-level fields [gf[g], gf[g + 1]) of its tile's
+  // rows and owns counted slots [gk[g], gk[g + 1]) (numbered subtree by subtree); Kl = the largest
+  // group's slots (the LDS cursors are per group)
+  int32_t ngrp, Kl;
+  int32_t gf[kMaxGroups + 1];
+  int32_t gk[kMaxGroups + 1];
 };
 
 constexpr int kWalkMaxK = 256;     // round 6: was 64 (wide nested beans went to the level engine)

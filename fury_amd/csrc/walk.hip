@@ -43,11 +43,11 @@ struct WShared {
   uint32_t* req;            // [2][nn + 1]: window words, scanned into window offsets
   uint64_t* wsum;           // [K][NT / 64] (pass 1) / [16] (pass 2) scan scratch
   uint32_t* pool;           // window words
-  int32_t* ow;              // [3][nn]: output window (values / offsets / payload) of node n in
-                            // opool, -1: stored straight to HBM
-  uint32_t* olen;           // [3][nn]: its bytes
-  int64_t* oe;              // [2][nn]: the tile's first entry (E0) / payload byte (B0) of node n
-  uint32_t* oreq;           // [3 nn + 1]: window bytes, scanned into window offsets
+  int32_t* ow;              // [2][nn]: output window (values / offsets) of node n in opool,
+                            // -1: stored straight to HBM
+  uint32_t* olen;           // [2][nn]: its bytes
+  int64_t* oe;              // [nn]: the tile's first entry (E0) of node n
+  uint32_t* oreq;           // [2 nn + 1]: window bytes, scanned into window offsets
   uint8_t* opool;           // output windows
   uint8_t* pf;              // prefetch landing zone
   uint8_t* stg;             // staged rows
@@ -81,13 +81,13 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   b = (b + 15) & ~size_t(15);
   const bool ow = write && out > 0;
   l.oe = b;
-  b += ow ? 8 * 2 * static_cast<size_t>(nn) : 0;
+  b += ow ? 8 * static_cast<size_t>(nn) : 0;
   l.ow = b;
-  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
+  b += ow ? 4 * 2 * static_cast<size_t>(nn) : 0;
   l.olen = b;
-  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
+  b += ow ? 4 * 2 * static_cast<size_t>(nn) : 0;
   l.oreq = b;
-  b += ow ? 4 * (3 * static_cast<size_t>(nn) + 1) : 0;
+  b += ow ? 4 * (2 * static_cast<size_t>(nn) + 1) : 0;
   b = (b + 15) & ~size_t(15);
   l.opool = b;
   b += ow ? out : 0;
@@ -101,7 +101,7 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
 }
 
 __device__ inline WShared walk_shared(uint8_t* base, const TreeArgs& a, int nt, bool write) {
-  const WLayout l = walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0,
+  const WLayout l = walk_layout(a.nn, a.Kl, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0,
                                 a.out_cap);
   WShared s;
   s.cur = reinterpret_cast<uint32_t*>(base + l.cur);
@@ -164,13 +164,33 @@ struct WCtx {
   int64_t row;
   int64_t wave_row;         // the row of lane 0 of this wave (ballots of row-aligned nodes)
   int tid;
-  // count pass: items (fields, elements, keys, values) the row's walk may still visit, 2 x its
-  // bytes + 64.  A row the encoder wrote holds every item in its own bytes (an 8-B slot, or >= 1 B
-  // per fixed-width element), so only a malformed row whose slots alias other bytes runs out --
-  // its walk would otherwise grow with the product of the aliased counts -- and is reported (the
-  // prepare fails, so the write pass, which visits the same items, never meets such a row).
+  // count pass: items (fields, elements, keys, values) the walk of the current top-level field
+  // may still visit, 2 x the row's bytes + 64.  A row the encoder wrote holds every item in its
+  // own bytes (an 8-B slot, or >= 1 B per fixed-width element), so only a malformed row whose slots
+  // alias other bytes runs out -- its walk would otherwise grow with the product of the aliased
+  // counts -- and is reported (the prepare fails, so the write pass, which visits the same items,
+  // never meets such a row).  Per top-level field, so that field groups see the same budget.
   mutable int32_t left;
+  int kg0;                  // the group's first counted slot (LDS cursors / bases are per group)
+  int f0, f1;               // the group's top-level fields
 };
+
+// Tile t and field group g of this workgroup.  One group: t = blockIdx.x.  Several: the grid is
+// ceil(tiles / 8) x 8 x ngrp blocks and the groups of a tile are consecutive blocks of ONE XCD
+// (blocks go to the 8 XCDs round robin), so they read the tile's rows through the same L2 at about
+// the same time.  Returns false for the padding blocks past the last tile.
+__device__ __forceinline__ bool wgroup(const TreeArgs& a, int64_t* t, int* g) {
+  const int64_t b = blockIdx.x;
+  if (a.ngrp <= 1) {
+    *t = b;
+    *g = 0;
+    return true;
+  }
+  const int64_t q = b >> 3;
+  *g = static_cast<int>(q % a.ngrp);
+  *t = (q / a.ngrp) * 8 + (b & 7);
+  return *t < a.ntiles;
+}
 
 // Charges a container's items to the row's budget (count pass): false, and the row reported, when
 // it is spent.  (Null structs are free: their fields read nothing.)  The level engine (deeper
@@ -231,10 +251,10 @@ __device__ __forceinline__ void wbits_run(const WCtx& c, int n, int which, uint8
 }
 
 // Output windows (write pass, a.out_cap > 0): the tile's entries of a node that is not row-aligned
-// (values of fixed-width / DECIMAL nodes, Arrow offsets of LIST / MAP / STRING / BINARY nodes) and
-// the payload bytes of every STRING / BINARY node are assembled in LDS and stored as whole lines at
-// the end of the tile: per-lane 1-8 B stores straight to HBM left partial lines (WRITE_SIZE 1.98x
-// the column bytes at 4M depth-3 rows).  A node whose window did not fit the
+// (values of fixed-width / DECIMAL nodes, Arrow offsets of LIST / MAP / STRING / BINARY nodes) are
+// assembled in LDS and stored as whole lines at the end of the tile (STRING / BINARY payload bytes
+// go straight to HBM, each row's run contiguous): per-lane 1-8 B stores straight to HBM left
+// partial lines (WRITE_SIZE 1.98x the column bytes at 4M depth-3 rows).  A node whose window did not fit the
 // pool (ow < 0), and the row-aligned ones (coalesced already), store to HBM.
 __device__ __forceinline__ int32_t wwin(const WCtx& c, int which, int n) {
   return c.a->out_cap ? c.sh->ow[which * c.a->nn + n] : -1;
@@ -342,11 +362,11 @@ __device__ __forceinline__ bool wentry(const WCtx& c, CTNode& N, int n, int64_t 
   *pcs = 0;
   if (W && !top && N.validity && !(a.skip & 2)) wbit(c, N, n, 0, N.validity, e, valid);
   if (ty == FURY_TYPE_STRING || ty == FURY_TYPE_BINARY) {
-    uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+    uint32_t* cu = c.sh->cur + (N.k - c.kg0) * static_cast<int>(blockDim.x) + c.tid;
     const uint32_t c0 = *cu;
     *cu = c0 + cnt;
     if (W) {
-      const int64_t bp = c.sh->kb[N.k] + c0;
+      const int64_t bp = c.sh->kb[N.k - c.kg0] + c0;
       if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(bp + cnt));
       if (valid && N.values && !(a.skip & 1)) wput_bytes(c, N, n, bp, pos, cnt);
     }
@@ -371,12 +391,12 @@ __device__ __forceinline__ bool wentry(const WCtx& c, CTNode& N, int n, int64_t 
   if (ty == FURY_TYPE_STRUCT) {
     *pm = (W || valid) ? static_cast<uint32_t>(N.num_children) : 0u;
   } else if (ty == FURY_TYPE_LIST || ty == FURY_TYPE_MAP) {
-    uint32_t* cu = c.sh->cur + N.k * static_cast<int>(blockDim.x) + c.tid;
+    uint32_t* cu = c.sh->cur + (N.k - c.kg0) * static_cast<int>(blockDim.x) + c.tid;
     const uint32_t c0 = *cu;
     *pm = cnt;
     *cu = c0 + cnt;
     if (W) {
-      *pcs = c.sh->kb[N.k] + c0;
+      *pcs = c.sh->kb[N.k - c.kg0] + c0;
       if (N.offsets && !(a.skip & 8)) wput_off(c, N, n, e, static_cast<int32_t>(*pcs + cnt));
     }
   }
@@ -451,13 +471,16 @@ __device__ __forceinline__ bool wvalue(const WCtx& c, int n, int64_t e, bool nul
   }
 }
 
-// The top level of one row (every thread of the workgroup, live or not: ballots).
+// The top level of one row, the group's fields (every thread of the workgroup, live or not:
+// ballots).
 template <bool W, int MD>
 __device__ __forceinline__ void walk_row(const WCtx& c, bool live) {
   const TreeArgs& a = *c.a;
   const Rows& R = *c.R;
   const int64_t base = live ? gl(a.offs)[c.row] : 0;
-  if (!W) c.left = live ? static_cast<int32_t>(min<int64_t>(2 * (gl(a.offs)[c.row + 1] - base) + 64, 1 << 30)) : 0;
+  const int32_t budget =
+      live ? static_cast<int32_t>(min<int64_t>(2 * (gl(a.offs)[c.row + 1] - base) + 64, 1 << 30)) : 0;
+  if (!W) c.left = budget;
   if (a.root) {                                  // collection batch: the entry IS the value
     bool valid = false;
     if (live) valid = wvalue<0, W, MD>(c, 0, c.row, false, 0, 0, base);
@@ -471,9 +494,10 @@ __device__ __forceinline__ void walk_row(const WCtx& c, bool live) {
     if (!rowok) raise_oob(a.err, c.row);
   }
   const int64_t hb = tbm(a.ntop);
-  for (int f = 0; f < a.ntop; f++) {
+  for (int f = c.f0; f < c.f1; f++) {
     CTNode& N = tn(a, f);
     if (N.width > 0 ? !W : !(W || N.walk)) continue;
+    if (!W) c.left = budget;
     const int64_t slotp = base + hb + 8 * f;
     // the null bit and the slot / value together: one round trip
     uint32_t nb = 1;
@@ -532,7 +556,10 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
   const WShared sh = walk_shared(wsm, a, NT, false);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t t = blockIdx.x;
+  int64_t t;
+  int g;
+  if (!wgroup(a, &t, &g)) return;                // (uniform: a padding block)
+  const int kg0 = a.gk[g], kn = a.gk[g + 1] - kg0, f0 = a.gf[g], f1 = a.gf[g + 1];
   const int64_t r0 = t * NT;
   const int64_t nr = min<int64_t>(NT, a.nrows - r0);
   const int64_t total = gl(a.offs)[a.nrows];
@@ -540,17 +567,17 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   __shared__ uint64_t tacc[16];
   const WClock clk{a.dbg ? tacc : nullptr};
   clk.start();
-  for (int k = 0; k < a.K; k++) sh.cur[k * NT + tid] = 0;
+  for (int k = 0; k < kn; k++) sh.cur[k * NT + tid] = 0;
   const Rows R = walk_stage<NT>(a, sh.stg, r0, nr, total);
   if (a.prefetch) walk_prefetch(a, sh, r0, tid, total, R.hi);
   __syncthreads();
   clk.mark(0);
-  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0};
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0, kg0, f0, f1};
   walk_row<false, MD>(c, live);
   clk.mark(1);
-  // in-tile exclusive prefix of every slot over the rows (row = thread)
+  // in-tile exclusive prefix of every slot of the group over the rows (row = thread)
   uint64_t* wsum = sh.wsum;
-  for (int k = 0; k < a.K; k++) {
+  for (int k = 0; k < kn; k++) {
     const uint64_t v = sh.cur[k * NT + tid];
     const uint64_t inc = tw_scan64(v);
     if (lane == 63) wsum[k * (NT / 64) + wave] = inc;
@@ -558,7 +585,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   }
   lds_barrier();   // (LDS only)
   bool over = false;
-  for (int k = 0; k < a.K; k++) {
+  for (int k = 0; k < kn; k++) {
     uint64_t pre = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < NT / 64; w++) {
@@ -567,7 +594,7 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
       tot += s;
     }
     over |= tot >= (1ull << 32);
-    if (live) gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] =
+    if (live) gl(a.rowpre)[static_cast<int64_t>(kg0 + k) * a.nrows + r0 + tid] =
         static_cast<uint32_t>(pre + sh.cur[k * NT + tid]);
     if (tid == 0) sh.kb[k] = static_cast<int64_t>(tot);
   }
@@ -576,8 +603,9 @@ __global__ __launch_bounds__(NT) void walk_count_kernel(TreeArgs a) {
   clk.mark(2);
   for (int n = tid; n < a.nn; n += NT) {
     CTNode& N = tn(a, n);
-    const int64_t ent = N.ek < 0 ? nr : sh.kb[N.ek];
-    const int64_t byt = (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY) ? sh.kb[N.k] : 0;
+    if (N.top < f0 || N.top >= f1) continue;   // another group's node
+    const int64_t ent = N.ek < 0 ? nr : sh.kb[N.ek - kg0];
+    const int64_t byt = (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY) ? sh.kb[N.k - kg0] : 0;
     a.cnt[n * a.stride + t] = ent;
     a.byt[n * a.stride + t] = byt;
   }
@@ -594,7 +622,10 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t wsm[];
   const WShared sh = walk_shared(wsm, a, NT, true);
   const int tid = threadIdx.x;
-  const int64_t t = blockIdx.x;
+  int64_t t;
+  int g;
+  if (!wgroup(a, &t, &g)) return;                // (uniform: a padding block)
+  const int kg0 = a.gk[g], kn = a.gk[g + 1] - kg0, f0 = a.gf[g], f1 = a.gf[g + 1];
   const int64_t r0 = t * NT;
   const int64_t nr = min<int64_t>(NT, a.nrows - r0);
   const int64_t total = gl(a.offs)[a.nrows];
@@ -613,18 +644,20 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
     return (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY)
                ? a.byt[n * a.stride + tc] : a.cnt[N.first_child * a.stride + tc];
   };
-  for (int k = 0; k < a.K; k++) {
-    uint32_t c = live ? gl(a.rowpre)[static_cast<int64_t>(k) * a.nrows + r0 + tid] : 0u;
-    if (tcr != tc0) c += static_cast<uint32_t>(slot_base(k, tcr) - slot_base(k, tc0));
+  for (int k = 0; k < kn; k++) {
+    uint32_t c = live ? gl(a.rowpre)[static_cast<int64_t>(kg0 + k) * a.nrows + r0 + tid] : 0u;
+    if (tcr != tc0) c += static_cast<uint32_t>(slot_base(kg0 + k, tcr) - slot_base(kg0 + k, tc0));
     sh.cur[k * NT + tid] = c;
   }
-  for (int k = tid; k < a.K; k += NT) sh.kb[k] = slot_base(k, tc0);
-  // bitmap windows of the nodes that are not row-aligned: words covering the tile's entries
+  for (int k = tid; k < kn; k += NT) sh.kb[k] = slot_base(kg0 + k, tc0);
+  // bitmap windows of the group's nodes that are not row-aligned: words covering the tile's entries
+  // (another group's nodes get none: its flush must not store their words)
   for (int i = tid; i < 2 * nn; i += NT) {
     const int n = i < nn ? i : i - nn;
     CTNode& N = tn(a, n);
-    const bool want = N.ek >= 0 && (i < nn ? N.validity != nullptr
-                                           : (N.type == FURY_TYPE_BOOL && N.values != nullptr));
+    const bool want = N.ek >= 0 && N.top >= f0 && N.top < f1 &&
+                      (i < nn ? N.validity != nullptr
+                              : (N.type == FURY_TYPE_BOOL && N.values != nullptr));
     uint32_t words = 0;
     if (want) {
       const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
@@ -636,24 +669,25 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   if (tid == 0) sh.req[2 * nn] = 0;
   // output windows: the tile's range of each node's values / offsets / payload (wput_*)
   if (a.out_cap) {
-    for (int i = tid; i < 3 * nn; i += NT) {
+    for (int i = tid; i < 2 * nn; i += NT) {
       const int which = i / nn, n = i - which * nn;
       CTNode& N = tn(a, n);
       const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
       int64_t bytes = 0;
+      const bool mine = N.ek >= 0 && N.top >= f0 && N.top < f1;
       if (which == 0) {
-        if (N.ek >= 0 && N.values && N.type != FURY_TYPE_BOOL &&
+        if (mine && N.values && N.type != FURY_TYPE_BOOL &&
             (N.width > 0 || N.type == FURY_TYPE_DECIMAL))
           bytes = (e1 - e0) * (N.width > 0 ? N.width : 16);
-      } else if (which == 1) {
+      } else {
         sh.oe[n] = e0;
-        if (N.ek >= 0 && N.offsets) bytes = 4 * (e1 - e0);
+        if (mine && N.offsets) bytes = 4 * (e1 - e0);
       }
       if (bytes > static_cast<int64_t>(a.out_cap)) bytes = 0;     // straight to HBM
       sh.olen[i] = static_cast<uint32_t>(bytes);
       sh.oreq[i] = bytes > 0 ? static_cast<uint32_t>((bytes + 31) & ~int64_t(15)) : 0u;
     }
-    if (tid == 0) sh.oreq[3 * nn] = 0;
+    if (tid == 0) sh.oreq[2 * nn] = 0;
   }
   Rows R{a.rows, sh.stg, 0, 0, 0};
   if constexpr (STG) R = walk_stage<NT>(a, sh.stg, r0, nr, total);
@@ -661,8 +695,8 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
   if (a.out_cap) {
-    block_scan_u32<NT>(sh.oreq, 3 * nn + 1, sh.wsum);
-    for (int i = tid; i < 3 * nn; i += NT)
+    block_scan_u32<NT>(sh.oreq, 2 * nn + 1, sh.wsum);
+    for (int i = tid; i < 2 * nn; i += NT)
       sh.ow[i] = sh.olen[i] > 0 && sh.oreq[i + 1] <= a.out_cap ? static_cast<int32_t>(sh.oreq[i]) : -1;
   }
   const uint32_t pool_words = a.pool_cap / 4;
@@ -674,7 +708,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   for (uint32_t i = tid; i < used; i += NT) sh.pool[i] = 0;
   lds_barrier();   // (LDS only)
   clk.mark(0);
-  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0};
+  WCtx c{&a, &sh, &R, total, r0 + tid, r0 + (tid & ~63), tid, 0, kg0, f0, f1};
   walk_row<true, MD>(c, live);
   clk.mark(1);
   lds_barrier();   // (LDS only: the walk's column stores need not land before the flush)
@@ -704,14 +738,13 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   // output windows -> HBM, a wave per window: the range [E0, E1) / [B0, B1) is this tile's alone
   if (a.out_cap) {
     const int wave = tid >> 6;
-    for (int i = wave; i < 3 * nn; i += NT / 64) {
+    for (int i = wave; i < 2 * nn; i += NT / 64) {
       const int32_t o = sh.ow[i];
       if (o < 0) continue;
       const int which = i / nn, n = i - which * nn;
       CTNode& N = tn(a, n);
       uint8_t* dst = which == 0 ? N.values + sh.oe[n] * (N.width > 0 ? N.width : 16)
-                   : which == 1 ? reinterpret_cast<uint8_t*>(N.offsets + sh.oe[n] + 1)
-                                : N.values + sh.oe[nn + n];
+                                : reinterpret_cast<uint8_t*>(N.offsets + sh.oe[n] + 1);
       wave_store_window(dst, sh.opool + o, sh.olen[i]);
     }
   }
@@ -722,7 +755,7 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
 }  // namespace
 
 size_t walk_lds(const TreeArgs& a, int nt, bool write) {
-  return walk_layout(a.nn, a.K, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0, a.out_cap).end;
+  return walk_layout(a.nn, a.Kl, nt, a.stage_cap, a.pool_cap, write, a.prefetch != 0, a.out_cap).end;
 }
 size_t walk_write_lds(int nn, int K, int nt, uint32_t stage, uint32_t pool, bool prefetch,
                       uint32_t out) {
@@ -737,7 +770,9 @@ int walk_launch(const TreeArgs& a, int nt, bool write, hipStream_t hs) {
   auto go = [&](auto kern) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(a.ntiles)), dim3(nt), lds, hs, a);
+    // field groups: ceil(tiles / 8) x 8 x groups blocks (wgroup)
+    const int64_t blocks = a.ngrp <= 1 ? a.ntiles : (a.ntiles + 7) / 8 * 8 * a.ngrp;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(blocks)), dim3(nt), lds, hs, a);
   };
   // instances per schema depth (a level of the inlined walk keeps ~30 VGPRs live)
 #define FURY_WALK(MD)                                                                        \

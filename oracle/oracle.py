@@ -340,7 +340,7 @@ def count_walk_flags(fields: Sequence[F], rows: np.ndarray, row_offsets: np.ndar
                      nrows: int) -> int:
     """ERR_* bits of the device row walk's COUNT pass (fury_decode_prepare), restated in
     row_oracle.c fo_count_walk: the container checks over the nodes that hold or contain a
-    counted slot, and the per-row item budget (ERR_BUDGET: a device limit)."""
+    counted slot, and the item budget per top-level field of a row (ERR_BUDGET: a device limit)."""
     keep: list = []
     if nrows == 0:
         return 0

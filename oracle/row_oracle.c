@@ -653,9 +653,10 @@ static void fo_read_value(const fo_view* v, int64_t ordinal, const fury_field* f
  * The device's two-phase nested decode (fury_decode_prepare, then fury_decode_execute) reports
  * the errors of its COUNT walk first: a walk of each row over the nodes that hold or contain a
  * counted slot (LIST / MAP elements, STRING / BINARY bytes -- walk.hip TNode.walk), with the same
- * container checks and a per-row item budget of 2 x the row's bytes + 64 (a row the encoder wrote
- * holds every item in its own bytes; a corrupted row whose slots alias other bytes would make the
- * walk grow with the product of the aliased counts).  fo_count_walk restates that walk exactly
+ * container checks and an item budget of 2 x the row's bytes + 64 per top-level field of a row
+ * (a row the encoder wrote holds every item in its own bytes; a corrupted row whose slots alias
+ * other bytes would make the walk grow with the product of the aliased counts; per field since
+ * round 6, when the device walks a wide bean's top-level fields in groups).  fo_count_walk restates that walk exactly
  * (walk.hip walk_row / wvalue / wcharge) so a test can predict which error the prepare reports;
  * FO_ERR_BUDGET is the device's own limit, not a reference exception.
  * ---------------------------------------------------------------------------------------- */
@@ -668,7 +669,7 @@ static int fo_walks(const fury_field* f) {
   return 0;
 }
 
-static _Thread_local int64_t g_left;  /* the row's remaining item budget (-1: spent) */
+static _Thread_local int64_t g_left;  /* the field's remaining item budget (-1: spent) */
 
 static int fo_charge(const fury_field* f, int valid, int64_t m) {
   int64_t items = f->type_id == FURY_TYPE_MAP ? 2 * m
@@ -717,11 +718,12 @@ int32_t fo_count_walk(const fury_field* fields, int32_t nfields, const uint8_t* 
   for (int64_t i = 0; i < nrows; i++) {
     int64_t base = row_offsets[i];
     int64_t budget = 2 * (row_offsets[i + 1] - base) + 64;
-    g_left = budget < (1 << 30) ? budget : (1 << 30);
+    if (budget > (1 << 30)) budget = 1 << 30;
     int rowok = fo_span_ok(base, hb + 8LL * nfields);
     if (!rowok) g_flags |= FO_ERR_OOB;
     for (int k = 0; k < nfields; k++) {
       if (fo_type_width(fields[k].type_id) > 0 || !fo_walks(&fields[k])) continue;
+      g_left = budget;
       int nul = !rowok || ((rows[base + (k >> 3)] >> (k & 7)) & 1);
       fo_cwalk(&fields[k], nul, rowok ? fo_get_i64(rows + base + hb + 8 * k) : 0, base);
     }

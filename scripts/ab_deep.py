@@ -25,6 +25,7 @@ def main():
                     "many STRING fields plus a list of structs (the walk's 64-counted-node limit)")
     ap.add_argument("--modes", default="3,1", help="nested_decode settings (3 tile BFS, 2 row "
                     "walk -- at most 5 levels, else the level engine --, 1 level engine)")
+    ap.add_argument("--tune", default="", help="key=value,... tunings set first (e.g. walk_group_k=8)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -34,6 +35,9 @@ def main():
     from tests.test_tree import _beans, _deep_fields
     dev = torch.device("cuda:0")
     L = N.lib()
+    for kv in [x for x in args.tune.split(",") if x]:
+        k, v = kv.split("=")
+        assert L.fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
     from fury_amd import types as T
     cases = [("levels", int(x)) for x in args.levels.split(",") if x]
     cases += [("counted", int(x)) for x in args.wide.split(",") if x]
@@ -56,7 +60,7 @@ def main():
         offs = torch.cat([b0.row_offsets[:-1] + i * tot for i in range(reps)] +
                          [torch.tensor([reps * tot], dtype=torch.int64, device=dev)])
         batch = RowBatch(rows, offs, n, enc.schema_hash)
-        res = {kind: levels, "rows": n, "row_bytes": reps * tot}
+        res = {kind: levels, "rows": n, "row_bytes": reps * tot, "tune": args.tune}
         ref = None
         for mode in [int(x) for x in args.modes.split(",")]:
             assert L.fury_set_tuning(b"nested_decode", mode) == 0

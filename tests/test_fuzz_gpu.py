@@ -47,7 +47,7 @@ def _decode(enc, batch):
 
 
 def _shape(fields):
-    """(levels, counted nodes) of a schema: the row walk takes <= 5 levels, <= 64 counted nodes."""
+    """(levels, counted nodes) of a schema: the row walk takes <= 5 levels, <= 256 counted nodes."""
     def walk(f, d):
         lv, k = d + 1, int(f.type_id in COUNTED)
         for c in f.children:
@@ -101,6 +101,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
     levels, counted = _shape(fields)
     L = N.lib()
     old = L.fury_get_tuning(b"nested_decode")
+    old_gk = L.fury_get_tuning(b"walk_group_k")
     seen = []
     try:
         for trial in range(3):
@@ -108,11 +109,13 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
             if len(bad):
                 pos = rng.integers(0, len(bad), int(rng.integers(1, 40)))
                 bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
-            for mode in ((4, 3, 2, 1) if enc.nested else (3,)):
-                L.fury_set_tuning(b"nested_decode", mode)
-                walkable = levels <= 5 and counted <= 64
+            # 21: the row walk in field groups of one counted slot (walk_group_k 1)
+            for mode in ((4, 3, 2, 21, 1) if enc.nested else (3,)):
+                L.fury_set_tuning(b"walk_group_k", 1 if mode == 21 else old_gk)
+                L.fury_set_tuning(b"nested_decode", 2 if mode == 21 else mode)
+                walkable = levels <= 5 and counted <= 256
                 engine = ("bfs" if mode == 4 or (mode == 3 and not walkable)
-                          else "walk" if mode in (2, 3) and walkable else "levels")
+                          else "walk" if mode in (2, 3, 21) and walkable else "levels")
                 walk = engine != "levels" and walkable
                 want = _expected(O, fields, enc.nested, engine, bad, offs, n)
                 try:
@@ -138,4 +141,5 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
         assert_columns_equal(fields, _decode(enc, _batch(enc, rows, offs, n, dev)), ref, n)
     finally:
         L.fury_set_tuning(b"nested_decode", old)
+        L.fury_set_tuning(b"walk_group_k", old_gk)
     print(f"seed {seed}: {seen}")

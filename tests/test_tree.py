@@ -38,7 +38,7 @@ def engines():
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "walk_threads", "walk_stage", "walk_pool",
                                                        "walk_stage_write", "walk_threads_write",
                                                        "walk_out", "bfs_threads", "bfs_rows",
-                                                       "bfs_stage", "bfs_arena")}
+                                                       "bfs_stage", "bfs_arena", "walk_group_k")}
     yield
     for k, v in old.items():
         _tune(k, v)
@@ -99,6 +99,12 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
         _tune("walk_out", wo)
         walk = _decode_plan(enc, batch)
         assert_columns_equal(fields, walk, ref, n)
+    # field groups (walk_group_k): a workgroup per (tile, group of top-level fields); 1 = about one
+    # counted slot per group, the most groups the schema splits into
+    for gk in (1, 2):
+        _tune("walk_group_k", gk)
+        assert_columns_equal(fields, _decode_plan(enc, batch), ref, n)
+    _tune("walk_group_k", 16)
     # tile BFS: threads / tile rows, a stage far smaller than the tile (rows read from HBM), an
     # arena too small for the tile (the batch falls back to the row walk), and the defaults
     from fury_amd import _native as N
@@ -118,10 +124,10 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
             assert L.fury_get_tuning(b"bfs_fallbacks") > fb     # the arena leg really fell back
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 21])
 def test_tree_decode_large_batch(oracle, dev, engines, mode):
     """400k depth-3 rows (thousands of tiles, multi-chunk tile scans) == the oracle's decode, level
-    engine (1), row walk (2) and tile BFS (3)."""
+    engine (1), row walk (2), row walk in field groups of one counted slot (21) and tile BFS (4)."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     from tests.test_device import _nested_beans, _nested_fields
@@ -132,7 +138,9 @@ def test_tree_decode_large_batch(oracle, dev, engines, mode):
     enc = Encoders.bean(fields, device=dev)
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_decode", mode)
+    if mode == 21:                             # the row walk in field groups of one counted slot
+        _tune("walk_group_k", 1)
+    _tune("nested_decode", 2 if mode == 21 else mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
@@ -150,7 +158,7 @@ def test_collections_both_engines(oracle, dev, engines, mode, kind):
         test_array_encoder_batch_vs_oracle(oracle, dev, kind)
 
 
-@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 21])
 def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     """Tiles whose bytes exceed the stage (rows of very different sizes): the rows past the stage
     are read from HBM, the result is the oracle's."""
@@ -170,7 +178,9 @@ def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     n = len(beans)
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
-    _tune("nested_decode", mode)
+    if mode == 21:                             # the row walk in field groups of one counted slot
+        _tune("walk_group_k", 1)
+    _tune("nested_decode", 2 if mode == 21 else mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
 
@@ -385,12 +395,19 @@ def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
         pos = rng.integers(lo, len(bad), 24)
         bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
         res = {}
-        for mode in (4, 3, 2, 1):
-            _tune("nested_decode", mode)
+        for mode in (4, 3, 2, 21, 1):          # 21: the row walk in field groups of one slot
+            _tune("walk_group_k", 1 if mode == 21 else 16)
+            _tune("nested_decode", 2 if mode == 21 else mode)
             try:
                 res[mode] = [column_to_host(c) for c in enc.decode_batch(_batch(enc, bad, offs, n, dev))]
             except (IndexOutOfBoundsException, UnsupportedOperationException) as e:
                 res[mode] = type(e)
+        _tune("walk_group_k", 16)
+        # the grouped walk checks and charges exactly what the one-group walk does
+        if isinstance(res[2], type) or isinstance(res[21], type):
+            assert res[21] == res[2], (res[2], res[21])
+        else:
+            assert_columns_equal(fields, res[21], res[2], n)
         # a raise need not agree: the walk reports rows whose aliased slots would make it visit
         # more items than the row has bytes (its item budget), the level engine batches whose
         # elements or payload bytes outnumber the batch's row bytes; two decodes agree
@@ -496,8 +513,9 @@ def test_random_nested_schemas(oracle, dev, engines, seed):
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     ref = oracle.decode(fields, want, want_offs, n)
-    for mode in (4, 3, 2, 1):
-        _tune("nested_decode", mode)
+    for mode in (4, 3, 2, 21, 1):              # 21: the row walk in field groups of one slot
+        _tune("walk_group_k", 1 if mode == 21 else 16)
+        _tune("nested_decode", 2 if mode == 21 else mode)
         got = _decode_plan(enc, batch) if enc.nested else None
         if got is None:
             from fury_amd.encoder import column_to_host
@@ -533,9 +551,10 @@ def _levels(f):
 @pytest.mark.parametrize("nstr", [126, 254])
 def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
     """Beans with 128 / 256 counted nodes (STRING fields + a LIST of a STRING struct): round 6 lifts
-    the row walk's 64-counted-node limit to 256 (per-row cursors sized into the LDS by stepping the
-    tile rows down), so these decode through the walk (nested_decode 2) -- and the tile BFS (4) and
-    the level engine (1) -- to the oracle's columns."""
+    the row walk's 64-counted-node limit to 256 and walks such beans in field groups (a workgroup
+    per tile and group of top-level fields, walk_group_k slots each: 8 / 16 groups at the default
+    16, the 32-group cap at 4, one group at 0), so these decode through the walk (nested_decode 2)
+    -- and the tile BFS (4) and the level engine (1) -- to the oracle's columns."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     fields = ([T.not_null_field("id", T.INT64)] + [T.field(f"s{i:03d}", T.STRING) for i in range(nstr)]
@@ -548,6 +567,7 @@ def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     ref = oracle.decode(fields, want, want_offs, n)
-    for mode in (2, 4, 1):
+    for mode, gk in ((2, 16), (2, 4), (2, 0), (4, 16), (1, 16)):
+        _tune("walk_group_k", gk)
         _tune("nested_decode", mode)
         assert_columns_equal(fields, _decode_plan(enc, batch), ref, n)
