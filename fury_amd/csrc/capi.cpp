@@ -1093,6 +1093,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_skip(value);
     return FURY_OK;
   }
+  if (std::string(key) == "var_dec_pipe") {
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_pipe: 0..2");
+    set_var_dec_pipe(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "var_dec_rows") {
     if (value != 0 && (value < 64 || value > 512 || value % 64))
       return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_rows: 0 or 64..512 in steps of 64");
@@ -1126,9 +1131,9 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_walk_tuning(0, static_cast<uint32_t>(value));
     return FURY_OK;
   }
-  if (std::string(key) == "walk_group_k") {
-    if (value < 0 || value > 256) return set_error(FURY_ERR_INVALID_ARGUMENT, "walk_group_k: 0..256 (0: one field group)");
-    set_walk_tuning(8, static_cast<uint32_t>(value));
+  if (std::string(key) == "walk_group_k" || std::string(key) == "walk_group_min") {
+    if (value < 0 || value > 256) return set_error(FURY_ERR_INVALID_ARGUMENT, std::string(key) + ": 0..256");
+    set_walk_tuning(std::string(key) == "walk_group_k" ? 8 : 9, static_cast<uint32_t>(value));
     return FURY_OK;
   }
   if (std::string(key) == "walk_out") {
@@ -1187,9 +1192,11 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_prefetch") return static_cast<int32_t>(walk_tuning(4));
   if (key && std::string(key) == "walk_threads_write") return static_cast<int32_t>(walk_tuning(6));
   if (key && std::string(key) == "walk_group_k") return static_cast<int32_t>(walk_tuning(8));
+  if (key && std::string(key) == "walk_group_min") return static_cast<int32_t>(walk_tuning(9));
   if (key && std::string(key) == "walk_out") return static_cast<int32_t>(walk_tuning(7));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
+  if (key && std::string(key) == "var_dec_pipe") return var_dec_pipe();
   if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_wide") return var_wide_mode();
   if (key && std::string(key) == "wide_threads") return wide_threads(false);

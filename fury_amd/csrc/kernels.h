@@ -96,7 +96,7 @@ struct VarArgs {
   int32_t help_now;          // look-backs help a silent predecessor at once (test hook, tuning
                              // "lookback_help"); 0 in production
   int32_t skip;              // diagnostics (tuning "var_skip"): phases skipped, outputs WRONG
-  int32_t pad_;
+  int32_t dec_pipe;          // decode_var_reg: persistent workgroups, two row stages (var_dec_pipe)
   uint32_t* err;             // the launch stream's device error slot (device_error_word) or NULL
 };
 
@@ -204,6 +204,8 @@ int host_decode_inplace();
 int var_dec_rows();                   // tuning "var_dec_rows" (var.hip): 0 = planned
 void set_var_dec_rows(int v);
 int var_dec_rows_rejected();          // forced tiles whose images did not fit (plan used instead)
+int var_dec_pipe();                   // tuning "var_dec_pipe" (var.hip)
+void set_var_dec_pipe(int v);
 int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
 void set_var_dec_cover(int v);
 int lookback_help_mode();

@@ -132,11 +132,15 @@ std::atomic<uint32_t> g_walk_out{40 * 1024};     // tuning "walk_out": LDS outpu
 std::atomic<int> g_walk_prefetch = 1;            // tuning "walk_prefetch": waves pull their rows into L2 first
                                     // (bit 0: write pass, bit 1: count pass)
 std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnostics (TreeArgs.skip)
-// tuning "walk_group_k": field groups (round 6) -- a schema with more counted slots than this walks
-// its top-level fields in groups of about this many slots, a workgroup per (tile, group): the LDS
-// cursors (4 B x slots x rows) of a 128-slot bean held one 64-row count tile per ~5 waves of a CU;
-// 0 = one group
-std::atomic<int> g_walk_group_k = 16;
+// Field groups (round 6): a schema with more than "walk_group_min" counted slots walks its
+// top-level fields in groups of about "walk_group_k" slots, a workgroup per (tile, group): the LDS
+// cursors (4 B x slots x rows) of a 128-slot bean held one 64-row count tile per ~5 waves of a CU.
+// 1M beans of 128 / 200 counted nodes (scripts/r06_group2.sh): one group 22.5 / 39.0 ms, groups
+// of 16 / 8 / 4 / 2 slots 9.7 / 7.2 / 6.8 / 6.9 and 13.8 / 10.2 / 10.2 / 10.2 ms, the level engine
+// 16.5 / 25.7 ms.  The depth-3 schema (9 slots) in groups of 4 / 2 / 1: 2.64 / 2.99 / 3.25 vs
+// 2.53 ms -- at <= 16 slots the cursors do not limit the tiles per CU, so it stays one group.
+std::atomic<int> g_walk_group_k = 4;     // tuning "walk_group_k" (0 = one group)
+std::atomic<int> g_walk_group_min = 16;  // tuning "walk_group_min"
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 
 }  // namespace
@@ -174,6 +178,7 @@ void set_walk_tuning(int which, uint32_t v) {
   else if (which == 5) g_walk_skip = static_cast<int>(v);
   else if (which == 7) g_walk_out = (v + 15) & ~15u;
   else if (which == 8) g_walk_group_k = static_cast<int>(v);
+  else if (which == 9) g_walk_group_min = static_cast<int>(v);
   else g_walk_threads_w = static_cast<int>(v);
 }
 uint32_t walk_tuning(int which) {
@@ -182,7 +187,8 @@ uint32_t walk_tuning(int which) {
          : which == 4 ? static_cast<uint32_t>(g_walk_prefetch)
          : which == 5 ? static_cast<uint32_t>(g_walk_skip)
          : which == 7 ? g_walk_out.load()
-         : which == 8 ? static_cast<uint32_t>(g_walk_group_k) : static_cast<uint32_t>(g_walk_threads_w);
+         : which == 8 ? static_cast<uint32_t>(g_walk_group_k)
+         : which == 9 ? static_cast<uint32_t>(g_walk_group_min) : static_cast<uint32_t>(g_walk_threads_w);
 }
 
 struct TreePlan {
@@ -201,6 +207,7 @@ struct TreePlan {
   uint32_t pool_cap = 0, out_cap = 0;  // write pass: bitmap-window / output-window LDS bytes
   int32_t knode[kWalkMaxK] = {};
   int32_t ngrp = 1, Kl = 0;           // field groups (TreeArgs)
+  int32_t prefetch = 0;               // walk_prefetch bits of this plan
   int32_t gf[kMaxGroups + 1] = {}, gk[kMaxGroups + 1] = {};
   int32_t lvl[kMaxLevels + 1] = {};   // first node of each level
   // tile BFS (bfs.hip)
@@ -238,7 +245,7 @@ int tree_launch(const TreePlan& p, bool write, const TNode* dev_nodes, const uin
   a.stage_cap = write ? p.stage_cap_w : p.stage_cap;
   a.dbg = tree_debug_buffer();
   a.stride = p.stride;
-  a.prefetch = (g_walk_prefetch >> (write ? 0 : 1)) & 1;
+  a.prefetch = (p.prefetch >> (write ? 0 : 1)) & 1;
   a.skip = write ? g_walk_skip.load() : 0;
   a.rowpre = p.rowpre;
   a.K = p.K;
@@ -404,7 +411,7 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
     const int gk0 = g_walk_group_k.load();
     p->ngrp = 1;
     p->gf[0] = p->gk[0] = 0;
-    if (gk0 > 0 && K > gk0 && ntop > 1 && !s->root) {
+    if (gk0 > 0 && K > g_walk_group_min.load() && ntop > 1 && !s->root) {
       for (int target = gk0;; target *= 2) {
         int g = 0, acc = 0;
         for (int f = 0; f < ntop && g < kMaxGroups; f++) {
@@ -481,22 +488,27 @@ int tree_prepare(const fury_schema* s, const uint8_t* rows, const int64_t* offs,
   // a thread per row; the stage holds the tile's rows up to walk_stage bytes (the rest are read
   // from HBM), the bitmap-window pool walk_pool bytes
   p->nt = g_walk_threads;
+  // Field groups read only their fields' slots and payloads: the L2 pull of whole rows (per group)
+  // and the count stage cost more than they save (1M beans of 128 counted nodes, groups of 4:
+  // 9.9 -> 7.1 ms without the pull, 6.9 ms without the stage too; scripts/r06_group2.sh)
+  p->prefetch = p->ngrp > 1 ? 0 : g_walk_prefetch.load();
+  const uint32_t cstage = p->ngrp > 1 ? 0u : (g_walk_stage + 15) & ~15u;
   // the count pass's per-row counters (4 B x counted nodes x rows) must fit one workgroup too:
   // a bean of ~200+ STRING fields counts on 64-row tiles
   while (p->nt > 64 &&
-         walk_count_lds(nn, p->Kl, p->nt, (g_walk_stage + 15) & ~15u, (g_walk_prefetch & 2) != 0) > kWalkLdsMax)
+         walk_count_lds(nn, p->Kl, p->nt, cstage, (p->prefetch & 2) != 0) > kWalkLdsMax)
     p->nt /= 2;
   const int tw = g_walk_threads_w.load();
   p->ntw = tw % p->nt == 0 && tw >= p->nt ? tw : p->nt;
   p->tile_rows = p->nt;
-  p->stage_cap = (g_walk_stage + 15) & ~15u;
+  p->stage_cap = cstage;
   p->stage_cap_w = (g_walk_stage_w + 15) & ~15u;
   if (p->ntw > 256 && p->stage_cap_w) p->ntw = 256;   // 512-row write tiles: unstaged instance only
   p->pool_cap = g_walk_pool;
   p->out_cap = g_walk_out;
   // The write pass's LDS (cursors: K x rows, node tables, windows) must fit one workgroup: wide
   // schemas (many counted nodes / nodes) step down the tile rows, then the windows.
-  const bool pfw = (g_walk_prefetch & 1) != 0;
+  const bool pfw = (p->prefetch & 1) != 0;
   for (;;) {
     if (walk_write_lds(nn, p->Kl, p->ntw, p->stage_cap_w, p->pool_cap, pfw, p->out_cap) <= kWalkLdsMax) break;
     if (p->ntw > p->nt) p->ntw /= 2;

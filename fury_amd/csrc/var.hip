@@ -203,6 +203,12 @@ void set_var_dec_rows(int v) { g_dec_rows = v; }
 // is read from HBM by the rows' threads).  95 (scripts/ab_dec.py legs, interleaved): mixed 10M
 // 0.542 -> 0.508 ms (its tiles grow 448 -> 512 rows), C4 4M unchanged (0.229 ms); 80 or less slows C4.
 static std::atomic<int> g_dec_cover = 95;
+// tuning "var_dec_pipe" (round 6): 0 one tile per workgroup; 1 persistent
+// workgroups with two row stages of the planned size (fewer workgroups per CU); 2 the same with
+// the planned LDS split into images + two half stages (the tile rows shrink to fit)
+static std::atomic<int> g_dec_pipe = 0;
+int var_dec_pipe() { return g_dec_pipe; }
+void set_var_dec_pipe(int v) { g_dec_pipe = v; }
 int var_dec_cover() { return g_dec_cover; }
 void set_var_dec_cover(int v) { g_dec_cover = v; }
 
@@ -212,7 +218,7 @@ void set_var_dec_cover(int v) { g_dec_cover = v; }
 // bound sizing); a tile whose payload outgrows its image stores that column straight to HBM and
 // rows past the stage are read from HBM (both correct, slower), so the estimate only moves speed.
 // mixed (C3): 512-row tiles.
-void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) {
+void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage, int pipe = 0) {
   constexpr int64_t kBudget = 80 * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
   double row = a.fixed_size, img_row = 0, img_fix = 0;
   for (int k = 0; k < a.ncols; k++) {
@@ -243,18 +249,18 @@ void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage) 
     if (im <= kBudget / 2) {
       *tile = R;
       *img = static_cast<uint32_t>(im);
-      *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
+      *stage = static_cast<uint32_t>(((kBudget - *img) / (pipe == 2 ? 2 : 1)) & ~int64_t(15));
       return;
     }
     g_dec_rows_rejected.fetch_add(1);
   }
   for (int R = kDecThreads; R >= 64; R -= 64) {
     const int64_t im = (static_cast<int64_t>(img_row * R * mi + img_fix) + 1023) & ~int64_t(1023);
-    const int64_t st = (kBudget - im) & ~int64_t(15);
+    const int64_t st = ((kBudget - im) / (pipe == 2 ? 2 : 1)) & ~int64_t(15);
     if (st >= static_cast<int64_t>(row * R * mr * g_dec_cover / 100.0) + 64 || R == 64) {
       *tile = R;
       *img = static_cast<uint32_t>(std::min<int64_t>(im, kBudget / 2));
-      *stage = static_cast<uint32_t>((kBudget - *img) & ~int64_t(15));
+      *stage = static_cast<uint32_t>(((kBudget - *img) / (pipe == 2 ? 2 : 1)) & ~int64_t(15));
       return;
     }
   }
@@ -272,7 +278,8 @@ int launch_decode_var(const VarArgs& a, const uint8_t* rows, const int64_t* offs
   if (a.ncols <= kRegCols) {
     VarArgs b = a;
     uint32_t img = 0, stage = 0;
-    dec_tile_plan(a, &b.tile_rows, &img, &stage);
+    b.dec_pipe = dec_pipe_k(reg_dec_k(a.ncols)) ? g_dec_pipe.load() : 0;
+    dec_tile_plan(a, &b.tile_rows, &img, &stage, b.dec_pipe);
     const int64_t nt = (a.nrows + b.tile_rows - 1) / b.tile_rows;
     // status words: tiles x K (the instance's column count), zeroed per launch
     const size_t wsb = static_cast<size_t>(nt) * reg_dec_k(a.ncols) * 8;

@@ -1375,7 +1375,7 @@ __device__ __forceinline__ void store_bits_shifted(uint8_t* bits, const uint32_t
 
 #ifdef FURY_VAR_DEC
 // (K <= 4: at most 128 VGPRs, so two 512-thread workgroups share a CU -- the LDS plan assumes two)
-template <int K, int M>
+template <int K, int M, bool PIPE = false>
 __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <= 4 ? 4 : 1))) void decode_var_reg(VarArgs a, const uint8_t* __restrict__ rows,
                                                               const int64_t* __restrict__ offs,
                                                               uint64_t* __restrict__ status,
@@ -1393,35 +1393,54 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
   // the look-back helps itself (look_back_help): a predecessor that has published nothing for a
   // long time -- not dispatched yet, under any dispatch order -- has its aggregate computed from
   // its rows by the waiting wave, so no wait depends on a workgroup that is not running.
-  const int64_t b = static_cast<int64_t>(blockIdx.x), nb = gridDim.x;
   const int64_t TR = a.tile_rows;                 // rows per tile (<= NT, a multiple of 64)
+  const int64_t nb = (a.nrows + TR - 1) / TR;     // tiles
   constexpr int NW = NT / 64;
-  const int64_t r0 = b * TR;
-  const int nr = static_cast<int>(min<int64_t>(TR, a.nrows - r0));
-  const bool live = tid < nr;
-  const int64_t r = live ? r0 + tid : r0;
   const int64_t total = offs[a.nrows];            // the batch: every read stays in [0, total)
   // The tile's row bytes [offs[r0], offs[r0 + nr]) (up to stage_cap of them) are staged in LDS by
   // coalesced LDS-DMA pieces; header, string and list reads of rows inside the staged range read
   // LDS, the rest HBM.  (Per-lane row reads from HBM touched one cache line per lane per
   // instruction and fetched every line from L2 again for the header and for each value: 40M L1
   // misses vs 11.5M staged on 10M mixed rows, TCP_TCC_READ_REQ.)
-  uint8_t* const stg = reinterpret_cast<uint8_t*>(oimg) + img_cap;
-  uintptr_t sa_lo = 0, sa_hi = 0;                 // absolute addresses held by stg
-  const int64_t base0 = offs[r];                  // issued before the staging (its own round trip)
-  {
+  // PIPE (round 6, tuning "var_dec_pipe"; its own instances -- the loop costs the one-tile kernel
+  // 30-50 VGPRs): a persistent grid whose workgroups take tiles blockIdx, + gridDim, ... with TWO
+  // stages: the next tile's LDS-DMA is issued once the current
+  // tile's prefixes are resolved (its last global loads), so it lands during the offsets and the
+  // image store-out (vmcnt is in order: issued earlier, every wait on a load of the tile would wait
+  // for it too).
+  uint8_t* const stg0 = reinterpret_cast<uint8_t*>(oimg) + img_cap;
+  uint8_t* const stg1 = stg0 + (PIPE ? stage_cap : 0u);
+  auto stage_tile = [&](int64_t t, uint8_t* sp, uintptr_t* lo, uintptr_t* hi) {
+    const int64_t t0 = t * TR;
+    const int64_t tn = min<int64_t>(TR, a.nrows - t0);
     const int64_t tt = max<int64_t>(total, 0);
-    const int64_t g0 = min<int64_t>(max<int64_t>(offs[r0], 0), tt);
-    const int64_t g1 = min<int64_t>(max<int64_t>(offs[r0 + nr], g0), tt);
-    sa_lo = reinterpret_cast<uintptr_t>(rows + g0) & ~uintptr_t(15);
-    sa_hi = min<uintptr_t>(reinterpret_cast<uintptr_t>(rows + g1), sa_lo + stage_cap);
+    const int64_t g0 = min<int64_t>(max<int64_t>(offs[t0], 0), tt);
+    const int64_t g1 = min<int64_t>(max<int64_t>(offs[t0 + tn], g0), tt);
+    *lo = reinterpret_cast<uintptr_t>(rows + g0) & ~uintptr_t(15);
+    *hi = min<uintptr_t>(reinterpret_cast<uintptr_t>(rows + g1), *lo + stage_cap);
     uint32_t at = 0;
-    if (sa_hi > sa_lo)
-      stage_range<NT>(stg, at, reinterpret_cast<const uint8_t*>(sa_lo),
-                      reinterpret_cast<const uint8_t*>(sa_hi));
-    // the output images are zeroed while the pieces are in flight
+    if (*hi > *lo)
+      stage_range<NT>(sp, at, reinterpret_cast<const uint8_t*>(*lo), reinterpret_cast<const uint8_t*>(*hi));
+    else
+      *hi = *lo;
+  };
+  auto zero_images = [&]() {
     for (uint32_t i = 16 * tid; i < img_cap; i += 16 * NT)
       *reinterpret_cast<__attribute__((ext_vector_type(4))) uint32_t*>(reinterpret_cast<uint8_t*>(oimg) + i) = 0;
+  };
+  uintptr_t nx_lo = 0, nx_hi = 0;                 // the next tile's staged range (dec_pipe)
+  int64_t b = static_cast<int64_t>(blockIdx.x);
+  for (int it = 0;; it++) {
+  uint8_t* const stg = (it & 1) ? stg1 : stg0;
+  const int64_t r0 = b * TR;
+  const int nr = static_cast<int>(min<int64_t>(TR, a.nrows - r0));
+  const bool live = tid < nr;
+  const int64_t r = live ? r0 + tid : r0;
+  uintptr_t sa_lo = nx_lo, sa_hi = nx_hi;         // absolute addresses held by stg
+  const int64_t base0 = offs[r];                  // issued before the staging (its own round trip)
+  if (it == 0) {
+    stage_tile(b, stg, &sa_lo, &sa_hi);
+    zero_images();                                // (while the pieces are in flight)
     __syncthreads();
   }
   const int64_t lim = total - a.fixed_size;       // last byte a row header may start at
@@ -1701,6 +1720,9 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
       }
     }
   }
+  const int64_t nxt = b + static_cast<int64_t>(gridDim.x);
+  const bool more = PIPE && nxt < nb;
+  if (more) stage_tile(nxt, (it & 1) ? stg0 : stg1, &nx_lo, &nx_hi);
   lds_barrier();   // (LDS only: the column / status stores need not land first)
   // Arrow offsets; columns whose range did not fit the image go straight to HBM (rare)
 #pragma unroll
@@ -1776,6 +1798,13 @@ __global__ __launch_bounds__(kDecThreads) __attribute__((amdgpu_waves_per_eu(K <
     }
     if (c.elem_validity)
       store_bits_shifted<NT>(c.elem_validity, reinterpret_cast<const uint32_t*>(im + vb), gb, n);
+  }
+  if constexpr (!PIPE) break;
+  if (!more) break;
+  __syncthreads();   // the images are read out, the next stage has landed (vmcnt)
+  zero_images();
+  lds_barrier();
+  b = nxt;
   }
 }
 #endif  // FURY_VAR_DEC
@@ -2085,6 +2114,24 @@ int launch_encode_var_reg(const VarArgs& b, int64_t* offs, uint8_t* rows, int64_
 int launch_measure_tiles(const VarArgs& b, int64_t* tsum, int64_t ntiles, hipStream_t stream);
 // The register-staged instances: K in {2, 3, 4, 6, 8, 12, 16} columns (the schema's fields rounded
 // up; the decode's look-back status words are tiles x K) x mode (kind_of, from reg_mode).
+// The instances with a persistent two-stage variant (VarArgs.dec_pipe): the C4 (3 columns) and
+// C3 (6 columns) shapes -- an A/B, not every width.
+constexpr bool dec_pipe_k(int k) { return k == 3 || k == 6; }
+
+// Workgroups of a persistent decode_var_reg launch (VarArgs.dec_pipe): the resident count, at most
+// the tiles.
+inline int64_t dec_pipe_grid(const void* kern, int64_t nt, size_t lds) {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }();
+  (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds));
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kDecThreads, lds) != hipSuccess || per < 1) per = 1;
+  return std::min<int64_t>(nt, static_cast<int64_t>(per) * cus);
+}
+
 inline int reg_dec_k(int ncols) {
   return ncols <= 4 ? (ncols < 2 ? 2 : ncols) : ncols <= 6 ? 6 : ncols <= 8 ? 8 : ncols <= 12 ? 12 : 16;
 }

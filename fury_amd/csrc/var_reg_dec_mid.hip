@@ -6,8 +6,15 @@
 namespace fury {
 
 #define FURY_DREG_M(KK, M)                                                                     \
-  hipLaunchKernelGGL((decode_var_reg<KK, M>), dim3(nt), dim3(kDecThreads), img + stage, stream, a, \
-                     rows, offs, status, img, stage);
+  if (a.dec_pipe && dec_pipe_k(KK)) {                                                          \
+    const size_t lds = img + 2 * static_cast<size_t>(stage);                                   \
+    const void* kf = reinterpret_cast<const void*>(decode_var_reg<KK, M, dec_pipe_k(KK)>);     \
+    hipLaunchKernelGGL((decode_var_reg<KK, M, dec_pipe_k(KK)>), dim3(dec_pipe_grid(kf, nt, lds)), \
+                       dim3(kDecThreads), lds, stream, a, rows, offs, status, img, stage);     \
+  } else {                                                                                     \
+    hipLaunchKernelGGL((decode_var_reg<KK, M>), dim3(nt), dim3(kDecThreads), img + stage, stream, \
+                       a, rows, offs, status, img, stage);                                     \
+  }
 #define FURY_DREG(KK)                                                                          \
   case KK:                                                                                     \
     if (mode == kSeqBytes) { FURY_DREG_M(KK, kSeqBytes) }                                      \

@@ -299,9 +299,10 @@ int fury_trim_workspace(int32_t device);
  * for deep schemas: "rowenc_rows" (128 / 256 / 512 threads per group), "rowenc_tile" (rows per group,
  * 0 = threads), "rowenc_img" (LDS image bytes); row-walk decode "walk_threads" /
  * "walk_threads_write" (128 / 256 / 512), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
- * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass), "walk_group_k" (a schema
- * with more counted nodes walks its top-level fields in groups of about this many, a workgroup per
- * tile and group; default 16, 0 = one group); flat schemas of 17-256
+ * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass), "walk_group_k" /
+ * "walk_group_min" (a schema with more than walk_group_min counted nodes, default 16, walks its
+ * top-level fields in groups of about walk_group_k counted nodes, default 4, a workgroup per tile
+ * and group; 0 = one group); flat schemas of 17-256
  * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_threads" /
  * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (register-staged encode / decode phases
  * skipped: outputs WRONG, timing only),

@@ -102,6 +102,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
     L = N.lib()
     old = L.fury_get_tuning(b"nested_decode")
     old_gk = L.fury_get_tuning(b"walk_group_k")
+    old_gmin = L.fury_get_tuning(b"walk_group_min")
     seen = []
     try:
         for trial in range(3):
@@ -112,6 +113,7 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
             # 21: the row walk in field groups of one counted slot (walk_group_k 1)
             for mode in ((4, 3, 2, 21, 1) if enc.nested else (3,)):
                 L.fury_set_tuning(b"walk_group_k", 1 if mode == 21 else old_gk)
+                L.fury_set_tuning(b"walk_group_min", 0 if mode == 21 else old_gmin)
                 L.fury_set_tuning(b"nested_decode", 2 if mode == 21 else mode)
                 walkable = levels <= 5 and counted <= 256
                 engine = ("bfs" if mode == 4 or (mode == 3 and not walkable)
@@ -142,4 +144,5 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
     finally:
         L.fury_set_tuning(b"nested_decode", old)
         L.fury_set_tuning(b"walk_group_k", old_gk)
+        L.fury_set_tuning(b"walk_group_min", old_gmin)
     print(f"seed {seed}: {seen}")

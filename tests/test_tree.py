@@ -38,10 +38,18 @@ def engines():
     old = {k: L.fury_get_tuning(k.encode()) for k in ("nested_decode", "walk_threads", "walk_stage", "walk_pool",
                                                        "walk_stage_write", "walk_threads_write",
                                                        "walk_out", "bfs_threads", "bfs_rows",
-                                                       "bfs_stage", "bfs_arena", "walk_group_k")}
+                                                       "bfs_stage", "bfs_arena", "walk_group_k",
+                                                       "walk_group_min")}
     yield
     for k, v in old.items():
         _tune(k, v)
+
+
+def _groups(gk):
+    """Row-walk field groups of about gk counted slots on every schema (None: the defaults --
+    groups of 4 slots past 16 slots)."""
+    _tune("walk_group_min", 16 if gk is None else 0)
+    _tune("walk_group_k", 4 if gk is None else gk)
 
 
 def _schemas():
@@ -102,9 +110,9 @@ def test_tree_decode_equals_oracle_and_level_engine(oracle, dev, engines, name, 
     # field groups (walk_group_k): a workgroup per (tile, group of top-level fields); 1 = about one
     # counted slot per group, the most groups the schema splits into
     for gk in (1, 2):
-        _tune("walk_group_k", gk)
+        _groups(gk)
         assert_columns_equal(fields, _decode_plan(enc, batch), ref, n)
-    _tune("walk_group_k", 16)
+    _groups(None)
     # tile BFS: threads / tile rows, a stage far smaller than the tile (rows read from HBM), an
     # arena too small for the tile (the batch falls back to the row walk), and the defaults
     from fury_amd import _native as N
@@ -139,7 +147,7 @@ def test_tree_decode_large_batch(oracle, dev, engines, mode):
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
     if mode == 21:                             # the row walk in field groups of one counted slot
-        _tune("walk_group_k", 1)
+        _groups(1)
     _tune("nested_decode", 2 if mode == 21 else mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
@@ -179,7 +187,7 @@ def test_tree_decode_skewed_rows(oracle, dev, engines, mode):
     batch = enc.encode_batch([column_to_device(c, dev) for c in host], n)
     want, want_offs = oracle.encode(fields, host, n)
     if mode == 21:                             # the row walk in field groups of one counted slot
-        _tune("walk_group_k", 1)
+        _groups(1)
     _tune("nested_decode", 2 if mode == 21 else mode)
     got = _decode_plan(enc, batch)
     assert_columns_equal(fields, got, oracle.decode(fields, want, want_offs, n), n)
@@ -396,13 +404,13 @@ def test_deep_schema_corrupt_rows(oracle, dev, engines, levels):
         bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
         res = {}
         for mode in (4, 3, 2, 21, 1):          # 21: the row walk in field groups of one slot
-            _tune("walk_group_k", 1 if mode == 21 else 16)
+            _groups(1 if mode == 21 else None)
             _tune("nested_decode", 2 if mode == 21 else mode)
             try:
                 res[mode] = [column_to_host(c) for c in enc.decode_batch(_batch(enc, bad, offs, n, dev))]
             except (IndexOutOfBoundsException, UnsupportedOperationException) as e:
                 res[mode] = type(e)
-        _tune("walk_group_k", 16)
+        _groups(None)
         # the grouped walk checks and charges exactly what the one-group walk does
         if isinstance(res[2], type) or isinstance(res[21], type):
             assert res[21] == res[2], (res[2], res[21])
@@ -514,7 +522,7 @@ def test_random_nested_schemas(oracle, dev, engines, seed):
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     ref = oracle.decode(fields, want, want_offs, n)
     for mode in (4, 3, 2, 21, 1):              # 21: the row walk in field groups of one slot
-        _tune("walk_group_k", 1 if mode == 21 else 16)
+        _groups(1 if mode == 21 else None)
         _tune("nested_decode", 2 if mode == 21 else mode)
         got = _decode_plan(enc, batch) if enc.nested else None
         if got is None:
@@ -552,9 +560,10 @@ def _levels(f):
 def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
     """Beans with 128 / 256 counted nodes (STRING fields + a LIST of a STRING struct): round 6 lifts
     the row walk's 64-counted-node limit to 256 and walks such beans in field groups (a workgroup
-    per tile and group of top-level fields, walk_group_k slots each: 8 / 16 groups at the default
-    16, the 32-group cap at 4, one group at 0), so these decode through the walk (nested_decode 2)
-    -- and the tile BFS (4) and the level engine (1) -- to the oracle's columns."""
+    per tile and group of top-level fields, walk_group_k slots each: 32 groups at the default 4 --
+    the cap, reached by doubling the group size for 256 --, 8 / 16 at 16, one group at 0), so these
+    decode through the walk (nested_decode 2) -- and the tile BFS (4) and the level engine (1) --
+    to the oracle's columns."""
     from fury_amd.beans import beans_to_columns
     from fury_amd.encoder import Encoders, column_to_device
     fields = ([T.not_null_field("id", T.INT64)] + [T.field(f"s{i:03d}", T.STRING) for i in range(nstr)]
@@ -567,7 +576,7 @@ def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
     want, want_offs = oracle.encode(fields, host, n)
     assert np.array_equal(batch.rows.cpu().numpy(), want)
     ref = oracle.decode(fields, want, want_offs, n)
-    for mode, gk in ((2, 16), (2, 4), (2, 0), (4, 16), (1, 16)):
+    for mode, gk in ((2, 4), (2, 16), (2, 0), (4, 4), (1, 4)):
         _tune("walk_group_k", gk)
         _tune("nested_decode", mode)
         assert_columns_equal(fields, _decode_plan(enc, batch), ref, n)
