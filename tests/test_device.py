@@ -821,6 +821,36 @@ def test_reg_decode_every_width_and_kind_mode(oracle, dev, mode, ncols):
     assert_columns_equal(fields, [column_to_host(c) for c in w.finish()], ref, n)
 
 
+@pytest.mark.parametrize("pipe", [1, 2])
+@pytest.mark.parametrize("mode", sorted(_REG_MODES))
+@pytest.mark.parametrize("ncols,n", [(3, 1300), (5, 1300), (6, 400_001)])
+def test_var_decode_pipe(oracle, dev, pipe, mode, ncols, n):
+    """The persistent two-stage decode (tuning var_dec_pipe: 1 the planned tiles, two stages; 2
+    half stages), instances K = 3 and 6: workgroups take tiles blockIdx, + gridDim, ... -- 400k rows
+    give every workgroup several tiles -- and the decode and rows->Arrow are oracle-exact."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import ArrowWriter, column_to_host
+    kinds = _REG_MODES[mode]
+    fields = []
+    for i in range(ncols):
+        k = kinds[i % len(kinds)]
+        fields.append(T.array_field(f"f{i:02d}", T.INT64) if k == "list" else T.field(f"f{i:02d}", k))
+    host = gen_columns("wide", fields, n, seed=ncols * 11 + len(mode), null_pct=10, str_max=40,
+                       list_max=9, list_null_pct=10, elem_null_pct=10)
+    L = N.lib()
+    assert L.fury_set_tuning(b"var_dec_pipe", pipe) == 0
+    try:
+        enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+        want, want_offs = oracle.encode(fields, host, n)
+        w = ArrowWriter(enc)
+        w.write(batch)
+        assert_columns_equal(fields, [column_to_host(c) for c in w.finish()],
+                             oracle.decode(fields, want, want_offs, n), n)
+    finally:
+        L.fury_set_tuning(b"var_dec_pipe", 0)
+    assert L.fury_get_tuning(b"lookback_timeouts") == 0
+
+
 def test_wide_var_schema_large_batch(oracle, dev):
     """A 40-field schema over 300k rows (>1,000 workgroups chained by the look-back)."""
     fields = _wide_fields(40)
