@@ -219,7 +219,10 @@ void set_var_dec_cover(int v) { g_dec_cover = v; }
 // rows past the stage are read from HBM (both correct, slower), so the estimate only moves speed.
 // mixed (C3): 512-row tiles.
 void dec_tile_plan(const VarArgs& a, int* tile, uint32_t* img, uint32_t* stage, int pipe = 0) {
-  constexpr int64_t kBudget = 80 * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
+#ifndef FURY_DEC_BUDGET_KB
+#define FURY_DEC_BUDGET_KB 80                     // (-D: A/B builds, scripts/r06_dec256.sh)
+#endif
+  constexpr int64_t kBudget = FURY_DEC_BUDGET_KB * 1024 - 1024;   // dynamic LDS per workgroup (+ static ~0.2 KB)
   double row = a.fixed_size, img_row = 0, img_fix = 0;
   for (int k = 0; k < a.ncols; k++) {
     const VarCol& c = hcol(a, k);

@@ -1227,7 +1227,10 @@ __device__ __forceinline__ bool is_seq(const Col& c) {
 // words shared with the neighbouring tiles; fixed-width fields leave as coalesced column stores
 // while predecessors publish.
 constexpr int kDecImg = 24 * 1024;
-constexpr int kDecThreads = 512;   // register-staged decode: threads (and maximum rows) per tile
+#ifndef FURY_DEC_THREADS
+#define FURY_DEC_THREADS 512           // (-D: A/B builds of the tile shape, scripts/r06_dec256.sh)
+#endif
+constexpr int kDecThreads = FURY_DEC_THREADS;   // register-staged decode: threads (and maximum rows) per tile
 
 
 // Count (string bytes / list elements) of column k summed over the rows of tile j, by one wave,
