@@ -1194,6 +1194,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "walk_group_k") return static_cast<int32_t>(walk_tuning(8));
   if (key && std::string(key) == "walk_group_min") return static_cast<int32_t>(walk_tuning(9));
   if (key && std::string(key) == "walk_out") return static_cast<int32_t>(walk_tuning(7));
+  if (key && std::string(key) == "walk_skip") return static_cast<int32_t>(walk_tuning(5));
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
   if (key && std::string(key) == "var_dec_pipe") return var_dec_pipe();
