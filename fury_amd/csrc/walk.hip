@@ -43,11 +43,11 @@ struct WShared {
   uint32_t* req;            // [2][nn + 1]: window words, scanned into window offsets
   uint64_t* wsum;           // [K][NT / 64] (pass 1) / [16] (pass 2) scan scratch
   uint32_t* pool;           // window words
-  int32_t* ow;              // [2][nn]: output window (values / offsets) of node n in opool,
-                            // -1: stored straight to HBM
-  uint32_t* olen;           // [2][nn]: its bytes
-  int64_t* oe;              // [nn]: the tile's first entry (E0) of node n
-  uint32_t* oreq;           // [2 nn + 1]: window bytes, scanned into window offsets
+  int32_t* ow;              // [3][nn]: output window (values / offsets / payload) of node n in
+                            // opool, -1: stored straight to HBM
+  uint32_t* olen;           // [3][nn]: its bytes
+  int64_t* oe;              // [2][nn]: the tile's first entry (E0) / payload byte (B0) of node n
+  uint32_t* oreq;           // [3 nn + 1]: window bytes, scanned into window offsets
   uint8_t* opool;           // output windows
   uint8_t* pf;              // prefetch landing zone
   uint8_t* stg;             // staged rows
@@ -81,13 +81,13 @@ __host__ __device__ inline WLayout walk_layout(int nn, int K, int nt, uint32_t s
   b = (b + 15) & ~size_t(15);
   const bool ow = write && out > 0;
   l.oe = b;
-  b += ow ? 8 * static_cast<size_t>(nn) : 0;
+  b += ow ? 8 * 2 * static_cast<size_t>(nn) : 0;
   l.ow = b;
-  b += ow ? 4 * 2 * static_cast<size_t>(nn) : 0;
+  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
   l.olen = b;
-  b += ow ? 4 * 2 * static_cast<size_t>(nn) : 0;
+  b += ow ? 4 * 3 * static_cast<size_t>(nn) : 0;
   l.oreq = b;
-  b += ow ? 4 * (2 * static_cast<size_t>(nn) + 1) : 0;
+  b += ow ? 4 * (3 * static_cast<size_t>(nn) + 1) : 0;
   b = (b + 15) & ~size_t(15);
   l.opool = b;
   b += ow ? out : 0;
@@ -251,10 +251,11 @@ __device__ __forceinline__ void wbits_run(const WCtx& c, int n, int which, uint8
 }
 
 // Output windows (write pass, a.out_cap > 0): the tile's entries of a node that is not row-aligned
-// (values of fixed-width / DECIMAL nodes, Arrow offsets of LIST / MAP / STRING / BINARY nodes) are
-// assembled in LDS and stored as whole lines at the end of the tile (STRING / BINARY payload bytes
-// go straight to HBM, each row's run contiguous): per-lane 1-8 B stores straight to HBM left
-// partial lines (WRITE_SIZE 1.98x the column bytes at 4M depth-3 rows).  A node whose window did not fit the
+// (values of fixed-width / DECIMAL nodes, Arrow offsets of LIST / MAP / STRING / BINARY nodes) and
+// the tile's payload bytes of every STRING / BINARY node (round 6; row-aligned ones too: a tile's
+// payload range [B0, B1) is its own) are assembled in LDS and stored as whole lines at the end of
+// the tile: per-lane 1-8 B stores straight to HBM left partial lines (WRITE_SIZE 1.98x the column
+// bytes at 4M depth-3 rows).  A node whose window did not fit the
 // pool (ow < 0), and the row-aligned ones (coalesced already), store to HBM.
 __device__ __forceinline__ int32_t wwin(const WCtx& c, int which, int n) {
   return c.a->out_cap ? c.sh->ow[which * c.a->nn + n] : -1;
@@ -273,12 +274,17 @@ __device__ __forceinline__ void wput_off(const WCtx& c, CTNode& N, int n, int64_
   else gl(N.offsets)[e + 1] = v;
   if (e == 0) gl(N.offsets)[0] = 0;
 }
-// cnt payload bytes of the batch at pos -> payload byte bp of STRING / BINARY node n (straight to
-// HBM: a second, LDS-window instance of tcopy_to inlined in the walk took it from 125 to 242
-// VGPRs, out of line still to 143).
+// cnt payload bytes of the batch at pos -> payload byte bp of STRING / BINARY node n: into the
+// node's payload window when it has one, else straight to HBM.  (Round 4: a second, inlined
+// instance of tcopy_to took the walk from 125 to 242 VGPRs; tcopy_to is out of line, and the
+// write pass's occupancy is set by its LDS, not its 64 VGPRs.)
 __device__ __forceinline__ void wput_bytes(const WCtx& c, CTNode& N, int n, int64_t bp, int64_t pos,
                                            uint32_t cnt) {
-  tcopy_out(N.values + bp, *c.R, pos, cnt);
+  const int32_t o = wwin(c, 2, n);
+  if (o >= 0)
+    tcopy_to(lds_ptr<uint8_t>(c.sh->opool + o + (bp - c.sh->oe[c.a->nn + n])), *c.R, pos, cnt);
+  else
+    tcopy_out(N.values + bp, *c.R, pos, cnt);
 }
 
 // m fixed-width elements of a LIST / MAP side (write pass) at entries cs, cs + 1, ...: values one
@@ -669,25 +675,35 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   if (tid == 0) sh.req[2 * nn] = 0;
   // output windows: the tile's range of each node's values / offsets / payload (wput_*)
   if (a.out_cap) {
-    for (int i = tid; i < 2 * nn; i += NT) {
+    for (int i = tid; i < 3 * nn; i += NT) {
       const int which = i / nn, n = i - which * nn;
       CTNode& N = tn(a, n);
-      const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
       int64_t bytes = 0;
-      const bool mine = N.ek >= 0 && N.top >= f0 && N.top < f1;
-      if (which == 0) {
-        if (mine && N.values && N.type != FURY_TYPE_BOOL &&
-            (N.width > 0 || N.type == FURY_TYPE_DECIMAL))
-          bytes = (e1 - e0) * (N.width > 0 ? N.width : 16);
+      const bool grp = N.top >= f0 && N.top < f1;
+      const bool mine = N.ek >= 0 && grp;
+      if (which == 2) {                          // payload window: row-aligned nodes too
+        if (grp && N.values && (N.type == FURY_TYPE_STRING || N.type == FURY_TYPE_BINARY) &&
+            !(a.skip & 1)) {
+          const int64_t b0 = a.byt[n * a.stride + tc0];
+          sh.oe[nn + n] = b0;
+          bytes = a.byt[n * a.stride + tc1] - b0;
+        }
       } else {
-        sh.oe[n] = e0;
-        if (mine && N.offsets) bytes = 4 * (e1 - e0);
+        const int64_t e0 = a.cnt[n * a.stride + tc0], e1 = a.cnt[n * a.stride + tc1];
+        if (which == 0) {
+          if (mine && N.values && N.type != FURY_TYPE_BOOL &&
+              (N.width > 0 || N.type == FURY_TYPE_DECIMAL))
+            bytes = (e1 - e0) * (N.width > 0 ? N.width : 16);
+        } else {
+          sh.oe[n] = e0;
+          if (mine && N.offsets) bytes = 4 * (e1 - e0);
+        }
       }
       if (bytes > static_cast<int64_t>(a.out_cap)) bytes = 0;     // straight to HBM
       sh.olen[i] = static_cast<uint32_t>(bytes);
       sh.oreq[i] = bytes > 0 ? static_cast<uint32_t>((bytes + 31) & ~int64_t(15)) : 0u;
     }
-    if (tid == 0) sh.oreq[2 * nn] = 0;
+    if (tid == 0) sh.oreq[3 * nn] = 0;
   }
   Rows R{a.rows, sh.stg, 0, 0, 0};
   if constexpr (STG) R = walk_stage<NT>(a, sh.stg, r0, nr, total);
@@ -695,8 +711,8 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   __syncthreads();
   block_scan_u32<NT>(sh.req, 2 * nn + 1, sh.wsum);   // (req[2nn] = 0 -> the total)
   if (a.out_cap) {
-    block_scan_u32<NT>(sh.oreq, 2 * nn + 1, sh.wsum);
-    for (int i = tid; i < 2 * nn; i += NT)
+    block_scan_u32<NT>(sh.oreq, 3 * nn + 1, sh.wsum);
+    for (int i = tid; i < 3 * nn; i += NT)
       sh.ow[i] = sh.olen[i] > 0 && sh.oreq[i + 1] <= a.out_cap ? static_cast<int32_t>(sh.oreq[i]) : -1;
   }
   const uint32_t pool_words = a.pool_cap / 4;
@@ -738,13 +754,14 @@ __global__ __launch_bounds__(NT) void walk_write_kernel(TreeArgs a) {
   // output windows -> HBM, a wave per window: the range [E0, E1) / [B0, B1) is this tile's alone
   if (a.out_cap) {
     const int wave = tid >> 6;
-    for (int i = wave; i < 2 * nn; i += NT / 64) {
+    for (int i = wave; i < 3 * nn; i += NT / 64) {
       const int32_t o = sh.ow[i];
       if (o < 0) continue;
       const int which = i / nn, n = i - which * nn;
       CTNode& N = tn(a, n);
       uint8_t* dst = which == 0 ? N.values + sh.oe[n] * (N.width > 0 ? N.width : 16)
-                                : reinterpret_cast<uint8_t*>(N.offsets + sh.oe[n] + 1);
+                   : which == 1 ? reinterpret_cast<uint8_t*>(N.offsets + sh.oe[n] + 1)
+                                : N.values + sh.oe[nn + n];
       wave_store_window(dst, sh.opool + o, sh.olen[i]);
     }
   }

@@ -845,54 +845,53 @@ def _alloc_host_node(f: Field, m: int, nbytes: int, zeros=np.zeros) -> Column:
 def _alloc_nodes(order, entries, nbytes, validity: bool, device) -> List[Column]:
     """The output buffers of every schema node (breadth-first ``order``) carved from ONE device
     allocation: bitmaps (validity, BOOL values; zeroed -- the decode only sets bits of shared
-    words) first, so a single memset clears them, then values / payloads / offsets, each 256-B
-    aligned.  One allocation and one memset instead of a few
-    per node (~17 nodes: the per-tensor cost was a third of a 400k-row decode's wall time)."""
+    words) first, so a single memset clears them, then the int32 Arrow offsets, then values /
+    payloads, each 256-B aligned.  One allocation and one memset instead of a few per node (~17
+    nodes: the per-tensor cost was a third of a 400k-row decode's wall time), and the views of
+    each region cut by ONE split_with_sizes call (round 6: per-view slicing in Python cost ~1 ms
+    for a 128-field bean)."""
     def al(x):
         return (x + 255) & ~255
-    plan = []            # per node: list of (kind, nbytes) in node order
-    zero_total = 0
-    rest_total = 0
+    regions = {"z": [], "o": [], "e": []}       # per region: (node, name, nbytes)
     for i, (f, _first) in enumerate(order):
         m, nb, t = int(entries[i]), int(nbytes[i]), f.type_id
-        parts = {}
         if validity:
-            parts["validity"] = ("z", (m + 7) // 8 + 4)
+            regions["z"].append((i, "validity", (m + 7) // 8 + 4))
         if t == BOOL:
-            parts["values"] = ("z", (m + 7) // 8 + 4)
+            regions["z"].append((i, "values", (m + 7) // 8 + 4))
         elif type_width(t) > 0:
-            parts["values"] = ("e", m * type_width(t) + 8)
+            regions["e"].append((i, "values", m * type_width(t) + 8))
         elif t in (STRING, BINARY):
-            parts["values"] = ("e", max(nb, 1))
-            parts["offsets"] = ("e", 4 * (m + 1))
+            regions["e"].append((i, "values", max(nb, 1)))
+            regions["o"].append((i, "offsets", 4 * (m + 1)))
         elif t == DECIMAL:
-            parts["values"] = ("e", 16 * m + 16)
+            regions["e"].append((i, "values", 16 * m + 16))
         elif t in (LIST, MAP):
-            parts["offsets"] = ("e", 4 * (m + 1))
+            regions["o"].append((i, "offsets", 4 * (m + 1)))
         elif t != STRUCT:
             raise UnsupportedOperationException(f"no device decode for {f}")
-        for kind, n in parts.values():
-            if kind == "z":
-                zero_total += al(n)
-            else:
-                rest_total += al(n)
-        plan.append(parts)
-    arena = torch.empty(max(zero_total + rest_total, 256), dtype=torch.uint8, device=device)
-    if zero_total:
-        arena[:zero_total].zero_()
-    zo, ro = 0, zero_total
-    cols = []
-    for parts in plan:
-        views = {}
-        for name, (kind, n) in parts.items():
-            if kind == "z":
-                v, zo = arena[zo:zo + n], zo + al(n)
-            else:
-                v, ro = arena[ro:ro + n], ro + al(n)
-            views[name] = v.view(torch.int32) if name == "offsets" else v
-        cols.append(Column(values=views.get("values"), validity=views.get("validity"),
-                           offsets=views.get("offsets")))
-    return cols
+    size = {k: sum(al(n) for _, _, n in v) for k, v in regions.items()}
+    arena = torch.empty(max(size["z"] + size["o"] + size["e"], 256), dtype=torch.uint8, device=device)
+    if size["z"]:
+        arena[:size["z"]].zero_()
+    views = [dict() for _ in order]
+    base = 0
+    for k in ("z", "o", "e"):
+        segs = regions[k]
+        if segs:
+            region = arena[base:base + size[k]]
+            unit = 4 if k == "o" else 1
+            if unit == 4:
+                region = region.view(torch.int32)
+            sizes = []
+            for _, _, n in segs:                 # each view, then its padding to 256 B
+                sizes += [n // unit, (al(n) - n) // unit]
+            parts = region.split_with_sizes(sizes)
+            for j, (i, name, _) in enumerate(segs):
+                views[i][name] = parts[2 * j]
+        base += size[k]
+    return [Column(values=v.get("values"), validity=v.get("validity"), offsets=v.get("offsets"))
+            for v in views]
 
 
 class _CollectionEncoder(RowEncoder):
