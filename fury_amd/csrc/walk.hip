@@ -276,8 +276,8 @@ __device__ __forceinline__ void wput_off(const WCtx& c, CTNode& N, int n, int64_
 }
 // cnt payload bytes of the batch at pos -> payload byte bp of STRING / BINARY node n: into the
 // node's payload window when it has one, else straight to HBM.  (Round 4: a second, inlined
-// instance of tcopy_to took the walk from 125 to 242 VGPRs; tcopy_to is out of line, and the
-// write pass's occupancy is set by its LDS, not its 64 VGPRs.)
+// instance of tcopy_to took the walk from 125 to 242 VGPRs; tcopy_to is out of line: the depth-3
+// instance stays at 126.)
 __device__ __forceinline__ void wput_bytes(const WCtx& c, CTNode& N, int n, int64_t bp, int64_t pos,
                                            uint32_t cnt) {
   const int32_t o = wwin(c, 2, n);
