@@ -1093,6 +1093,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_skip(value);
     return FURY_OK;
   }
+  if (std::string(key) == "fixed_enc") {
+    if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_enc: 0..4");
+    set_fixed_enc(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "var_dec_pipe") {
     if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_pipe: 0..2");
     set_var_dec_pipe(value);
@@ -1198,6 +1203,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
   if (key && std::string(key) == "var_dec_pipe") return var_dec_pipe();
+  if (key && std::string(key) == "fixed_enc") return fixed_enc();
   if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_wide") return var_wide_mode();
   if (key && std::string(key) == "wide_threads") return wide_threads(false);

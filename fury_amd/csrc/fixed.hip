@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "internal.h"
+#include <atomic>
 #include "kernels.h"
 
 namespace fury {
@@ -450,6 +451,13 @@ int launch_blocks(bool encode, const FixedArgs& a, uint8_t* rows, hipStream_t st
 // 92 / 88 GB/s encode / decode, profiles/r02_host_direct.json).
 static thread_local bool t_host_direct = false;
 void set_thread_host_direct(bool on) { t_host_direct = on; }
+// tuning "fixed_enc" (round 6 A/B, scripts/r06_fixed_enc.sh, profiles/r06_fixed_enc_ab.txt): the
+// fast-path encode's column gather with 0: 8 loads per lane in flight (rounds 1-5), 2: 16 (the
+// default: Struct-100 encode 0.291 -> 0.286 ms, six alternating runs), 3: 32 (0.291), 4: 16 loads
+// and 8 16-B stores (0.287); 1: pair mode, 16-B column loads of two rows per lane (0.320)
+static std::atomic<int> g_fixed_enc{2};
+void set_fixed_enc(int v) { g_fixed_enc = v; }
+int fixed_enc() { return g_fixed_enc; }
 
 namespace {
 
@@ -489,8 +497,8 @@ bool pair_ok(const FixedArgs& a) {
 // Kernel choice (round-1/2 A/B sweeps, profiles/r01_ab_fixed*.json, r02_host_direct*.json; the
 // measured-slower pipelined persistent kernels, padded LDS rows, deep encode gather, pair-mode
 // encode and XCD-contiguous tile order were removed in round 3):
-//   fast path (8-byte columns, no validity): non-temporal loads + stores; the encode gathers 8
-//     column loads per lane; the decode keeps the whole tile in flight (16 loads per lane) and
+//   fast path (8-byte columns, no validity): non-temporal loads + stores; the encode gathers 16
+//     column loads per lane (round 6: 1.7 % faster than 8 on this ROCm; tuning fixed_enc); the decode keeps the whole tile in flight (16 loads per lane) and
 //     stores pairs of rows as 16-B column accesses;
 //   general path (narrow types, validity, > 128 fields): the same tile kernels with per-column
 //     width / validity handling;
@@ -507,6 +515,18 @@ int launch_encode_fixed(const FixedArgs& a, uint8_t* rows, hipStream_t stream, b
     if (t_host_direct)                                                                        \
       return launch_tile_kernel(encode_fixed_kernel<RR, true, 0>, RR, a.row_size, a.nrows,    \
                                 stream, a, rows);                                             \
+    if (g_fixed_enc == 1 && pair_ok(a))                                                       \
+      return launch_tile_kernel(encode_fixed_kernel<RR, true, 3, kUnroll, 4, true>, RR,       \
+                                a.row_size, a.nrows, stream, a, rows);                        \
+    if (g_fixed_enc == 2)                                                                     \
+      return launch_tile_kernel(encode_fixed_kernel<RR, true, 3, 16>, RR, a.row_size,         \
+                                a.nrows, stream, a, rows);                                    \
+    if (g_fixed_enc == 3)                                                                     \
+      return launch_tile_kernel(encode_fixed_kernel<RR, true, 3, 32>, RR, a.row_size,         \
+                                a.nrows, stream, a, rows);                                    \
+    if (g_fixed_enc == 4)                                                                     \
+      return launch_tile_kernel(encode_fixed_kernel<RR, true, 3, 16, 8>, RR, a.row_size,      \
+                                a.nrows, stream, a, rows);                                    \
     return launch_tile_kernel(encode_fixed_kernel<RR, true, 3>, RR, a.row_size, a.nrows,      \
                               stream, a, rows);                                               \
   }

@@ -308,7 +308,11 @@ int fury_trim_workspace(int32_t device);
  * skipped: outputs WRONG, timing only),
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs
  * WRONG, timing only).  Variable-length decode tile plan: "var_dec_cover" (percent of a tile's
- * row bytes the LDS stage must hold, default 95), "var_dec_rows" (forced tile rows, 0 = plan).
+ * row bytes the LDS stage must hold, default 95), "var_dec_rows" (forced tile rows, 0 = plan),
+ * "var_dec_pipe" (0 one tile per workgroup, default; 1 / 2 persistent workgroups with two row
+ * stages, the 3- and 6-column instances -- measured slower, kept for A/B).  Fixed-width encode:
+ * "fixed_enc" (column loads per lane in flight: 2 = 16, default; 0 = 8; 3 = 32; 4 = 16 with 8
+ * stores; 1 = 16-B pair loads).
  * Host path: "host_decode_inplace" (0 / 1).
  * fury_get_tuning only: "unframe_walks" = streams the walk parsed (wholly or from the first frame
  * the repair could not place), "unframe_repairs" = streams the parallel repair parsed,
