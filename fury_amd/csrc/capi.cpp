@@ -886,6 +886,16 @@ int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* ro
   return decode_impl(s, rows, row_offsets, nrows, cols, stream, true, "fury_rows_to_arrow");
 }
 
+// tuning "wide_engine" (round 6): the engine of a 17-256-field flat variable-length schema's plan --
+// 0 auto (default), 1 the wide tiles (wide.hip), 2 the row walk (walk.hip, field groups past 16
+// counted fields).  Auto takes the walk when the batch's average row (one 8-byte read) exceeds
+// "wide_walk_row" bytes: the wide tiles stage 64 rows in at most 96 KB, so longer rows are read
+// from HBM lane by lane (1M rows, scripts/ab_deep.py --flat / --wide33, profiles/r06_wide_engine.jsonl:
+// id + 126 STRING fields, 2.45 KB rows: wide 15.9 ms, walk 6.1 ms; 40 fields, 785 B: 1.70 vs 1.95;
+// tests' 33-field schema, 520 B: 0.89 vs 1.70).
+static std::atomic<int> g_wide_engine{0};
+static std::atomic<int> g_wide_walk_row{1536};
+
 int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                         int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
                         fury_decode_plan** plan, void* stream) {
@@ -906,8 +916,21 @@ int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* r
   std::vector<int64_t> totals(2 * nn, 0);
   // flat variable-length schemas of 17-256 fields: the wide kernels' count pass + scan, kept for
   // the execute (the tile bases), one host sync for the sequence fields' totals
-  const bool wide = nrows > 0 && !s->generic && !s->is_fixed && s->num_fields > 16 /* kRegCols: the register-staged kernels below */ &&
-                    s->num_fields <= kMaxWideVarCols && var_wide_mode();
+  const bool wide_shape = nrows > 0 && !s->generic && !s->is_fixed && s->num_fields > 16 /* kRegCols: the register-staged kernels below */ &&
+                          s->num_fields <= kMaxWideVarCols && var_wide_mode();
+  int engine = g_wide_engine.load();
+  if (wide_shape && engine == 0) {
+    int64_t bytes = 0;
+    int st = check_hip(hipMemcpyAsync(&bytes, row_offsets + nrows, 8, hipMemcpyDeviceToHost, hs),
+                       "hipMemcpyAsync batch bytes");
+    if (!st) st = check_hip(hipStreamSynchronize(hs), "hipStreamSynchronize");
+    if (st) {
+      delete p;
+      return st;
+    }
+    engine = bytes > static_cast<int64_t>(g_wide_walk_row.load()) * nrows ? 2 : 1;
+  }
+  const bool wide = wide_shape && engine != 2;
   if (wide) {
     VarArgs a;
     DeviceTable dt;
@@ -1098,6 +1121,16 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_fixed_enc(value);
     return FURY_OK;
   }
+  if (std::string(key) == "wide_engine") {
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "wide_engine: 0..2");
+    g_wide_engine = value;
+    return FURY_OK;
+  }
+  if (std::string(key) == "wide_walk_row") {
+    if (value < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "wide_walk_row: bytes >= 0");
+    g_wide_walk_row = value;
+    return FURY_OK;
+  }
   if (std::string(key) == "var_dec_pipe") {
     if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "var_dec_pipe: 0..2");
     set_var_dec_pipe(value);
@@ -1203,6 +1236,8 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "host_decode_inplace") return host_decode_inplace();
   if (key && std::string(key) == "var_dec_rows") return var_dec_rows();
   if (key && std::string(key) == "var_dec_pipe") return var_dec_pipe();
+  if (key && std::string(key) == "wide_engine") return g_wide_engine.load();
+  if (key && std::string(key) == "wide_walk_row") return g_wide_walk_row.load();
   if (key && std::string(key) == "fixed_enc") return fixed_enc();
   if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_wide") return var_wide_mode();

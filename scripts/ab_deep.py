@@ -25,6 +25,11 @@ def main():
                     "many STRING fields plus a list of structs (the walk's 64-counted-node limit)")
     ap.add_argument("--modes", default="3,1", help="nested_decode settings (3 tile BFS, 2 row "
                     "walk -- at most 5 levels, else the level engine --, 1 level engine)")
+    ap.add_argument("--flat", default="", help="comma list of STRING-field counts: a flat bean of "
+                    "id + that many STRING fields (--modes: wide_engine settings, 1 wide tiles, "
+                    "2 row walk)")
+    ap.add_argument("--wide33", action="store_true", help="also tests' _wide_fields(33) (wide_engine "
+                    "legs as --flat)")
     ap.add_argument("--tune", default="", help="key=value,... tunings set first (e.g. walk_group_k=8)")
     args = ap.parse_args()
     import numpy as np
@@ -41,9 +46,18 @@ def main():
     from fury_amd import types as T
     cases = [("levels", int(x)) for x in args.levels.split(",") if x]
     cases += [("counted", int(x)) for x in args.wide.split(",") if x]
+    cases += [("flat", int(x)) for x in args.flat.split(",") if x]
+    if args.wide33:
+        cases.append(("wide33", 33))
     for kind, levels in cases:
         if kind == "levels":
             fields = _deep_fields(levels)
+        elif kind == "flat":
+            fields = ([T.not_null_field("id", T.INT64)] +
+                      [T.field(f"s{i:03d}", T.STRING) for i in range(levels)])
+        elif kind == "wide33":
+            from tests.test_device import _wide_fields
+            fields = _wide_fields(33)
         else:
             fields = ([T.not_null_field("id", T.INT64)] +
                       [T.field(f"s{i:03d}", T.STRING) for i in range(levels - 2)] +
@@ -62,8 +76,9 @@ def main():
         batch = RowBatch(rows, offs, n, enc.schema_hash)
         res = {kind: levels, "rows": n, "row_bytes": reps * tot, "tune": args.tune}
         ref = None
+        key = b"wide_engine" if kind in ("flat", "wide33") else b"nested_decode"
         for mode in [int(x) for x in args.modes.split(",")]:
-            assert L.fury_set_tuning(b"nested_decode", mode) == 0
+            assert L.fury_set_tuning(key, mode) == 0
             out = enc.decode_batch(batch)
             torch.cuda.synchronize()
             got = [x for c in out for x in (c.values, c.validity, c.offsets)]
@@ -84,7 +99,8 @@ def main():
                 torch.cuda.synchronize()
                 xs.append(a.elapsed_time(b) / args.iters)
             res[f"decode_ms_mode{mode}"] = round(statistics.median(xs), 3)
-        assert L.fury_set_tuning(b"nested_decode", 3) == 0
+        assert L.fury_set_tuning(b"nested_decode", 2) == 0
+        assert L.fury_set_tuning(b"wide_engine", 1) == 0
         res["bfs_fallbacks"] = L.fury_get_tuning(b"bfs_fallbacks")
         print(json.dumps(res), flush=True)
     del np

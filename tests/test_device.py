@@ -793,6 +793,31 @@ def test_wide_var_schemas_bit_exact(oracle, dev, ncols, n, str_max):
     assert N.lib().fury_get_tuning(b"lookback_timeouts") == 0
 
 
+@pytest.mark.parametrize("engine", [1, 2, 0])
+@pytest.mark.parametrize("ncols,n,str_max", [(17, 3001, 40), (33, 2049, 64), (64, 700, 300),
+                                             (200, 300, 24)])
+def test_wide_plan_engines(oracle, dev, engine, ncols, n, str_max):
+    """The plan decode (fury_decode_prepare / execute, what decode_batch runs for 17-256 flat
+    fields) through each engine of tuning wide_engine -- 1 the wide tiles, 2 the row walk (field
+    groups past 16 counted fields), 0 auto by the average row -- decodes to the oracle's columns."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import column_to_host
+    fields = _wide_fields(ncols)
+    host = gen_columns("wide", fields, n, seed=ncols * 3 + n, null_pct=10, str_max=str_max,
+                       list_max=12, list_null_pct=10, elem_null_pct=10)
+    enc, batch, _ = _roundtrip(oracle, None, n, dev, fields=fields, cols=host)
+    want, want_offs = oracle.encode(fields, host, n)
+    ref = oracle.decode(fields, want, want_offs, n)
+    L = N.lib()
+    old = L.fury_get_tuning(b"wide_engine")
+    assert L.fury_set_tuning(b"wide_engine", engine) == 0
+    try:
+        dec = [column_to_host(c) for c in enc.decode_batch(batch)]
+    finally:
+        L.fury_set_tuning(b"wide_engine", old)
+    assert_columns_equal(fields, dec, ref, n)
+
+
 _REG_MODES = {"bytes": [T.INT32, T.STRING, T.BOOL, T.INT64, T.STRING, T.FLOAT64],
               "lists": [T.INT64, "list", T.BOOL, T.FLOAT32, "list"],
               "all": [T.INT32, T.STRING, "list", T.BOOL, T.INT16]}
