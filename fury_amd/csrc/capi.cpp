@@ -889,12 +889,13 @@ int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* ro
 // tuning "wide_engine" (round 6): the engine of a 17-256-field flat variable-length schema's plan --
 // 0 auto (default), 1 the wide tiles (wide.hip), 2 the row walk (walk.hip, field groups past 16
 // counted fields).  Auto takes the walk when the batch's average row (one 8-byte read) exceeds
-// "wide_walk_row" bytes: the wide tiles stage 64 rows in at most 96 KB, so longer rows are read
-// from HBM lane by lane (1M rows, scripts/ab_deep.py --flat / --wide33, profiles/r06_wide_engine.jsonl:
-// id + 126 STRING fields, 2.45 KB rows: wide 15.9 ms, walk 6.1 ms; 40 fields, 785 B: 1.70 vs 1.95;
-// tests' 33-field schema, 520 B: 0.89 vs 1.70).
+// "wide_walk_row" bytes: the wide tiles stage 64 rows in at most 96 KB and read the rest from HBM
+// lane by lane (1M rows, scripts/ab_deep.py --flat / --wide33, profiles/r06_wide_engine.jsonl; id +
+// N STRING fields, wide vs walk: N = 126 / 2.45 KB rows 15.9 vs 6.1 ms, 90 / 1.75 KB 10.0 vs 4.3,
+// 70 / 1.37 KB 5.45 vs 3.34, 55 / 1.07 KB 3.82 vs 2.65, 40 / 785 B 1.72 vs 1.95; the tests'
+// 33-field schema, 520 B: 0.90 vs 1.70).
 static std::atomic<int> g_wide_engine{0};
-static std::atomic<int> g_wide_walk_row{1536};
+static std::atomic<int> g_wide_walk_row{896};
 
 int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                         int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
