@@ -726,13 +726,39 @@ using namespace fury;
 
 extern "C" {
 
+// tuning "wide_enc_engine" (round 6): the encode of a 17-256-field flat variable-length schema -- 0
+// auto, 1 the wide tiles (wide.hip), 2 the row-walk encode (rowenc.hip, as nested schemas).  Auto
+// takes the row walk when the rows' estimated average (the header + each variable-length column's
+// capacity / rows) exceeds "wide_walk_row" bytes, as the decode plan does.  The rows are the same
+// bytes either way (the Java layout).
+static std::atomic<int> g_wide_enc_engine{1};
+static std::atomic<int> g_wide_walk_row{896};
+
+static bool wide_encode_by_walk(const fury_schema* s, const fury_column* cols, int64_t nrows) {
+  if (s->generic || s->is_fixed || s->num_fields <= 16 || s->num_fields > kMaxWideVarCols ||
+      !var_wide_mode() || !cols || nrows <= 0)
+    return false;
+  const int mode = g_wide_enc_engine.load();
+  if (mode != 0) return mode == 2;
+  double row = s->fixed_size;
+  for (int k = 0; k < s->num_fields; k++) {
+    const int kind = s->plan[k].kind;
+    if (kind == kBytes && cols[k].values) row += static_cast<double>(cols[k].capacity) / nrows + 4;
+    if (kind == kDecimal) row += 16;
+    if (kind == kListFixed && cols[k].child && cols[k].child->values)
+      row += 16 + static_cast<double>(cols[k].child->capacity) / nrows;
+  }
+  return row > g_wide_walk_row.load();
+}
+
 int fury_row_measure(const fury_schema* s, const fury_column* cols, int64_t nrows,
                      int64_t* row_offsets, void* stream) {
   int st = common_checks(s, cols, nrows, "fury_row_measure", static_cast<hipStream_t>(stream));
   if (st) return st;
   if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
   if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
-  if (s->generic) return gen_measure(s, cols, nrows, row_offsets, static_cast<hipStream_t>(stream));
+  if (s->generic || wide_encode_by_walk(s, cols, nrows))
+    return gen_measure(s, cols, nrows, row_offsets, static_cast<hipStream_t>(stream));
   VarArgs a;
   DeviceTable dt;
   st = var_args(s, cols, nrows, false, false, &a, &dt, static_cast<hipStream_t>(stream));
@@ -760,7 +786,7 @@ int fury_row_encode(const fury_schema* s, const fury_column* cols, int64_t nrows
   if (!row_offsets)
     return set_error(FURY_ERR_INVALID_ARGUMENT,
                      "variable-length schema needs row_offsets from fury_row_measure");
-  if (s->generic) {
+  if (s->generic || wide_encode_by_walk(s, cols, nrows)) {
     GenArgs g;
     DeviceTable dt;
     st = gen_args(s, cols, nrows, false, false, &g, &dt, hs);
@@ -794,7 +820,7 @@ int fury_row_encode_measured(const fury_schema* s, const fury_column* cols, int6
   }
   if (!row_offsets) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets is null");
   if (misaligned(row_offsets, 8)) return set_error(FURY_ERR_INVALID_ARGUMENT, "row_offsets misaligned");
-  if (s->generic) {
+  if (s->generic || wide_encode_by_walk(s, cols, nrows)) {
     st = gen_measure(s, cols, nrows, row_offsets, hs);
     if (st || nrows == 0) return st;
     GenArgs g;
@@ -895,7 +921,6 @@ int fury_rows_to_arrow(const fury_schema* s, const void* rows, const int64_t* ro
 // 70 / 1.37 KB 5.45 vs 3.34, 55 / 1.07 KB 3.82 vs 2.65, 40 / 785 B 1.72 vs 1.95; the tests'
 // 33-field schema, 520 B: 0.90 vs 1.70).
 static std::atomic<int> g_wide_engine{0};
-static std::atomic<int> g_wide_walk_row{896};
 
 int fury_decode_prepare(const fury_schema* s, const void* rows, const int64_t* row_offsets,
                         int64_t nrows, int64_t* node_entries, int64_t* node_bytes,
@@ -1127,6 +1152,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     g_wide_engine = value;
     return FURY_OK;
   }
+  if (std::string(key) == "wide_enc_engine") {
+    if (value < 0 || value > 2) return set_error(FURY_ERR_INVALID_ARGUMENT, "wide_enc_engine: 0..2");
+    g_wide_enc_engine = value;
+    return FURY_OK;
+  }
   if (std::string(key) == "wide_walk_row") {
     if (value < 0) return set_error(FURY_ERR_INVALID_ARGUMENT, "wide_walk_row: bytes >= 0");
     g_wide_walk_row = value;
@@ -1239,6 +1269,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "var_dec_pipe") return var_dec_pipe();
   if (key && std::string(key) == "wide_engine") return g_wide_engine.load();
   if (key && std::string(key) == "wide_walk_row") return g_wide_walk_row.load();
+  if (key && std::string(key) == "wide_enc_engine") return g_wide_enc_engine.load();
   if (key && std::string(key) == "fixed_enc") return fixed_enc();
   if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_wide") return var_wide_mode();

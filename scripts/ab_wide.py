@@ -23,6 +23,10 @@ def main():
     ap.add_argument("--tune", action="append", default=[],
                     help="key=value fury_set_tuning before timing (repeatable)")
     ap.add_argument("--no-plan", action="store_true", help="skip the plan-API decode leg")
+    ap.add_argument("--flat", type=int, default=0, help="id + this many STRING fields instead of "
+                    "tests' _wide_fields(--ncols)")
+    ap.add_argument("--enc-engines", default="", help="comma list of wide_enc_engine settings: "
+                    "encode_ms per setting, rows checked equal to the first")
     args = ap.parse_args()
     import torch
     from fury_amd.encoder import Encoders, _tree_bytes, column_to_device
@@ -32,7 +36,9 @@ def main():
     for kv in args.tune:
         k, v = kv.split("=")
         assert N.lib().fury_set_tuning(k.encode(), int(v)) == 0, N.last_error()
-    fields = _wide_fields(args.ncols)
+    from fury_amd import types as T
+    fields = (([T.not_null_field("id", T.INT64)] + [T.field(f"s{i:03d}", T.STRING) for i in range(args.flat)])
+              if args.flat else _wide_fields(args.ncols))
     n = args.rows
     host = gen_columns("wide", fields, n, seed=7, null_pct=10, str_max=args.str_max, list_max=6)
     dev = torch.device("cuda:0")
@@ -57,7 +63,20 @@ def main():
             e.synchronize()
             best = min(best, s.elapsed_time(e))
         return best
-    res = {"ncols": args.ncols, "rows": n, "row_bytes": row_bytes, "column_bytes": col_bytes}
+    res = {"ncols": len(fields), "rows": n, "row_bytes": row_bytes, "column_bytes": col_bytes}
+    if args.enc_engines:
+        ref = None
+        for m in [int(x) for x in args.enc_engines.split(",")]:
+            assert N.lib().fury_set_tuning(b"wide_enc_engine", m) == 0
+            rows.zero_()
+            res[f"encode_ms_engine{m}"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
+            torch.cuda.synchronize()
+            got = rows[:row_bytes].clone()
+            if ref is None:
+                ref = got
+            else:
+                res[f"rows_equal_engine{m}"] = bool(torch.equal(ref, got))
+        assert N.lib().fury_set_tuning(b"wide_enc_engine", 1) == 0
     out = enc.decode_batch(batch)                       # allocated once (bound sizing)
     res["encode_ms"] = timed(lambda: enc.encode_measured_into(cols, n, rows, offs))
     res["decode_flat_ms"] = timed(lambda: enc.decode_batch(batch, out=out))
