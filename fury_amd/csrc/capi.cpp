@@ -730,8 +730,11 @@ extern "C" {
 // auto, 1 the wide tiles (wide.hip), 2 the row-walk encode (rowenc.hip, as nested schemas).  Auto
 // takes the row walk when the rows' estimated average (the header + each variable-length column's
 // capacity / rows) exceeds "wide_walk_row" bytes, as the decode plan does.  The rows are the same
-// bytes either way (the Java layout).
-static std::atomic<int> g_wide_enc_engine{1};
+// bytes either way (the Java layout).  1M rows, wide vs walk (scripts/ab_wide.py --enc-engines,
+// profiles/r06_wide_enc_engine.jsonl): id + 126 / 70 / 55 / 40 STRING fields (3.2 / 1.8 / 1.4 / 1.0
+// KB rows) 9.56 / 5.22 / 4.10 / 2.59 vs 6.76 / 3.67 / 2.91 / 2.15 ms; the tests' 33-field schema
+// (581 B rows) 0.51 vs 1.07 ms.
+static std::atomic<int> g_wide_enc_engine{0};
 static std::atomic<int> g_wide_walk_row{896};
 
 static bool wide_encode_by_walk(const fury_schema* s, const fury_column* cols, int64_t nrows) {

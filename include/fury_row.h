@@ -305,7 +305,8 @@ int fury_trim_workspace(int32_t device);
  * and group; 0 = one group); flat schemas of 17-256
  * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_engine" (the plan's engine
  * for them: 0 auto -- the row walk when the batch's average row exceeds "wide_walk_row" bytes,
- * default 896 --, 1 wide tiles, 2 row walk), "wide_threads" /
+ * default 896 --, 1 wide tiles, 2 row walk; "wide_enc_engine" the same for the encode, by the
+ * columns' estimated row), "wide_threads" /
  * "wide_enc_threads" (256 / 512 / 1024); diagnostics "var_skip" (register-staged encode / decode phases
  * skipped: outputs WRONG, timing only),
  * "tree_debug" (phase clocks) and "walk_skip" (bitmask of write-pass phases skipped: outputs

@@ -818,6 +818,35 @@ def test_wide_plan_engines(oracle, dev, engine, ncols, n, str_max):
     assert_columns_equal(fields, dec, ref, n)
 
 
+@pytest.mark.parametrize("engine", [1, 2, 0])
+@pytest.mark.parametrize("ncols,n,str_max", [(17, 2049, 40), (33, 1500, 64), (64, 700, 300),
+                                             (200, 300, 24)])
+def test_wide_encode_engines(oracle, dev, engine, ncols, n, str_max):
+    """The encode of a 17-256-field flat schema through each engine of tuning wide_enc_engine --
+    1 the wide tiles, 2 the row-walk encode (rowenc.hip), 0 auto by the estimated row -- measured
+    and two-pass: the rows are the oracle's bytes."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders
+    fields = _wide_fields(ncols)
+    host = gen_columns("wide", fields, n, seed=ncols * 5 + n, null_pct=10, str_max=str_max,
+                       list_max=12, list_null_pct=10, elem_null_pct=10)
+    want, want_offs = oracle.encode(fields, host, n)
+    L = N.lib()
+    old = L.fury_get_tuning(b"wide_enc_engine")
+    assert L.fury_set_tuning(b"wide_enc_engine", engine) == 0
+    try:
+        enc = Encoders.bean(fields, device=dev)
+        cols = _dev_cols(host, dev)
+        batch = enc.encode_batch(cols, n)
+        rows, offs, total = _encode_measured(enc, cols, n, dev)
+    finally:
+        L.fury_set_tuning(b"wide_enc_engine", old)
+    assert np.array_equal(batch.row_offsets.cpu().numpy(), want_offs)
+    assert np.array_equal(batch.rows.cpu().numpy(), want)
+    assert np.array_equal(offs.cpu().numpy(), want_offs)
+    assert np.array_equal(rows[:total].cpu().numpy(), want)
+
+
 _REG_MODES = {"bytes": [T.INT32, T.STRING, T.BOOL, T.INT64, T.STRING, T.FLOAT64],
               "lists": [T.INT64, "list", T.BOOL, T.FLOAT32, "list"],
               "all": [T.INT32, T.STRING, "list", T.BOOL, T.INT16]}
