@@ -1145,6 +1145,11 @@ int fury_set_tuning(const char* key, int32_t value) {
     set_var_skip(value);
     return FURY_OK;
   }
+  if (std::string(key) == "fixed_dec") {
+    if (value < 0 || value > 3) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_dec: 0..3");
+    set_fixed_dec(value);
+    return FURY_OK;
+  }
   if (std::string(key) == "fixed_enc") {
     if (value < 0 || value > 4) return set_error(FURY_ERR_INVALID_ARGUMENT, "fixed_enc: 0..4");
     set_fixed_enc(value);
@@ -1274,6 +1279,7 @@ int32_t fury_get_tuning(const char* key) {
   if (key && std::string(key) == "wide_walk_row") return g_wide_walk_row.load();
   if (key && std::string(key) == "wide_enc_engine") return g_wide_enc_engine.load();
   if (key && std::string(key) == "fixed_enc") return fixed_enc();
+  if (key && std::string(key) == "fixed_dec") return fixed_dec();
   if (key && std::string(key) == "var_skip") return var_skip();
   if (key && std::string(key) == "var_wide") return var_wide_mode();
   if (key && std::string(key) == "wide_threads") return wide_threads(false);

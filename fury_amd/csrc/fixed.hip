@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kThreads) void encode_fixed_kernel(FixedArgs a,
 
 // D = 16-B row-tile loads per lane in flight (4 default, 16 "deep": the whole 64-row Struct-100
 // tile in one round trip); P = pair mode (16-B column stores of rows 2q, 2q + 1).
-template <int R, bool kFast, int NT, int D = 4, bool P = false>
+template <int R, bool kFast, int NT, int D = 4, bool P = false, int SU = kUnroll>
 __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
                                                                  const uint8_t* __restrict__ rows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -284,9 +284,9 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
     static_assert(kFast, "pair mode is fast-path only");
     constexpr int H = R / 2;
     const int total2 = a.ncols * H;
-    for (int base = threadIdx.x; base < total2; base += kThreads * kUnroll) {
+    for (int base = threadIdx.x; base < total2; base += kThreads * SU) {
 #pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
+      for (int u = 0; u < SU; u++) {
         const int idx = base + u * kThreads;
         if (__builtin_amdgcn_readfirstlane(idx - lane) >= total2) break;
         const int c = col_of<H>(idx, total2, lane);
@@ -308,9 +308,9 @@ __global__ __launch_bounds__(kThreads) void decode_fixed_kernel(FixedArgs a,
     return;
   }
   const int total = a.ncols * R;
-  for (int base = threadIdx.x; base < total; base += kThreads * kUnroll) {
+  for (int base = threadIdx.x; base < total; base += kThreads * SU) {
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {
+    for (int u = 0; u < SU; u++) {
       const int idx = base + u * kThreads;
       if (__builtin_amdgcn_readfirstlane(idx - lane) >= total) break;   // wave-uniform exit
       const int c = col_of<R>(idx, total, lane);
@@ -456,6 +456,11 @@ void set_thread_host_direct(bool on) { t_host_direct = on; }
 // default: Struct-100 encode 0.291 -> 0.286 ms, six alternating runs), 3: 32 (0.291), 4: 16 loads
 // and 8 16-B stores (0.287); 1: pair mode, 16-B column loads of two rows per lane (0.320)
 static std::atomic<int> g_fixed_enc{2};
+// tuning "fixed_dec" (round 6 A/B): the fast-path decode's column stores per lane in flight, 0: 8
+// (default), 1: 16, 2: 4; 3: 8 with 8 row loads per lane in flight instead of 16
+static std::atomic<int> g_fixed_dec{0};
+void set_fixed_dec(int v) { g_fixed_dec = v; }
+int fixed_dec() { return g_fixed_dec; }
 void set_fixed_enc(int v) { g_fixed_enc = v; }
 int fixed_enc() { return g_fixed_enc; }
 
@@ -551,6 +556,15 @@ int launch_decode_fixed(const FixedArgs& a, const uint8_t* rows, hipStream_t str
     if (t_host_direct)                                                                        \
       return launch_tile_kernel(decode_fixed_kernel<RR, true, 0>, RR, a.row_size, a.nrows,    \
                                 stream, a, r);                                                \
+    if (pair && g_fixed_dec == 1)                                                             \
+      return launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, true, 16>, RR,           \
+                                a.row_size, a.nrows, stream, a, r);                           \
+    if (pair && g_fixed_dec == 2)                                                             \
+      return launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, true, 4>, RR,            \
+                                a.row_size, a.nrows, stream, a, r);                           \
+    if (pair && g_fixed_dec == 3)                                                             \
+      return launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 8, true>, RR,                \
+                                a.row_size, a.nrows, stream, a, r);                           \
     return pair ? launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, true>, RR,          \
                                      a.row_size, a.nrows, stream, a, r)                       \
                 : launch_tile_kernel(decode_fixed_kernel<RR, true, 3, 16, false>, RR,         \

@@ -206,6 +206,8 @@ void set_var_dec_rows(int v);
 int var_dec_rows_rejected();          // forced tiles whose images did not fit (plan used instead)
 int fixed_enc();                      // tuning "fixed_enc" (fixed.hip)
 void set_fixed_enc(int v);
+int fixed_dec();                      // tuning "fixed_dec" (fixed.hip)
+void set_fixed_dec(int v);
 int var_dec_pipe();                   // tuning "var_dec_pipe" (var.hip)
 void set_var_dec_pipe(int v);
 int var_dec_cover();                  // tuning "var_dec_cover" (var.hip): stage coverage, percent
