@@ -146,3 +146,56 @@ def test_corrupt_rows_random_schemas(oracle, dev, seed):
         L.fury_set_tuning(b"walk_group_k", old_gk)
         L.fury_set_tuning(b"walk_group_min", old_gmin)
     print(f"seed {seed}: {seen}")
+
+
+@pytest.mark.parametrize("seed", list(range(8)))
+def test_corrupt_rows_wide_flat_engines(oracle, dev, seed):
+    """Corrupted rows of 17-40-field flat schemas through the plan decode's two engines (round 6,
+    tuning wide_engine): the wide tiles (1) must give the oracle's flat outcome, the row walk (2)
+    the oracle's walk outcome (its count pass and item budget restated) -- the same exceptions or
+    the same columns."""
+    from fury_amd import _native as N
+    from fury_amd.encoder import Encoders, IndexOutOfBoundsException, UnsupportedOperationException
+    from fury_amd.workloads import gen_columns
+    from oracle import oracle as O
+    from tests.test_bounds import _batch
+    from tests.test_device import _wide_fields
+    from fury_amd.encoder import column_to_host
+    rng = np.random.default_rng(11000 + seed)
+    fields = _wide_fields(int(rng.integers(17, 41)))
+    n = int(rng.integers(50, 500))
+    host = gen_columns("wide", fields, n, seed=seed, null_pct=10, str_max=40, list_max=8,
+                       list_null_pct=10, elem_null_pct=10)
+    enc = Encoders.bean(fields, device=dev)
+    rows, offs = oracle.encode(fields, host, n)
+    offs = np.asarray(offs, np.int64).copy()
+    L = N.lib()
+    old = L.fury_get_tuning(b"wide_engine")
+    seen = []
+    try:
+        for trial in range(3):
+            bad = rows.copy()
+            pos = rng.integers(0, len(bad), int(rng.integers(1, 30)))
+            bad[pos] = rng.integers(0, 256, len(pos)).astype(np.uint8)
+            for engine in (1, 2):
+                assert L.fury_set_tuning(b"wide_engine", engine) == 0
+                want = _expected(O, fields, engine == 2, "walk" if engine == 2 else "levels",
+                                 bad, offs, n)
+                try:
+                    got = [column_to_host(c) for c in enc.decode_batch(_batch(enc, bad, offs, n, dev))]
+                    enc.device_status()
+                    err = None
+                except IndexOutOfBoundsException:
+                    err = "oob"
+                except UnsupportedOperationException as e:
+                    err = "budget" if "decode budget" in str(e) else "map"
+                where = f"trial {trial}, engine {engine}"
+                seen.append(f"{engine}:{err or 'decoded'}")
+                if isinstance(want, str):
+                    assert err == want, f"{where}: oracle says {want}, device {err or 'decoded'}"
+                else:
+                    assert err is None, f"{where}: oracle decodes, device raises {err}"
+                    assert_columns_equal(fields, got, want, n)
+    finally:
+        L.fury_set_tuning(b"wide_engine", old)
+    print(f"seed {seed}: {len(fields)} fields, {seen}")
