@@ -1,6 +1,7 @@
 #!/bin/bash
 # Pipelined register encode: var tests, then tuning A/B on mixed (C3) and nested (C4); the walk
-# A/B legs first when WALK=1.
+# A/B legs first when WALK=1.  (Record of the round-5 experiment, DESIGN §4d: the pipelined encode
+# and its tuning "var_enc_pipe" were removed after it measured slower, so this no longer runs.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
