@@ -139,7 +139,10 @@ std::atomic<int> g_walk_skip = 0;                // tuning "walk_skip": diagnost
 // of 16 / 8 / 4 / 2 slots 9.7 / 7.2 / 6.8 / 6.9 and 13.8 / 10.2 / 10.2 / 10.2 ms, the level engine
 // 16.5 / 25.7 ms.  The depth-3 schema (9 slots) in groups of 4 / 2 / 1: 2.64 / 2.99 / 3.25 vs
 // 2.53 ms -- at <= 16 slots the cursors do not limit the tiles per CU, so it stays one group.
-std::atomic<int> g_walk_group_k = 4;     // tuning "walk_group_k" (0 = one group)
+// With the payload windows (late round 6, profiles/r06_walk_group_size_payload_windows.jsonl)
+// groups of 8 took over: 128 counted nodes 6.52 vs 6.89 ms (4), flat id + 126 STRING fields 5.83
+// vs 6.14; 200 counted nodes 9.47 (4 doubles to 8 there: at most 32 groups).
+std::atomic<int> g_walk_group_k = 8;     // tuning "walk_group_k" (0 = one group)
 std::atomic<int> g_walk_group_min = 16;  // tuning "walk_group_min"
 uint64_t* g_tree_dbg = nullptr;  // tuning "tree_debug": phase accumulators (device, 80 words)
 

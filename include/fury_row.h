@@ -301,7 +301,7 @@ int fury_trim_workspace(int32_t device);
  * "walk_threads_write" (128 / 256 / 512), "walk_stage" / "walk_stage_write" / "walk_pool" / "walk_out"
  * (LDS bytes), "walk_prefetch" (bit 0 write pass, bit 1 count pass), "walk_group_k" /
  * "walk_group_min" (a schema with more than walk_group_min counted nodes, default 16, walks its
- * top-level fields in groups of about walk_group_k counted nodes, default 4, a workgroup per tile
+ * top-level fields in groups of about walk_group_k counted nodes, default 8, a workgroup per tile
  * and group; 0 = one group); flat schemas of 17-256
  * fields: "var_wide" (1 wide tiles, default; 0 generic var tiles), "wide_engine" (the plan's engine
  * for them: 0 auto -- the row walk when the batch's average row exceeds "wide_walk_row" bytes,

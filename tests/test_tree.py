@@ -47,9 +47,9 @@ def engines():
 
 def _groups(gk):
     """Row-walk field groups of about gk counted slots on every schema (None: the defaults --
-    groups of 4 slots past 16 slots)."""
+    groups of 8 slots past 16 slots)."""
     _tune("walk_group_min", 16 if gk is None else 0)
-    _tune("walk_group_k", 4 if gk is None else gk)
+    _tune("walk_group_k", 8 if gk is None else gk)
 
 
 def _schemas():
@@ -560,8 +560,8 @@ def _levels(f):
 def test_walk_wide_counted_nodes(oracle, dev, engines, nstr):
     """Beans with 128 / 256 counted nodes (STRING fields + a LIST of a STRING struct): round 6 lifts
     the row walk's 64-counted-node limit to 256 and walks such beans in field groups (a workgroup
-    per tile and group of top-level fields, walk_group_k slots each: 32 groups at the default 4 --
-    the cap, reached by doubling the group size for 256 --, 8 / 16 at 16, one group at 0), so these
+    per tile and group of top-level fields, walk_group_k slots each: 16 / 32 groups at the default
+    8, 32 at 4 -- the cap, reached by doubling the group size --, 8 / 16 at 16, one group at 0), so these
     decode through the walk (nested_decode 2) -- and the tile BFS (4) and the level engine (1) --
     to the oracle's columns."""
     from fury_amd.beans import beans_to_columns
